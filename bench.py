@@ -1,0 +1,225 @@
+"""Benchmark of the old->new mesh transfer step (PMMG_interpMetricsAndFields).
+
+One step = one full pmmg_hip_locate_interp over one group: bbox + seed
+grids + Morton sort + volume/surface locate + metric/field interpolation +
+fallbacks, with every input already resident in HBM (device-mode C-ABI).
+
+Multi-GPU (torchrun, one process per GPU): every rank owns one group of the
+same size, exactly as ParMmg shards the step by group (the per-group work is
+independent, src/interpmesh_pmmg.c:690-730), so there is no collective in the
+data path and the scaling is weak.  `value` = points located+interpolated by
+all ranks / max-over-ranks step time.
+
+Prints ONE JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from parmmg_amd import configs, synth  # noqa: E402
+from parmmg_amd.transfer import TransferContext  # noqa: E402
+
+METRIC = "new-mesh points located+interpolated/sec (Mpts/s) and HBM GB/s, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def build_workload(w: configs.Workload, rank: int):
+    t0 = time.time()
+    bg = synth.lattice(w.kind, w.n_old, jitter=0.0)
+    new = synth.lattice(w.kind, w.n_new, jitter=w.jitter_new, seed=synth.SEED + rank, with_trias=False)
+    met = synth.solution(w.metric, bg.xyz)
+    fields = [synth.solution(f, bg.xyz) for f in w.fields]
+    pclass = synth.classes(new)
+    log(f"[bench r{rank}] workload {w.name}: bg {bg.ne} tets / {bg.np} verts / {bg.nt} trias, new {new.np} verts, "
+        f"K={w.K}, generated in {time.time() - t0:.1f}s")
+    return bg, new, met, fields, pclass
+
+
+def pmc_traffic(workload: str):
+    """HBM bytes per k_vol launch from the committed rocprofv3 PMC summary
+    (profiles/pmc_<workload>.json, produced by tools/pmc_summary.py), or None."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get("k_vol_hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(w, bg, new, met, fields, pclass, budget_s: float):
+    """The oracle (C port of the reference path, 1 thread) on a bounded sample:
+    the full per-iteration precompute (faceAreas, triaNormals, nodeTrias, as the
+    reference times it) plus locate+interpolate of the first S points in
+    lattice order; the full-step rate is extrapolated from the sample."""
+    from oracle import oracle as O
+
+    B = O.Background(bg, met, fields, w.hausd)
+    order = np.arange(1, new.np + 1, dtype=np.int32)
+    s = min(new.np, 20000)
+    r = O.run(B, new.xyz, pclass, order[:s])
+    per_pt = r["t_locate"] / s
+    s2 = int(min(new.np, max(s, budget_s / max(per_pt, 1e-9))))
+    if s2 > s:
+        r = O.run(B, new.xyz, pclass, order[:s2])
+        s = s2
+    t_pre, t_loc = r["t_precompute"], r["t_locate"]
+    nproc = int((pclass[:s] != 0).sum())
+    ntot = int((pclass != 0).sum())
+    t_full = t_pre + t_loc * ntot / max(nproc, 1)
+    return {
+        "value": ntot / t_full / 1e6,
+        "unit": "Mpts/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"oracle (C restatement, 1 thread) on {w.name}: full precompute over {bg.ne} tets "
+                  f"({t_pre:.2f}s) + locate/interp of the first {s} new points in lattice order "
+                  f"({t_loc:.2f}s), extrapolated to all {ntot} points",
+        "t_precompute_s": t_pre,
+        "t_sample_s": t_loc,
+        "sample_points": nproc,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="cfg4", choices=sorted(configs.SHORT))
+    ap.add_argument("--nosort", action="store_true")
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+
+    w = configs.SHORT[args.config]
+    bg, new, met, fields, pclass = build_workload(w, rank)
+
+    ctx = TransferContext(local, sort=not args.nosort)
+    d_xyz, d_tetv, d_adja = ctx.upload(bg.xyz), ctx.upload(bg.tetv), ctx.upload(bg.adja)
+    d_triv, d_adjt = ctx.upload(bg.triv), ctx.upload(bg.adjt)
+    d_met = ctx.upload(met)
+    d_f = [ctx.upload(f) for f in fields]
+    d_qxyz, d_pc = ctx.upload(new.xyz), ctx.upload(pclass)
+    d_mo = ctx.empty((new.np, w.met_size), np.float64)
+    d_fo = [ctx.empty((new.np, f.shape[1]), np.float64) for f in fields]
+    d_elem = ctx.empty((new.np,), np.int32)
+    d_hit = ctx.empty((new.np,), np.int8)
+
+    def step():
+        ctx.set_background(d_xyz, d_tetv, d_adja, d_triv, d_adjt, w.hausd)
+        ctx.set_solutions(d_met, d_f)
+        ctx.locate_interp(d_qxyz, d_pc, d_mo, d_fo, d_elem, d_hit, sync=False)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    st0 = ctx.sync()
+    # timed region: barrier + device sync on both sides
+    barrier()
+    ctx.sync()
+    ms_vol = []
+    ms_tot = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        st = ctx.sync()  # per-step event times of this step (sync adds no device work)
+        ms_vol.append(st.ms_vol)
+        ms_tot.append(st.ms_total)
+    barrier()
+    ctx.sync()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    npts = int(st.nvol + st.nbdy)
+    ms_per_step = elapsed / args.steps * 1e3
+    value = npts * world / (elapsed / args.steps) / 1e6
+    (np_o, ne_o, _), (np_n, _, _) = w.counts()
+    B = w.algorithmic_bytes(npts)
+    per_pt = B / npts
+    kvol_ms = float(np.mean(ms_vol))
+    kvol_bytes = per_pt * st.nvol
+    achieved = kvol_bytes / (kvol_ms * 1e-3) / 1e9
+    traffic = pmc_traffic(w.name)
+    out = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "Mpts/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (Kuhn lattices, analytic metric/fields, splitmix64 jitter)",
+        "config": {
+            "workload": w.name,
+            "description": w.description,
+            "background_tets": ne_o, "background_verts": np_o, "new_points": np_n,
+            "located_points_per_gpu": npts, "K_doubles_per_vertex": w.K,
+            "parallelism": f"one group per GPU x{world} (weak, no data-path collective)",
+            "morton_sort": not args.nosort,
+        },
+        "gbps_algorithmic_step": round(B / (ms_per_step * 1e-3) / 1e9, 1),
+        "device_ms": {"step_total": round(float(np.mean(ms_tot)), 4), "k_vol": round(kvol_ms, 4),
+                      "prepare": round(st.ms_prepare, 4), "sort": round(st.ms_sort, 4),
+                      "k_bdy": round(st.ms_bdy, 4), "fallback": round(st.ms_fallback, 4)},
+        "locate_stats": {k: v for k, v in st.as_dict().items() if not k.startswith("ms_")},
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "k_vol",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "algorithmic_bytes_per_point": round(per_pt, 2),
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(w, bg, new, met, fields, pclass, args.cpu_baseline_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

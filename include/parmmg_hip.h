@@ -1,0 +1,163 @@
+/*
+ * parmmg_hip.h — C-ABI of the MI355X (gfx950) old->new mesh transfer module.
+ *
+ * This is the drop-in boundary for ParMmg's metric/field interpolation step.
+ * It replaces, per group, the body of
+ *
+ *   int PMMG_interpMetricsAndFields(PMMG_pParMesh parmesh, int *permNodGlob)
+ *       reference: src/interpmesh_pmmg.c:663-741, prototype src/parmmg.h:472,
+ *       called once per remeshing iteration from src/libparmmg1.c:829
+ *
+ * and, below it, the static per-group worker
+ *
+ *   PMMG_interpMetricsAndFields_mesh(...)      src/interpmesh_pmmg.c:477-649
+ *
+ * together with everything it reaches: PMMG_locatePointVol / _Bdy
+ * (src/locate_pmmg.c:786-883, :587-723), the barycentric evaluation
+ * (src/barycoord_pmmg.c) and the interpolators bound through the
+ * PMMG_interp{2,3,4}bar function pointers (src/parmmgexterns.c:4-6,
+ * bound by PMMG_setfunc src/libparmmg_tools.c:595-612).
+ *
+ * Conventions (all entry points):
+ *  - Plain pointers and sizes only; no torch or HIP types in signatures.
+ *  - Return 1 on success, 0 on failure: the internal ParMmg convention of
+ *    PMMG_interpMetricsAndFields (NOT the public PMMG_SUCCESS=0 convention).
+ *  - Arrays are "row r = entity r+1": ParMmg entities are 1-based, entry 0 is
+ *    unused.  A host shim passes e.g. `met->m + met->size` for the metric and
+ *    `mesh->adja + 1` for the tetra adjacency, so no copy is needed for those.
+ *  - Entity ids stored INSIDE arrays keep the reference encoding: vertex ids
+ *    in tetv/triv are 1-based, adja holds 4*k'+i' (0 = boundary face,
+ *    src/locate_pmmg.c:821), adjt holds 3*k'+i' (0 = surface border,
+ *    src/locate_pmmg.c:635).
+ *  - `where` = PMMG_HIP_HOST: pointers are host memory, calls copy and are
+ *    synchronous.  `where` = PMMG_HIP_DEVICE: pointers are device memory on
+ *    the context's device; set_* calls only record the pointers (no copy) and
+ *    pmmg_hip_locate_interp enqueues on the context stream (use
+ *    pmmg_hip_sync before reading results or stats).
+ *  - The module is reentrant per context (the reference is not: it uses
+ *    static warning flags and global function pointers).
+ */
+#ifndef PARMMG_HIP_H
+#define PARMMG_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PMMG_HIP_HOST   0
+#define PMMG_HIP_DEVICE 1
+
+/* Per-point classification supplied by the caller (the host shim derives it
+ * from Mmg tags in the reference's visitation loop, src/interpmesh_pmmg.c:535-550). */
+#define PMMG_PT_SKIP 0   /* invalid, MG_REQ (copied by PMMG_copyMetricsAndFields_point) or unreferenced */
+#define PMMG_PT_VOL  1   /* volume point   -> PMMG_locatePointVol path */
+#define PMMG_PT_BDY  2   /* MG_BDY point   -> PMMG_locatePointBdy path */
+
+/* Located-element kind written to hit_out (diagnostics + parity checking). */
+#define PMMG_HIT_NONE         0  /* not processed (PMMG_PT_SKIP) */
+#define PMMG_HIT_VOL_WALK     1  /* adjacency walk accepted the tetra          locate_pmmg.c:814-815 */
+#define PMMG_HIT_VOL_EXHAUST  2  /* exhaustive scan: lowest-index accepted      locate_pmmg.c:743-762 */
+#define PMMG_HIT_VOL_CLOSEST  3  /* not located: closest tetra, nearest vertex  locate_pmmg.c:764-767 */
+#define PMMG_HIT_BDY_FACE     4  /* tria walk accepted, interior of the tria    locate_pmmg.c:624-627 */
+#define PMMG_HIT_BDY_EDGE     5  /* tria walk accepted, on an edge (isBorder)   barycoord_pmmg.c:109-120 */
+#define PMMG_HIT_BDY_VERTEX   6  /* tria walk accepted, at a vertex (isBorder)  barycoord_pmmg.c:109-120 */
+#define PMMG_HIT_BDY_WEDGE    7  /* edge shadow wedge                           locate_pmmg.c:643-649 */
+#define PMMG_HIT_BDY_CONE     8  /* vertex shadow cone                          locate_pmmg.c:651-657 */
+#define PMMG_HIT_BDY_EXHAUST  9  /* exhaustive tria scan: lowest-index accepted locate_pmmg.c:483-503 */
+#define PMMG_HIT_BDY_STALE   10  /* not located, re-evaluation accepted         locate_pmmg.c:505-509 */
+#define PMMG_HIT_BDY_CLOSEST 11  /* not located: closest tria, nearest vertex   locate_pmmg.c:511,681 */
+
+#define PMMG_HIT_CODE(h) ((h) & 15)
+#define PMMG_HIT_LOC(h)  (((h) >> 4) & 3)
+
+typedef struct pmmg_hip_ctx pmmg_hip_ctx;
+
+/* Counters of one pmmg_hip_locate_interp call (the reference's debug-only
+ * PMMG_locateStats, src/locate_pmmg.h:45-50, plus per-phase device times). */
+typedef struct {
+  int64_t nvol;          /* volume queries */
+  int64_t nbdy;          /* surface queries */
+  int64_t nvol_walk, nvol_exhaust, nvol_closest;
+  int64_t nbdy_face, nbdy_edge, nbdy_vertex, nbdy_wedge, nbdy_cone;
+  int64_t nbdy_exhaust, nbdy_stale, nbdy_closest;
+  int64_t steps_total;   /* walk steps, volume + surface */
+  int64_t stepmax;
+  /* device time in milliseconds, measured with HIP events on the context stream */
+  float ms_prepare;      /* bbox, seed grids, surface CSR, query compaction */
+  float ms_sort;         /* Morton sort of the queries */
+  float ms_vol;          /* volume locate + interpolate kernel */
+  float ms_bdy;          /* surface locate + interpolate kernel */
+  float ms_fallback;     /* exhaustive / closest kernels */
+  float ms_total;        /* whole call, first to last event */
+} pmmg_hip_stats;
+
+/* Options (bit flags) for pmmg_hip_create. */
+#define PMMG_HIP_OPT_NOSORT 1   /* process queries in input order (no Morton sort) */
+
+/* Create a context on HIP device `device`.  Returns NULL on failure. */
+pmmg_hip_ctx *pmmg_hip_create(int device, int options);
+void pmmg_hip_destroy(pmmg_hip_ctx *ctx);
+
+/* Background (pre-remesh) mesh of one group: the reference's oldMesh after
+ * PMMG_update_oldGrps (src/grpsplit_pmmg.c:1224).
+ *   np    vertices, xyz[3*np]        (MMG5_Point.c, packed)
+ *   ne    tetrahedra, tetv[4*ne]     (MMG5_Tetra.v, packed), adja[4*ne] (= &mesh->adja[1])
+ *   nt    boundary trias, triv[3*nt] (MMG5_Tria.v, packed),  adjt[3*nt] (= &mesh->adjt[1])
+ *   hausd surface distance tolerance (oldMesh->info.hausd, src/locate_pmmg.c:253,315,363)
+ * nt may be 0 (then no PMMG_PT_BDY query may be submitted). */
+int pmmg_hip_set_background(pmmg_hip_ctx *ctx, int np, const double *xyz,
+                            int ne, const int *tetv, const int *adja,
+                            int nt, const int *triv, const int *adjt,
+                            double hausd, int where);
+
+/* Background solutions: the metric (met_size 0 = none, 1 = iso, 6 = aniso,
+ * storage m11,m12,m13,m22,m23,m33 as MMG5 stores it) and nfield fields of
+ * size field_size[j] (1, 3 or 6; size 6 fields use the inverse-tensor
+ * interpolation, src/interpmesh_pmmg.c:582-593,623-634).
+ * met[met_size*np], fields[j][field_size[j]*np] (= sol->m + sol->size). */
+int pmmg_hip_set_solutions(pmmg_hip_ctx *ctx, int met_size, const double *met,
+                           int nfield, const int *field_size,
+                           const double *const *fields, int where);
+
+/* Locate every new point with pclass != PMMG_PT_SKIP and interpolate the
+ * metric and fields into it.
+ *   np_new         new-mesh vertices; xyz_new[3*np_new], pclass[np_new]
+ *   met_out        [met_size*np_new] (may be NULL iff met_size == 0)
+ *   fields_out[j]  [field_size[j]*np_new]
+ *   elem_out       [np_new] located tetra/tria id (1-based), may be NULL
+ *   hit_out        [np_new] PMMG_HIT_* code in bits 0-3; for EDGE / WEDGE the
+ *                  local edge, for VERTEX / CONE the local vertex of the tria
+ *                  in bits 4-5 (PMMG_HIT_CODE / PMMG_HIT_LOC); may be NULL
+ *   stats          may be NULL (with PMMG_HIP_DEVICE it is filled at pmmg_hip_sync)
+ * Rows of points that are skipped, and rows whose tensor inversion fails
+ * (MMG5_invmat, src/interpmesh_pmmg.c:258-267), are left untouched, as in the
+ * reference. */
+int pmmg_hip_locate_interp(pmmg_hip_ctx *ctx, int np_new, const double *xyz_new,
+                           const uint8_t *pclass, double *met_out,
+                           double *const *fields_out, int *elem_out,
+                           int8_t *hit_out, pmmg_hip_stats *stats, int where);
+
+/* Wait for all work queued on the context; fills the stats of the last
+ * PMMG_HIP_DEVICE call.  Returns 1/0. */
+int pmmg_hip_sync(pmmg_hip_ctx *ctx, pmmg_hip_stats *stats);
+
+/* Device memory helpers for callers that keep data resident (bench, shims
+ * that reuse buffers across iterations). */
+void *pmmg_hip_malloc(pmmg_hip_ctx *ctx, int64_t bytes);
+int   pmmg_hip_free(pmmg_hip_ctx *ctx, void *dptr);
+int   pmmg_hip_memcpy_h2d(pmmg_hip_ctx *ctx, void *dst, const void *src, int64_t bytes);
+int   pmmg_hip_memcpy_d2h(pmmg_hip_ctx *ctx, void *dst, const void *src, int64_t bytes);
+
+/* Last error message of the context (static storage inside ctx). */
+const char *pmmg_hip_last_error(pmmg_hip_ctx *ctx);
+
+/* Number of visible HIP devices (0 when none / no driver). */
+int pmmg_hip_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PARMMG_HIP_H */

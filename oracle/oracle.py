@@ -1,0 +1,170 @@
+"""ctypes front-end of the CPU oracle (oracle/pmmg_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, as the checker / CPU baseline.  The product
+path (parmmg_amd/) never imports it.  Parity status: see pmmg_oracle.h
+("parity unpinned" at the Mmg arithmetic boundary).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SO = os.path.join(HERE, "liboracle.so")
+
+MODE_FAITHFUL, MODE_FRESH = 0, 1
+EPS = 1.0e-06
+
+
+class _Bg(ctypes.Structure):
+    _fields_ = [("np", ctypes.c_int), ("ne", ctypes.c_int), ("nt", ctypes.c_int),
+                ("xyz", ctypes.c_void_p), ("tetv", ctypes.c_void_p), ("adja", ctypes.c_void_p),
+                ("triv", ctypes.c_void_p), ("adjt", ctypes.c_void_p), ("hausd", ctypes.c_double),
+                ("met_size", ctypes.c_int), ("met", ctypes.c_void_p), ("nfield", ctypes.c_int),
+                ("field_size", ctypes.c_void_p), ("field", ctypes.c_void_p)]
+
+
+class _Q(ctypes.Structure):
+    _fields_ = [("np", ctypes.c_int), ("xyz", ctypes.c_void_p), ("pclass", ctypes.c_void_p),
+                ("nvisit", ctypes.c_int), ("visit", ctypes.c_void_p)]
+
+
+class _Out(ctypes.Structure):
+    _fields_ = [("met", ctypes.c_void_p), ("field", ctypes.c_void_p), ("elem", ctypes.c_void_p),
+                ("hit", ctypes.c_void_p), ("loc", ctypes.c_void_p), ("minbary", ctypes.c_void_p),
+                ("steps", ctypes.c_void_p)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(SO):
+            subprocess.check_call(["make", "-s", "-C", HERE])
+        L = ctypes.CDLL(SO)
+        vp, ci, cd = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
+        L.orc_interp_mesh.argtypes = [vp, vp, vp, ci, vp]
+        L.orc_interp_mesh.restype = ci
+        L.orc_eval_in_element.argtypes = [vp, vp, ci, ci, ci, ci, vp, vp]
+        L.orc_eval_in_element.restype = ci
+        L.orc_tetra_minbary.argtypes = [vp, ci, vp]
+        L.orc_tetra_minbary.restype = cd
+        L.orc_tria_accepts.argtypes = [vp, ci, vp, vp]
+        L.orc_tria_accepts.restype = ci
+        for n in ("orc_first_accepting_tetra", "orc_closest_tetra", "orc_first_accepting_tria", "orc_closest_tria"):
+            getattr(L, n).argtypes = [vp, vp]
+            getattr(L, n).restype = ci
+        L.orc_wedge_test.argtypes = [vp, ci, ci, vp]
+        L.orc_wedge_test.restype = ci
+        L.orc_cone_test.argtypes = [vp, ci, ci, vp]
+        L.orc_cone_test.restype = ci
+        L.orc_invmat.argtypes = [vp, vp]
+        L.orc_invmat.restype = ci
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+class Background:
+    """Holds an orc_background built from a Mesh + solutions (keeps arrays alive)."""
+
+    def __init__(self, mesh, met, fields, hausd=0.01):
+        self.mesh = mesh
+        self.met = None if met is None else np.ascontiguousarray(met, np.float64)
+        self.fields = [np.ascontiguousarray(f, np.float64) for f in fields]
+        self._fsz = (ctypes.c_int * max(1, len(self.fields)))(*[f.shape[1] for f in self.fields])
+        self._fpt = (ctypes.c_void_p * max(1, len(self.fields)))(*[_p(f) for f in self.fields])
+        self.s = _Bg(mesh.np, mesh.ne, mesh.nt, _p(mesh.xyz), _p(mesh.tetv), _p(mesh.adja), _p(mesh.triv),
+                     _p(mesh.adjt), float(hausd), 0 if self.met is None else self.met.shape[1], _p(self.met),
+                     len(self.fields), ctypes.cast(self._fsz, ctypes.c_void_p),
+                     ctypes.cast(self._fpt, ctypes.c_void_p))
+
+    @property
+    def ref(self):
+        return ctypes.byref(self.s)
+
+
+def run(bg: Background, xyz_new, pclass, visit, mode=MODE_FAITHFUL):
+    """Sequential reference-order run.  Returns dict of per-point arrays."""
+    xyz_new = np.ascontiguousarray(xyz_new, np.float64)
+    pclass = np.ascontiguousarray(pclass, np.uint8)
+    visit = np.ascontiguousarray(visit, np.int32)
+    npn = xyz_new.shape[0]
+    out = {
+        "met": None if bg.met is None else np.full((npn, bg.met.shape[1]), np.nan),
+        "fields": [np.full((npn, f.shape[1]), np.nan) for f in bg.fields],
+        "elem": np.zeros(npn, np.int32), "hit": np.zeros(npn, np.int8), "loc": np.full(npn, -1, np.int8),
+        "minbary": np.zeros(npn), "steps": np.zeros(npn, np.int32),
+    }
+    fpt = (ctypes.c_void_p * max(1, len(out["fields"])))(*[_p(f) for f in out["fields"]])
+    o = _Out(_p(out["met"]), ctypes.cast(fpt, ctypes.c_void_p), _p(out["elem"]), _p(out["hit"]), _p(out["loc"]),
+             _p(out["minbary"]), _p(out["steps"]))
+    q = _Q(npn, _p(xyz_new), _p(pclass), visit.shape[0], _p(visit))
+    timing = (ctypes.c_double * 2)()
+    if not lib().orc_interp_mesh(bg.ref, ctypes.byref(q), ctypes.byref(o), int(mode), timing):
+        raise RuntimeError("oracle run failed")
+    out["t_precompute"], out["t_locate"] = timing[0], timing[1]
+    return out
+
+
+def eval_in_element(bg: Background, x, is_bdy, elem, hit, loc):
+    """Values the reference arithmetic gives for x evaluated in (elem, hit, loc)."""
+    x = np.ascontiguousarray(x, np.float64)
+    met = None if bg.met is None else np.full(bg.met.shape[1], np.nan)
+    fr = [np.full(f.shape[1], np.nan) for f in bg.fields]
+    fpt = (ctypes.c_void_p * max(1, len(fr)))(*[_p(f) for f in fr])
+    ok = lib().orc_eval_in_element(bg.ref, _p(x), int(is_bdy), int(elem), int(hit), int(loc), _p(met),
+                                   ctypes.cast(fpt, ctypes.c_void_p))
+    if not ok:
+        raise ValueError(f"cannot evaluate hit={hit} elem={elem}")
+    return met, fr
+
+
+def tetra_minbary(bg, k, x):
+    return lib().orc_tetra_minbary(bg.ref, int(k), _p(np.ascontiguousarray(x, np.float64)))
+
+
+def tria_accepts(bg, k, x):
+    mb = ctypes.c_double()
+    ok = lib().orc_tria_accepts(bg.ref, int(k), _p(np.ascontiguousarray(x, np.float64)), ctypes.byref(mb))
+    return bool(ok), mb.value
+
+
+def first_accepting_tetra(bg, x):
+    return lib().orc_first_accepting_tetra(bg.ref, _p(np.ascontiguousarray(x, np.float64)))
+
+
+def closest_tetra(bg, x):
+    return lib().orc_closest_tetra(bg.ref, _p(np.ascontiguousarray(x, np.float64)))
+
+
+def first_accepting_tria(bg, x):
+    return lib().orc_first_accepting_tria(bg.ref, _p(np.ascontiguousarray(x, np.float64)))
+
+
+def closest_tria(bg, x):
+    return lib().orc_closest_tria(bg.ref, _p(np.ascontiguousarray(x, np.float64)))
+
+
+def wedge_test(bg, k, l, x):
+    return lib().orc_wedge_test(bg.ref, int(k), int(l), _p(np.ascontiguousarray(x, np.float64)))
+
+
+def cone_test(bg, k, iloc, x):
+    return lib().orc_cone_test(bg.ref, int(k), int(iloc), _p(np.ascontiguousarray(x, np.float64)))
+
+
+def invmat(m):
+    m = np.ascontiguousarray(m, np.float64)
+    mi = np.zeros(6)
+    ok = lib().orc_invmat(_p(m), _p(mi))
+    return bool(ok), mi

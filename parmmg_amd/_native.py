@@ -1,0 +1,93 @@
+"""ctypes bindings of the native libraries.
+
+The product path is ``libpmmg_hip.so`` (include/parmmg_hip.h) and the C host
+layer ``libpmmg_host.so``.  Loading fails loudly when a library is missing:
+there is no Python or CPU fallback for the transfer step.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+from . import build as _build
+
+c_int, c_int64, c_double, c_void_p, c_char_p = ctypes.c_int, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p, ctypes.c_char_p
+P = ctypes.POINTER
+
+
+class HipStats(ctypes.Structure):
+    """``pmmg_hip_stats`` of include/parmmg_hip.h."""
+
+    _fields_ = [
+        ("nvol", c_int64), ("nbdy", c_int64),
+        ("nvol_walk", c_int64), ("nvol_exhaust", c_int64), ("nvol_closest", c_int64),
+        ("nbdy_face", c_int64), ("nbdy_edge", c_int64), ("nbdy_vertex", c_int64), ("nbdy_wedge", c_int64),
+        ("nbdy_cone", c_int64), ("nbdy_exhaust", c_int64), ("nbdy_stale", c_int64), ("nbdy_closest", c_int64),
+        ("steps_total", c_int64), ("stepmax", c_int64),
+        ("ms_prepare", ctypes.c_float), ("ms_sort", ctypes.c_float), ("ms_vol", ctypes.c_float),
+        ("ms_bdy", ctypes.c_float), ("ms_fallback", ctypes.c_float), ("ms_total", ctypes.c_float),
+    ]
+
+    def as_dict(self) -> dict:
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+# C-ABI of include/parmmg_hip.h: name -> (restype, argtypes)
+HIP_API = {
+    "pmmg_hip_create": (c_void_p, [c_int, c_int]),
+    "pmmg_hip_destroy": (None, [c_void_p]),
+    "pmmg_hip_set_background": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p,
+                                        c_void_p, c_double, c_int]),
+    "pmmg_hip_set_solutions": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int]),
+    "pmmg_hip_locate_interp": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_void_p, P(HipStats), c_int]),
+    "pmmg_hip_sync": (c_int, [c_void_p, P(HipStats)]),
+    "pmmg_hip_malloc": (c_void_p, [c_void_p, c_int64]),
+    "pmmg_hip_free": (c_int, [c_void_p, c_void_p]),
+    "pmmg_hip_memcpy_h2d": (c_int, [c_void_p, c_void_p, c_void_p, c_int64]),
+    "pmmg_hip_memcpy_d2h": (c_int, [c_void_p, c_void_p, c_void_p, c_int64]),
+    "pmmg_hip_last_error": (c_char_p, [c_void_p]),
+    "pmmg_hip_device_count": (c_int, []),
+}
+
+SYNTH_API = {
+    "synth_counts": (c_int, [c_int, c_int, P(c_int64)]),
+    "synth_vertices": (c_int, [c_int, c_int, c_double, ctypes.c_uint64, c_void_p, c_void_p]),
+    "synth_tetra": (c_int, [c_int, c_int, c_void_p, c_void_p]),
+    "synth_trias": (c_int64, [c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "synth_field": (c_int, [c_int, c_int64, c_void_p, c_void_p]),
+    "synth_field_size": (c_int, [c_int]),
+    "synth_visit_order": (c_int64, [c_int, c_void_p, c_int, c_void_p]),
+    "synth_classes": (c_int, [c_int64, c_void_p, c_int, c_void_p]),
+}
+
+_cache: dict[str, ctypes.CDLL] = {}
+
+
+def _load(path: str, api: dict, what: str) -> ctypes.CDLL:
+    if path in _cache:
+        return _cache[path]
+    if not os.path.exists(path):
+        raise RuntimeError(f"{what} is not built ({path}); run `python -m parmmg_amd.build` "
+                           "(there is no fallback path)")
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in api.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _cache[path] = lib
+    return lib
+
+
+def hip_lib() -> ctypes.CDLL:
+    """The product HIP module (include/parmmg_hip.h)."""
+    return _load(_build.HIP_SO, HIP_API, "libpmmg_hip.so")
+
+
+def synth_lib() -> ctypes.CDLL:
+    return _load(_build.SYNTH_SO, SYNTH_API, "libpmmg_synth.so")
+
+
+def host_lib() -> ctypes.CDLL:
+    hip_lib()  # resolve the dependency from the same directory first
+    return _load(_build.HOST_SO, {}, "libpmmg_host.so")

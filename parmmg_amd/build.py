@@ -1,0 +1,102 @@
+"""In-tree build of the native libraries (no cmake, no JIT cache).
+
+* ``parmmg_amd/libpmmg_hip.so``   — the product: HIP kernels + C-ABI of
+  ``include/parmmg_hip.h`` (hipcc, gfx950 only, ``-ffp-contract=off``).
+* ``parmmg_amd/libpmmg_host.so``  — the product's C host layer
+  (``csrc/pmmg_host.c``: group loop / point classification of
+  ``PMMG_interpMetricsAndFields``), linked against libpmmg_hip.so.
+* ``parmmg_amd/libpmmg_synth.so`` — synthetic-mesh generator (tests/bench).
+* ``oracle/liboracle.so``         — the CPU restatement (test infrastructure).
+
+Outputs are .so files next to their sources; they are git-ignored but travel
+to the GPU box with the working tree.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "parmmg_amd")
+CSRC = os.path.join(PKG, "csrc")
+INC = os.path.join(ROOT, "include")
+ORACLE = os.path.join(ROOT, "oracle")
+
+HIP_SO = os.path.join(PKG, "libpmmg_hip.so")
+HOST_SO = os.path.join(PKG, "libpmmg_host.so")
+SYNTH_SO = os.path.join(PKG, "libpmmg_synth.so")
+ORACLE_SO = os.path.join(ORACLE, "liboracle.so")
+
+ARCH = "gfx950"
+
+
+def _hipcc() -> str:
+    for cand in (shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found: the HIP module cannot be built")
+
+
+def _run(cmd: list[str]) -> None:
+    proc = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if proc.returncode != 0:
+        sys.stderr.write(proc.stdout)
+        raise RuntimeError("build command failed: " + " ".join(cmd))
+
+
+def _stale(out: str, deps: list[str]) -> bool:
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_hip(force: bool = False) -> str:
+    src = os.path.join(CSRC, "pmmg_hip.hip")
+    deps = [src, os.path.join(INC, "parmmg_hip.h"), __file__]
+    if force or _stale(HIP_SO, deps):
+        _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
+              f"-I{INC}", "-o", HIP_SO, src])
+    return HIP_SO
+
+
+def build_host(force: bool = False) -> str:
+    src = os.path.join(CSRC, "pmmg_host.c")
+    deps = [src, os.path.join(CSRC, "pmmg_host.h"), os.path.join(INC, "parmmg_hip.h"), HIP_SO, __file__]
+    if force or _stale(HOST_SO, deps):
+        _run(["gcc", "-O2", "-std=c99", "-Wall", "-Wextra", "-fPIC", "-shared", f"-I{INC}", f"-I{CSRC}",
+              "-o", HOST_SO, src, f"-L{PKG}", "-lpmmg_hip", "-Wl,-rpath,$ORIGIN"])
+    return HOST_SO
+
+
+def build_synth(force: bool = False) -> str:
+    src = os.path.join(CSRC, "pmmg_synth.c")
+    deps = [src, os.path.join(CSRC, "pmmg_synth.h"), __file__]
+    if force or _stale(SYNTH_SO, deps):
+        _run(["gcc", "-O2", "-std=c99", "-fopenmp", "-Wall", "-Wextra", "-fPIC", "-shared", "-o", SYNTH_SO, src,
+              "-lm"])
+    return SYNTH_SO
+
+
+def build_oracle(force: bool = False) -> str:
+    src = os.path.join(ORACLE, "pmmg_oracle.c")
+    deps = [src, os.path.join(ORACLE, "pmmg_oracle.h"), __file__]
+    if force or _stale(ORACLE_SO, deps):
+        # -ffp-contract=off: keep the reference's rounding (no FMA contraction)
+        _run(["gcc", "-O2", "-std=c99", "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wextra", "-fPIC",
+              "-shared", "-o", ORACLE_SO, src, "-lm"])
+    return ORACLE_SO
+
+
+def build_all(force: bool = False) -> None:
+    build_hip(force)
+    build_host(force)
+    build_synth(force)
+    build_oracle(force)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)
+    print("built:", HIP_SO, HOST_SO, SYNTH_SO, ORACLE_SO)

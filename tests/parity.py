@@ -1,0 +1,150 @@
+"""Parity checking of the HIP module against the CPU oracle.
+
+Contract (BASELINE.json north_star):
+  (i)   a volume point whose reference tetra has min barycentric coordinate
+        > MMG5_EPS is located in the IDENTICAL tetra (surface face hits are
+        only reported: near domain edges a tria of the adjacent face can accept
+        the point within hausd, so the reference's own answer is path dependent);
+  (ii)  every other point lands in an element the reference accepts (walk /
+        wedge / cone criteria), or in the reference's exhaustive result
+        (lowest-index accepting element, else the closest element);
+  (iii) the interpolated metric and fields equal the reference interpolator
+        evaluated in the element the module chose — checked bit for bit
+        (tolerance written here: 1e-12 relative, and the exact-match count is
+        reported).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from oracle import oracle as O
+from parmmg_amd import synth
+from parmmg_amd.transfer import TransferContext
+
+EPS = O.EPS
+REL_TOL = 1e-12
+
+VOL_WALK, VOL_EXHAUST, VOL_CLOSEST = 1, 2, 3
+BDY_FACE, BDY_EDGE, BDY_VERTEX, BDY_WEDGE, BDY_CONE, BDY_EXHAUST, BDY_STALE, BDY_CLOSEST = range(4, 12)
+
+
+def make_case(kind=synth.CUBE, n_old=6, n_new=7, metric=synth.F_ANI,
+              fields=(synth.F_SCALAR, synth.F_VECTOR, synth.F_TENSOR, synth.F_AFFINE),
+              jitter_old=0.0, jitter_new=0.2, req_every=0, hausd=0.01, seed=synth.SEED, with_ref=True):
+    bg = synth.lattice(kind, n_old, jitter=jitter_old)
+    new = synth.lattice(kind, n_new, jitter=jitter_new, seed=seed)
+    met = None if metric is None else synth.solution(metric, bg.xyz)
+    fs = [synth.solution(w, bg.xyz) for w in fields]
+    pc = synth.classes(new, req_every)
+    B = O.Background(bg, met, fs, hausd)
+    case = dict(bg=bg, new=new, met=met, fields=fs, pclass=pc, B=B, hausd=hausd)
+    if with_ref:
+        vis = synth.visit_order(new)
+        case["ref"] = O.run(B, new.xyz, pc, vis, O.MODE_FRESH)
+        case["ref_faithful"] = O.run(B, new.xyz, pc, vis, O.MODE_FAITHFUL)
+    return case
+
+
+def run_gpu(case, sort=True, ctx=None):
+    bg, new = case["bg"], case["new"]
+    own = ctx is None
+    ctx = ctx or TransferContext(0, sort=sort)
+    try:
+        ctx.set_background(bg.xyz, bg.tetv, bg.adja, bg.triv, bg.adjt, case["hausd"])
+        ctx.set_solutions(case["met"], case["fields"])
+        npn = new.np
+        met_out = None if case["met"] is None else np.full((npn, case["met"].shape[1]), np.nan)
+        f_out = [np.full((npn, f.shape[1]), np.nan) for f in case["fields"]]
+        elem = np.zeros(npn, np.int32)
+        hit = np.zeros(npn, np.int8)
+        st = ctx.locate_interp(new.xyz, case["pclass"], met_out, f_out, elem, hit)
+        return dict(met=met_out, fields=f_out, elem=elem, hit=hit, stats=st.as_dict())
+    finally:
+        if own:
+            ctx.close()
+
+
+def _same(a, b):
+    """bit-equal or both NaN (rows left untouched by a failed tensor inversion)"""
+    return np.all((a == b) | (np.isnan(a) & np.isnan(b)))
+
+
+def _relerr(a, b):
+    d = np.abs(a - b)
+    s = np.maximum(np.abs(a), np.abs(b))
+    with np.errstate(invalid="ignore", divide="ignore"):
+        r = np.where(s > 0, d / s, d)
+    r = np.where(np.isnan(a) & np.isnan(b), 0.0, r)
+    return float(np.nanmax(np.where(np.isnan(r), np.inf, r))) if r.size else 0.0
+
+
+def check(case, gpu, max_points=None):
+    """Return a report dict; raises AssertionError on a contract violation."""
+    B, new, pc, ref = case["B"], case["new"], case["pclass"], case.get("ref")
+    code = (gpu["hit"].astype(np.int32) & 15)
+    loc = (gpu["hit"].astype(np.int32) >> 4) & 3
+    rep = dict(n=0, exact=0, maxrel=0.0, class_i=0, class_i_same=0, hits={}, ref_hits={})
+    # skipped rows untouched
+    skip = pc == 0
+    if case["met"] is not None:
+        assert np.isnan(gpu["met"][skip]).all(), "skipped rows were written"
+    assert (code[skip] == 0).all()
+    assert (code[~skip] != 0).all(), f"{int((code[~skip] == 0).sum())} points not processed"
+    idx = np.nonzero(~skip)[0]
+    if max_points is not None and idx.size > max_points:
+        idx = np.random.default_rng(0).choice(idx, max_points, replace=False)
+    for c in np.unique(code[idx]):
+        rep["hits"][int(c)] = int((code[idx] == c).sum())
+    if ref is not None:
+        for c in np.unique(ref["hit"][idx]):
+            rep["ref_hits"][int(c)] = int((ref["hit"][idx] == c).sum())
+    for i in idx:
+        x = new.xyz[i]
+        is_bdy = pc[i] == 2
+        h, k, l = int(code[i]), int(gpu["elem"][i]), int(loc[i])
+        # (ii) acceptance of the chosen element
+        if h == VOL_WALK:
+            assert not is_bdy and O.tetra_minbary(B, k, x) > -EPS, (i, h, k)
+        elif h == VOL_EXHAUST:
+            assert k == O.first_accepting_tetra(B, x), (i, h, k)
+        elif h == VOL_CLOSEST:
+            assert O.first_accepting_tetra(B, x) == 0 and k == O.closest_tetra(B, x), (i, h, k)
+        elif h in (BDY_FACE, BDY_EDGE, BDY_VERTEX):
+            ok, _ = O.tria_accepts(B, k, x)
+            assert is_bdy and ok, (i, h, k)
+        elif h == BDY_WEDGE:
+            assert O.wedge_test(B, k, l, x) == 4, (i, h, k, l)
+        elif h == BDY_CONE:
+            assert O.cone_test(B, k, l, x) == 1, (i, h, k, l)
+        elif h == BDY_EXHAUST:
+            assert k == O.first_accepting_tria(B, x), (i, h, k)
+        elif h in (BDY_STALE, BDY_CLOSEST):
+            assert O.first_accepting_tria(B, x) == 0 and k == O.closest_tria(B, x), (i, h, k)
+        else:
+            raise AssertionError(f"unknown hit {h} at {i}")
+        # (iii) values = reference arithmetic in the chosen element
+        met, fr = O.eval_in_element(B, x, is_bdy, k, h, l)
+        got = ([gpu["met"][i]] if met is not None else []) + [f[i] for f in gpu["fields"]]
+        want = ([met] if met is not None else []) + fr
+        same = all(_same(g, w) for g, w in zip(got, want))
+        rel = max(_relerr(g, w) for g, w in zip(got, want))
+        rep["exact"] += int(same)
+        rep["maxrel"] = max(rep["maxrel"], rel)
+        assert rel <= REL_TOL, (i, h, k, rel, got, want)
+        rep["n"] += 1
+        # (i) identical element where the reference is unambiguous
+        if ref is not None:
+            rh = int(ref["hit"][i])
+            if rh in (VOL_WALK, VOL_EXHAUST) and ref["minbary"][i] > EPS:
+                rep["class_i"] += 1
+                same_elem = int(ref["elem"][i]) == k
+                rep["class_i_same"] += int(same_elem)
+                assert same_elem, f"class (i) point {i}: reference elem {ref['elem'][i]} hit {rh}, module elem {k} hit {h}"
+            elif rh == BDY_FACE and ref["minbary"][i] > EPS:
+                # surface hits are path dependent near domain edges (a tria of
+                # the adjacent face may accept within hausd): reported, class (ii)
+                rep.setdefault("srf_face", 0)
+                rep.setdefault("srf_face_same", 0)
+                rep["srf_face"] += 1
+                rep["srf_face_same"] += int(int(ref["elem"][i]) == k)
+    return rep

@@ -1,0 +1,107 @@
+"""Parity of the HIP module with the CPU oracle (runs on the MI355X).
+
+Sizes are chosen so the oracle's per-point checks finish in seconds; the
+contract is documented in tests/parity.py."""
+import numpy as np
+import pytest
+
+from parity import check, make_case, run_gpu
+from parmmg_amd import synth
+
+C, S = synth.CUBE, synth.SHELL
+
+CASES = {
+    "cube-ani-6-7": dict(kind=C, n_old=6, n_new=7),
+    "cube-iso-req-8-11": dict(kind=C, n_old=8, n_new=11, metric=synth.F_ISO,
+                              fields=(synth.F_SCALAR, synth.F_AFFINE), req_every=7),
+    "shell-ani-8-12": dict(kind=S, n_old=8, n_new=12),
+    "shell-iso-12-16": dict(kind=S, n_old=12, n_new=16, metric=synth.F_ISO, fields=(synth.F_SCALAR,)),
+    "cube-jitterbg-10-13": dict(kind=C, n_old=10, n_new=13, jitter_old=0.15),
+    "cube-nomet-tensor-5-9": dict(kind=C, n_old=5, n_new=9, metric=None, fields=(synth.F_TENSOR, synth.F_AFFINE_VEC)),
+    "cube-coarse-new-9-4": dict(kind=C, n_old=9, n_new=4),
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sort", [True, False], ids=["morton", "nosort"])
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_parity_small(name, sort):
+    case = make_case(**CASES[name])
+    gpu = run_gpu(case, sort=sort)
+    rep = check(case, gpu)
+    print(name, sort, rep, gpu["stats"])
+    assert rep["n"] == int((case["pclass"] != 0).sum())
+    assert rep["class_i"] == rep["class_i_same"]
+
+
+@pytest.mark.gpu
+def test_fallback_paths_outside_domain():
+    """Points pushed outside the background make the walks get stuck; the
+    exhaustive / closest kernels must reproduce the reference semantics."""
+    case = make_case(kind=C, n_old=5, n_new=6, with_ref=False)
+    new = case["new"]
+    rng = np.random.default_rng(7)
+    vol = np.nonzero(case["pclass"] == 1)[0]
+    bdy = np.nonzero(case["pclass"] == 2)[0]
+    pick_v = rng.choice(vol, 10, replace=False)
+    pick_b = rng.choice(bdy, 10, replace=False)
+    new.xyz[pick_v, 0] = 1.0 + rng.uniform(0.001, 0.2, 10)   # outside the cube: closest tetra
+    new.xyz[pick_b[:5], 2] = -0.05                            # beyond hausd: exhaustive -> stale/closest
+    new.xyz[pick_b[5:], 2] = -0.004                           # within hausd of the bottom face
+    case["B"] = __import__("oracle.oracle", fromlist=["Background"]).Background(
+        case["bg"], case["met"], case["fields"], case["hausd"])
+    gpu = run_gpu(case)
+    rep = check(case, gpu)
+    print(rep, gpu["stats"])
+    assert gpu["stats"]["nvol_closest"] + gpu["stats"]["nvol_exhaust"] >= 1
+
+
+@pytest.mark.gpu
+def test_invmat_failure_leaves_rows_untouched():
+    """MMG5_invmat failure (zero tensor) -> the output row is not written
+    (src/interpmesh_pmmg.c:258-267)."""
+    case = make_case(kind=C, n_old=4, n_new=5, metric=synth.F_ANI, fields=(synth.F_TENSOR,), with_ref=False)
+    case["met"][:40] = 0.0
+    from oracle import oracle as O
+    case["B"] = O.Background(case["bg"], case["met"], case["fields"], case["hausd"])
+    gpu = run_gpu(case)
+    rep = check(case, gpu)
+    assert np.isnan(gpu["met"]).any(), "expected untouched rows"
+    print(rep)
+
+
+@pytest.mark.gpu
+def test_host_layer_groups_and_hsiz():
+    """C host layer (PMMG_interpMetricsAndFields mirror): two groups, REQ
+    points copied, hsiz > 0 replaces the metric by a constant."""
+    from parmmg_amd.transfer import TAG_BDY, TAG_REQ, TransferContext, interp_metrics_and_fields
+
+    olds, news, cases = [], [], []
+    for n_old, n_new in ((5, 6), (6, 5)):
+        case = make_case(kind=C, n_old=n_old, n_new=n_new, with_ref=False)
+        new = case["new"]
+        tag = np.where(new.isbdy == 1, TAG_BDY, 0).astype(np.uint16)
+        tag[::11] |= TAG_REQ
+        olds.append(dict(mesh=case["bg"], met=case["met"], fields=case["fields"], hausd=case["hausd"]))
+        met = np.full((new.np, 6), np.nan)
+        fs = [np.full((new.np, f.shape[1]), np.nan) for f in case["fields"]]
+        news.append(dict(xyz=new.xyz, tag=tag, tetv=new.tetv, met=met, fields=fs,
+                         elem=np.zeros(new.np, np.int32), hit=np.zeros(new.np, np.int8)))
+        cases.append(case)
+    with TransferContext(0) as ctx:
+        ier, st = interp_metrics_and_fields(ctx, olds, news, input_met=1, hsiz=0.0)
+        assert ier == 1
+        for case, g in zip(cases, news):
+            req = (g["tag"] & TAG_REQ) != 0
+            assert np.isnan(g["met"][req]).all()
+            case["pclass"] = np.where(req, 0, np.where(case["new"].isbdy == 1, 2, 1)).astype(np.uint8)
+            rep = check(case, dict(met=g["met"], fields=g["fields"], elem=g["elem"], hit=g["hit"]))
+            assert rep["n"] == int((~req).sum())
+        # hsiz > 0: constant metric, fields still interpolated
+        for g in news:
+            g["met"][:] = np.nan
+        ier, st = interp_metrics_and_fields(ctx, olds, news, input_met=1, hsiz=0.05)
+        assert ier == 1
+        for g in news:
+            np.testing.assert_array_equal(g["met"][:, 0], np.full(g["met"].shape[0], 1.0 / 0.05 ** 2))
+            np.testing.assert_array_equal(g["met"][:, 1], 0.0)
