@@ -102,7 +102,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="cfg4", choices=sorted(configs.SHORT))
-    ap.add_argument("--nosort", action="store_true")
+    ap.add_argument("--sort", default="auto", choices=["auto", "on", "off"],
+                    help="query order: Morton binning (on), input order (off), or automatic")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -121,7 +122,7 @@ def main():
     w = configs.SHORT[args.config]
     bg, new, met, fields, pclass = build_workload(w, rank)
 
-    ctx = TransferContext(local, sort=not args.nosort)
+    ctx = TransferContext(local, sort={"auto": None, "on": True, "off": False}[args.sort])
     d_xyz, d_tetv, d_adja = ctx.upload(bg.xyz), ctx.upload(bg.tetv), ctx.upload(bg.adja)
     d_triv, d_adjt = ctx.upload(bg.triv), ctx.upload(bg.adjt)
     d_met = ctx.upload(met)
@@ -194,10 +195,12 @@ def main():
             "background_tets": ne_o, "background_verts": np_o, "new_points": np_n,
             "located_points_per_gpu": npts, "K_doubles_per_vertex": w.K,
             "parallelism": f"one group per GPU x{world} (weak, no data-path collective)",
-            "morton_sort": not args.nosort,
+            "query_order": args.sort,
+            "morton_binned": bool(st.sorted),
         },
         "gbps_algorithmic_step": round(B / (ms_per_step * 1e-3) / 1e9, 1),
         "device_ms": {"step_total": round(float(np.mean(ms_tot)), 4), "k_vol": round(kvol_ms, 4),
+                      "k_vol_locate": round(st.ms_vol_locate, 4),
                       "prepare": round(st.ms_prepare, 4), "sort": round(st.ms_sort, 4),
                       "k_bdy": round(st.ms_bdy, 4), "fallback": round(st.ms_fallback, 4)},
         "locate_stats": {k: v for k, v in st.as_dict().items() if not k.startswith("ms_")},

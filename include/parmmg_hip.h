@@ -68,6 +68,9 @@ extern "C" {
 #define PMMG_HIT_BDY_EXHAUST  9  /* exhaustive tria scan: lowest-index accepted locate_pmmg.c:483-503 */
 #define PMMG_HIT_BDY_STALE   10  /* not located, re-evaluation accepted         locate_pmmg.c:505-509 */
 #define PMMG_HIT_BDY_CLOSEST 11  /* not located: closest tria, nearest vertex   locate_pmmg.c:511,681 */
+#define PMMG_HIT_VOL_SCAN    12  /* tetra-centric scan: lowest-index accepting tetra, i.e. the
+                                    reference's exhaustive semantics (locate_pmmg.c:743-762)
+                                    obtained for every query in one pass */
 
 #define PMMG_HIT_CODE(h) ((h) & 15)
 #define PMMG_HIT_LOC(h)  (((h) >> 4) & 3)
@@ -80,21 +83,32 @@ typedef struct {
   int64_t nvol;          /* volume queries */
   int64_t nbdy;          /* surface queries */
   int64_t nvol_walk, nvol_exhaust, nvol_closest;
+  int64_t nvol_scan;     /* volume queries located by the tetra-centric scan */
   int64_t nbdy_face, nbdy_edge, nbdy_vertex, nbdy_wedge, nbdy_cone;
   int64_t nbdy_exhaust, nbdy_stale, nbdy_closest;
   int64_t steps_total;   /* walk steps, volume + surface */
   int64_t stepmax;
+  int64_t sorted;        /* 1 if the queries were Morton-binned, 0 if processed in input order */
   /* device time in milliseconds, measured with HIP events on the context stream */
-  float ms_prepare;      /* bbox, seed grids, surface CSR, query compaction */
-  float ms_sort;         /* Morton sort of the queries */
-  float ms_vol;          /* volume locate + interpolate kernel */
+  float ms_prepare;      /* bbox, seed grids, input-order coherence test */
+  float ms_sort;         /* query order: Morton binning, or stable class compaction */
+  float ms_vol;          /* volume locate + interpolate kernels */
   float ms_bdy;          /* surface locate + interpolate kernel */
   float ms_fallback;     /* exhaustive / closest kernels */
   float ms_total;        /* whole call, first to last event */
+  float ms_vol_locate;   /* the volume walk kernel alone (part of ms_vol) */
 } pmmg_hip_stats;
 
-/* Options (bit flags) for pmmg_hip_create. */
-#define PMMG_HIP_OPT_NOSORT 1   /* process queries in input order (no Morton sort) */
+/* Options (bit flags) for pmmg_hip_create.  Default: Morton-bin the queries
+ * unless a sampled test finds the input numbering already spatially coherent
+ * (mean distance between consecutive points < 4 mean spacings). */
+#define PMMG_HIP_OPT_NOSORT 1   /* always process queries in input order */
+#define PMMG_HIP_OPT_SORT   2   /* always Morton-bin the queries */
+#define PMMG_HIP_OPT_SCAN   4   /* volume points by a tetra-centric scan (lowest-index accepting
+                                   tetra for every query) instead of per-query walks; pays off
+                                   only when the new mesh has many more points than the
+                                   background has tetra */
+#define PMMG_HIP_OPT_SPLIT  8   /* volume walk and interpolation as two kernels (default: fused) */
 
 /* Create a context on HIP device `device`.  Returns NULL on failure. */
 pmmg_hip_ctx *pmmg_hip_create(int device, int options);

@@ -60,6 +60,8 @@ def lib():
         for n in ("orc_first_accepting_tetra", "orc_closest_tetra", "orc_first_accepting_tria", "orc_closest_tria"):
             getattr(L, n).argtypes = [vp, vp]
             getattr(L, n).restype = ci
+        L.orc_closest_value.argtypes = [vp, ci, vp]
+        L.orc_closest_value.restype = cd
         L.orc_wedge_test.argtypes = [vp, ci, ci, vp]
         L.orc_wedge_test.restype = ci
         L.orc_cone_test.argtypes = [vp, ci, ci, vp]
@@ -145,6 +147,10 @@ def first_accepting_tetra(bg, x):
 
 def closest_tetra(bg, x):
     return lib().orc_closest_tetra(bg.ref, _p(np.ascontiguousarray(x, np.float64)))
+
+
+def closest_value(bg, k, x):
+    return lib().orc_closest_value(bg.ref, int(k), _p(np.ascontiguousarray(x, np.float64)))
 
 
 def first_accepting_tria(bg, x):

@@ -25,7 +25,8 @@ static const int kIprv2[3] = {2, 0, 1};                                      /* 
 
 enum {
   HIT_NONE = 0, HIT_VOL_WALK, HIT_VOL_EXHAUST, HIT_VOL_CLOSEST, HIT_BDY_FACE, HIT_BDY_EDGE,
-  HIT_BDY_VERTEX, HIT_BDY_WEDGE, HIT_BDY_CONE, HIT_BDY_EXHAUST, HIT_BDY_STALE, HIT_BDY_CLOSEST
+  HIT_BDY_VERTEX, HIT_BDY_WEDGE, HIT_BDY_CONE, HIT_BDY_EXHAUST, HIT_BDY_STALE, HIT_BDY_CLOSEST,
+  HIT_VOL_SCAN /* the module's tetra-centric scan: exhaustive semantics */
 };
 
 /* PMMG_barycoord, src/barycoord_pmmg.h:41-44 */
@@ -639,7 +640,7 @@ int orc_eval_in_element(const orc_background *bg, const double *x, int is_bdy, i
   bcoord b[4];
   if (!is_bdy) {
     if (elem < 1 || elem > bg->ne) return 0;
-    if (hit == HIT_VOL_WALK || hit == HIT_VOL_EXHAUST) {
+    if (hit == HIT_VOL_WALK || hit == HIT_VOL_EXHAUST || hit == HIT_VOL_SCAN) {
       double fa[12];
       double vol = tet_geom(bg, elem, fa);
       bc3d_evaluate(bg, elem, fa, vol, x, b);
@@ -720,6 +721,14 @@ int orc_first_accepting_tetra(const orc_background *bg, const double *x) {
     if (orc_tetra_minbary(bg, k, x) > -ORC_EPS) return k;
   }
   return 0;
+}
+
+double orc_closest_value(const orc_background *bg, int k, const double *x) {
+  double fa[12];
+  bcoord b[4];
+  double vol = tet_geom(bg, k, fa);
+  bc3d_evaluate(bg, k, fa, vol, x, b);
+  return fabs(b[0].val) * vol;
 }
 
 int orc_closest_tetra(const orc_background *bg, const double *x) {

@@ -97,6 +97,10 @@ int orc_tria_accepts(const orc_background *bg, int k, const double *x, double *m
  * none); closest tetra by |bary_min|*vol, closest tria by centroid distance. */
 int orc_first_accepting_tetra(const orc_background *bg, const double *x);
 int orc_closest_tetra(const orc_background *bg, const double *x);
+/* |bary_min| * vol of x in tetra k: the reference's closest-tetra metric
+ * (locate_pmmg.c:453-458); exact ties are broken by evaluation order in the
+ * reference (walk first, then index order) and by lowest index here. */
+double orc_closest_value(const orc_background *bg, int k, const double *x);
 int orc_first_accepting_tria(const orc_background *bg, const double *x);
 int orc_closest_tria(const orc_background *bg, const double *x);
 /* Fresh-state shadow tests (wedge returns 4 when x lies in the shadow wedge of

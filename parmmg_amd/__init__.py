@@ -6,6 +6,6 @@ The product is the HIP module ``libpmmg_hip.so`` behind the C-ABI of
 package only builds and binds them (``build``, ``_native``, ``transfer``) and
 provides the synthetic workloads (``synth``, ``configs``).
 """
-from .transfer import TransferContext, device_count, interp_metrics_and_fields, transfer  # noqa: F401
+from .transfer import TransferContext, device_count, interp_metrics_and_fields  # noqa: F401
 
-__all__ = ["TransferContext", "device_count", "interp_metrics_and_fields", "transfer"]
+__all__ = ["TransferContext", "device_count", "interp_metrics_and_fields"]

@@ -20,12 +20,13 @@ class HipStats(ctypes.Structure):
 
     _fields_ = [
         ("nvol", c_int64), ("nbdy", c_int64),
-        ("nvol_walk", c_int64), ("nvol_exhaust", c_int64), ("nvol_closest", c_int64),
+        ("nvol_walk", c_int64), ("nvol_exhaust", c_int64), ("nvol_closest", c_int64), ("nvol_scan", c_int64),
         ("nbdy_face", c_int64), ("nbdy_edge", c_int64), ("nbdy_vertex", c_int64), ("nbdy_wedge", c_int64),
         ("nbdy_cone", c_int64), ("nbdy_exhaust", c_int64), ("nbdy_stale", c_int64), ("nbdy_closest", c_int64),
-        ("steps_total", c_int64), ("stepmax", c_int64),
+        ("steps_total", c_int64), ("stepmax", c_int64), ("sorted", c_int64),
         ("ms_prepare", ctypes.c_float), ("ms_sort", ctypes.c_float), ("ms_vol", ctypes.c_float),
         ("ms_bdy", ctypes.c_float), ("ms_fallback", ctypes.c_float), ("ms_total", ctypes.c_float),
+        ("ms_vol_locate", ctypes.c_float),
     ]
 
     def as_dict(self) -> dict:

@@ -1,0 +1,530 @@
+// pmmg_device.hpp — device-side arithmetic of the transfer step (included by
+// pmmg_hip.hip only).
+//
+// Every floating-point expression keeps the reference's operation order
+// (files cited per function) and the module is built with -ffp-contract=off,
+// so the same element gives bit-identical barycentric coordinates and
+// interpolated values as the reference arithmetic (oracle/pmmg_oracle.c).
+// All small arrays are indexed with compile-time indices only (runtime picks
+// go through the sel* helpers), which keeps them in registers: a runtime
+// index into a local array sends it to scratch memory on CDNA.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "parmmg_hip.h"
+
+namespace pmmg {
+
+constexpr double kEps = 1.e-06;     // MMG5_EPS
+constexpr double kEpsD2 = 1.0e-200; // MMG5_EPSD2
+constexpr int kMaxSlot = 8;         // metric + up to 7 fields
+constexpr int kHist = 8;            // visited-element history of a walk
+constexpr int kBlock = 256;
+constexpr int kFanMax = 64;
+
+struct Bg {
+  const double *xyz;
+  const int4 *tetv;
+  const int4 *adja;
+  const int *triv;
+  const int *adjt;
+  int np, ne, nt;
+  double hausd;
+};
+
+// one solution array: code 1 = scalar, 3 = vector (both P1 iso
+// interpolation), 6 = symmetric tensor (inverse-tensor interpolation)
+struct Slot {
+  const double *in;
+  double *out;
+  int code;
+};
+
+struct Slots {
+  Slot s[kMaxSlot];
+  int n;
+  int has_met; // slot 0 is the metric (boundary points treat it differently)
+};
+
+struct Frame {
+  unsigned long long key_lo[3], key_hi[3];
+  double lo[3], ext[3];
+  double inv_vol[3], inv_srf[3], inv_bin[3];
+};
+
+struct DevStats {
+  unsigned long long cnt[16];
+  unsigned long long steps;
+  unsigned int stepmax;
+  int nvol, nbdy;
+  int nfb_vol, nfb_bdy;
+  int coherent;
+  int pad[2];
+};
+
+// ------------------------------------------------------------ small helpers
+
+__device__ __forceinline__ unsigned long long dkey(double d) {
+  unsigned long long u = (unsigned long long)__double_as_longlong(d);
+  return (u >> 63) ? ~u : (u | 0x8000000000000000ULL);
+}
+__device__ __forceinline__ double dunkey(unsigned long long k) {
+  unsigned long long u = (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFULL) : ~k;
+  return __longlong_as_double((long long)u);
+}
+
+__device__ __forceinline__ int sel4(const int4 &a, int i) {
+  return i == 0 ? a.x : (i == 1 ? a.y : (i == 2 ? a.z : a.w));
+}
+__device__ __forceinline__ int sel3i(int a, int b, int c, int i) { return i == 0 ? a : (i == 1 ? b : c); }
+__device__ __forceinline__ double sel3d(double a, double b, double c, int i) { return i == 0 ? a : (i == 1 ? b : c); }
+
+__device__ __forceinline__ void load_pt(const double *xyz, int v, double *p) {
+  const double *q = xyz + 3 * (size_t)(v - 1);
+  p[0] = q[0];
+  p[1] = q[1];
+  p[2] = q[2];
+}
+
+__device__ __forceinline__ int wave_append(int *counter, bool pred) {
+  unsigned long long m = __ballot(pred);
+  if (m == 0ULL) return -1;
+  int lane = __lane_id();
+  int leader = __ffsll((long long)m) - 1;
+  int base = 0;
+  if (lane == leader) base = atomicAdd(counter, __popcll(m));
+  base = __shfl(base, leader);
+  int rank = __popcll(m & ((1ULL << lane) - 1ULL));
+  return pred ? base + rank : -1;
+}
+
+// XCD-aware block order (cdna_hip_programming.md T1): blocks are dealt
+// round-robin over the 8 XCDs, each with a private 4 MiB L2.  Giving XCD x the
+// contiguous range of logical blocks [x*n/8, (x+1)*n/8) keeps spatially
+// adjacent queries (which walk the same tetra) on one L2.  Bijective for any n.
+__device__ __forceinline__ int xcd_block() {
+  const int b = blockIdx.x, n = gridDim.x;
+  const int x = b & 7, q = n >> 3, r = n & 7;
+  const int base = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+  return base + (b >> 3);
+}
+
+// Grid-stride iteration over [0, n) split into 8 contiguous chunks, one per
+// XCD (blockIdx % 8), for kernels launched with a fixed grid (a multiple of 8).
+// iters is uniform across a block, so wave-collective code may run per iteration.
+struct XcdChunk {
+  long long start, hi, stride;
+  int iters;
+};
+__device__ __forceinline__ XcdChunk xcd_chunk(long long n) {
+  const int x = blockIdx.x & 7, bpx = gridDim.x >> 3, bi = blockIdx.x >> 3;
+  XcdChunk c;
+  const long long lo = n * x / 8;
+  c.hi = n * (x + 1) / 8;
+  c.stride = (long long)bpx * blockDim.x;
+  c.iters = (int)((c.hi - lo + c.stride - 1) / c.stride);
+  c.start = lo + (long long)bi * blockDim.x + threadIdx.x;
+  return c;
+}
+
+__device__ __forceinline__ uint32_t expand10(uint32_t v) {
+  v &= 0x3ffu;
+  v = (v | (v << 16)) & 0x030000FFu;
+  v = (v | (v << 8)) & 0x0300F00Fu;
+  v = (v | (v << 4)) & 0x030C30C3u;
+  v = (v | (v << 2)) & 0x09249249u;
+  return v;
+}
+
+__device__ __forceinline__ int cell_coord(double x, double lo, double inv, int g) {
+  double t = (x - lo) * inv;
+  int c = (t > 0.0) ? (int)t : 0;
+  return c < g ? c : g - 1;
+}
+
+// ------------------------------------------------------------ tetra geometry
+
+// MMG5_nonUnitNorPts: (b-a)x(c-a)
+__device__ __forceinline__ void nonunit_normal(const double *a, const double *b, const double *c, double *n) {
+  double abx = b[0] - a[0], aby = b[1] - a[1], abz = b[2] - a[2];
+  double acx = c[0] - a[0], acy = c[1] - a[1], acz = c[2] - a[2];
+  n[0] = aby * acz - abz * acy;
+  n[1] = abz * acx - abx * acz;
+  n[2] = abx * acy - aby * acx;
+}
+
+// MMG5_orvol
+__device__ __forceinline__ double orvol4(const double *p0, const double *p1, const double *p2, const double *p3) {
+  double ax = p2[0] - p0[0], ay = p2[1] - p0[1], az = p2[2] - p0[2];
+  double bx = p3[0] - p0[0], by = p3[1] - p0[1], bz = p3[2] - p0[2];
+  return (p1[0] - p0[0]) * (ay * bz - az * by) + (p1[1] - p0[1]) * (az * bx - ax * bz) +
+         (p1[2] - p0[2]) * (ax * by - ay * bx);
+}
+
+// PMMG_barycoord3d_compute (barycoord_pmmg.c:238-257) on face normals recomputed
+// from the vertices (PMMG_precompute_faceAreas, locate_pmmg.c:107-119); the
+// reference's 96 B/tetra faceAreas array is never stored.  b[f] unsorted.
+__device__ __forceinline__ double tet_bary(const double *x, const double *p0, const double *p1, const double *p2,
+                                           const double *p3, double *b) {
+  double vol = orvol4(p0, p1, p2, p3);
+  double n[3];
+  nonunit_normal(p1, p2, p3, n); // face 0: idir {1,2,3}
+  b[0] = -((x[0] - p1[0]) * n[0] + (x[1] - p1[1]) * n[1] + (x[2] - p1[2]) * n[2]) / vol;
+  nonunit_normal(p0, p3, p2, n); // face 1: idir {0,3,2}
+  b[1] = -((x[0] - p0[0]) * n[0] + (x[1] - p0[1]) * n[1] + (x[2] - p0[2]) * n[2]) / vol;
+  nonunit_normal(p0, p1, p3, n); // face 2: idir {0,1,3}
+  b[2] = -((x[0] - p0[0]) * n[0] + (x[1] - p0[1]) * n[1] + (x[2] - p0[2]) * n[2]) / vol;
+  nonunit_normal(p0, p2, p1, n); // face 3: idir {0,2,1}
+  b[3] = -((x[0] - p0[0]) * n[0] + (x[1] - p0[1]) * n[1] + (x[2] - p0[2]) * n[2]) / vol;
+  return vol;
+}
+
+// Order of the reference's qsort (glibc merge sort: stable) = ascending
+// (value, index).  The reference only consumes the sorted order for the inside
+// test, the walk direction and isBorder; PMMG_barycoord_get de-permutes the
+// values again, so the interpolation uses the unsorted b[] directly.
+__device__ __forceinline__ bool before(double va, int a, double vb, int b) {
+  return (va < vb) || (va == vb && a < b);
+}
+
+__device__ __forceinline__ void ranks4(const double *b, int *r) {
+#pragma unroll
+  for (int f = 0; f < 4; f++) {
+    int c = 0;
+#pragma unroll
+    for (int g = 0; g < 4; g++)
+      if (g != f && before(b[g], g, b[f], f)) c++;
+    r[f] = c;
+  }
+}
+
+__device__ __forceinline__ void ranks3(const double *b, int *r) {
+#pragma unroll
+  for (int f = 0; f < 3; f++) {
+    int c = 0;
+#pragma unroll
+    for (int g = 0; g < 3; g++)
+      if (g != f && before(b[g], g, b[f], f)) c++;
+    r[f] = c;
+  }
+}
+
+__device__ __forceinline__ double min4(const double *b) {
+  double m = b[0];
+  m = b[1] < m ? b[1] : m;
+  m = b[2] < m ? b[2] : m;
+  m = b[3] < m ? b[3] : m;
+  return m;
+}
+
+// PMMG_barycoord3d_getClosest / 2d_getClosest (barycoord_pmmg.c:371-404): unit
+// coordinate on the nearest vertex (first minimum in vertex order)
+template <int NV>
+__device__ __forceinline__ void closest_vertex(const double *x, const double (*p)[3], double *phi) {
+  double d[3];
+  for (int i = 0; i < 3; i++) d[i] = x[i] - p[0][i];
+  double mn = sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+  int it = 0;
+#pragma unroll
+  for (int j = 1; j < NV; j++) {
+    for (int i = 0; i < 3; i++) d[i] = x[i] - p[j][i];
+    double nrm = sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+    if (nrm < mn) { mn = nrm; it = j; }
+  }
+#pragma unroll
+  for (int j = 0; j < NV; j++) phi[j] = (j == it) ? 1.0 : 0.0;
+}
+
+// ------------------------------------------------------------ MMG5_invmat
+
+// Symmetric 3x3 inverse (m11,m12,m13,m22,m23,m33), restated from Mmg
+// @889d408: diagonal shortcut below MMG5_EPS off-diagonal, failure on a zero
+// matrix or |det| < MMG5_EPSD2.  Results are produced in registers and only
+// stored when the inversion succeeds.
+__device__ __forceinline__ bool invmat(const double *m, double *mi) {
+  double vmax = fabs(m[1]), maxx = fabs(m[2]);
+  if (maxx > vmax) vmax = maxx;
+  maxx = fabs(m[4]);
+  if (maxx > vmax) vmax = maxx;
+  double r0, r1, r2, r3, r4, r5;
+  bool ok;
+  if (vmax < kEps) {
+    r0 = 1. / m[0];
+    r3 = 1. / m[3];
+    r5 = 1. / m[5];
+    r1 = r2 = r4 = 0.0;
+    ok = true;
+  } else {
+    double vm = fabs(m[0]);
+#pragma unroll
+    for (int k = 1; k < 6; k++) {
+      double mx = fabs(m[k]);
+      if (mx > vm) vm = mx;
+    }
+    double aa = m[3] * m[5] - m[4] * m[4];
+    double bb = m[4] * m[2] - m[1] * m[5];
+    double cc = m[1] * m[4] - m[2] * m[3];
+    double det = m[0] * aa + m[1] * bb + m[2] * cc;
+    ok = !(vm == 0.0) && !(fabs(det) < kEpsD2);
+    det = 1.0 / det;
+    r0 = aa * det;
+    r1 = bb * det;
+    r2 = cc * det;
+    r3 = (m[0] * m[5] - m[2] * m[2]) * det;
+    r4 = (m[1] * m[2] - m[0] * m[4]) * det;
+    r5 = (m[0] * m[3] - m[1] * m[1]) * det;
+  }
+  mi[0] = r0; mi[1] = r1; mi[2] = r2; mi[3] = r3; mi[4] = r4; mi[5] = r5;
+  return ok;
+}
+
+__device__ __forceinline__ void load6(const double *p, double *m) {
+  const double2 *q = reinterpret_cast<const double2 *>(p);
+  double2 a = q[0], b = q[1], c = q[2];
+  m[0] = a.x; m[1] = a.y; m[2] = b.x; m[3] = b.y; m[4] = c.x; m[5] = c.y;
+}
+
+__device__ __forceinline__ void store6(double *p, const double *m) {
+  double2 *q = reinterpret_cast<double2 *>(p);
+  q[0] = make_double2(m[0], m[1]);
+  q[1] = make_double2(m[2], m[3]);
+  q[2] = make_double2(m[4], m[5]);
+}
+
+// ------------------------------------------------------------ interpolators
+
+// PMMG_interp{3,4}bar_iso (interpmesh_pmmg.c:125-149, 206-230):
+// out[j] = 0; out[j] += phi_i * old[v_i][j], i ascending
+template <int NV, int SZ>
+__device__ __forceinline__ void interp_iso(const double *in, const int *v, const double *phi, double *out) {
+  double row[NV][SZ];
+#pragma unroll
+  for (int i = 0; i < NV; i++)
+#pragma unroll
+    for (int j = 0; j < SZ; j++) row[i][j] = in[(size_t)SZ * (v[i] - 1) + j];
+  double acc[SZ];
+#pragma unroll
+  for (int j = 0; j < SZ; j++) acc[j] = 0.0;
+#pragma unroll
+  for (int i = 0; i < NV; i++)
+#pragma unroll
+    for (int j = 0; j < SZ; j++) acc[j] += phi[i] * row[i][j];
+#pragma unroll
+  for (int j = 0; j < SZ; j++) out[j] = acc[j];
+}
+
+// PMMG_interp{3,4}bar_ani (interpmesh_pmmg.c:166-190, 247-270):
+// M = invmat( sum_i phi_i invmat(M_i) ), row untouched if any inversion fails
+template <int NV>
+__device__ __forceinline__ void interp_ani(const double *in, const int *v, const double *phi, double *out) {
+  double m[NV][6];
+#pragma unroll
+  for (int i = 0; i < NV; i++) load6(in + 6 * (size_t)(v[i] - 1), m[i]);
+  double mint[6], mi[6];
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < NV; i++) {
+    ok = invmat(m[i], mi) && ok;
+#pragma unroll
+    for (int s = 0; s < 6; s++) mint[s] = (i == 0) ? phi[0] * mi[s] : mint[s] + phi[i] * mi[s];
+  }
+  double r[6];
+  if (invmat(mint, r) && ok) store6(out, r);
+}
+
+template <int NV, int CODE>
+__device__ __forceinline__ void interp_code(const Slot &sl, int ip, const int *v, const double *phi) {
+  if (CODE == 6) interp_ani<NV>(sl.in, v, phi, sl.out + 6 * (size_t)(ip - 1));
+  else interp_iso<NV, CODE>(sl.in, v, phi, sl.out + (size_t)CODE * (ip - 1));
+}
+
+template <int NV>
+__device__ __forceinline__ void interp_dyn(const Slot &sl, int ip, const int *v, const double *phi) {
+  if (sl.code == 6) interp_code<NV, 6>(sl, ip, v, phi);
+  else if (sl.code == 3) interp_code<NV, 3>(sl, ip, v, phi);
+  else interp_code<NV, 1>(sl, ip, v, phi);
+}
+
+// PMMG_interp2bar_{iso,ani} (interpmesh_pmmg.c:50-110) on edge l of a tria
+__device__ __forceinline__ void interp_edge(const Slot &sl, int ip, const int *v, int l, const double *phi) {
+  const int i0 = l == 0 ? 1 : (l == 1 ? 2 : 0); // MMG5_inxt2[l]
+  const int i1 = l == 0 ? 2 : (l == 1 ? 0 : 1); // MMG5_iprv2[l]
+  const int v0 = sel3i(v[0], v[1], v[2], i0), v1 = sel3i(v[0], v[1], v[2], i1);
+  const double f0 = sel3d(phi[0], phi[1], phi[2], i0), f1 = sel3d(phi[0], phi[1], phi[2], i1);
+  if (sl.code == 6) {
+    double m[6], mi0[6], mi1[6], mint[6], r[6];
+    load6(sl.in + 6 * (size_t)(v0 - 1), m);
+    bool ok = invmat(m, mi0);
+    load6(sl.in + 6 * (size_t)(v1 - 1), m);
+    ok = invmat(m, mi1) && ok;
+#pragma unroll
+    for (int s = 0; s < 6; s++) mint[s] = f0 * mi0[s] + f1 * mi1[s];
+    if (invmat(mint, r) && ok) store6(sl.out + 6 * (size_t)(ip - 1), r);
+  } else {
+    sl.out[ip - 1] = f0 * sl.in[v0 - 1] + f1 * sl.in[v1 - 1];
+  }
+}
+
+__device__ __forceinline__ void copy_row(const Slot &sl, int ip, int vsrc) {
+  double *out = sl.out + (size_t)sl.code * (ip - 1);
+  const double *in = sl.in + (size_t)sl.code * (vsrc - 1);
+  if (sl.code == 6) {
+    double m[6];
+    load6(in, m);
+    store6(out, m);
+  } else if (sl.code == 3) {
+    out[0] = in[0]; out[1] = in[1]; out[2] = in[2];
+  } else {
+    out[0] = in[0];
+  }
+}
+
+// boundary point (interpmesh_pmmg.c:563-595): metric by vertex copy / edge /
+// face, every field by interp3bar
+__device__ __forceinline__ void interp_bdy(const Slots &S, int ip, const int *v, const double *phi, int edge,
+                                           int vertex) {
+  for (int s = 0; s < S.n; s++) {
+    const Slot &sl = S.s[s];
+    if (s == 0 && S.has_met) {
+      if (vertex >= 0) copy_row(sl, ip, sel3i(v[0], v[1], v[2], vertex));
+      else if (edge >= 0) interp_edge(sl, ip, v, edge, phi);
+      else interp_dyn<3>(sl, ip, v, phi);
+    } else {
+      interp_dyn<3>(sl, ip, v, phi);
+    }
+  }
+}
+
+// ------------------------------------------------------------ tria geometry
+
+struct TriGeom {
+  int v[3];
+  double p[3][3];
+  double n[3]; // unit normal
+  double q;    // |nonunit normal| (ptr->qual)
+};
+
+// vertices + PMMG_precompute_triaNormals (locate_pmmg.c:74-87)
+__device__ __forceinline__ void tri_load(const Bg &bg, int k, TriGeom &t) {
+  const int *tv = bg.triv + 3 * (size_t)(k - 1);
+  t.v[0] = tv[0];
+  t.v[1] = tv[1];
+  t.v[2] = tv[2];
+  load_pt(bg.xyz, t.v[0], t.p[0]);
+  load_pt(bg.xyz, t.v[1], t.p[1]);
+  load_pt(bg.xyz, t.v[2], t.p[2]);
+  nonunit_normal(t.p[0], t.p[1], t.p[2], t.n);
+  t.q = sqrt(t.n[0] * t.n[0] + t.n[1] * t.n[1] + t.n[2] * t.n[2]);
+  double dd = 1.0 / t.q;
+  t.n[0] *= dd;
+  t.n[1] *= dd;
+  t.n[2] *= dd;
+}
+
+// PMMG_quickarea (barycoord_pmmg.c:44-61)
+__device__ __forceinline__ double quickarea(const double *a, const double *b, const double *c, const double *n) {
+  double abx = b[0] - a[0], aby = b[1] - a[1], abz = b[2] - a[2];
+  double acx = c[0] - a[0], acy = c[1] - a[1], acz = c[2] - a[2];
+  double a0 = aby * acz - abz * acy, a1 = abz * acx - abx * acz, a2 = abx * acy - aby * acx;
+  return a0 * n[0] + a1 * n[1] + a2 * n[2];
+}
+
+// PMMG_barycoord2d_compute (barycoord_pmmg.c:191-223): vertices / area of
+// `pv`, unit normal n; returns the normal distance
+__device__ __forceinline__ double tri_bary(const double *x, const double (*pv)[3], double q, const double *n, double *b) {
+  double dist = 0.0, proj[3];
+  for (int i = 0; i < 3; i++) dist += (x[i] - pv[0][i]) * n[i];
+  for (int i = 0; i < 3; i++) proj[i] = x[i] - dist * n[i];
+  b[0] = quickarea(proj, pv[1], pv[2], n) / q;
+  b[1] = quickarea(proj, pv[2], pv[0], n) / q;
+  b[2] = quickarea(proj, pv[0], pv[1], n) / q;
+  return dist;
+}
+
+__device__ __forceinline__ void tri_pick(const TriGeom &t, int i, double *p) {
+  p[0] = sel3d(t.p[0][0], t.p[1][0], t.p[2][0], i);
+  p[1] = sel3d(t.p[0][1], t.p[1][1], t.p[2][1], i);
+  p[2] = sel3d(t.p[0][2], t.p[1][2], t.p[2][2], i);
+}
+
+// PMMG_locatePointInWedge (locate_pmmg.c:286-334): -1 too far, 4 inside (phi
+// written), else the local vertex whose cone must be tested
+__device__ __forceinline__ int tri_wedge(double hausd, const TriGeom &t, int l, const double *x, double *phi) {
+  const int i0 = l == 0 ? 1 : (l == 1 ? 2 : 0), i1 = l == 0 ? 2 : (l == 1 ? 0 : 1);
+  double p0[3], p1[3];
+  tri_pick(t, i0, p0);
+  tri_pick(t, i1, p1);
+  double p[3], a[3], norm2 = 0.0, alpha = 0.0, dist = 0.0;
+  for (int d = 0; d < 3; d++) p[d] = x[d] - p0[d];
+  for (int d = 0; d < 3; d++) a[d] = p1[d] - p0[d];
+  for (int d = 0; d < 3; d++) norm2 += a[d] * a[d];
+  for (int d = 0; d < 3; d++) alpha += a[d] * p[d];
+  for (int d = 0; d < 3; d++) p[d] -= (alpha / norm2) * a[d];
+  for (int d = 0; d < 3; d++) dist += p[d] * p[d];
+  dist = sqrt(dist);
+  if (dist > hausd) return -1;
+  if (alpha < 0.0) return i0;
+  if (alpha > norm2) return i1;
+  const double w0 = 1.0 - alpha / norm2, w1 = alpha / norm2;
+  phi[0] = (l == 0) ? 0.0 : (i0 == 0 ? w0 : w1);
+  phi[1] = (l == 1) ? 0.0 : (i0 == 1 ? w0 : w1);
+  phi[2] = (l == 2) ? 0.0 : (i0 == 2 ? w0 : w1);
+  return 4;
+}
+
+__device__ __forceinline__ bool cone_edge_ok(const double *xyz, int jp, const double *p0, const double *p) {
+  double p1[3], a[3], alpha = 0.0;
+  load_pt(xyz, jp, p1);
+  for (int d = 0; d < 3; d++) a[d] = p1[d] - p0[d];
+  for (int d = 0; d < 3; d++) alpha += a[d] * p[d];
+  return !(alpha > 0.0);
+}
+
+// PMMG_locatePointInCone (locate_pmmg.c:209-270) with a fresh visited state
+// per query: x is in the shadow cone of vertex ip iff |x-p(ip)| <= hausd and
+// every surface edge leaving ip makes a non-acute angle with x-p(ip).  The
+// vertex's trias are reached by rotating through adjt around ip (manifold
+// fan) instead of the reference's node->trias CSR; the edge set is the same.
+__device__ __forceinline__ bool tri_cone(const Bg &bg, int k, int iloc, const TriGeom &t, const double *x) {
+  const int ip = sel3i(t.v[0], t.v[1], t.v[2], iloc);
+  double p0[3], p[3], dist = 0.0;
+  tri_pick(t, iloc, p0);
+  for (int d = 0; d < 3; d++) p[d] = x[d] - p0[d];
+  for (int d = 0; d < 3; d++) dist += p[d] * p[d];
+  dist = sqrt(dist);
+  if (dist > bg.hausd) return false;
+  {
+    double q[3];
+    for (int o = 1; o <= 2; o++) {
+      int j = (iloc + o) % 3;
+      tri_pick(t, j, q);
+      double a[3], alpha = 0.0;
+      for (int d = 0; d < 3; d++) a[d] = q[d] - p0[d];
+      for (int d = 0; d < 3; d++) alpha += a[d] * p[d];
+      if (alpha > 0.0) return false;
+    }
+  }
+  for (int dir = 0; dir < 2; dir++) {
+    int tcur = k;
+    int e = dir == 0 ? (iloc + 1) % 3 : (iloc + 2) % 3; // an edge of tcur incident to ip
+    for (int it = 0; it < kFanMax; it++) {
+      int code = bg.adjt[3 * (size_t)(tcur - 1) + e];
+      int tn = code / 3, en = code % 3;
+      if (tn == 0) break;
+      if (tn == k) return true;
+      const int *tvn = bg.triv + 3 * (size_t)(tn - 1);
+      int w0 = tvn[0], w1 = tvn[1], w2 = tvn[2];
+      int lvn = (w0 == ip) ? 0 : ((w1 == ip) ? 1 : 2);
+      int j1 = sel3i(w0, w1, w2, (lvn + 1) % 3), j2 = sel3i(w0, w1, w2, (lvn + 2) % 3);
+      if (!cone_edge_ok(bg.xyz, j1, p0, p) || !cone_edge_ok(bg.xyz, j2, p0, p)) return false;
+      int ea = (lvn + 1) % 3, eb = (lvn + 2) % 3;
+      e = (ea == en) ? eb : ea;
+      tcur = tn;
+    }
+  }
+  return true;
+}
+
+} // namespace pmmg

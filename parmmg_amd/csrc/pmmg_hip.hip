@@ -3,27 +3,26 @@
 //
 // Replaces, behind the C-ABI of include/parmmg_hip.h, the per-group body of
 // PMMG_interpMetricsAndFields (reference src/interpmesh_pmmg.c:477-741):
-//   * PMMG_locatePointVol      src/locate_pmmg.c:786-883  -> k_vol (one lane per query)
-//   * PMMG_locatePointBdy      src/locate_pmmg.c:587-723  -> k_bdy (one lane per query)
-//   * exhaustive / closest     src/locate_pmmg.c:477-515, 737-770 -> k_*_exhaust_*
-//   * PMMG_barycoord*          src/barycoord_pmmg.c       -> inline device arithmetic
-//   * PMMG_interp{2,3,4}bar_*  src/interpmesh_pmmg.c:50-296 -> interp_* device functions
+//   PMMG_locatePointVol      src/locate_pmmg.c:786-883   -> k_vol_locate (one lane per query)
+//   PMMG_interp4bar_*        src/interpmesh_pmmg.c:206-270 -> k_vol_interp<slot layout>
+//   PMMG_locatePointBdy      src/locate_pmmg.c:587-723   -> k_bdy (locate + interpolate)
+//   exhaustive / closest     src/locate_pmmg.c:477-515, 737-770 -> k_*_exhaust*, k_*_finish
+// Device arithmetic lives in pmmg_device.hpp.
 //
-// Numerics: every floating-point expression keeps the reference's operation
-// order and the module is compiled with -ffp-contract=off, so a query located
-// in the same element as the reference gets bit-identical barycentric
-// coordinates and interpolated values.
-//
-// Design (DESIGN.md has the roofline and byte accounting):
-//   1. bbox of the background, coarse seed grids (volume: sampled tetra ids by
-//      cell, deterministic atomicMin; surface: tria ids by cell);
-//   2. queries keyed by (class, 30-bit Morton code) and radix-sorted so that a
-//      wavefront's 64 lanes walk neighbouring tetra (gathers hit L2);
-//   3. k_vol / k_bdy: seeded adjacency walk with an 8-entry visited history,
-//      then the interpolation fused in the same lane; stuck / over-long walks
-//      are appended (wavefront ballot + one atomic per wave) to a fallback list;
-//   4. fallback kernels reproduce the reference's exhaustive semantics exactly
-//      (lowest-index accepting element, else closest element) by brute force.
+// Pipeline of one pmmg_hip_locate_interp (all on the context stream):
+//   1. bbox of the background (ordered-integer atomics)           k_bbox
+//   2. volume seed grid: per cell, the sampled tetra whose first
+//      vertex is closest to the cell centre (64-bit atomicMin:
+//      deterministic); surface seed grid: tria centroids           k_seed_vol, k_seed_srf
+//   3. query order: Morton binning of the queries per class
+//      (count / exclusive scan / scatter), or, when the input order
+//      is already spatially coherent, a stable class compaction     k_bin_*, DeviceSelect
+//   4. volume: lean walk kernel writing the located tetra per query,
+//      then an interpolation kernel specialised on the slot layout
+//      so that every row gather is issued before any math           k_vol_locate, k_vol_interp
+//   5. surface: tria walk + wedge/cone + interpolation              k_bdy
+//   6. queries whose walk got stuck / ran too long: brute-force
+//      scans with the reference's exhaustive semantics              k_*_exhaust*, k_*_finish
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -36,373 +35,46 @@
 
 #include <vector>
 
-#include "parmmg_hip.h"
+#include "pmmg_device.hpp"
+
+using namespace pmmg;
 
 namespace {
 
-constexpr double kEps = 1.e-06;     // MMG5_EPS
-constexpr double kEpsD2 = 1.0e-200; // MMG5_EPSD2
-constexpr int kMaxSlot = 12;        // metric + up to 11 fields per launch
-constexpr int kHist = 8;            // visited-element history per walk
-constexpr int kBlock = 256;
-constexpr int kFanMax = 64;
+// ---------------------------------------------------------------- prepare
 
-struct Bg {
-  const double *xyz;
-  const int4 *tetv;
-  const int4 *adja;
-  const int *triv;
-  const int *adjt;
-  int np, ne, nt;
-  double hausd;
-};
-
-struct Slot {
-  const double *in;
-  double *out;
-  int size;
-  int ani;
-};
-
-struct Slots {
-  Slot s[kMaxSlot];
-  int n;
-  int has_met; // slot 0 is the metric
-};
-
-// bbox-derived frame, written on the device (no host round trip)
-struct Frame {
-  unsigned long long key_lo[3], key_hi[3]; // ordered-integer bbox accumulators
-  double lo[3];
-  double inv_vol[3], inv_srf[3], inv_mort[3];
-};
-
-struct DevStats {
-  unsigned long long cnt[16];
-  unsigned long long steps;
-  unsigned int stepmax;
-  int nvol, nbdy;
-  int nfb_vol, nfb_bdy;
-  int ncl_vol, ncl_bdy;
-};
-
-// ---------------------------------------------------------------- helpers
-
-__device__ __forceinline__ unsigned long long dkey(double d) {
-  unsigned long long u = (unsigned long long)__double_as_longlong(d);
-  return (u >> 63) ? ~u : (u | 0x8000000000000000ULL);
-}
-__device__ __forceinline__ double dunkey(unsigned long long k) {
-  unsigned long long u = (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFULL) : ~k;
-  return __longlong_as_double((long long)u);
-}
-
-__device__ __forceinline__ int sel4(const int4 &a, int i) {
-  return i == 0 ? a.x : (i == 1 ? a.y : (i == 2 ? a.z : a.w));
-}
-
-__device__ __forceinline__ void load_pt(const Bg &bg, int v, double *p) {
-  const double *q = bg.xyz + 3 * (size_t)(v - 1);
-  p[0] = q[0];
-  p[1] = q[1];
-  p[2] = q[2];
-}
-
-// MMG5_nonUnitNorPts: (b-a)x(c-a)
-__device__ __forceinline__ void nonunit_normal(const double *a, const double *b, const double *c, double *n) {
-  double abx = b[0] - a[0], aby = b[1] - a[1], abz = b[2] - a[2];
-  double acx = c[0] - a[0], acy = c[1] - a[1], acz = c[2] - a[2];
-  n[0] = aby * acz - abz * acy;
-  n[1] = abz * acx - abx * acz;
-  n[2] = abx * acy - aby * acx;
-}
-
-// MMG5_orvol
-__device__ __forceinline__ double orvol4(const double *p0, const double *p1, const double *p2, const double *p3) {
-  double ax = p2[0] - p0[0], ay = p2[1] - p0[1], az = p2[2] - p0[2];
-  double bx = p3[0] - p0[0], by = p3[1] - p0[1], bz = p3[2] - p0[2];
-  return (p1[0] - p0[0]) * (ay * bz - az * by) + (p1[1] - p0[1]) * (az * bx - ax * bz) +
-         (p1[2] - p0[2]) * (ax * by - ay * bx);
-}
-
-// PMMG_barycoord3d_compute (barycoord_pmmg.c:238-257) on freshly computed
-// face normals (PMMG_precompute_faceAreas, locate_pmmg.c:107-119) — the
-// reference's faceAreas array is recomputed, not stored (96 B/tetra saved).
-// Returns vol (pt->qual); b[f] unsorted barycentric coordinates.
-__device__ __forceinline__ double tet_bary(const double *x, const double *p0, const double *p1, const double *p2,
-                                           const double *p3, double *b) {
-  double vol = orvol4(p0, p1, p2, p3);
-  double n[3];
-  // face 0: idir {1,2,3}
-  nonunit_normal(p1, p2, p3, n);
-  b[0] = -((x[0] - p1[0]) * n[0] + (x[1] - p1[1]) * n[1] + (x[2] - p1[2]) * n[2]) / vol;
-  // face 1: idir {0,3,2}
-  nonunit_normal(p0, p3, p2, n);
-  b[1] = -((x[0] - p0[0]) * n[0] + (x[1] - p0[1]) * n[1] + (x[2] - p0[2]) * n[2]) / vol;
-  // face 2: idir {0,1,3}
-  nonunit_normal(p0, p1, p3, n);
-  b[2] = -((x[0] - p0[0]) * n[0] + (x[1] - p0[1]) * n[1] + (x[2] - p0[2]) * n[2]) / vol;
-  // face 3: idir {0,2,1}
-  nonunit_normal(p0, p2, p1, n);
-  b[3] = -((x[0] - p0[0]) * n[0] + (x[1] - p0[1]) * n[1] + (x[2] - p0[2]) * n[2]) / vol;
-  return vol;
-}
-
-// rank of entry a in the stable ascending order of (value, index)
-__device__ __forceinline__ bool before(double va, int a, double vb, int b) {
-  return (va < vb) || (va == vb && a < b);
-}
-
-__device__ __forceinline__ void ranks4(const double *b, int *r) {
-#pragma unroll
-  for (int f = 0; f < 4; f++) {
-    int c = 0;
-#pragma unroll
-    for (int g = 0; g < 4; g++)
-      if (g != f && before(b[g], g, b[f], f)) c++;
-    r[f] = c;
-  }
-}
-
-__device__ __forceinline__ void ranks3(const double *b, int *r) {
-#pragma unroll
-  for (int f = 0; f < 3; f++) {
-    int c = 0;
-#pragma unroll
-    for (int g = 0; g < 3; g++)
-      if (g != f && before(b[g], g, b[f], f)) c++;
-    r[f] = c;
-  }
-}
-
-// sorted[0].val of PMMG_barycoord*_evaluate
-__device__ __forceinline__ double min4(const double *b) {
-  double m = b[0];
-  m = b[1] < m ? b[1] : m;
-  m = b[2] < m ? b[2] : m;
-  m = b[3] < m ? b[3] : m;
-  return m;
-}
-
-// MMG5_invmat restated (symmetric 3x3, m11,m12,m13,m22,m23,m33)
-__device__ __forceinline__ bool invmat(const double *m, double *mi) {
-  double vmax = fabs(m[1]), maxx = fabs(m[2]);
-  if (maxx > vmax) vmax = maxx;
-  maxx = fabs(m[4]);
-  if (maxx > vmax) vmax = maxx;
-  if (vmax < kEps) {
-    mi[0] = 1. / m[0];
-    mi[3] = 1. / m[3];
-    mi[5] = 1. / m[5];
-    mi[1] = mi[2] = mi[4] = 0.0;
-    return true;
-  }
-  vmax = fabs(m[0]);
-#pragma unroll
-  for (int k = 1; k < 6; k++) {
-    maxx = fabs(m[k]);
-    if (maxx > vmax) vmax = maxx;
-  }
-  if (vmax == 0.0) return false;
-  double aa = m[3] * m[5] - m[4] * m[4];
-  double bb = m[4] * m[2] - m[1] * m[5];
-  double cc = m[1] * m[4] - m[2] * m[3];
-  double det = m[0] * aa + m[1] * bb + m[2] * cc;
-  if (fabs(det) < kEpsD2) return false;
-  det = 1.0 / det;
-  mi[0] = aa * det;
-  mi[1] = bb * det;
-  mi[2] = cc * det;
-  mi[3] = (m[0] * m[5] - m[2] * m[2]) * det;
-  mi[4] = (m[1] * m[2] - m[0] * m[4]) * det;
-  mi[5] = (m[0] * m[3] - m[1] * m[1]) * det;
-  return true;
-}
-
-__device__ __forceinline__ void load6(const double *p, double *m) {
-  const double2 *q = reinterpret_cast<const double2 *>(p);
-  double2 a = q[0], b = q[1], c = q[2];
-  m[0] = a.x; m[1] = a.y; m[2] = b.x; m[3] = b.y; m[4] = c.x; m[5] = c.y;
-}
-
-__device__ __forceinline__ void store6(double *p, const double *m) {
-  double2 *q = reinterpret_cast<double2 *>(p);
-  q[0] = make_double2(m[0], m[1]);
-  q[1] = make_double2(m[2], m[3]);
-  q[2] = make_double2(m[4], m[5]);
-}
-
-// interp{3,4}bar_iso: out[j] = 0; out[j] += phi_i * old[v_i][j] (i ascending)
-template <int NV, int SZ>
-__device__ __forceinline__ void iso_rows(const double *in, const int *v, const double *phi, double *out) {
-  double acc[SZ];
-#pragma unroll
-  for (int j = 0; j < SZ; j++) acc[j] = 0.0;
-#pragma unroll
-  for (int i = 0; i < NV; i++) {
-    const double *row = in + (size_t)SZ * (v[i] - 1);
-#pragma unroll
-    for (int j = 0; j < SZ; j++) acc[j] += phi[i] * row[j];
-  }
-#pragma unroll
-  for (int j = 0; j < SZ; j++) out[j] = acc[j];
-}
-
-template <int NV>
-__device__ __forceinline__ void iso_rows_dyn(int size, const double *in, const int *v, const double *phi, double *out) {
-  for (int j = 0; j < size; j++) out[j] = 0.0;
-  for (int i = 0; i < NV; i++)
-    for (int j = 0; j < size; j++) out[j] += phi[i] * in[(size_t)size * (v[i] - 1) + j];
-}
-
-// interp{3,4}bar_ani: M = invmat( sum_i phi_i invmat(M_i) ); untouched on failure
-template <int NV>
-__device__ __forceinline__ void ani_rows(const double *in, const int *v, const double *phi, double *out) {
-  double mint[6], m[6], mi[6];
-  bool ok = true;
-#pragma unroll
-  for (int i = 0; i < NV; i++) {
-    load6(in + 6 * (size_t)(v[i] - 1), m);
-    ok = ok && invmat(m, mi);
-#pragma unroll
-    for (int s = 0; s < 6; s++) mint[s] = (i == 0) ? phi[0] * mi[s] : mint[s] + phi[i] * mi[s];
-  }
-  if (!ok) return;
-  double r[6];
-  if (invmat(mint, r)) store6(out, r);
-}
-
-template <int NV>
-__device__ __forceinline__ void interp_slot(const Slot &sl, int ip, const int *v, const double *phi) {
-  double *out = sl.out + (size_t)sl.size * (ip - 1);
-  if (sl.ani) {
-    ani_rows<NV>(sl.in, v, phi, out);
-  } else if (sl.size == 1) {
-    iso_rows<NV, 1>(sl.in, v, phi, out);
-  } else if (sl.size == 3) {
-    iso_rows<NV, 3>(sl.in, v, phi, out);
-  } else if (sl.size == 6) {
-    iso_rows<NV, 6>(sl.in, v, phi, out);
-  } else {
-    iso_rows_dyn<NV>(sl.size, sl.in, v, phi, out);
-  }
-}
-
-// volume point: PMMG_interp4bar for the metric + 4bar_{ani,iso} per field (interpmesh_pmmg.c:612-636)
-__device__ __forceinline__ void interp_vol(const Slots &S, int ip, const int *v, const double *phi) {
-  for (int s = 0; s < S.n; s++) interp_slot<4>(S.s[s], ip, v, phi);
-}
-
-// interp2bar_{iso,ani} (interpmesh_pmmg.c:50-110): edge l of the tria
-__device__ __forceinline__ void interp_edge(const Slot &sl, int ip, const int *v, int l, const double *phi) {
-  const int i0 = (l + 1) % 3, i1 = (l + 2) % 3; // MMG5_inxt2[l], MMG5_iprv2[l]
-  double *out = sl.out + (size_t)sl.size * (ip - 1);
-  if (sl.size == 6) {
-    double m[6], mi0[6], mi1[6], mint[6], r[6];
-    load6(sl.in + 6 * (size_t)(v[i0] - 1), m);
-    if (!invmat(m, mi0)) return;
-    load6(sl.in + 6 * (size_t)(v[i1] - 1), m);
-    if (!invmat(m, mi1)) return;
-#pragma unroll
-    for (int s = 0; s < 6; s++) mint[s] = phi[i0] * mi0[s] + phi[i1] * mi1[s];
-    if (invmat(mint, r)) store6(out, r);
-  } else {
-    out[0] = phi[i0] * sl.in[v[i0] - 1] + phi[i1] * sl.in[v[i1] - 1];
-  }
-}
-
-__device__ __forceinline__ void copy_row(const Slot &sl, int ip, int vsrc) {
-  double *out = sl.out + (size_t)sl.size * (ip - 1);
-  const double *in = sl.in + (size_t)sl.size * (vsrc - 1);
-  for (int j = 0; j < sl.size; j++) out[j] = in[j];
-}
-
-// boundary point (interpmesh_pmmg.c:563-595): metric by vertex copy / edge /
-// face, every field by interp3bar
-__device__ __forceinline__ void interp_bdy(const Slots &S, int ip, const int *v, const double *phi, int edge,
-                                           int vertex) {
-  for (int s = 0; s < S.n; s++) {
-    const Slot &sl = S.s[s];
-    if (s == 0 && S.has_met) {
-      if (vertex >= 0) copy_row(sl, ip, v[vertex]);
-      else if (edge >= 0) interp_edge(sl, ip, v, edge, phi);
-      else interp_slot<3>(sl, ip, v, phi);
-    } else {
-      interp_slot<3>(sl, ip, v, phi);
+// one launch initialises the per-call state: frame accumulators, stats,
+// seed grids, bin counters
+__global__ __launch_bounds__(kBlock) void k_reset(Frame *fr, DevStats *st, unsigned long long *grid, long long ng,
+                                                  int *sgrid, long long nsg, int *cnt, long long ncnt, int keep_coherent) {
+  const long long tid = blockIdx.x * (long long)blockDim.x + threadIdx.x, nth = (long long)gridDim.x * blockDim.x;
+  if (tid == 0) {
+    for (int d = 0; d < 3; d++) {
+      fr->key_lo[d] = ~0ULL;
+      fr->key_hi[d] = 0ULL;
     }
+    int coh = st->coherent;
+    unsigned int *w = reinterpret_cast<unsigned int *>(st);
+    for (size_t j = 0; j < sizeof(DevStats) / 4; j++) w[j] = 0u;
+    if (keep_coherent) st->coherent = coh;
   }
-}
-
-__device__ __forceinline__ int wave_append(int *counter, bool pred) {
-  unsigned long long m = __ballot(pred);
-  if (m == 0ULL) return -1;
-  int lane = __lane_id();
-  int leader = __ffsll((long long)m) - 1;
-  int base = 0;
-  if (lane == leader) base = atomicAdd(counter, __popcll(m));
-  base = __shfl(base, leader);
-  int rank = __popcll(m & ((1ULL << lane) - 1ULL));
-  return pred ? base + rank : -1;
-}
-
-__device__ __forceinline__ int cell_coord(double x, double lo, double inv, int g) {
-  double t = (x - lo) * inv;
-  int c = (t > 0.0) ? (int)t : 0;
-  return c < g ? c : g - 1;
-}
-
-// seed element of the grid cell of x; empty cell -> smallest id within a
-// 2-cell ring (deterministic), else element 1
-__device__ int grid_seed(const int *cell, int g, const double *lo, const double *inv, const double *x) {
-  int ci = cell_coord(x[0], lo[0], inv[0], g);
-  int cj = cell_coord(x[1], lo[1], inv[1], g);
-  int ck = cell_coord(x[2], lo[2], inv[2], g);
-  int s = cell[ci + (size_t)g * (cj + (size_t)g * ck)];
-  if (s != INT_MAX) return s;
-  for (int r = 1; r <= 2; r++) {
-    int best = INT_MAX;
-    for (int dk = -r; dk <= r; dk++)
-      for (int dj = -r; dj <= r; dj++)
-        for (int di = -r; di <= r; di++) {
-          if (max(abs(di), max(abs(dj), abs(dk))) != r) continue;
-          int a = ci + di, b = cj + dj, c = ck + dk;
-          if (a < 0 || b < 0 || c < 0 || a >= g || b >= g || c >= g) continue;
-          int v = cell[a + (size_t)g * (b + (size_t)g * c)];
-          best = v < best ? v : best;
-        }
-    if (best != INT_MAX) return best;
-  }
-  return 1;
-}
-
-__device__ __forceinline__ uint32_t expand10(uint32_t v) {
-  v &= 0x3ffu;
-  v = (v | (v << 16)) & 0x030000FFu;
-  v = (v | (v << 8)) & 0x0300F00Fu;
-  v = (v | (v << 4)) & 0x030C30C3u;
-  v = (v | (v << 2)) & 0x09249249u;
-  return v;
-}
-
-// ---------------------------------------------------------------- prepare kernels
-
-__global__ void k_frame_init(Frame *fr) {
-  for (int d = 0; d < 3; d++) {
-    fr->key_lo[d] = ~0ULL;
-    fr->key_hi[d] = 0ULL;
-  }
+  for (long long j = tid; j < ng; j += nth) grid[j] = ~0ULL;
+  for (long long j = tid; j < nsg; j += nth) sgrid[j] = INT_MAX;
+  for (long long j = tid; j < ncnt; j += nth) cnt[j] = 0;
 }
 
 __global__ __launch_bounds__(kBlock) void k_bbox(const double *xyz, int np, Frame *fr) {
   __shared__ unsigned long long slo[3][kBlock / 64], shi[3][kBlock / 64];
   unsigned long long lo[3] = {~0ULL, ~0ULL, ~0ULL}, hi[3] = {0ULL, 0ULL, 0ULL};
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < np; i += gridDim.x * blockDim.x) {
+#pragma unroll
     for (int d = 0; d < 3; d++) {
       unsigned long long k = dkey(xyz[3 * (size_t)i + d]);
       lo[d] = k < lo[d] ? k : lo[d];
       hi[d] = k > hi[d] ? k : hi[d];
     }
   }
+#pragma unroll
   for (int d = 0; d < 3; d++) {
     for (int off = 32; off > 0; off >>= 1) {
       unsigned long long a = __shfl_down(lo[d], off), b = __shfl_down(hi[d], off);
@@ -426,90 +98,181 @@ __global__ __launch_bounds__(kBlock) void k_bbox(const double *xyz, int np, Fram
   }
 }
 
-__global__ void k_frame_final(Frame *fr, int g, int gs) {
+__global__ void k_frame_final(Frame *fr, int g, int gs, int gb) {
   for (int d = 0; d < 3; d++) {
     double lo = dunkey(fr->key_lo[d]), hi = dunkey(fr->key_hi[d]);
     double ext = hi - lo;
     fr->lo[d] = lo;
+    fr->ext[d] = ext;
     fr->inv_vol[d] = ext > 0.0 ? (double)g / ext : 0.0;
     fr->inv_srf[d] = ext > 0.0 ? (double)gs / ext : 0.0;
-    fr->inv_mort[d] = ext > 0.0 ? 1024.0 / ext : 0.0;
+    fr->inv_bin[d] = ext > 0.0 ? (double)gb / ext : 0.0;
   }
 }
 
-// volume seed grid from a sample of tetra: cell of the first vertex -> min id
-__global__ __launch_bounds__(kBlock) void k_seed_vol(Bg bg, const Frame *fr, int *cell, int g, long long nsamp) {
+// volume seeds: per cell, the sampled tetra whose first vertex is closest to
+// the cell centre; key = (float(dist^2) bits << 32) | id -> deterministic min
+__global__ __launch_bounds__(kBlock) void k_seed_vol(Bg bg, const Frame *fr, unsigned long long *cell, int g,
+                                                     long long nsamp) {
   for (long long s = blockIdx.x * (long long)blockDim.x + threadIdx.x; s < nsamp;
        s += (long long)gridDim.x * blockDim.x) {
     int k = 1 + (int)((s * (long long)bg.ne) / nsamp);
     int v0 = bg.tetv[k - 1].x;
     if (v0 <= 0) continue;
     double p[3];
-    load_pt(bg, v0, p);
-    int ci = cell_coord(p[0], fr->lo[0], fr->inv_vol[0], g);
-    int cj = cell_coord(p[1], fr->lo[1], fr->inv_vol[1], g);
-    int ck = cell_coord(p[2], fr->lo[2], fr->inv_vol[2], g);
-    atomicMin(&cell[ci + (size_t)g * (cj + (size_t)g * ck)], k);
+    load_pt(bg.xyz, v0, p);
+    int c[3];
+    float d2 = 0.f;
+    for (int d = 0; d < 3; d++) {
+      c[d] = cell_coord(p[d], fr->lo[d], fr->inv_vol[d], g);
+      double ctr = fr->lo[d] + (c[d] + 0.5) / (fr->inv_vol[d] > 0.0 ? fr->inv_vol[d] : 1.0);
+      float dd = (float)(p[d] - ctr);
+      d2 += dd * dd;
+    }
+    unsigned long long key = ((unsigned long long)__float_as_uint(d2) << 32) | (unsigned)k;
+    atomicMin(&cell[c[0] + (size_t)g * (c[1] + (size_t)g * c[2])], key);
   }
 }
 
-// surface seed grid: cell of each tria centroid -> min id
+// surface seeds: cell of each tria centroid -> min id
 __global__ __launch_bounds__(kBlock) void k_seed_srf(Bg bg, const Frame *fr, int *cell, int g) {
   for (int k = 1 + blockIdx.x * blockDim.x + threadIdx.x; k <= bg.nt; k += gridDim.x * blockDim.x) {
-    int a = bg.triv[3 * (size_t)(k - 1)];
-    if (a <= 0) continue;
+    const int *tv = bg.triv + 3 * (size_t)(k - 1);
+    if (tv[0] <= 0) continue;
     double p0[3], p1[3], p2[3];
-    load_pt(bg, a, p0);
-    load_pt(bg, bg.triv[3 * (size_t)(k - 1) + 1], p1);
-    load_pt(bg, bg.triv[3 * (size_t)(k - 1) + 2], p2);
-    double c[3];
-    for (int d = 0; d < 3; d++) c[d] = (p0[d] + p1[d] + p2[d]) * (1.0 / 3.0);
-    int ci = cell_coord(c[0], fr->lo[0], fr->inv_srf[0], g);
-    int cj = cell_coord(c[1], fr->lo[1], fr->inv_srf[1], g);
-    int ck = cell_coord(c[2], fr->lo[2], fr->inv_srf[2], g);
-    atomicMin(&cell[ci + (size_t)g * (cj + (size_t)g * ck)], k);
+    load_pt(bg.xyz, tv[0], p0);
+    load_pt(bg.xyz, tv[1], p1);
+    load_pt(bg.xyz, tv[2], p2);
+    int c[3];
+    for (int d = 0; d < 3; d++) c[d] = cell_coord((p0[d] + p1[d] + p2[d]) * (1.0 / 3.0), fr->lo[d], fr->inv_srf[d], g);
+    atomicMin(&cell[c[0] + (size_t)g * (c[1] + (size_t)g * c[2])], k);
   }
 }
 
-// query keys: (class, Morton) ; counts of volume / surface queries
-__global__ __launch_bounds__(kBlock) void k_keys(const double *xyz, const uint8_t *pclass, int np, const Frame *fr,
-                                                 int nosort, uint32_t *keys, int *vals, DevStats *st) {
-  __shared__ int cv, cb;
-  if (threadIdx.x == 0) { cv = 0; cb = 0; }
-  __syncthreads();
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < np) {
-    int c = pclass[i];
-    uint32_t key;
-    if (c == PMMG_PT_VOL || c == PMMG_PT_BDY) {
-      // NOSORT: the input index replaces the Morton code (< 2^30), so a full
-      // 32-bit sort keeps each class in input order
-      uint32_t m = (uint32_t)i & 0x3FFFFFFFu;
-      if (!nosort) {
-        uint32_t q[3];
-        for (int d = 0; d < 3; d++) {
-          double t = (xyz[3 * (size_t)i + d] - fr->lo[d]) * fr->inv_mort[d];
-          int u = t > 0.0 ? (int)t : 0;
-          q[d] = (uint32_t)(u > 1023 ? 1023 : u);
+__device__ __forceinline__ int seed_vol(const unsigned long long *cell, int g, const Frame *fr, const double *x) {
+  int ci = cell_coord(x[0], fr->lo[0], fr->inv_vol[0], g);
+  int cj = cell_coord(x[1], fr->lo[1], fr->inv_vol[1], g);
+  int ck = cell_coord(x[2], fr->lo[2], fr->inv_vol[2], g);
+  unsigned long long s = cell[ci + (size_t)g * (cj + (size_t)g * ck)];
+  if (s != ~0ULL) return (int)(unsigned)(s & 0xFFFFFFFFULL);
+  for (int r = 1; r <= 2; r++) {
+    unsigned long long best = ~0ULL;
+    for (int dk = -r; dk <= r; dk++)
+      for (int dj = -r; dj <= r; dj++)
+        for (int di = -r; di <= r; di++) {
+          if (max(abs(di), max(abs(dj), abs(dk))) != r) continue;
+          int a = ci + di, b = cj + dj, c = ck + dk;
+          if (a < 0 || b < 0 || c < 0 || a >= g || b >= g || c >= g) continue;
+          unsigned long long v = cell[a + (size_t)g * (b + (size_t)g * c)];
+          unsigned long long id = v & 0xFFFFFFFFULL;
+          if (v != ~0ULL && id < best) best = id;
         }
-        m = (expand10(q[0]) << 2) | (expand10(q[1]) << 1) | expand10(q[2]);
-      }
-      key = (c == PMMG_PT_VOL ? 0u : (1u << 30)) | m;
-      atomicAdd(c == PMMG_PT_VOL ? &cv : &cb, 1);
-    } else {
-      key = 0xFFFFFFFFu;
-    }
-    keys[i] = key;
-    vals[i] = i + 1;
+    if (best != ~0ULL) return (int)best;
   }
+  return 1;
+}
+
+__device__ int seed_srf(const int *cell, int g, const Frame *fr, const double *x) {
+  int ci = cell_coord(x[0], fr->lo[0], fr->inv_srf[0], g);
+  int cj = cell_coord(x[1], fr->lo[1], fr->inv_srf[1], g);
+  int ck = cell_coord(x[2], fr->lo[2], fr->inv_srf[2], g);
+  int s = cell[ci + (size_t)g * (cj + (size_t)g * ck)];
+  if (s != INT_MAX) return s;
+  for (int r = 1; r <= 2; r++) {
+    int best = INT_MAX;
+    for (int dk = -r; dk <= r; dk++)
+      for (int dj = -r; dj <= r; dj++)
+        for (int di = -r; di <= r; di++) {
+          if (max(abs(di), max(abs(dj), abs(dk))) != r) continue;
+          int a = ci + di, b = cj + dj, c = ck + dk;
+          if (a < 0 || b < 0 || c < 0 || a >= g || b >= g || c >= g) continue;
+          int v = cell[a + (size_t)g * (b + (size_t)g * c)];
+          best = v < best ? v : best;
+        }
+    if (best != INT_MAX) return best;
+  }
+  return 1;
+}
+
+// ---------------------------------------------------------------- query order
+
+// Is the input numbering spatially coherent?  Mean distance between
+// consecutive points (sampled) against the mean spacing of np points in the
+// bbox of the sample; lattice / SCOTCH-renumbered meshes pass, shuffled
+// numberings fail.  Self-contained so it can run first and be read back early.
+__global__ __launch_bounds__(kBlock) void k_coherence(const double *xyz, int np, DevStats *st) {
+  __shared__ double ssum[kBlock], slo[3][kBlock], shi[3][kBlock];
+  double acc = 0.0, lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+  const int nsamp = 4096;
+  for (int s = threadIdx.x; s < nsamp; s += blockDim.x) {
+    long long i = ((long long)s * (np - 1)) / nsamp;
+    double d2 = 0.0;
+    for (int d = 0; d < 3; d++) {
+      double a = xyz[3 * (size_t)i + d], b = xyz[3 * (size_t)(i + 1) + d];
+      double t = b - a;
+      d2 += t * t;
+      lo[d] = fmin(lo[d], a);
+      hi[d] = fmax(hi[d], a);
+    }
+    acc += sqrt(d2);
+  }
+  ssum[threadIdx.x] = acc;
+  for (int d = 0; d < 3; d++) { slo[d][threadIdx.x] = lo[d]; shi[d][threadIdx.x] = hi[d]; }
   __syncthreads();
   if (threadIdx.x == 0) {
-    if (cv) atomicAdd(&st->nvol, cv);
-    if (cb) atomicAdd(&st->nbdy, cb);
+    double tot = 0.0, L[3] = {1e300, 1e300, 1e300}, H[3] = {-1e300, -1e300, -1e300};
+    for (int j = 0; j < kBlock; j++) {
+      tot += ssum[j];
+      for (int d = 0; d < 3; d++) { L[d] = fmin(L[d], slo[d][j]); H[d] = fmax(H[d], shi[d][j]); }
+    }
+    double mean = tot / nsamp;
+    double vol = fmax(H[0] - L[0], 1e-300) * fmax(H[1] - L[1], 1e-300) * fmax(H[2] - L[2], 1e-300);
+    double h = cbrt(vol / (double)(np > 1 ? np : 1));
+    st->coherent = (np > 1 && mean < 4.0 * h) ? 1 : 0;
   }
 }
 
-// ---------------------------------------------------------------- stats aggregation
+// Morton binning: bin = (class, Morton code of the gb^3 cell); rank inside the
+// bin from the counter (order inside a bin is irrelevant: each query's result
+// is a pure function of the query)
+__global__ __launch_bounds__(kBlock) void k_bin_count(const double *xyz, const uint8_t *pclass, int np, const Frame *fr,
+                                                      int gb, int nbins, int *cnt, int2 *binrank) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= np) return;
+  int c = pclass[i];
+  if (c != PMMG_PT_VOL && c != PMMG_PT_BDY) {
+    binrank[i] = make_int2(-1, 0);
+    return;
+  }
+  uint32_t q[3];
+  for (int d = 0; d < 3; d++) q[d] = (uint32_t)cell_coord(xyz[3 * (size_t)i + d], fr->lo[d], fr->inv_bin[d], gb);
+  int bin = (int)((expand10(q[0]) << 2) | (expand10(q[1]) << 1) | expand10(q[2])) + (c == PMMG_PT_BDY ? nbins : 0);
+  int r = atomicAdd(&cnt[bin], 1);
+  binrank[i] = make_int2(bin, r);
+}
+
+__global__ __launch_bounds__(kBlock) void k_bin_scatter(int np, const int2 *binrank, const int *off, int nbins,
+                                                        int *order_v, int *order_b) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= np) return;
+  int2 br = binrank[i];
+  if (br.x < 0) return;
+  if (br.x < nbins) order_v[off[br.x] + br.y] = i + 1;
+  else order_b[off[br.x] - off[nbins] + br.y] = i + 1;
+}
+
+__global__ void k_bin_total(const int *off, const int *cnt, int nbins, DevStats *st) {
+  st->nvol = off[nbins];
+  st->nbdy = off[2 * nbins - 1] + cnt[2 * nbins - 1] - off[nbins];
+}
+
+struct IsClass {
+  const uint8_t *pclass;
+  int c;
+  __host__ __device__ __forceinline__ bool operator()(const int &ip) const { return pclass[ip - 1] == c; }
+};
+
+// ---------------------------------------------------------------- stats
 
 struct BlockStats {
   unsigned int cnt[16];
@@ -530,284 +293,438 @@ __device__ __forceinline__ void bstats_flush(BlockStats *b, DevStats *st) {
   }
 }
 
-// ---------------------------------------------------------------- volume locate + interpolate
+// per-wave aggregation of the walk statistics (one LDS atomic per wave and counter)
+__device__ __forceinline__ void wave_stats(BlockStats *bs, bool active, int hit, int steps) {
+  unsigned int s = active ? (unsigned)steps : 0u, mx = s;
+  for (int off = 32; off > 0; off >>= 1) {
+    s += __shfl_down(s, off);
+    unsigned o = __shfl_down(mx, off);
+    mx = o > mx ? o : mx;
+  }
+  if (__lane_id() == 0) {
+    if (s) atomicAdd(&bs->steps, (unsigned long long)s);
+    atomicMax(&bs->stepmax, mx);
+  }
+  int h = active ? hit : 0;
+  unsigned long long any = __ballot(h > 0);
+  while (any) {
+    int first = __shfl(h, __ffsll((long long)any) - 1);
+    unsigned long long same = __ballot(h == first);
+    if (__lane_id() == 0) atomicAdd(&bs->cnt[first], (unsigned)__popcll(same));
+    any &= ~same;
+  }
+}
+
+// ---------------------------------------------------------------- volume
 
 // PMMG_locatePointVol (locate_pmmg.c:786-883) from a grid seed instead of the
-// previous point's tetra; visited set = last kHist tetra.
-__global__ __launch_bounds__(kBlock) void k_vol(Bg bg, const Frame *fr, const int *grid, int g, const double *qxyz,
-                                                const int *order, Slots S, int *elem_out, int8_t *hit_out,
-                                                int *fb_list, DevStats *st, int maxstep) {
+// previous point's tetra; visited set = the last kHist tetra.  vloc[i] = the
+// accepting tetra, or 0 when the walk got stuck / exceeded maxstep (the query
+// then goes to the exhaustive kernels).
+//
+// Stepping through face f into k' = adja/4, the 3 vertices of f are shared:
+// their coordinates stay in registers and only the tetv/adja rows of k' and
+// its opposite vertex tetv[k'][adja%4] are fetched (5 loads per step instead
+// of 14).
+__device__ __forceinline__ int4 load_row_or_zero(const int4 *rows, int code) {
+  return code > 0 ? rows[(code >> 2) - 1] : make_int4(0, 0, 0, 0);
+}
+
+__device__ __forceinline__ void pick_pt(int id, const int4 &tv, const double (*p)[3], double *out) {
+  const int j = id == tv.x ? 0 : (id == tv.y ? 1 : (id == tv.z ? 2 : 3));
+#pragma unroll
+  for (int d = 0; d < 3; d++) out[d] = j == 0 ? p[0][d] : (j == 1 ? p[1][d] : (j == 2 ? p[2][d] : p[3][d]));
+}
+
+// the walk of one query; returns 1 found (k, tv, b = its barycentric
+// coordinates), 2 stuck, 3 over-long
+__device__ __forceinline__ int walk_vol(const Bg &bg, const unsigned long long *grid, int g, const Frame *fr,
+                                        const double *x, int maxstep, int &k, int4 &tv, double *b, int &steps) {
+  k = seed_vol(grid, g, fr, x);
+  tv = bg.tetv[k - 1];
+  int4 ad = bg.adja[k - 1];
+  double p[4][3];
+  load_pt(bg.xyz, tv.x, p[0]);
+  load_pt(bg.xyz, tv.y, p[1]);
+  load_pt(bg.xyz, tv.z, p[2]);
+  load_pt(bg.xyz, tv.w, p[3]);
+  int hist[kHist];
+#pragma unroll
+  for (int h = 0; h < kHist; h++) hist[h] = 0;
+  for (;;) {
+    ++steps;
+    tet_bary(x, p[0], p[1], p[2], p[3], b);
+    if (min4(b) > -kEps) return 1;
+    int r[4];
+    ranks4(b, r);
+    int f = -1, nrank = 4;
+#pragma unroll
+    for (int ff = 0; ff < 4; ff++) {
+      int iel = sel4(ad, ff) >> 2;
+      bool vis = false;
+#pragma unroll
+      for (int h = 0; h < kHist; h++) vis = vis || (hist[h] == iel);
+      if (iel != 0 && !vis && r[ff] < nrank) { f = ff; nrank = r[ff]; }
+    }
+    if (f < 0) return 2;            // stuck -> exhaustive
+    if (steps >= maxstep) return 3; // over-long -> exhaustive
+    const int code = sel4(ad, f);
+    const int next = code >> 2, iopp = code & 3;
+    const int4 tn = bg.tetv[next - 1];
+    ad = bg.adja[next - 1];
+    double pn[3];
+    load_pt(bg.xyz, sel4(tn, iopp), pn);
+    double q[4][3];
+#pragma unroll
+    for (int l = 0; l < 4; l++) {
+      if (l == iopp) { q[l][0] = pn[0]; q[l][1] = pn[1]; q[l][2] = pn[2]; }
+      else pick_pt(sel4(tn, l), tv, p, q[l]);
+    }
+#pragma unroll
+    for (int l = 0; l < 4; l++)
+#pragma unroll
+      for (int d = 0; d < 3; d++) p[l][d] = q[l][d];
+#pragma unroll
+    for (int h = kHist - 1; h > 0; h--) hist[h] = hist[h - 1];
+    hist[0] = k;
+    k = next;
+    tv = tn;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_vol_locate(Bg bg, const Frame *fr, const unsigned long long *grid, int g,
+                                                       const double *qxyz, const int *order, int *vloc, int *fb,
+                                                       DevStats *st, int maxstep) {
   __shared__ BlockStats bs;
   bstats_init(&bs);
   __syncthreads();
   const int nvol = st->nvol;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nvol; i += gridDim.x * blockDim.x) {
-    const int ip = order[i];
-    double x[3];
-    x[0] = qxyz[3 * (size_t)(ip - 1)];
-    x[1] = qxyz[3 * (size_t)(ip - 1) + 1];
-    x[2] = qxyz[3 * (size_t)(ip - 1) + 2];
-    int k = grid_seed(grid, g, fr->lo, fr->inv_vol, x);
-    int hist[kHist];
-#pragma unroll
-    for (int h = 0; h < kHist; h++) hist[h] = 0;
-    int steps = 0, status = 0;
-    int4 tv;
-    double b[4];
-    for (;;) {
-      ++steps;
-      tv = bg.tetv[k - 1];
-      const int4 ad = bg.adja[k - 1];
-      double p0[3], p1[3], p2[3], p3[3];
-      load_pt(bg, tv.x, p0);
-      load_pt(bg, tv.y, p1);
-      load_pt(bg, tv.z, p2);
-      load_pt(bg, tv.w, p3);
-      tet_bary(x, p0, p1, p2, p3, b);
-      if (min4(b) > -kEps) { status = 1; break; }
-      int r[4];
-      ranks4(b, r);
-      int next = 0, nrank = 4;
-#pragma unroll
-      for (int f = 0; f < 4; f++) {
-        int iel = sel4(ad, f) >> 2;
-        bool vis = false;
-#pragma unroll
-        for (int h = 0; h < kHist; h++) vis = vis || (hist[h] == iel);
-        if (iel != 0 && !vis && r[f] < nrank) { next = iel; nrank = r[f]; }
-      }
-      if (next == 0) { status = 2; break; }          // stuck -> exhaustive
-      if (steps >= maxstep) { status = 3; break; }   // over-long -> exhaustive
-#pragma unroll
-      for (int h = kHist - 1; h > 0; h--) hist[h] = hist[h - 1];
-      hist[0] = k;
-      k = next;
+  const int stride = gridDim.x * blockDim.x;
+  const int iters = (nvol + stride - 1) / stride;
+  for (int it = 0; it < iters; it++) {
+    const int i = it * stride + xcd_block() * blockDim.x + threadIdx.x;
+    const bool active = i < nvol;
+    int status = 0, steps = 0, k = 0, ip = 0;
+    if (active) {
+      ip = order[i];
+      double x[3], b[4];
+      load_pt(qxyz, ip, x);
+      int4 tv;
+      status = walk_vol(bg, grid, g, fr, x, maxstep, k, tv, b, steps);
+      vloc[i] = status == 1 ? k : 0;
     }
-    if (status == 1) {
-      int v[4] = {tv.x, tv.y, tv.z, tv.w};
-      interp_vol(S, ip, v, b);
-      if (elem_out) elem_out[ip - 1] = k;
-      if (hit_out) hit_out[ip - 1] = PMMG_HIT_VOL_WALK;
-      atomicAdd(&bs.cnt[PMMG_HIT_VOL_WALK], 1u);
-    }
-    int slot = wave_append(&st->nfb_vol, status != 1);
-    if (status != 1) fb_list[slot] = ip;
-    atomicAdd(&bs.steps, (unsigned long long)steps);
-    atomicMax(&bs.stepmax, (unsigned)steps);
+    int slot = wave_append(&st->nfb_vol, active && status != 1);
+    if (active && status != 1) fb[slot] = ip;
+    wave_stats(&bs, active, status == 1 ? PMMG_HIT_VOL_WALK : 0, steps);
   }
   __syncthreads();
   bstats_flush(&bs, st);
 }
 
-// ---------------------------------------------------------------- surface locate + interpolate
-
-struct TriGeom {
-  int v[3];
-  double p[3][3];
-  double n[3];  // unit normal
-  double q;     // |nonunit normal| (ptr->qual)
-};
-
-__device__ __forceinline__ void tri_load(const Bg &bg, int k, TriGeom &t) {
-  const int *tv = bg.triv + 3 * (size_t)(k - 1);
-  t.v[0] = tv[0];
-  t.v[1] = tv[1];
-  t.v[2] = tv[2];
-  load_pt(bg, t.v[0], t.p[0]);
-  load_pt(bg, t.v[1], t.p[1]);
-  load_pt(bg, t.v[2], t.p[2]);
-  // PMMG_precompute_triaNormals, locate_pmmg.c:74-87
-  nonunit_normal(t.p[0], t.p[1], t.p[2], t.n);
-  t.q = sqrt(t.n[0] * t.n[0] + t.n[1] * t.n[1] + t.n[2] * t.n[2]);
-  double dd = 1.0 / t.q;
-  t.n[0] *= dd;
-  t.n[1] *= dd;
-  t.n[2] *= dd;
-}
-
-// PMMG_quickarea
-__device__ __forceinline__ double quickarea(const double *a, const double *b, const double *c, const double *n) {
-  double abx = b[0] - a[0], aby = b[1] - a[1], abz = b[2] - a[2];
-  double acx = c[0] - a[0], acy = c[1] - a[1], acz = c[2] - a[2];
-  double a0 = aby * acz - abz * acy, a1 = abz * acx - abx * acz, a2 = abx * acy - aby * acx;
-  return a0 * n[0] + a1 * n[1] + a2 * n[2];
-}
-
-// PMMG_barycoord2d_compute (barycoord_pmmg.c:191-223) with vertices/area of
-// tria `pv` and unit normal n; returns the normal distance
-__device__ __forceinline__ double tri_bary(const double *x, const double (*pv)[3], double q, const double *n, double *b) {
-  double dist = 0.0, proj[3];
-  for (int i = 0; i < 3; i++) dist += (x[i] - pv[0][i]) * n[i];
-  for (int i = 0; i < 3; i++) proj[i] = x[i] - dist * n[i];
-  b[0] = quickarea(proj, pv[1], pv[2], n) / q;
-  b[1] = quickarea(proj, pv[2], pv[0], n) / q;
-  b[2] = quickarea(proj, pv[0], pv[1], n) / q;
-  return dist;
-}
-
-// PMMG_locatePointInWedge (locate_pmmg.c:286-334): -1 too far, 4 inside (phi
-// written), else the local vertex whose cone must be tested
-__device__ __forceinline__ int tri_wedge(const double hausd, const TriGeom &t, int l, const double *x, double *phi) {
-  const int i0 = (l + 1) % 3, i1 = (l + 2) % 3;
-  const double *p0 = t.p[i0], *p1 = t.p[i1];
-  double p[3], a[3], norm2 = 0.0, alpha = 0.0, dist = 0.0;
-  for (int d = 0; d < 3; d++) p[d] = x[d] - p0[d];
-  for (int d = 0; d < 3; d++) a[d] = p1[d] - p0[d];
-  for (int d = 0; d < 3; d++) norm2 += a[d] * a[d];
-  for (int d = 0; d < 3; d++) alpha += a[d] * p[d];
-  for (int d = 0; d < 3; d++) p[d] -= (alpha / norm2) * a[d];
-  for (int d = 0; d < 3; d++) dist += p[d] * p[d];
-  dist = sqrt(dist);
-  if (dist > hausd) return -1;
-  if (alpha < 0.0) return i0;
-  if (alpha > norm2) return i1;
-  phi[l] = 0.0;
-  phi[i0] = 1.0 - alpha / norm2;
-  phi[i1] = alpha / norm2;
-  return 4;
-}
-
-__device__ __forceinline__ bool cone_edge_ok(const Bg &bg, int jp, const double *p0, const double *p) {
-  double p1[3], a[3], alpha = 0.0;
-  load_pt(bg, jp, p1);
-  for (int d = 0; d < 3; d++) a[d] = p1[d] - p0[d];
-  for (int d = 0; d < 3; d++) alpha += a[d] * p[d];
-  return !(alpha > 0.0);
-}
-
-// PMMG_locatePointInCone (locate_pmmg.c:209-270) with a fresh visited state:
-// x is in the shadow cone of vertex ip iff |x-p(ip)| <= hausd and every
-// surface edge leaving ip makes a non-acute angle with x-p(ip).  The
-// vertex's trias are reached by rotating through adjt (manifold fan) instead
-// of the reference's node->trias CSR; the set of edges tested is the same.
-__device__ bool tri_cone(const Bg &bg, int k, int iloc, const int *tv, const double *x) {
-  const int ip = tv[iloc];
-  double p0[3], p[3], dist = 0.0;
-  load_pt(bg, ip, p0);
-  for (int d = 0; d < 3; d++) p[d] = x[d] - p0[d];
-  for (int d = 0; d < 3; d++) dist += p[d] * p[d];
-  dist = sqrt(dist);
-  if (dist > bg.hausd) return false;
-  // tria k itself
-  if (!cone_edge_ok(bg, tv[(iloc + 1) % 3], p0, p) || !cone_edge_ok(bg, tv[(iloc + 2) % 3], p0, p)) return false;
-  // rotate both ways around ip
-  for (int dir = 0; dir < 2; dir++) {
-    int t = k, lv = iloc;
-    int e = dir == 0 ? (lv + 1) % 3 : (lv + 2) % 3; // an edge of t incident to ip
-    for (int it = 0; it < kFanMax; it++) {
-      int code = bg.adjt[3 * (size_t)(t - 1) + e];
-      int tn = code / 3, en = code % 3;
-      if (tn == 0) break;      // open fan: continue with the other direction
-      if (tn == k) return true; // closed fan fully visited
-      const int *tvn = bg.triv + 3 * (size_t)(tn - 1);
-      int w0 = tvn[0], w1 = tvn[1], w2 = tvn[2];
-      int lvn = (w0 == ip) ? 0 : ((w1 == ip) ? 1 : 2);
-      int o1 = (lvn + 1) % 3, o2 = (lvn + 2) % 3;
-      int j1 = o1 == 0 ? w0 : (o1 == 1 ? w1 : w2);
-      int j2 = o2 == 0 ? w0 : (o2 == 1 ? w1 : w2);
-      if (!cone_edge_ok(bg, j1, p0, p) || !cone_edge_ok(bg, j2, p0, p)) return false;
-      // the other edge of tn incident to ip
-      int ea = (lvn + 1) % 3, eb = (lvn + 2) % 3;
-      e = (ea == en) ? eb : ea;
-      t = tn;
-    }
+// interpolation of located volume queries; the slot layout is a template
+// (codes 1 / 3 / 6, 0 = none) so every row gather is unconditional and can be
+// issued before any arithmetic; C0 < 0 selects the runtime-layout variant
+template <int C0, int C1, int C2, int C3, int C4, int C5>
+__device__ __forceinline__ void interp_vol_layout(const Slots &S, int ip, const int *v, const double *phi) {
+  if constexpr (C0 < 0) {
+    for (int s = 0; s < S.n; s++) interp_dyn<4>(S.s[s], ip, v, phi);
+  } else {
+    if constexpr (C0 > 0) interp_code<4, C0>(S.s[0], ip, v, phi);
+    if constexpr (C1 > 0) interp_code<4, C1>(S.s[1], ip, v, phi);
+    if constexpr (C2 > 0) interp_code<4, C2>(S.s[2], ip, v, phi);
+    if constexpr (C3 > 0) interp_code<4, C3>(S.s[3], ip, v, phi);
+    if constexpr (C4 > 0) interp_code<4, C4>(S.s[4], ip, v, phi);
+    if constexpr (C5 > 0) interp_code<4, C5>(S.s[5], ip, v, phi);
   }
-  return true;
 }
 
-__global__ __launch_bounds__(kBlock) void k_bdy(Bg bg, const Frame *fr, const int *sgrid, int gs, const double *qxyz,
-                                                const int *order, Slots S, int *elem_out, int8_t *hit_out,
-                                                int *fb_list, DevStats *st, int maxstep) {
+template <int C0, int C1, int C2, int C3, int C4, int C5>
+__global__ __launch_bounds__(kBlock) void k_vol_interp(Bg bg, const double *qxyz, const int *order, const int *vloc,
+                                                       Slots S, int *elem_out, int8_t *hit_out, const DevStats *st) {
+  const int nvol = st->nvol;
+  for (int i = xcd_block() * blockDim.x + threadIdx.x; i < nvol; i += gridDim.x * blockDim.x) {
+    const int k = vloc[i];
+    if (k == 0) continue;
+    const int ip = order[i];
+    double x[3], p0[3], p1[3], p2[3], p3[3], phi[4];
+    load_pt(qxyz, ip, x);
+    const int4 tv = bg.tetv[k - 1];
+    load_pt(bg.xyz, tv.x, p0);
+    load_pt(bg.xyz, tv.y, p1);
+    load_pt(bg.xyz, tv.z, p2);
+    load_pt(bg.xyz, tv.w, p3);
+    tet_bary(x, p0, p1, p2, p3, phi);
+    const int v[4] = {tv.x, tv.y, tv.z, tv.w};
+    interp_vol_layout<C0, C1, C2, C3, C4, C5>(S, ip, v, phi);
+    if (elem_out) elem_out[ip - 1] = k;
+    if (hit_out) hit_out[ip - 1] = PMMG_HIT_VOL_WALK;
+  }
+}
+
+// walk + interpolation in one pass (default): the located tetra's vertex ids
+// and barycentric coordinates are still in registers for the row gathers
+template <int C0, int C1, int C2, int C3, int C4, int C5>
+__global__ __launch_bounds__(kBlock) void k_vol_fused(Bg bg, const Frame *fr, const unsigned long long *grid, int g,
+                                                      const double *qxyz, const int *order, Slots S, int *elem_out,
+                                                      int8_t *hit_out, int *fb, DevStats *st, int maxstep) {
   __shared__ BlockStats bs;
   bstats_init(&bs);
   __syncthreads();
-  const int nvol = st->nvol, nbdy = st->nbdy;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nbdy; i += gridDim.x * blockDim.x) {
-    const int ip = order[nvol + i];
-    double x[3];
-    x[0] = qxyz[3 * (size_t)(ip - 1)];
-    x[1] = qxyz[3 * (size_t)(ip - 1) + 1];
-    x[2] = qxyz[3 * (size_t)(ip - 1) + 2];
-    int k = grid_seed(sgrid, gs, fr->lo, fr->inv_srf, x);
-    int hist[kHist];
-#pragma unroll
-    for (int h = 0; h < kHist; h++) hist[h] = 0;
-    int steps = 0, hit = 0, edge = -1, vertex = -1;
-    TriGeom t;
-    double phi[3];
-    for (;;) {
-      ++steps;
-      tri_load(bg, k, t);
-      double b[3];
-      double dist = tri_bary(x, t.p, t.q, t.n, b);
-      int r[3];
-      ranks3(b, r);
-      double bmin = b[0];
-      bmin = b[1] < bmin ? b[1] : bmin;
-      bmin = b[2] < bmin ? b[2] : bmin;
-      phi[0] = b[0];
-      phi[1] = b[1];
-      phi[2] = b[2];
-      // PMMG_locatePointInTria: accept if inside and |dist| <= hausd
-      if (bmin > -kEps && !(fabs(dist) > bg.hausd)) {
-        // PMMG_barycoord_isBorder on the sorted coordinates
-        int f0 = r[0] == 0 ? 0 : (r[1] == 0 ? 1 : 2);
-        int f1 = r[0] == 1 ? 0 : (r[1] == 1 ? 1 : 2);
-        int f2 = r[0] == 2 ? 0 : (r[1] == 2 ? 1 : 2);
-        double b1 = f1 == 0 ? b[0] : (f1 == 1 ? b[1] : b[2]);
-        hit = PMMG_HIT_BDY_FACE;
-        if (bmin < kEps) {
-          if (b1 < kEps) { vertex = f2; hit = PMMG_HIT_BDY_VERTEX; }
-          else { edge = f0; hit = PMMG_HIT_BDY_EDGE; }
-        }
-        break;
+  const int nvol = st->nvol;
+  const int stride = gridDim.x * blockDim.x;
+  const int iters = (nvol + stride - 1) / stride;
+  for (int it = 0; it < iters; it++) {
+    const int i = it * stride + xcd_block() * blockDim.x + threadIdx.x;
+    const bool active = i < nvol;
+    int status = 0, steps = 0, k = 0, ip = 0;
+    if (active) {
+      ip = order[i];
+      double x[3], b[4];
+      load_pt(qxyz, ip, x);
+      int4 tv;
+      status = walk_vol(bg, grid, g, fr, x, maxstep, k, tv, b, steps);
+      if (status == 1) {
+        const int v[4] = {tv.x, tv.y, tv.z, tv.w};
+        interp_vol_layout<C0, C1, C2, C3, C4, C5>(S, ip, v, b);
+        if (elem_out) elem_out[ip - 1] = k;
+        if (hit_out) hit_out[ip - 1] = PMMG_HIT_VOL_WALK;
       }
-      const int *ad = bg.adjt + 3 * (size_t)(k - 1);
-      int next = 0;
-      bool done = false;
-      for (int j = 0; j < 3 && !done && next == 0; j++) {
-        int f = r[0] == j ? 0 : (r[1] == j ? 1 : 2);
-        int k1 = ad[f] / 3;
-        if (!k1) continue;
-        bool vis = false;
+    }
+    int slot = wave_append(&st->nfb_vol, active && status != 1);
+    if (active && status != 1) fb[slot] = ip;
+    wave_stats(&bs, active, status == 1 ? PMMG_HIT_VOL_WALK : 0, steps);
+  }
+  __syncthreads();
+  bstats_flush(&bs, st);
+}
+
+// ---------------------------------------------------------------- volume, tetra-centric scan
+
+// Volume queries counting-sorted into a uniform row-major grid of cells (the
+// sorted coordinates are stored contiguously per cell).
+__global__ __launch_bounds__(kBlock) void k_qcount(const double *xyz, const uint8_t *pclass, int np, const Frame *fr,
+                                                   int gq, int *cnt, int2 *binrank) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= np) return;
+  if (pclass[i] != PMMG_PT_VOL) {
+    binrank[i] = make_int2(-1, 0);
+    return;
+  }
+  int c[3];
+  for (int d = 0; d < 3; d++) c[d] = cell_coord(xyz[3 * (size_t)i + d], fr->lo[d], fr->inv_bin[d], gq);
+  int cell = c[0] + gq * (c[1] + gq * c[2]);
+  int r = atomicAdd(&cnt[cell], 1);
+  binrank[i] = make_int2(cell, r);
+}
+
+__global__ __launch_bounds__(kBlock) void k_qscatter(int np, const double *xyz, const int2 *binrank, const int *off,
+                                                     int *order, double *qs, int *res) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= np) return;
+  int2 br = binrank[i];
+  if (br.x < 0) return;
+  int pos = off[br.x] + br.y;
+  order[pos] = i + 1;
+  qs[3 * (size_t)pos] = xyz[3 * (size_t)i];
+  qs[3 * (size_t)pos + 1] = xyz[3 * (size_t)i + 1];
+  qs[3 * (size_t)pos + 2] = xyz[3 * (size_t)i + 2];
+  res[pos] = INT_MAX;
+}
+
+__global__ void k_qtotal(const int *off, int ncells, DevStats *st) { st->nvol = off[ncells]; }
+
+// One thread per background tetra (contiguous tetra ranges per XCD): the
+// tetra's bbox, inflated by the acceptance tolerance (an accepted point has
+// every barycentric coordinate > -EPS, hence lies within 3 EPS of the tetra's
+// extent of it), selects the query cells to test; an accepting tetra lowers
+// res[q] with atomicMin, so res ends as the lowest-index accepting tetra —
+// the reference's exhaustive-search result — for every query at once.
+__global__ __launch_bounds__(kBlock) void k_vol_scan(Bg bg, const Frame *fr, int gq, const int *off, const double *qs,
+                                                     int *res, DevStats *st) {
+  const int x8 = blockIdx.x & 7, bpx = gridDim.x >> 3, bi = blockIdx.x >> 3;
+  const long long lo_k = (long long)bg.ne * x8 / 8, hi_k = (long long)bg.ne * (x8 + 1) / 8;
+  unsigned long long tests = 0;
+  for (long long kk = lo_k + (long long)bi * blockDim.x + threadIdx.x; kk < hi_k; kk += (long long)bpx * blockDim.x) {
+    const int k = (int)kk + 1;
+    const int4 tv = bg.tetv[k - 1];
+    if (tv.x <= 0) continue;
+    double p0[3], p1[3], p2[3], p3[3];
+    load_pt(bg.xyz, tv.x, p0);
+    load_pt(bg.xyz, tv.y, p1);
+    load_pt(bg.xyz, tv.z, p2);
+    load_pt(bg.xyz, tv.w, p3);
+    double lo[3], hi[3];
+    int c0[3], c1[3];
 #pragma unroll
-        for (int h = 0; h < kHist; h++) vis = vis || (hist[h] == k1);
-        if (vis) {
-          double wphi[3] = {phi[0], phi[1], phi[2]};
-          int il = tri_wedge(bg.hausd, t, f, x, wphi);
-          if (il < 0) continue;
-          if (il == 4) {
-            phi[0] = wphi[0]; phi[1] = wphi[1]; phi[2] = wphi[2];
-            edge = f;
-            hit = PMMG_HIT_BDY_WEDGE;
-            done = true;
-          } else if (tri_cone(bg, k, il, t.v, x)) {
-            vertex = il;
-            hit = PMMG_HIT_BDY_CONE;
-            done = true;
+    for (int d = 0; d < 3; d++) {
+      lo[d] = fmin(fmin(p0[d], p1[d]), fmin(p2[d], p3[d]));
+      hi[d] = fmax(fmax(p0[d], p1[d]), fmax(p2[d], p3[d]));
+      double pad = 8.0 * kEps * (hi[d] - lo[d]) + 1e-300;
+      lo[d] -= pad;
+      hi[d] += pad;
+      c0[d] = cell_coord(lo[d], fr->lo[d], fr->inv_bin[d], gq);
+      c1[d] = cell_coord(hi[d], fr->lo[d], fr->inv_bin[d], gq);
+    }
+    for (int ck = c0[2]; ck <= c1[2]; ck++)
+      for (int cj = c0[1]; cj <= c1[1]; cj++) {
+        const int row = gq * (cj + gq * ck);
+        const int q0 = off[row + c0[0]], q1 = off[row + c1[0] + 1];
+        for (int q = q0; q < q1; q++) {
+          double x[3];
+          load_pt(qs, q + 1, x);
+          if (x[0] < lo[0] || x[0] > hi[0] || x[1] < lo[1] || x[1] > hi[1] || x[2] < lo[2] || x[2] > hi[2]) continue;
+          double b[4];
+          tet_bary(x, p0, p1, p2, p3, b);
+          tests++;
+          if (min4(b) > -kEps) atomicMin(&res[q], k);
+        }
+      }
+  }
+  for (int o = 32; o > 0; o >>= 1) tests += __shfl_down(tests, o);
+  if (__lane_id() == 0 && tests) atomicAdd(&st->steps, tests);
+}
+
+// interpolation of the scanned queries (sorted positions, coordinates read
+// back contiguously); queries with no accepting tetra go to the closest-tetra
+// fallback
+template <int C0, int C1, int C2, int C3, int C4, int C5>
+__global__ __launch_bounds__(kBlock) void k_vol_interp_scan(Bg bg, const double *qs, const int *order, const int *res,
+                                                            Slots S, int *elem_out, int8_t *hit_out, int *fb,
+                                                            DevStats *st) {
+  __shared__ unsigned int nloc;
+  if (threadIdx.x == 0) nloc = 0;
+  __syncthreads();
+  const int nvol = st->nvol;
+  const int stride = gridDim.x * blockDim.x;
+  const int iters = (nvol + stride - 1) / stride;
+  for (int it = 0; it < iters; it++) {
+    const int i = it * stride + xcd_block() * blockDim.x + threadIdx.x;
+    const bool active = i < nvol;
+    int k = INT_MAX, ip = 0;
+    if (active) {
+      k = res[i];
+      ip = order[i];
+      if (k != INT_MAX) {
+        double x[3], p0[3], p1[3], p2[3], p3[3], phi[4];
+        load_pt(qs, i + 1, x);
+        const int4 tv = bg.tetv[k - 1];
+        load_pt(bg.xyz, tv.x, p0);
+        load_pt(bg.xyz, tv.y, p1);
+        load_pt(bg.xyz, tv.z, p2);
+        load_pt(bg.xyz, tv.w, p3);
+        tet_bary(x, p0, p1, p2, p3, phi);
+        const int v[4] = {tv.x, tv.y, tv.z, tv.w};
+        interp_vol_layout<C0, C1, C2, C3, C4, C5>(S, ip, v, phi);
+        if (elem_out) elem_out[ip - 1] = k;
+        if (hit_out) hit_out[ip - 1] = PMMG_HIT_VOL_SCAN;
+      }
+    }
+    const bool miss = active && k == INT_MAX;
+    int slot = wave_append(&st->nfb_vol, miss);
+    if (miss) fb[slot] = ip;
+    unsigned long long okm = __ballot(active && k != INT_MAX);
+    if (__lane_id() == 0 && okm) atomicAdd(&nloc, (unsigned)__popcll(okm));
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && nloc) atomicAdd(&st->cnt[PMMG_HIT_VOL_SCAN], (unsigned long long)nloc);
+}
+
+// ---------------------------------------------------------------- surface
+
+__global__ __launch_bounds__(kBlock) void k_bdy(Bg bg, const Frame *fr, const int *sgrid, int gs, const double *qxyz,
+                                                const int *order, Slots S, int *elem_out, int8_t *hit_out, int *fb,
+                                                DevStats *st, int maxstep) {
+  __shared__ BlockStats bs;
+  bstats_init(&bs);
+  __syncthreads();
+  const XcdChunk ch = xcd_chunk(st->nbdy);
+  for (int it = 0; it < ch.iters; it++) {
+    const int i = (int)(ch.start + it * ch.stride);
+    const bool active = i < ch.hi;
+    int steps = 0, hit = 0, ip = 0;
+    if (active) {
+      ip = order[i];
+      double x[3];
+      load_pt(qxyz, ip, x);
+      int k = seed_srf(sgrid, gs, fr, x);
+      int hist[kHist];
+#pragma unroll
+      for (int h = 0; h < kHist; h++) hist[h] = 0;
+      int edge = -1, vertex = -1;
+      TriGeom t;
+      double phi[3];
+      for (;;) {
+        ++steps;
+        tri_load(bg, k, t);
+        double b[3];
+        double dist = tri_bary(x, t.p, t.q, t.n, b);
+        int r[3];
+        ranks3(b, r);
+        double bmin = b[0];
+        bmin = b[1] < bmin ? b[1] : bmin;
+        bmin = b[2] < bmin ? b[2] : bmin;
+        phi[0] = b[0];
+        phi[1] = b[1];
+        phi[2] = b[2];
+        // PMMG_locatePointInTria: inside and |dist| <= hausd
+        if (bmin > -kEps && !(fabs(dist) > bg.hausd)) {
+          // PMMG_barycoord_isBorder on the sorted coordinates
+          int f0 = r[0] == 0 ? 0 : (r[1] == 0 ? 1 : 2);
+          int f1 = r[0] == 1 ? 0 : (r[1] == 1 ? 1 : 2);
+          int f2 = r[0] == 2 ? 0 : (r[1] == 2 ? 1 : 2);
+          double b1 = sel3d(b[0], b[1], b[2], f1);
+          hit = PMMG_HIT_BDY_FACE;
+          if (bmin < kEps) {
+            if (b1 < kEps) { vertex = f2; hit = PMMG_HIT_BDY_VERTEX; }
+            else { edge = f0; hit = PMMG_HIT_BDY_EDGE; }
           }
-          continue;
+          break;
         }
-        next = k1;
-      }
-      if (done) break;
-      if (next == 0) { hit = 0; break; }          // stuck -> exhaustive
-      if (steps >= maxstep) { hit = 0; break; }
+        const int *ad = bg.adjt + 3 * (size_t)(k - 1);
+        const int a0 = ad[0], a1 = ad[1], a2 = ad[2];
+        int next = 0;
+        bool done = false;
+        for (int j = 0; j < 3 && !done && next == 0; j++) {
+          int f = r[0] == j ? 0 : (r[1] == j ? 1 : 2);
+          int k1 = sel3i(a0, a1, a2, f) / 3;
+          if (!k1) continue;
+          bool vis = false;
 #pragma unroll
-      for (int h = kHist - 1; h > 0; h--) hist[h] = hist[h - 1];
-      hist[0] = k;
-      k = next;
+          for (int h = 0; h < kHist; h++) vis = vis || (hist[h] == k1);
+          if (vis) {
+            double w[3];
+            int il = tri_wedge(bg.hausd, t, f, x, w);
+            if (il < 0) continue;
+            if (il == 4) {
+              phi[0] = w[0]; phi[1] = w[1]; phi[2] = w[2];
+              edge = f;
+              hit = PMMG_HIT_BDY_WEDGE;
+              done = true;
+            } else if (tri_cone(bg, k, il, t, x)) {
+              vertex = il;
+              hit = PMMG_HIT_BDY_CONE;
+              done = true;
+            }
+            continue;
+          }
+          next = k1;
+        }
+        if (done) break;
+        if (next == 0 || steps >= maxstep) { hit = 0; break; } // -> exhaustive
+#pragma unroll
+        for (int h = kHist - 1; h > 0; h--) hist[h] = hist[h - 1];
+        hist[0] = k;
+        k = next;
+      }
+      if (hit) {
+        interp_bdy(S, ip, t.v, phi, edge, vertex);
+        if (elem_out) elem_out[ip - 1] = k;
+        if (hit_out) hit_out[ip - 1] = (int8_t)(hit | ((vertex >= 0 ? vertex : (edge >= 0 ? edge : 0)) << 4));
+      }
     }
-    if (hit) {
-      interp_bdy(S, ip, t.v, phi, edge, vertex);
-      if (elem_out) elem_out[ip - 1] = k;
-      if (hit_out) hit_out[ip - 1] = (int8_t)(hit | ((vertex >= 0 ? vertex : (edge >= 0 ? edge : 0)) << 4));
-      atomicAdd(&bs.cnt[hit], 1u);
-    }
-    int slot = wave_append(&st->nfb_bdy, hit == 0);
-    if (hit == 0) fb_list[slot] = ip;
-    atomicAdd(&bs.steps, (unsigned long long)steps);
-    atomicMax(&bs.stepmax, (unsigned)steps);
+    int slot = wave_append(&st->nfb_bdy, active && hit == 0);
+    if (active && hit == 0) fb[slot] = ip;
+    wave_stats(&bs, active, hit, steps);
   }
   __syncthreads();
   bstats_flush(&bs, st);
@@ -815,9 +732,9 @@ __global__ __launch_bounds__(kBlock) void k_bdy(Bg bg, const Frame *fr, const in
 
 // ---------------------------------------------------------------- exhaustive fallbacks (exact reference semantics)
 
-constexpr int kQB = 128; // queries staged in LDS per pass
+constexpr int kQB = 128; // fallback queries staged in LDS per pass
 
-// pass A (locate_pmmg.c:743-762): lowest-index tetra accepting each fallback query
+// lowest-index tetra accepting each fallback query (locate_pmmg.c:743-762)
 __global__ __launch_bounds__(kBlock) void k_vol_exhaust_accept(Bg bg, const double *qxyz, const int *fb,
                                                                const DevStats *st, int *best) {
   __shared__ double sx[kQB][3];
@@ -825,33 +742,28 @@ __global__ __launch_bounds__(kBlock) void k_vol_exhaust_accept(Bg bg, const doub
   for (int q0 = 0; q0 < nfb; q0 += kQB) {
     int nq = min(kQB, nfb - q0);
     __syncthreads();
-    for (int j = threadIdx.x; j < nq; j += blockDim.x) {
-      int ip = fb[q0 + j];
-      sx[j][0] = qxyz[3 * (size_t)(ip - 1)];
-      sx[j][1] = qxyz[3 * (size_t)(ip - 1) + 1];
-      sx[j][2] = qxyz[3 * (size_t)(ip - 1) + 2];
-    }
+    for (int j = threadIdx.x; j < nq; j += blockDim.x) load_pt(qxyz, fb[q0 + j], sx[j]);
     __syncthreads();
     for (int k = 1 + blockIdx.x * blockDim.x + threadIdx.x; k <= bg.ne; k += gridDim.x * blockDim.x) {
       int4 tv = bg.tetv[k - 1];
       if (tv.x <= 0) continue;
       double p0[3], p1[3], p2[3], p3[3];
-      load_pt(bg, tv.x, p0);
-      load_pt(bg, tv.y, p1);
-      load_pt(bg, tv.z, p2);
-      load_pt(bg, tv.w, p3);
+      load_pt(bg.xyz, tv.x, p0);
+      load_pt(bg.xyz, tv.y, p1);
+      load_pt(bg.xyz, tv.z, p2);
+      load_pt(bg.xyz, tv.w, p3);
       double lo[3], hi[3];
       for (int d = 0; d < 3; d++) {
         lo[d] = fmin(fmin(p0[d], p1[d]), fmin(p2[d], p3[d]));
         hi[d] = fmax(fmax(p0[d], p1[d]), fmax(p2[d], p3[d]));
+        // an accepted point has every barycentric coordinate > -EPS, so it
+        // lies inside the tetra's bbox inflated by 3 EPS of its extent
         double pad = 8.0 * kEps * (hi[d] - lo[d]) + 1e-300;
         lo[d] -= pad;
         hi[d] += pad;
       }
       for (int j = 0; j < nq; j++) {
         const double *x = sx[j];
-        // conservative reject: an accepted point has all bary > -EPS, i.e. lies
-        // in the tetra inflated by a few EPS of its extent
         if (x[0] < lo[0] || x[0] > hi[0] || x[1] < lo[1] || x[1] > hi[1] || x[2] < lo[2] || x[2] > hi[2]) continue;
         if (best[q0 + j] <= k) continue;
         double b[4];
@@ -862,58 +774,44 @@ __global__ __launch_bounds__(kBlock) void k_vol_exhaust_accept(Bg bg, const doub
   }
 }
 
-// closest tetra for queries nobody accepted: argmin |bary_min| * vol (locate_pmmg.c:453-458)
+// closest tetra of queries nobody accepts: argmin |bary_min| * vol
+// (locate_pmmg.c:453-458); pass 0 finds the minimum value, pass 1 the lowest
+// index reaching it
 __global__ __launch_bounds__(kBlock) void k_vol_exhaust_closest(Bg bg, const double *qxyz, const int *fb,
                                                                 const DevStats *st, const int *best,
                                                                 unsigned long long *ckey, int pass, int *cidx) {
   __shared__ double sx[kQB][3];
+  __shared__ int sneed[kQB];
   const int nfb = st->nfb_vol;
   for (int q0 = 0; q0 < nfb; q0 += kQB) {
     int nq = min(kQB, nfb - q0);
     __syncthreads();
     for (int j = threadIdx.x; j < nq; j += blockDim.x) {
-      int ip = fb[q0 + j];
-      sx[j][0] = qxyz[3 * (size_t)(ip - 1)];
-      sx[j][1] = qxyz[3 * (size_t)(ip - 1) + 1];
-      sx[j][2] = qxyz[3 * (size_t)(ip - 1) + 2];
+      load_pt(qxyz, fb[q0 + j], sx[j]);
+      sneed[j] = best[q0 + j] == INT_MAX;
     }
     __syncthreads();
     bool any = false;
-    for (int j = 0; j < nq; j++) any = any || (best[q0 + j] == INT_MAX);
+    for (int j = 0; j < nq; j++) any = any || sneed[j];
     if (!any) continue;
     for (int k = 1 + blockIdx.x * blockDim.x + threadIdx.x; k <= bg.ne; k += gridDim.x * blockDim.x) {
       int4 tv = bg.tetv[k - 1];
       if (tv.x <= 0) continue;
       double p0[3], p1[3], p2[3], p3[3];
-      load_pt(bg, tv.x, p0);
-      load_pt(bg, tv.y, p1);
-      load_pt(bg, tv.z, p2);
-      load_pt(bg, tv.w, p3);
+      load_pt(bg.xyz, tv.x, p0);
+      load_pt(bg.xyz, tv.y, p1);
+      load_pt(bg.xyz, tv.z, p2);
+      load_pt(bg.xyz, tv.w, p3);
       for (int j = 0; j < nq; j++) {
-        if (best[q0 + j] != INT_MAX) continue;
+        if (!sneed[j]) continue;
         double b[4];
         double vol = tet_bary(sx[j], p0, p1, p2, p3, b);
-        double val = fabs(min4(b)) * vol;
-        unsigned long long key = dkey(val);
+        unsigned long long key = dkey(fabs(min4(b)) * vol);
         if (pass == 0) atomicMin(&ckey[q0 + j], key);
         else if (key == ckey[q0 + j]) atomicMin(&cidx[q0 + j], k);
       }
     }
   }
-}
-
-// PMMG_barycoord3d_getClosest: unit coordinate at the nearest vertex
-__device__ __forceinline__ void closest_vertex(const double *x, const double (*p)[3], int nv, double *phi) {
-  double d[3];
-  for (int i = 0; i < 3; i++) d[i] = x[i] - p[0][i];
-  double mn = sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
-  int it = 0;
-  for (int j = 1; j < nv; j++) {
-    for (int i = 0; i < 3; i++) d[i] = x[i] - p[j][i];
-    double nrm = sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
-    if (nrm < mn) { mn = nrm; it = j; }
-  }
-  for (int j = 0; j < nv; j++) phi[j] = (j == it) ? 1.0 : 0.0;
 }
 
 __global__ __launch_bounds__(kBlock) void k_vol_finish(Bg bg, const double *qxyz, const int *fb, DevStats *st,
@@ -922,28 +820,30 @@ __global__ __launch_bounds__(kBlock) void k_vol_finish(Bg bg, const double *qxyz
   const int nfb = st->nfb_vol;
   for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nfb; j += gridDim.x * blockDim.x) {
     int ip = fb[j];
-    double x[3] = {qxyz[3 * (size_t)(ip - 1)], qxyz[3 * (size_t)(ip - 1) + 1], qxyz[3 * (size_t)(ip - 1) + 2]};
+    double x[3];
+    load_pt(qxyz, ip, x);
     int hit, k;
     if (best[j] != INT_MAX) { k = best[j]; hit = PMMG_HIT_VOL_EXHAUST; }
     else { k = cidx[j]; hit = PMMG_HIT_VOL_CLOSEST; }
     if (k == INT_MAX || k <= 0) continue;
     int4 tv = bg.tetv[k - 1];
     double p[4][3], phi[4];
-    load_pt(bg, tv.x, p[0]);
-    load_pt(bg, tv.y, p[1]);
-    load_pt(bg, tv.z, p[2]);
-    load_pt(bg, tv.w, p[3]);
+    load_pt(bg.xyz, tv.x, p[0]);
+    load_pt(bg.xyz, tv.y, p[1]);
+    load_pt(bg.xyz, tv.z, p[2]);
+    load_pt(bg.xyz, tv.w, p[3]);
     if (hit == PMMG_HIT_VOL_EXHAUST) tet_bary(x, p[0], p[1], p[2], p[3], phi);
-    else closest_vertex(x, p, 4, phi);
-    int v[4] = {tv.x, tv.y, tv.z, tv.w};
-    interp_vol(S, ip, v, phi);
+    else closest_vertex<4>(x, p, phi);
+    const int v[4] = {tv.x, tv.y, tv.z, tv.w};
+    for (int s = 0; s < S.n; s++) interp_dyn<4>(S.s[s], ip, v, phi);
     if (elem_out) elem_out[ip - 1] = k;
     if (hit_out) hit_out[ip - 1] = (int8_t)hit;
     atomicAdd(&st->cnt[hit], 1ULL);
   }
 }
 
-// surface pass A (locate_pmmg.c:483-503): lowest-index accepting tria
+// surface: pass 0 lowest-index accepting tria (locate_pmmg.c:483-503), pass 1
+// minimum centroid distance, pass 2 lowest index reaching it (:400-416)
 __global__ __launch_bounds__(kBlock) void k_bdy_exhaust(Bg bg, const double *qxyz, const int *fb, const DevStats *st,
                                                         int *best, unsigned long long *ckey, int pass, int *cidx) {
   __shared__ double sx[kQB][3];
@@ -951,12 +851,7 @@ __global__ __launch_bounds__(kBlock) void k_bdy_exhaust(Bg bg, const double *qxy
   for (int q0 = 0; q0 < nfb; q0 += kQB) {
     int nq = min(kQB, nfb - q0);
     __syncthreads();
-    for (int j = threadIdx.x; j < nq; j += blockDim.x) {
-      int ip = fb[q0 + j];
-      sx[j][0] = qxyz[3 * (size_t)(ip - 1)];
-      sx[j][1] = qxyz[3 * (size_t)(ip - 1) + 1];
-      sx[j][2] = qxyz[3 * (size_t)(ip - 1) + 2];
-    }
+    for (int j = threadIdx.x; j < nq; j += blockDim.x) load_pt(qxyz, fb[q0 + j], sx[j]);
     __syncthreads();
     for (int k = 1 + blockIdx.x * blockDim.x + threadIdx.x; k <= bg.nt; k += gridDim.x * blockDim.x) {
       if (bg.triv[3 * (size_t)(k - 1)] <= 0) continue;
@@ -972,12 +867,11 @@ __global__ __launch_bounds__(kBlock) void k_bdy_exhaust(Bg bg, const double *qxy
           if (bmin > -kEps && !(fabs(dist) > bg.hausd)) atomicMin(&best[q0 + j], k);
         } else {
           if (best[q0 + j] != INT_MAX) continue;
-          // centroid distance (locate_pmmg.c:400-416)
           double d[3] = {x[0], x[1], x[2]};
           for (int v = 0; v < 3; v++)
-            for (int i = 0; i < 3; i++) d[i] -= t.p[v][i] / 3.0;
+            for (int c = 0; c < 3; c++) d[c] -= t.p[v][c] / 3.0;
           double nrm = 0;
-          for (int i = 0; i < 3; i++) nrm += d[i] * d[i];
+          for (int c = 0; c < 3; c++) nrm += d[c] * d[c];
           nrm = sqrt(nrm);
           unsigned long long key = dkey(nrm);
           if (pass == 1) atomicMin(&ckey[q0 + j], key);
@@ -994,7 +888,8 @@ __global__ __launch_bounds__(kBlock) void k_bdy_finish(Bg bg, const double *qxyz
   const int nfb = st->nfb_bdy;
   for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nfb; j += gridDim.x * blockDim.x) {
     int ip = fb[j];
-    double x[3] = {qxyz[3 * (size_t)(ip - 1)], qxyz[3 * (size_t)(ip - 1) + 1], qxyz[3 * (size_t)(ip - 1) + 2]};
+    double x[3];
+    load_pt(qxyz, ip, x);
     int hit, k;
     double phi[3];
     TriGeom t;
@@ -1008,24 +903,18 @@ __global__ __launch_bounds__(kBlock) void k_bdy_finish(Bg bg, const double *qxyz
       if (k == INT_MAX || k <= 0) continue;
       tri_load(bg, k, t);
       // stale re-evaluation (locate_pmmg.c:505-509): vertices and area of the
-      // last tria, normal of the closest one
+      // last tria scanned (nt), normal of the closest one
       TriGeom ts;
       tri_load(bg, bg.nt, ts);
       double b[3];
-      double dist = 0.0;
-      {
-        double dd = 0.0;
-        for (int i = 0; i < 3; i++) dd += (x[i] - ts.p[0][i]) * t.n[i];
-        dist = dd;
-      }
-      tri_bary(x, ts.p, ts.q, t.n, b);
+      double dist = tri_bary(x, ts.p, ts.q, t.n, b);
       double bmin = fmin(b[0], fmin(b[1], b[2]));
       if (bmin > -kEps && !(fabs(dist) > bg.hausd)) {
         hit = PMMG_HIT_BDY_STALE;
         phi[0] = b[0]; phi[1] = b[1]; phi[2] = b[2];
       } else {
         hit = PMMG_HIT_BDY_CLOSEST;
-        closest_vertex(x, t.p, 3, phi);
+        closest_vertex<3>(x, t.p, phi);
       }
     }
     interp_bdy(S, ip, t.v, phi, -1, -1);
@@ -1035,11 +924,55 @@ __global__ __launch_bounds__(kBlock) void k_bdy_finish(Bg bg, const double *qxyz
   }
 }
 
-__global__ void k_fill_int(int *p, int n, int v) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = v;
+__global__ void k_fallback_init(int *a, int *b, unsigned long long *c, const int *count) {
+  const int n = *count;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    a[i] = INT_MAX;
+    b[i] = INT_MAX;
+    c[i] = ~0ULL;
+  }
 }
-__global__ void k_fill_u64(unsigned long long *p, int n, unsigned long long v) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = v;
+
+// ---------------------------------------------------------------- layout dispatch
+
+typedef void (*VolInterpFn)(Bg, const double *, const int *, const int *, Slots, int *, int8_t *, const DevStats *);
+typedef void (*ScanInterpFn)(Bg, const double *, const int *, const int *, Slots, int *, int8_t *, int *, DevStats *);
+typedef void (*FusedFn)(Bg, const Frame *, const unsigned long long *, int, const double *, const int *, Slots, int *,
+                        int8_t *, int *, DevStats *, int);
+
+struct LayoutEntry {
+  int c[6];
+  VolInterpFn fn;
+  ScanInterpFn sfn;
+  FusedFn ffn;
+};
+
+#define PMMG_LAYOUT(a, b, c, d, e, f)                                                                             \
+  {{a, b, c, d, e, f}, k_vol_interp<a, b, c, d, e, f>, k_vol_interp_scan<a, b, c, d, e, f>,                    \
+   k_vol_fused<a, b, c, d, e, f>}
+// common slot layouts (metric first): aniso metric + scalar/vector/tensor
+// (BASELINE cfg3/cfg4, libexamples cube-solphys.sol), iso metric + scalars
+// (cfg2, cfg5), metric only
+const LayoutEntry kLayouts[] = {
+    PMMG_LAYOUT(6, 1, 3, 6, 0, 0), PMMG_LAYOUT(6, 1, 3, 6, 1, 0), PMMG_LAYOUT(1, 1, 0, 0, 0, 0),
+    PMMG_LAYOUT(1, 1, 1, 1, 1, 1), PMMG_LAYOUT(1, 1, 1, 0, 0, 0), PMMG_LAYOUT(6, 0, 0, 0, 0, 0),
+    PMMG_LAYOUT(1, 0, 0, 0, 0, 0), PMMG_LAYOUT(6, 1, 0, 0, 0, 0), PMMG_LAYOUT(1, 1, 3, 6, 0, 0),
+};
+#undef PMMG_LAYOUT
+
+const LayoutEntry kGeneric = {{-1, 0, 0, 0, 0, 0}, k_vol_interp<-1, 0, 0, 0, 0, 0>,
+                               k_vol_interp_scan<-1, 0, 0, 0, 0, 0>, k_vol_fused<-1, 0, 0, 0, 0, 0>};
+
+const LayoutEntry &pick_layout(const Slots &S) {
+  for (const LayoutEntry &e : kLayouts) {
+    int n = 0;
+    while (n < 6 && e.c[n] > 0) n++;
+    if (n != S.n) continue;
+    bool ok = true;
+    for (int j = 0; j < n; j++) ok = ok && (S.s[j].code == e.c[j]);
+    if (ok) return e;
+  }
+  return kGeneric;
 }
 
 } // namespace
@@ -1066,15 +999,20 @@ struct pmmg_hip_ctx {
   DevBuf o_xyz, o_tetv, o_adja, o_triv, o_adjt, o_met;
   std::vector<DevBuf> o_f;
   // work buffers
-  DevBuf frame, stats, grid, sgrid, keys_in, keys_out, vals_in, vals_out, sort_tmp;
+  DevBuf frame, stats, grid, sgrid, cnt, off, binrank, order_v, order_b, vloc, scan_tmp, qs;
   DevBuf fb_vol, fb_bdy, best, ckey, cidx, bbest, bckey, bcidx;
   // host-mode staging
   DevBuf h_xyz, h_cls, h_met, h_elem, h_hit;
   std::vector<DevBuf> h_f;
   hipEvent_t ev[8] = {};
   bool pending = false;
-  int tpc = 64;
+  int tpc = 16;     // background tetra per volume seed cell
+  int spc = 1;      // sampled tetra per seed cell
+  int qpb = 8;      // queries per Morton bin (walk path)
+  int qpc = 1;      // queries per scan cell (scan path)
   int maxstep = 1 << 16;
+  int last_sorted = 0;
+  int *h_small = nullptr; // pinned host words for the two small read-backs
 };
 
 static void set_err(pmmg_hip_ctx *c, const char *fmt, ...) {
@@ -1086,13 +1024,13 @@ static void set_err(pmmg_hip_ctx *c, const char *fmt, ...) {
   fprintf(stderr, "[parmmg_hip] %s\n", c->err);
 }
 
-#define HIPCK(ctx, expr)                                                                  \
-  do {                                                                                    \
-    hipError_t e_ = (expr);                                                               \
-    if (e_ != hipSuccess) {                                                               \
-      set_err((ctx), "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
-      return 0;                                                                           \
-    }                                                                                     \
+#define HIPCK(ctx, expr)                                                                             \
+  do {                                                                                               \
+    hipError_t e_ = (expr);                                                                          \
+    if (e_ != hipSuccess) {                                                                          \
+      set_err((ctx), "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__);   \
+      return 0;                                                                                      \
+    }                                                                                                \
   } while (0)
 
 static int ensure(pmmg_hip_ctx *c, DevBuf &b, size_t bytes) {
@@ -1120,6 +1058,12 @@ static int upload(pmmg_hip_ctx *c, DevBuf &b, const void *src, size_t bytes) {
   return 1;
 }
 
+static int env_int(const char *name, int def) {
+  const char *e = getenv(name);
+  if (e && atoi(e) > 0) return atoi(e);
+  return def;
+}
+
 extern "C" {
 
 int pmmg_hip_device_count(void) {
@@ -1143,10 +1087,16 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
     return nullptr;
   }
   for (int i = 0; i < 8; i++) (void)hipEventCreate(&c->ev[i]);
-  const char *e = getenv("PMMG_HIP_TPC");
-  if (e && atoi(e) > 0) c->tpc = atoi(e);
-  e = getenv("PMMG_HIP_MAXSTEP");
-  if (e && atoi(e) > 0) c->maxstep = atoi(e);
+  if (hipHostMalloc((void **)&c->h_small, 64, hipHostMallocDefault) != hipSuccess) {
+    fprintf(stderr, "[parmmg_hip] cannot allocate pinned host memory\n");
+    delete c;
+    return nullptr;
+  }
+  c->tpc = env_int("PMMG_HIP_TPC", c->tpc);
+  c->spc = env_int("PMMG_HIP_SPC", c->spc);
+  c->qpb = env_int("PMMG_HIP_QPB", c->qpb);
+  c->qpc = env_int("PMMG_HIP_QPC", c->qpc);
+  c->maxstep = env_int("PMMG_HIP_MAXSTEP", c->maxstep);
   return c;
 }
 
@@ -1155,15 +1105,16 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   DevBuf *bufs[] = {&c->o_xyz, &c->o_tetv, &c->o_adja, &c->o_triv, &c->o_adjt, &c->o_met, &c->frame, &c->stats,
-                    &c->grid, &c->sgrid, &c->keys_in, &c->keys_out, &c->vals_in, &c->vals_out, &c->sort_tmp,
-                    &c->fb_vol, &c->fb_bdy, &c->best, &c->ckey, &c->cidx, &c->bbest, &c->bckey, &c->bcidx,
-                    &c->h_xyz, &c->h_cls, &c->h_met, &c->h_elem, &c->h_hit};
+                    &c->grid, &c->sgrid, &c->cnt, &c->off, &c->binrank, &c->order_v, &c->order_b, &c->vloc, &c->qs,
+                    &c->scan_tmp, &c->fb_vol, &c->fb_bdy, &c->best, &c->ckey, &c->cidx, &c->bbest, &c->bckey,
+                    &c->bcidx, &c->h_xyz, &c->h_cls, &c->h_met, &c->h_elem, &c->h_hit};
   for (DevBuf *b : bufs) release(*b);
   for (auto &b : c->o_f) release(b);
   for (auto &b : c->h_f) release(b);
   for (int i = 0; i < 8; i++)
     if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->h_small) (void)hipHostFree(c->h_small);
   delete c;
 }
 
@@ -1186,15 +1137,15 @@ int pmmg_hip_set_background(pmmg_hip_ctx *c, int np, const double *xyz, int ne, 
   c->bg.nt = nt;
   c->bg.hausd = hausd;
   if (where == PMMG_HIP_DEVICE) {
+    if (((uintptr_t)tetv & 15) || ((uintptr_t)adja & 15)) {
+      set_err(c, "set_background: device tetv/adja must be 16-byte aligned");
+      return 0;
+    }
     c->bg.xyz = xyz;
     c->bg.tetv = reinterpret_cast<const int4 *>(tetv);
     c->bg.adja = reinterpret_cast<const int4 *>(adja);
     c->bg.triv = triv;
     c->bg.adjt = adjt;
-    if (((uintptr_t)tetv & 15) || ((uintptr_t)adja & 15)) {
-      set_err(c, "set_background: device tetv/adja must be 16-byte aligned");
-      return 0;
-    }
     return 1;
   }
   if (!upload(c, c->o_xyz, xyz, sizeof(double) * 3 * (size_t)np)) return 0;
@@ -1227,20 +1178,22 @@ int pmmg_hip_set_solutions(pmmg_hip_ctx *c, int met_size, const double *met, int
     set_err(c, "set_solutions: metric pointer is NULL");
     return 0;
   }
-  for (int j = 0; j < nfield; j++)
-    if (!fields || !fields[j] || field_size[j] < 1 || field_size[j] > 64) {
-      set_err(c, "set_solutions: invalid field %d", j);
+  for (int j = 0; j < nfield; j++) {
+    // MMG5_Scalar / MMG5_Vector / MMG5_Tensor are the only solution types at vertices
+    if (!fields || !fields[j] || !(field_size[j] == 1 || field_size[j] == 3 || field_size[j] == 6)) {
+      set_err(c, "set_solutions: field %d has size %d (expected 1, 3 or 6)", j, field_size ? field_size[j] : -1);
       return 0;
     }
-  c->met_size = met_size;
-  c->nfield = nfield;
-  c->fsize.assign(field_size, field_size + nfield);
-  c->fin.resize(nfield);
+  }
   size_t np = (size_t)c->bg.np;
   if (np == 0) {
     set_err(c, "set_solutions: call pmmg_hip_set_background first");
     return 0;
   }
+  c->met_size = met_size;
+  c->nfield = nfield;
+  c->fsize.assign(field_size, field_size + nfield);
+  c->fin.resize(nfield);
   if (where == PMMG_HIP_DEVICE) {
     c->met = met;
     for (int j = 0; j < nfield; j++) c->fin[j] = fields[j];
@@ -1274,6 +1227,108 @@ static int blocks_for(long long n, int cap) {
   return (int)b;
 }
 
+// fallbacks are rare: read the two counts back and launch only what is needed
+static int launch_fallbacks(pmmg_hip_ctx *c, const Slots &S, const double *xyz_new, int *elem_out, int8_t *hit_out) {
+  const Bg &bg = c->bg;
+  hipStream_t s = c->stream;
+  DevStats *st = (DevStats *)c->stats.p;
+  HIPCK(c, hipMemcpyAsync(c->h_small, &st->nfb_vol, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+  HIPCK(c, hipStreamSynchronize(s));
+  const int nfb_vol = c->h_small[0], nfb_bdy = c->h_small[1];
+  const int fgrid = 1024;
+  if (nfb_vol > 0) {
+    hipLaunchKernelGGL(k_fallback_init, dim3(64), dim3(kBlock), 0, s, (int *)c->best.p, (int *)c->cidx.p,
+                       (unsigned long long *)c->ckey.p, (const int *)&st->nfb_vol);
+    hipLaunchKernelGGL(k_vol_exhaust_accept, dim3(fgrid), dim3(kBlock), 0, s, bg, xyz_new, (const int *)c->fb_vol.p,
+                       st, (int *)c->best.p);
+    for (int pass = 0; pass < 2; pass++)
+      hipLaunchKernelGGL(k_vol_exhaust_closest, dim3(fgrid), dim3(kBlock), 0, s, bg, xyz_new,
+                         (const int *)c->fb_vol.p, st, (const int *)c->best.p, (unsigned long long *)c->ckey.p, pass,
+                         (int *)c->cidx.p);
+    hipLaunchKernelGGL(k_vol_finish, dim3(64), dim3(kBlock), 0, s, bg, xyz_new, (const int *)c->fb_vol.p, st,
+                       (const int *)c->best.p, (const int *)c->cidx.p, S, elem_out, hit_out);
+  }
+  if (bg.nt > 0 && nfb_bdy > 0) {
+    hipLaunchKernelGGL(k_fallback_init, dim3(64), dim3(kBlock), 0, s, (int *)c->bbest.p, (int *)c->bcidx.p,
+                       (unsigned long long *)c->bckey.p, (const int *)&st->nfb_bdy);
+    for (int pass = 0; pass < 3; pass++)
+      hipLaunchKernelGGL(k_bdy_exhaust, dim3(256), dim3(kBlock), 0, s, bg, xyz_new, (const int *)c->fb_bdy.p, st,
+                         (int *)c->bbest.p, (unsigned long long *)c->bckey.p, pass, (int *)c->bcidx.p);
+    hipLaunchKernelGGL(k_bdy_finish, dim3(64), dim3(kBlock), 0, s, bg, xyz_new, (const int *)c->fb_bdy.p, st,
+                       (const int *)c->bbest.p, (const int *)c->bcidx.p, S, elem_out, hit_out);
+  }
+  HIPCK(c, hipGetLastError());
+  return 1;
+}
+
+// default volume path: counting-sort the volume queries into a uniform grid,
+// one tetra-centric scan, interpolation in cell order
+static int run_scan(pmmg_hip_ctx *c, const Slots &S, int np_new, const double *xyz_new, const uint8_t *pclass,
+                    int *elem_out, int8_t *hit_out, int gs) {
+  const Bg &bg = c->bg;
+  hipStream_t s = c->stream;
+  const size_t nq = (size_t)np_new;
+  const int gq = grid_dim(np_new, c->qpc, 1024);
+  const long long ncells = (long long)gq * gq * gq;
+  if (!ensure(c, c->cnt, 4 * (size_t)(ncells + 1)) || !ensure(c, c->off, 4 * (size_t)(ncells + 1)) ||
+      !ensure(c, c->binrank, 8 * nq) || !ensure(c, c->qs, 24 * nq))
+    return 0;
+  Frame *fr = (Frame *)c->frame.p;
+  DevStats *st = (DevStats *)c->stats.p;
+  int *sgrid = (int *)c->sgrid.p;
+  int *order_v = (int *)c->order_v.p, *order_b = (int *)c->order_b.p;
+  int *res = (int *)c->vloc.p;
+  c->last_sorted = 1;
+
+  HIPCK(c, hipEventRecord(c->ev[0], s));
+  const long long nsg = bg.nt > 0 ? (long long)gs * gs * gs : 0;
+  hipLaunchKernelGGL(k_reset, dim3(blocks_for(ncells + 1 > nsg ? ncells + 1 : nsg, 2048)), dim3(kBlock), 0, s, fr, st,
+                     (unsigned long long *)nullptr, 0LL, sgrid, nsg, (int *)c->cnt.p, ncells + 1, 0);
+  hipLaunchKernelGGL(k_bbox, dim3(blocks_for(bg.np, 1024)), dim3(kBlock), 0, s, bg.xyz, bg.np, fr);
+  hipLaunchKernelGGL(k_frame_final, dim3(1), dim3(1), 0, s, fr, 1, gs, gq);
+  if (bg.nt > 0) hipLaunchKernelGGL(k_seed_srf, dim3(blocks_for(bg.nt, 4096)), dim3(kBlock), 0, s, bg, fr, sgrid, gs);
+  HIPCK(c, hipGetLastError());
+  HIPCK(c, hipEventRecord(c->ev[1], s));
+
+  size_t tb = 0;
+  HIPCK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (int *)c->cnt.p, (int *)c->off.p, (int)(ncells + 1), s));
+  size_t tb2 = 0;
+  hipcub::CountingInputIterator<int> ids(1);
+  HIPCK(c, hipcub::DeviceSelect::If(nullptr, tb2, ids, order_b, &st->nbdy, (int64_t)np_new,
+                                    IsClass{pclass, PMMG_PT_BDY}, s));
+  if (!ensure(c, c->scan_tmp, tb > tb2 ? tb : tb2)) return 0;
+  hipLaunchKernelGGL(k_qcount, dim3(blocks_for(np_new, 1 << 30)), dim3(kBlock), 0, s, xyz_new, pclass, np_new, fr, gq,
+                     (int *)c->cnt.p, (int2 *)c->binrank.p);
+  HIPCK(c, hipcub::DeviceScan::ExclusiveSum(c->scan_tmp.p, tb, (int *)c->cnt.p, (int *)c->off.p, (int)(ncells + 1), s));
+  hipLaunchKernelGGL(k_qscatter, dim3(blocks_for(np_new, 1 << 30)), dim3(kBlock), 0, s, np_new, xyz_new,
+                     (const int2 *)c->binrank.p, (const int *)c->off.p, order_v, (double *)c->qs.p, res);
+  hipLaunchKernelGGL(k_qtotal, dim3(1), dim3(1), 0, s, (const int *)c->off.p, (int)ncells, st);
+  if (bg.nt > 0)
+    HIPCK(c, hipcub::DeviceSelect::If(c->scan_tmp.p, tb2, ids, order_b, &st->nbdy, (int64_t)np_new,
+                                      IsClass{pclass, PMMG_PT_BDY}, s));
+  HIPCK(c, hipGetLastError());
+  HIPCK(c, hipEventRecord(c->ev[2], s));
+
+  hipLaunchKernelGGL(k_vol_scan, dim3(8 * blocks_for((bg.ne + 7) / 8, 1 << 20)), dim3(kBlock), 0, s, bg, fr, gq,
+                     (const int *)c->off.p, (const double *)c->qs.p, res, st);
+  HIPCK(c, hipEventRecord(c->ev[6], s));
+  ScanInterpFn interp = pick_layout(S).sfn;
+  hipLaunchKernelGGL(interp, dim3(blocks_for(np_new, 1 << 30)), dim3(kBlock), 0, s, bg, (const double *)c->qs.p,
+                     (const int *)order_v, (const int *)res, S, elem_out, hit_out, (int *)c->fb_vol.p, st);
+  HIPCK(c, hipGetLastError());
+  HIPCK(c, hipEventRecord(c->ev[3], s));
+  if (bg.nt > 0) {
+    hipLaunchKernelGGL(k_bdy, dim3(8 * blocks_for((np_new + 7) / 8, 256)), dim3(kBlock), 0, s, bg, fr, sgrid, gs,
+                       xyz_new, order_b, S, elem_out, hit_out, (int *)c->fb_bdy.p, st, c->maxstep);
+    HIPCK(c, hipGetLastError());
+  }
+  HIPCK(c, hipEventRecord(c->ev[4], s));
+  if (!launch_fallbacks(c, S, xyz_new, elem_out, hit_out)) return 0;
+  HIPCK(c, hipEventRecord(c->ev[5], s));
+  c->pending = true;
+  return 1;
+}
+
 // core pipeline on device pointers; all launches on c->stream
 static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const uint8_t *pclass, double *met_out,
                       double *const *fields_out, int *elem_out, int8_t *hit_out) {
@@ -1284,95 +1339,109 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   S.has_met = c->met_size ? 1 : 0;
   if (c->met_size) {
     if (!met_out) { set_err(c, "locate_interp: met_out is NULL"); return 0; }
-    S.s[S.n++] = Slot{c->met, met_out, c->met_size, c->met_size == 6};
+    S.s[S.n++] = Slot{c->met, met_out, c->met_size};
   }
   for (int j = 0; j < c->nfield; j++) {
     if (!fields_out || !fields_out[j]) { set_err(c, "locate_interp: fields_out[%d] is NULL", j); return 0; }
-    S.s[S.n++] = Slot{c->fin[j], fields_out[j], c->fsize[j], c->fsize[j] == 6};
+    S.s[S.n++] = Slot{c->fin[j], fields_out[j], c->fsize[j]};
   }
   const int g = grid_dim(bg.ne, c->tpc, 1024);
   const int gs = bg.nt > 0 ? grid_dim(bg.nt, 2, 512) : 1;
-  if (!ensure(c, c->frame, sizeof(Frame))) return 0;
-  if (!ensure(c, c->stats, sizeof(DevStats))) return 0;
-  if (!ensure(c, c->grid, sizeof(int) * (size_t)g * g * g)) return 0;
-  if (!ensure(c, c->sgrid, sizeof(int) * (size_t)gs * gs * gs)) return 0;
-  size_t nq = (size_t)np_new;
-  if (!ensure(c, c->keys_in, 4 * nq) || !ensure(c, c->keys_out, 4 * nq) || !ensure(c, c->vals_in, 4 * nq) ||
-      !ensure(c, c->vals_out, 4 * nq))
-    return 0;
-  if (!ensure(c, c->fb_vol, 4 * nq) || !ensure(c, c->fb_bdy, 4 * nq) || !ensure(c, c->best, 4 * nq) ||
+  int bb = 1;
+  while (bb < 10 && (1LL << (3 * bb)) * c->qpb < (long long)np_new) bb++;
+  const int gb = 1 << bb, nbins = 1 << (3 * bb);
+  const size_t nq = (size_t)np_new;
+  if (!ensure(c, c->frame, sizeof(Frame)) || !ensure(c, c->stats, sizeof(DevStats)) ||
+      !ensure(c, c->grid, 8 * (size_t)g * g * g) || !ensure(c, c->sgrid, 4 * (size_t)gs * gs * gs) ||
+      !ensure(c, c->order_v, 4 * nq) || !ensure(c, c->order_b, 4 * nq) || !ensure(c, c->vloc, 4 * nq) ||
+      !ensure(c, c->fb_vol, 4 * nq) || !ensure(c, c->fb_bdy, 4 * nq) || !ensure(c, c->best, 4 * nq) ||
       !ensure(c, c->ckey, 8 * nq) || !ensure(c, c->cidx, 4 * nq) || !ensure(c, c->bbest, 4 * nq) ||
       !ensure(c, c->bckey, 8 * nq) || !ensure(c, c->bcidx, 4 * nq))
     return 0;
-  size_t tmp_bytes = 0;
-  HIPCK(c, hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                              (int *)nullptr, (int *)nullptr, np_new, 0, 32, s));
-  if (!ensure(c, c->sort_tmp, tmp_bytes)) return 0;
 
   Frame *fr = (Frame *)c->frame.p;
   DevStats *st = (DevStats *)c->stats.p;
-  int *grid = (int *)c->grid.p, *sgrid = (int *)c->sgrid.p;
+  unsigned long long *grid = (unsigned long long *)c->grid.p;
+  int *sgrid = (int *)c->sgrid.p;
+  int *order_v = (int *)c->order_v.p, *order_b = (int *)c->order_b.p;
 
+  if (c->options & PMMG_HIP_OPT_SCAN) return run_scan(c, S, np_new, xyz_new, pclass, elem_out, hit_out, gs);
+
+  // query order decision first: a 4096-point sample, read back early (one
+  // small synchronisation) unless the caller forced the order
+  int sorted = 1;
   HIPCK(c, hipEventRecord(c->ev[0], s));
-  HIPCK(c, hipMemsetAsync(st, 0, sizeof(DevStats), s));
-  hipLaunchKernelGGL(k_frame_init, dim3(1), dim3(1), 0, s, fr);
-  hipLaunchKernelGGL(k_bbox, dim3(blocks_for(bg.np, 1024)), dim3(kBlock), 0, s, bg.xyz, bg.np, fr);
-  hipLaunchKernelGGL(k_frame_final, dim3(1), dim3(1), 0, s, fr, g, gs);
-  HIPCK(c, hipMemsetD32Async(grid, INT_MAX, (size_t)g * g * g, s));
-  long long nsamp = 2LL * g * g * g;
-  if (nsamp > bg.ne) nsamp = bg.ne;
-  hipLaunchKernelGGL(k_seed_vol, dim3(blocks_for(nsamp, 4096)), dim3(kBlock), 0, s, bg, fr, grid, g, nsamp);
-  if (bg.nt > 0) {
-    HIPCK(c, hipMemsetD32Async(sgrid, INT_MAX, (size_t)gs * gs * gs, s));
-    hipLaunchKernelGGL(k_seed_srf, dim3(blocks_for(bg.nt, 4096)), dim3(kBlock), 0, s, bg, fr, sgrid, gs);
+  if (c->options & PMMG_HIP_OPT_NOSORT) {
+    sorted = 0;
+  } else if (!(c->options & PMMG_HIP_OPT_SORT)) {
+    hipLaunchKernelGGL(k_coherence, dim3(1), dim3(kBlock), 0, s, xyz_new, np_new, st);
+    HIPCK(c, hipMemcpyAsync(c->h_small, &st->coherent, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIPCK(c, hipStreamSynchronize(s));
+    sorted = c->h_small[0] ? 0 : 1;
   }
-  const int nosort = (c->options & PMMG_HIP_OPT_NOSORT) ? 1 : 0;
-  hipLaunchKernelGGL(k_keys, dim3(blocks_for(np_new, 1 << 30)), dim3(kBlock), 0, s, xyz_new, pclass, np_new, fr,
-                     nosort, (uint32_t *)c->keys_in.p, (int *)c->vals_in.p, st);
+  c->last_sorted = sorted;
+  if (sorted && (!ensure(c, c->cnt, 4 * (size_t)2 * nbins) || !ensure(c, c->off, 4 * (size_t)2 * nbins) ||
+                 !ensure(c, c->binrank, 8 * nq)))
+    return 0;
+
+  const long long ng = (long long)g * g * g, nsg = bg.nt > 0 ? (long long)gs * gs * gs : 0;
+  hipLaunchKernelGGL(k_reset, dim3(blocks_for(ng, 2048)), dim3(kBlock), 0, s, fr, st, grid, ng, sgrid, nsg,
+                     sorted ? (int *)c->cnt.p : nullptr, sorted ? 2LL * nbins : 0LL, 1);
+  hipLaunchKernelGGL(k_bbox, dim3(blocks_for(bg.np, 1024)), dim3(kBlock), 0, s, bg.xyz, bg.np, fr);
+  hipLaunchKernelGGL(k_frame_final, dim3(1), dim3(1), 0, s, fr, g, gs, gb);
+  long long nsamp = (long long)c->spc * ng;
+  if (nsamp > bg.ne) nsamp = bg.ne;
+  hipLaunchKernelGGL(k_seed_vol, dim3(blocks_for(nsamp, 8192)), dim3(kBlock), 0, s, bg, fr, grid, g, nsamp);
+  if (bg.nt > 0) hipLaunchKernelGGL(k_seed_srf, dim3(blocks_for(bg.nt, 4096)), dim3(kBlock), 0, s, bg, fr, sgrid, gs);
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[1], s));
-  HIPCK(c, hipcub::DeviceRadixSort::SortPairs(c->sort_tmp.p, tmp_bytes, (uint32_t *)c->keys_in.p,
-                                              (uint32_t *)c->keys_out.p, (int *)c->vals_in.p, (int *)c->vals_out.p,
-                                              np_new, 0, 32, s));
+
+  if (sorted) {
+    size_t tb = 0;
+    HIPCK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (int *)c->cnt.p, (int *)c->off.p, 2 * nbins, s));
+    if (!ensure(c, c->scan_tmp, tb)) return 0;
+    hipLaunchKernelGGL(k_bin_count, dim3(blocks_for(np_new, 1 << 30)), dim3(kBlock), 0, s, xyz_new, pclass, np_new, fr,
+                       gb, nbins, (int *)c->cnt.p, (int2 *)c->binrank.p);
+    HIPCK(c, hipcub::DeviceScan::ExclusiveSum(c->scan_tmp.p, tb, (int *)c->cnt.p, (int *)c->off.p, 2 * nbins, s));
+    hipLaunchKernelGGL(k_bin_scatter, dim3(blocks_for(np_new, 1 << 30)), dim3(kBlock), 0, s, np_new,
+                       (const int2 *)c->binrank.p, (const int *)c->off.p, nbins, order_v, order_b);
+    hipLaunchKernelGGL(k_bin_total, dim3(1), dim3(1), 0, s, (const int *)c->off.p, (const int *)c->cnt.p, nbins, st);
+  } else {
+    hipcub::CountingInputIterator<int> ids(1);
+    size_t tb = 0;
+    HIPCK(c, hipcub::DeviceSelect::If(nullptr, tb, ids, order_v, &st->nvol, (int64_t)np_new, IsClass{pclass, 1}, s));
+    if (!ensure(c, c->scan_tmp, tb)) return 0;
+    HIPCK(c, hipcub::DeviceSelect::If(c->scan_tmp.p, tb, ids, order_v, &st->nvol, (int64_t)np_new,
+                                      IsClass{pclass, PMMG_PT_VOL}, s));
+    HIPCK(c, hipcub::DeviceSelect::If(c->scan_tmp.p, tb, ids, order_b, &st->nbdy, (int64_t)np_new,
+                                      IsClass{pclass, PMMG_PT_BDY}, s));
+  }
+  HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[2], s));
-  const int *order = (const int *)c->vals_out.p;
-  hipLaunchKernelGGL(k_vol, dim3(blocks_for(np_new, 1 << 30)), dim3(kBlock), 0, s, bg, fr, grid, g, xyz_new, order, S,
-                     elem_out, hit_out, (int *)c->fb_vol.p, st, c->maxstep);
+
+  if (c->options & PMMG_HIP_OPT_SPLIT) {
+    hipLaunchKernelGGL(k_vol_locate, dim3(blocks_for(np_new, 1 << 30)), dim3(kBlock), 0, s, bg, fr, grid, g, xyz_new,
+                       order_v, (int *)c->vloc.p, (int *)c->fb_vol.p, st, c->maxstep);
+    HIPCK(c, hipEventRecord(c->ev[6], s));
+    VolInterpFn interp = pick_layout(S).fn;
+    hipLaunchKernelGGL(interp, dim3(blocks_for(np_new, 1 << 30)), dim3(kBlock), 0, s, bg, xyz_new, order_v,
+                       (const int *)c->vloc.p, S, elem_out, hit_out, st);
+  } else {
+    FusedFn fused = pick_layout(S).ffn;
+    hipLaunchKernelGGL(fused, dim3(blocks_for(np_new, 1 << 30)), dim3(kBlock), 0, s, bg, fr, grid, g, xyz_new,
+                       order_v, S, elem_out, hit_out, (int *)c->fb_vol.p, st, c->maxstep);
+    HIPCK(c, hipEventRecord(c->ev[6], s));
+  }
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[3], s));
   if (bg.nt > 0) {
-    hipLaunchKernelGGL(k_bdy, dim3(blocks_for(np_new, 2048)), dim3(kBlock), 0, s, bg, fr, sgrid, gs, xyz_new, order, S,
-                       elem_out, hit_out, (int *)c->fb_bdy.p, st, c->maxstep);
+    hipLaunchKernelGGL(k_bdy, dim3(8 * blocks_for((np_new + 7) / 8, 256)), dim3(kBlock), 0, s, bg, fr, sgrid, gs, xyz_new, order_b,
+                       S, elem_out, hit_out, (int *)c->fb_bdy.p, st, c->maxstep);
     HIPCK(c, hipGetLastError());
   }
   HIPCK(c, hipEventRecord(c->ev[4], s));
-  // fallbacks: every kernel reads its device-side count and exits when it is 0
-  int nfill = np_new;
-  hipLaunchKernelGGL(k_fill_int, dim3(blocks_for(nfill, 1024)), dim3(kBlock), 0, s, (int *)c->best.p, nfill, INT_MAX);
-  hipLaunchKernelGGL(k_fill_int, dim3(blocks_for(nfill, 1024)), dim3(kBlock), 0, s, (int *)c->cidx.p, nfill, INT_MAX);
-  hipLaunchKernelGGL(k_fill_u64, dim3(blocks_for(nfill, 1024)), dim3(kBlock), 0, s, (unsigned long long *)c->ckey.p,
-                     nfill, ~0ULL);
-  const int fgrid = 1024;
-  hipLaunchKernelGGL(k_vol_exhaust_accept, dim3(fgrid), dim3(kBlock), 0, s, bg, xyz_new, (const int *)c->fb_vol.p, st,
-                     (int *)c->best.p);
-  hipLaunchKernelGGL(k_vol_exhaust_closest, dim3(fgrid), dim3(kBlock), 0, s, bg, xyz_new, (const int *)c->fb_vol.p, st,
-                     (const int *)c->best.p, (unsigned long long *)c->ckey.p, 0, (int *)c->cidx.p);
-  hipLaunchKernelGGL(k_vol_exhaust_closest, dim3(fgrid), dim3(kBlock), 0, s, bg, xyz_new, (const int *)c->fb_vol.p, st,
-                     (const int *)c->best.p, (unsigned long long *)c->ckey.p, 1, (int *)c->cidx.p);
-  hipLaunchKernelGGL(k_vol_finish, dim3(256), dim3(kBlock), 0, s, bg, xyz_new, (const int *)c->fb_vol.p, st,
-                     (const int *)c->best.p, (const int *)c->cidx.p, S, elem_out, hit_out);
-  if (bg.nt > 0) {
-    hipLaunchKernelGGL(k_fill_int, dim3(blocks_for(nfill, 1024)), dim3(kBlock), 0, s, (int *)c->bbest.p, nfill, INT_MAX);
-    hipLaunchKernelGGL(k_fill_int, dim3(blocks_for(nfill, 1024)), dim3(kBlock), 0, s, (int *)c->bcidx.p, nfill, INT_MAX);
-    hipLaunchKernelGGL(k_fill_u64, dim3(blocks_for(nfill, 1024)), dim3(kBlock), 0, s,
-                       (unsigned long long *)c->bckey.p, nfill, ~0ULL);
-    for (int pass = 0; pass < 3; pass++)
-      hipLaunchKernelGGL(k_bdy_exhaust, dim3(256), dim3(kBlock), 0, s, bg, xyz_new, (const int *)c->fb_bdy.p, st,
-                         (int *)c->bbest.p, (unsigned long long *)c->bckey.p, pass, (int *)c->bcidx.p);
-    hipLaunchKernelGGL(k_bdy_finish, dim3(256), dim3(kBlock), 0, s, bg, xyz_new, (const int *)c->fb_bdy.p, st,
-                       (const int *)c->bbest.p, (const int *)c->bcidx.p, S, elem_out, hit_out);
-  }
-  HIPCK(c, hipGetLastError());
+
+  if (!launch_fallbacks(c, S, xyz_new, elem_out, hit_out)) return 0;
   HIPCK(c, hipEventRecord(c->ev[5], s));
   c->pending = true;
   return 1;
@@ -1387,6 +1456,7 @@ static int collect_stats(pmmg_hip_ctx *c, pmmg_hip_stats *out) {
   out->nvol_walk = (int64_t)h.cnt[PMMG_HIT_VOL_WALK];
   out->nvol_exhaust = (int64_t)h.cnt[PMMG_HIT_VOL_EXHAUST];
   out->nvol_closest = (int64_t)h.cnt[PMMG_HIT_VOL_CLOSEST];
+  out->nvol_scan = (int64_t)h.cnt[PMMG_HIT_VOL_SCAN];
   out->nbdy_face = (int64_t)h.cnt[PMMG_HIT_BDY_FACE];
   out->nbdy_edge = (int64_t)h.cnt[PMMG_HIT_BDY_EDGE];
   out->nbdy_vertex = (int64_t)h.cnt[PMMG_HIT_BDY_VERTEX];
@@ -1397,6 +1467,7 @@ static int collect_stats(pmmg_hip_ctx *c, pmmg_hip_stats *out) {
   out->nbdy_closest = (int64_t)h.cnt[PMMG_HIT_BDY_CLOSEST];
   out->steps_total = (int64_t)h.steps;
   out->stepmax = (int64_t)h.stepmax;
+  out->sorted = c->last_sorted;
   float ms = 0.f;
   HIPCK(c, hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
   out->ms_prepare = ms;
@@ -1404,6 +1475,8 @@ static int collect_stats(pmmg_hip_ctx *c, pmmg_hip_stats *out) {
   out->ms_sort = ms;
   HIPCK(c, hipEventElapsedTime(&ms, c->ev[2], c->ev[3]));
   out->ms_vol = ms;
+  HIPCK(c, hipEventElapsedTime(&ms, c->ev[2], c->ev[6]));
+  out->ms_vol_locate = ms;
   HIPCK(c, hipEventElapsedTime(&ms, c->ev[3], c->ev[4]));
   out->ms_bdy = ms;
   HIPCK(c, hipEventElapsedTime(&ms, c->ev[4], c->ev[5]));

@@ -65,9 +65,15 @@ def device_count() -> int:
 class TransferContext:
     """One ``pmmg_hip_ctx`` on a HIP device."""
 
-    def __init__(self, device: int = 0, sort: bool = True):
+    def __init__(self, device: int = 0, sort: bool | None = None, scan: bool = False, split: bool = False):
+        """Volume points are located by per-query adjacency walks (default)
+        or, with scan=True, by the tetra-centric scan.  sort=None picks the
+        query order automatically (Morton-bin unless the numbering is
+        coherent); True / False force binning / input order.  split=True runs
+        the walk and the interpolation as two kernels."""
         self.lib = hip_lib()
-        self.h = self.lib.pmmg_hip_create(int(device), 0 if sort else 1)
+        opts = (0 if sort is None else (2 if sort else 1)) | (4 if scan else 0) | (8 if split else 0)
+        self.h = self.lib.pmmg_hip_create(int(device), opts)
         if not self.h:
             raise RuntimeError(f"pmmg_hip_create({device}) failed: no usable HIP device (the transfer step has "
                                "no CPU fallback)")
@@ -151,7 +157,7 @@ class TransferContext:
         return st
 
 
-def transfer(mesh_old, met, fields, xyz_new, pclass, hausd=0.01, device=0, sort=True, ctx=None):
+def transfer(mesh_old, met, fields, xyz_new, pclass, hausd=0.01, device=0, sort=None, ctx=None):
     """One-shot host-mode transfer: returns (met_new, fields_new, elem, hit, stats)."""
     own = ctx is None
     ctx = ctx or TransferContext(device, sort=sort)

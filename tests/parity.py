@@ -25,6 +25,7 @@ EPS = O.EPS
 REL_TOL = 1e-12
 
 VOL_WALK, VOL_EXHAUST, VOL_CLOSEST = 1, 2, 3
+VOL_SCAN = 12
 BDY_FACE, BDY_EDGE, BDY_VERTEX, BDY_WEDGE, BDY_CONE, BDY_EXHAUST, BDY_STALE, BDY_CLOSEST = range(4, 12)
 
 
@@ -45,10 +46,10 @@ def make_case(kind=synth.CUBE, n_old=6, n_new=7, metric=synth.F_ANI,
     return case
 
 
-def run_gpu(case, sort=True, ctx=None):
+def run_gpu(case, sort=None, ctx=None, scan=False, split=False):
     bg, new = case["bg"], case["new"]
     own = ctx is None
-    ctx = ctx or TransferContext(0, sort=sort)
+    ctx = ctx or TransferContext(0, sort=sort, scan=scan, split=split)
     try:
         ctx.set_background(bg.xyz, bg.tetv, bg.adja, bg.triv, bg.adjt, case["hausd"])
         ctx.set_solutions(case["met"], case["fields"])
@@ -105,10 +106,13 @@ def check(case, gpu, max_points=None):
         # (ii) acceptance of the chosen element
         if h == VOL_WALK:
             assert not is_bdy and O.tetra_minbary(B, k, x) > -EPS, (i, h, k)
-        elif h == VOL_EXHAUST:
-            assert k == O.first_accepting_tetra(B, x), (i, h, k)
+        elif h in (VOL_EXHAUST, VOL_SCAN):
+            assert not is_bdy and k == O.first_accepting_tetra(B, x), (i, h, k)
         elif h == VOL_CLOSEST:
-            assert O.first_accepting_tetra(B, x) == 0 and k == O.closest_tetra(B, x), (i, h, k)
+            kb = O.closest_tetra(B, x)
+            assert O.first_accepting_tetra(B, x) == 0, (i, h, k)
+            # lowest index among exact ties (the reference: first evaluated)
+            assert k == kb or O.closest_value(B, k, x) == O.closest_value(B, kb, x), (i, h, k, kb)
         elif h in (BDY_FACE, BDY_EDGE, BDY_VERTEX):
             ok, _ = O.tria_accepts(B, k, x)
             assert is_bdy and ok, (i, h, k)
@@ -135,7 +139,7 @@ def check(case, gpu, max_points=None):
         # (i) identical element where the reference is unambiguous
         if ref is not None:
             rh = int(ref["hit"][i])
-            if rh in (VOL_WALK, VOL_EXHAUST) and ref["minbary"][i] > EPS:
+            if rh in (VOL_WALK, VOL_EXHAUST, VOL_SCAN) and ref["minbary"][i] > EPS:
                 rep["class_i"] += 1
                 same_elem = int(ref["elem"][i]) == k
                 rep["class_i_same"] += int(same_elem)

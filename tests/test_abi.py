@@ -1,0 +1,64 @@
+"""The C-ABI library loads and exports every symbol the headers declare; the
+product path never links the oracle and has no CPU fallback (CPU only)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from parmmg_amd import build
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared(header):
+    text = open(header).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(pmmg_[a-z0-9_]+)\s*\(", text)))
+
+
+def _exports(so):
+    out = subprocess.run(["nm", "-D", "--defined-only", so], stdout=subprocess.PIPE, text=True, check=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if line.strip()}
+
+
+def test_hip_module_exports_the_c_abi():
+    names = _declared(os.path.join(ROOT, "include", "parmmg_hip.h"))
+    assert len(names) >= 12
+    lib = ctypes.CDLL(build.HIP_SO)
+    exp = _exports(build.HIP_SO)
+    for n in names:
+        assert n in exp, n
+        getattr(lib, n)
+
+
+def test_host_layer_exports():
+    names = [n for n in _declared(os.path.join(ROOT, "parmmg_amd", "csrc", "pmmg_host.h"))]
+    exp = _exports(build.HOST_SO)
+    for n in names:
+        assert n in exp, n
+
+
+def test_hip_module_is_gfx950_code():
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "-n", build.HIP_SO], stdout=subprocess.PIPE,
+                         stderr=subprocess.STDOUT, text=True).stdout
+    blob = open(build.HIP_SO, "rb").read()
+    assert b"gfx950" in blob, out[:200]
+
+
+@pytest.mark.parametrize("so", [build.HIP_SO, build.HOST_SO])
+def test_product_does_not_link_the_oracle(so):
+    exp = _exports(so)
+    assert not any(s.startswith("orc_") for s in exp)
+    deps = subprocess.run(["readelf", "-d", so], stdout=subprocess.PIPE, text=True).stdout
+    assert "oracle" not in deps
+
+
+def test_no_cpu_fallback_without_gpu():
+    from parmmg_amd import transfer
+
+    if transfer.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        transfer.TransferContext(0)

@@ -22,20 +22,25 @@ CASES = {
 }
 
 
+MODES = {"auto": {}, "morton": dict(sort=True), "nosort": dict(sort=False), "split": dict(split=True),
+         "scan": dict(scan=True)}
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("sort", [True, False], ids=["morton", "nosort"])
+@pytest.mark.parametrize("mode", sorted(MODES))
 @pytest.mark.parametrize("name", sorted(CASES))
-def test_parity_small(name, sort):
+def test_parity_small(name, mode):
     case = make_case(**CASES[name])
-    gpu = run_gpu(case, sort=sort)
+    gpu = run_gpu(case, **MODES[mode])
     rep = check(case, gpu)
-    print(name, sort, rep, gpu["stats"])
+    print(name, mode, rep, gpu["stats"])
     assert rep["n"] == int((case["pclass"] != 0).sum())
     assert rep["class_i"] == rep["class_i_same"]
 
 
 @pytest.mark.gpu
-def test_fallback_paths_outside_domain():
+@pytest.mark.parametrize("mode", ["auto", "scan"])
+def test_fallback_paths_outside_domain(mode):
     """Points pushed outside the background make the walks get stuck; the
     exhaustive / closest kernels must reproduce the reference semantics."""
     case = make_case(kind=C, n_old=5, n_new=6, with_ref=False)
@@ -50,7 +55,7 @@ def test_fallback_paths_outside_domain():
     new.xyz[pick_b[5:], 2] = -0.004                           # within hausd of the bottom face
     case["B"] = __import__("oracle.oracle", fromlist=["Background"]).Background(
         case["bg"], case["met"], case["fields"], case["hausd"])
-    gpu = run_gpu(case)
+    gpu = run_gpu(case, **MODES[mode])
     rep = check(case, gpu)
     print(rep, gpu["stats"])
     assert gpu["stats"]["nvol_closest"] + gpu["stats"]["nvol_exhaust"] >= 1
