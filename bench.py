@@ -25,7 +25,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from parmmg_amd import configs, synth  # noqa: E402
+from parmmg_amd import configs, ranks, synth  # noqa: E402
 from parmmg_amd.transfer import TransferContext  # noqa: E402
 
 METRIC = "new-mesh points located+interpolated/sec (Mpts/s) and HBM GB/s, 1/2/4/8 GPU"
@@ -108,16 +108,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+    ri = ranks.init("nccl")
+    rank, world, local = ri.rank, ri.world, ri.local
 
     w = configs.SHORT[args.config]
     bg, new, met, fields, pclass = build_workload(w, rank)
@@ -138,15 +130,11 @@ def main():
         ctx.set_solutions(d_met, d_f)
         ctx.locate_interp(d_qxyz, d_pc, d_mo, d_fo, d_elem, d_hit, sync=False)
 
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
     for _ in range(args.warmup):
         step()
     st0 = ctx.sync()
     # timed region: barrier + device sync on both sides
-    barrier()
+    ranks.barrier(ri)
     ctx.sync()
     ms_vol = []
     ms_tot = []
@@ -156,19 +144,14 @@ def main():
         st = ctx.sync()  # per-step event times of this step (sync adds no device work)
         ms_vol.append(st.ms_vol)
         ms_tot.append(st.ms_total)
-    barrier()
+    ranks.barrier(ri)
     ctx.sync()
     elapsed = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
 
     npts = int(st.nvol + st.nbdy)
-    ms_per_step = elapsed / args.steps * 1e3
-    value = npts * world / (elapsed / args.steps) / 1e6
+    agg = ranks.aggregate(ri, npts, elapsed, args.steps)
+    ms_per_step = agg["ms_per_step"]
+    value = agg["mpts_per_s"]
     (np_o, ne_o, _), (np_n, _, _) = w.counts()
     B = w.algorithmic_bytes(npts)
     per_pt = B / npts
@@ -220,8 +203,7 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    ranks.finalize(ri)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,72 @@
+"""The bench's multi-rank path on CPU (gloo, world_size 2): every rank owns
+its own group (weak scaling, no data-path collective), the only reductions are
+the barrier, max of the step time and sum of the points."""
+import os
+import socket
+
+import numpy as np
+import torch.multiprocessing as mp
+
+from parmmg_amd import configs, ranks, synth
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    ri = ranks.init("gloo")
+    assert ri.distributed and ri.world == world and ri.rank == rank
+    # per-rank group, as bench.build_workload makes it (seed + rank)
+    new = synth.lattice(synth.CUBE, 4, jitter=0.2, seed=synth.SEED + rank, with_trias=False)
+    pclass = synth.classes(new)
+    npts = int((pclass != 0).sum())
+    ranks.barrier(ri)
+    elapsed = 0.5 + rank  # rank 1 is the slow one
+    agg = ranks.aggregate(ri, npts, elapsed, steps=5)
+    q.put((rank, npts, float(new.xyz.sum()), agg))
+    ranks.finalize(ri)
+
+
+def test_gloo_two_ranks_weak_aggregate():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (r0, n0, s0, a0), (r1, n1, s1, a1) = out
+    assert a0 == a1  # every rank sees the same reduced numbers
+    assert a0["points_per_step"] == n0 + n1
+    assert a0["elapsed_s"] == 1.5
+    np.testing.assert_allclose(a0["ms_per_step"], 1.5 / 5 * 1e3)
+    np.testing.assert_allclose(a0["mpts_per_s"], (n0 + n1) / (1.5 / 5) / 1e6)
+    assert s0 != s1  # each rank jitters its own group
+
+
+def test_single_process_no_group(monkeypatch):
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    ri = ranks.init("nccl")  # world 1: no process group, no device touched
+    assert not ri.distributed
+    agg = ranks.aggregate(ri, 1000, 2.0, steps=4)
+    assert agg["points_per_step"] == 1000 and agg["ms_per_step"] == 500.0
+
+
+def test_bench_configs_fit_one_gpu():
+    """Every bench workload's resident footprint fits a 288 GB GPU with room."""
+    for w in configs.SHORT.values():
+        (np_o, ne_o, nt_o), (np_n, _, _) = w.counts()
+        b = np_o * (24 + 8 * w.K) + ne_o * 32 + nt_o * 24 + np_n * (24 + 1 + 8 * w.K + 4 + 1)
+        assert b < 200e9, (w.name, b)
