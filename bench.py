@@ -49,49 +49,50 @@ def build_workload(w: configs.Workload, rank: int):
 
 
 def pmc_traffic(workload: str):
-    """HBM bytes per k_vol launch from the committed rocprofv3 PMC summary
-    (profiles/pmc_<workload>.json, produced by tools/pmc_summary.py), or None."""
-    path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
-    if not os.path.exists(path):
-        return None
+    """HBM bytes per launch of the dominant volume kernel from the newest
+    committed rocprofv3 PMC summary (profiles/rNN/pmc_<workload>.json, made by
+    tools/prof_summary.py from FETCH_SIZE / WRITE_SIZE passes of this bench),
+    or (None, None)."""
+    import glob
+
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_{workload}.json")))
+    if not paths:
+        return None, None
     try:
-        with open(path) as f:
+        with open(paths[-1]) as f:
             d = json.load(f)
-        return d.get("k_vol_hbm_bytes_per_launch")
+        return d.get("k_vol_hbm_bytes_per_launch"), os.path.relpath(paths[-1], ROOT)
     except Exception:
-        return None
+        return None, None
 
 
 def cpu_baseline(w, bg, new, met, fields, pclass, budget_s: float):
     """The oracle (C port of the reference path, 1 thread) on a bounded sample:
     the full per-iteration precompute (faceAreas, triaNormals, nodeTrias, as the
-    reference times it) plus locate+interpolate of the first S points in
-    lattice order; the full-step rate is extrapolated from the sample."""
+    reference's tim=2 timer includes it, src/libparmmg1.c:823-836) plus
+    locate+interpolate of new points in lattice order (the reference's warm
+    start kept) until `budget_s` seconds are used; the full-step time is the
+    precompute plus the sampled per-point time times all points."""
     from oracle import oracle as O
 
     B = O.Background(bg, met, fields, w.hausd)
     order = np.arange(1, new.np + 1, dtype=np.int32)
-    s = min(new.np, 20000)
-    r = O.run(B, new.xyz, pclass, order[:s])
-    per_pt = r["t_locate"] / s
-    s2 = int(min(new.np, max(s, budget_s / max(per_pt, 1e-9))))
-    if s2 > s:
-        r = O.run(B, new.xyz, pclass, order[:s2])
-        s = s2
+    r = O.run(B, new.xyz, pclass, order, budget_s=budget_s)
+    s = int(r["nvisited"])
     t_pre, t_loc = r["t_precompute"], r["t_locate"]
     nproc = int((pclass[:s] != 0).sum())
     ntot = int((pclass != 0).sum())
     t_full = t_pre + t_loc * ntot / max(nproc, 1)
     return {
-        "value": ntot / t_full / 1e6,
+        "value": round(ntot / t_full / 1e6, 4),
         "unit": "Mpts/s",
         "cores": 1,
         "kind": "port",
-        "sample": f"oracle (C restatement, 1 thread) on {w.name}: full precompute over {bg.ne} tets "
-                  f"({t_pre:.2f}s) + locate/interp of the first {s} new points in lattice order "
-                  f"({t_loc:.2f}s), extrapolated to all {ntot} points",
-        "t_precompute_s": t_pre,
-        "t_sample_s": t_loc,
+        "sample": f"oracle (C restatement of the reference path, 1 thread) on {w.name}: full precompute over "
+                  f"{bg.ne} tets ({t_pre:.2f}s) + locate/interp of the first {s} new points in lattice order "
+                  f"({t_loc:.2f}s, time-bounded), per-point rate extrapolated to all {ntot} points",
+        "t_precompute_s": round(t_pre, 3),
+        "t_sample_s": round(t_loc, 3),
         "sample_points": nproc,
     }
 
@@ -130,9 +131,12 @@ def main():
         ctx.set_solutions(d_met, d_f)
         ctx.locate_interp(d_qxyz, d_pc, d_mo, d_fo, d_elem, d_hit, sync=False)
 
-    for _ in range(args.warmup):
+    log(f"[bench r{rank}] inputs resident in HBM; warmup {args.warmup} steps")
+    for wi in range(args.warmup):
+        t_w = time.perf_counter()
         step()
-    st0 = ctx.sync()
+        st0 = ctx.sync()
+        log(f"[bench r{rank}] warmup {wi}: {1e3 * (time.perf_counter() - t_w):.2f} ms wall, device {st0.as_dict()}")
     # timed region: barrier + device sync on both sides
     ranks.barrier(ri)
     ctx.sync()
@@ -147,6 +151,7 @@ def main():
     ranks.barrier(ri)
     ctx.sync()
     elapsed = time.perf_counter() - t0
+    log(f"[bench r{rank}] timed {args.steps} steps: {1e3 * elapsed / args.steps:.3f} ms/step")
 
     npts = int(st.nvol + st.nbdy)
     agg = ranks.aggregate(ri, npts, elapsed, args.steps)
@@ -158,7 +163,7 @@ def main():
     kvol_ms = float(np.mean(ms_vol))
     kvol_bytes = per_pt * st.nvol
     achieved = kvol_bytes / (kvol_ms * 1e-3) / 1e9
-    traffic = pmc_traffic(w.name)
+    traffic, traffic_src = pmc_traffic(w.name)
     out = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -195,10 +200,14 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
+            "traffic_unit": "bytes per launch (FETCH_SIZE x2 + WRITE_SIZE)",
+            "traffic_source": traffic_src,
+            "algorithmic_bytes_per_launch": round(kvol_bytes),
             "algorithmic_bytes_per_point": round(per_pt, 2),
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log(f"[bench r{rank}] cpu baseline (oracle) on a bounded sample")
         out["cpu_baseline"] = cpu_baseline(w, bg, new, met, fields, pclass, args.cpu_baseline_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)

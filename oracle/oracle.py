@@ -51,6 +51,8 @@ def lib():
         vp, ci, cd = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
         L.orc_interp_mesh.argtypes = [vp, vp, vp, ci, vp]
         L.orc_interp_mesh.restype = ci
+        L.orc_interp_mesh_budget.argtypes = [vp, vp, vp, ci, cd, vp]
+        L.orc_interp_mesh_budget.restype = ci
         L.orc_eval_in_element.argtypes = [vp, vp, ci, ci, ci, ci, vp, vp]
         L.orc_eval_in_element.restype = ci
         L.orc_tetra_minbary.argtypes = [vp, ci, vp]
@@ -95,8 +97,10 @@ class Background:
         return ctypes.byref(self.s)
 
 
-def run(bg: Background, xyz_new, pclass, visit, mode=MODE_FAITHFUL):
-    """Sequential reference-order run.  Returns dict of per-point arrays."""
+def run(bg: Background, xyz_new, pclass, visit, mode=MODE_FAITHFUL, budget_s: float = 0.0):
+    """Sequential reference-order run.  Returns dict of per-point arrays.
+    With budget_s > 0 the locate+interp phase stops after about that many
+    seconds; out["nvisited"] is the number of visit entries processed."""
     xyz_new = np.ascontiguousarray(xyz_new, np.float64)
     pclass = np.ascontiguousarray(pclass, np.uint8)
     visit = np.ascontiguousarray(visit, np.int32)
@@ -112,8 +116,10 @@ def run(bg: Background, xyz_new, pclass, visit, mode=MODE_FAITHFUL):
              _p(out["minbary"]), _p(out["steps"]))
     q = _Q(npn, _p(xyz_new), _p(pclass), visit.shape[0], _p(visit))
     timing = (ctypes.c_double * 2)()
-    if not lib().orc_interp_mesh(bg.ref, ctypes.byref(q), ctypes.byref(o), int(mode), timing):
+    nv = lib().orc_interp_mesh_budget(bg.ref, ctypes.byref(q), ctypes.byref(o), int(mode), float(budget_s), timing)
+    if nv < 0:
         raise RuntimeError("oracle run failed")
+    out["nvisited"] = nv
     out["t_precompute"], out["t_locate"] = timing[0], timing[1]
     return out
 

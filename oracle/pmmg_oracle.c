@@ -588,14 +588,21 @@ static int state_init(orc_state *S, const orc_background *bg, int mode) {
 
 int orc_interp_mesh(const orc_background *bg, const orc_queries *q, orc_outputs *out, int mode,
                     double *timing) {
+  return orc_interp_mesh_budget(bg, q, out, mode, 0.0, timing) >= 0;
+}
+
+int orc_interp_mesh_budget(const orc_background *bg, const orc_queries *q, orc_outputs *out, int mode,
+                           double budget_s, double *timing) {
   orc_state S;
   double t0 = now_s();
-  if (!state_init(&S, bg, mode)) { state_free(&S); return 0; }
+  if (!state_init(&S, bg, mode)) { state_free(&S); return -1; }
   double t1 = now_s();
   int itet = 1, itria = 1; /* interpmesh_pmmg.c:529 */
   int nf = bg->nfield;
   double **frow = (double **)malloc(sizeof(double *) * (nf > 0 ? nf : 1));
-  for (int v = 0; v < q->nvisit; v++) {
+  int v = 0;
+  for (; v < q->nvisit; v++) {
+    if (budget_s > 0.0 && (v & 255) == 0 && v > 0 && now_s() - t1 > budget_s) break;
     int ip = q->visit[v];
     if (ip < 1 || ip > q->np) continue;
     int cls = q->pclass[ip - 1];
@@ -630,7 +637,7 @@ int orc_interp_mesh(const orc_background *bg, const orc_queries *q, orc_outputs 
   free(frow);
   state_free(&S);
   if (timing) { timing[0] = t1 - t0; timing[1] = t2 - t1; }
-  return 1;
+  return v;
 }
 
 /* ---------------- element-wise checkers ---------------- */

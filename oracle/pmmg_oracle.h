@@ -79,6 +79,13 @@ typedef struct {
 int orc_interp_mesh(const orc_background *bg, const orc_queries *q, orc_outputs *out,
                     int mode, double *timing);
 
+/* Same run, stopped once the locate+interp phase has used `budget_s` seconds
+ * (checked every 256 visited points; budget_s <= 0: no limit).  Returns the
+ * number of visit entries processed (CPU-baseline sampling in bench.py), or
+ * -1 on failure. */
+int orc_interp_mesh_budget(const orc_background *bg, const orc_queries *q, orc_outputs *out,
+                           int mode, double budget_s, double *timing);
+
 /* Re-evaluate one query in a given element / hit kind (as the GPU reports
  * it) with the reference arithmetic, writing the interpolated values into
  * met_row / field_rows (rows of the point, not whole arrays).  Used to check

@@ -1,0 +1,81 @@
+"""Summarise one tools/gpu_prof.sh run into profiles/<round>/:
+
+* kernel_stats.csv       rocprofv3 --kernel-trace --stats summary (copied)
+* kernels.json           per kernel: calls, average duration, VGPR/SGPR/LDS
+* pmc_<workload>.json    HBM bytes per launch of every kernel from the two
+                         PMC passes, corrected as MI355X_MICROARCH.md
+                         prescribes (FETCH_SIZE and WRITE_SIZE are in KiB;
+                         FETCH_SIZE counts half the bytes of wide reads on
+                         gfx950 -> doubled)
+* bench.json             the bench line of the same run
+
+  python tools/prof_summary.py gpurun_out/r1c profiles/r01
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+
+def per_dispatch(path):
+    """counter sum per dispatch, grouped by kernel name"""
+    disp = defaultdict(float)
+    name = {}
+    for r in csv.DictReader(open(path)):
+        d = int(r["Dispatch_Id"])
+        disp[d] += float(r["Counter_Value"])
+        name[d] = r["Kernel_Name"]
+    by = defaultdict(list)
+    for d, v in disp.items():
+        by[name[d]].append(v)
+    return by
+
+
+def short(k):
+    k = k.replace("(anonymous namespace)::", "").replace("void ", "")
+    return k.split("(")[0]
+
+
+def main(src, dst):
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
+    bench = json.loads(open(os.path.join(src, "bench.json")).read().strip().splitlines()[-1])
+    json.dump(bench, open(os.path.join(dst, "bench.json"), "w"), indent=1)
+    kern = {}
+    for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv"))):
+        k = short(r["Kernel_Name"])
+        e = kern.setdefault(k, dict(calls=0, total_ns=0, vgpr=int(r["VGPR_Count"]), sgpr=int(r["SGPR_Count"]),
+                                    lds=int(r["LDS_Block_Size"]), scratch=int(r["Scratch_Size"]),
+                                    grid=int(r["Grid_Size_X"]), block=int(r["Workgroup_Size_X"])))
+        e["calls"] += 1
+        e["total_ns"] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    for e in kern.values():
+        e["avg_us"] = round(e["total_ns"] / e["calls"] / 1e3, 3)
+    json.dump(kern, open(os.path.join(dst, "kernels.json"), "w"), indent=1)
+    fetch = per_dispatch(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"))
+    write = per_dispatch(os.path.join(src, "pmc_write", "run_counter_collection.csv"))
+    pmc = {"note": "bytes per launch; FETCH_SIZE/WRITE_SIZE are KiB; FETCH doubled (gfx950 wide-read correction, "
+                   "MI355X_MICROARCH.md HBM section); counters include Infinity-Cache hits",
+           "workload": bench["config"]["workload"], "kernels": {}}
+    for k in set(fetch) | set(write):
+        f = fetch.get(k, [0.0])
+        w = write.get(k, [0.0])
+        fb = 2.0 * 1024.0 * sum(f) / len(f)
+        wb = 1024.0 * sum(w) / len(w)
+        pmc["kernels"][short(k)] = {"fetch_bytes": fb, "write_bytes": wb, "hbm_bytes": fb + wb,
+                                    "fetch_raw_kib": sum(f) / len(f), "write_raw_kib": sum(w) / len(w)}
+    kv = [k for k in pmc["kernels"] if k.startswith("k_vol")]
+    if kv:
+        main_k = max(kv, key=lambda k: pmc["kernels"][k]["hbm_bytes"])
+        pmc["k_vol_kernel"] = main_k
+        pmc["k_vol_hbm_bytes_per_launch"] = pmc["kernels"][main_k]["hbm_bytes"]
+    json.dump(pmc, open(os.path.join(dst, f"pmc_{pmc['workload']}.json"), "w"), indent=1)
+    print(json.dumps({k: v for k, v in pmc.items() if k != "kernels"}, indent=1))
+    for k, e in sorted(kern.items(), key=lambda kv: -kv[1]["total_ns"]):
+        print(f"{e['avg_us']:10.1f} us x{e['calls']:3d}  vgpr {e['vgpr']:3d}  {k}")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
