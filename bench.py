@@ -105,6 +105,13 @@ def main():
     ap.add_argument("--config", default="cfg4", choices=sorted(configs.SHORT))
     ap.add_argument("--sort", default="auto", choices=["auto", "on", "off"],
                     help="query order: Morton binning (on), input order (off), or automatic")
+    ap.add_argument("--locate", default="walk", choices=["walk", "scan"],
+                    help="volume location: grid-seeded adjacency walks or the tetra-centric scan")
+    ap.add_argument("--fused", action="store_true", help="volume walk and interpolation as one kernel")
+    ap.add_argument("--tpc", type=int, default=0, help="background tetra per volume seed cell (0: module default)")
+    ap.add_argument("--spc", type=int, default=0, help="sampled tetra per seed cell (0: module default)")
+    ap.add_argument("--layout", default="tet8", choices=["tet8", "separate"],
+                    help="HBM layout of the tetra: packed {v[4], adja[4]} records or separate tetv/adja arrays")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -115,8 +122,17 @@ def main():
     w = configs.SHORT[args.config]
     bg, new, met, fields, pclass = build_workload(w, rank)
 
-    ctx = TransferContext(local, sort={"auto": None, "on": True, "off": False}[args.sort])
-    d_xyz, d_tetv, d_adja = ctx.upload(bg.xyz), ctx.upload(bg.tetv), ctx.upload(bg.adja)
+    for name in ("tpc", "spc"):
+        if getattr(args, name) > 0:
+            os.environ["PMMG_HIP_" + name.upper()] = str(getattr(args, name))  # read by pmmg_hip_create
+    ctx = TransferContext(local, fused=args.fused, sort={"auto": None, "on": True, "off": False}[args.sort],
+                          scan=args.locate == "scan")
+    from parmmg_amd.transfer import pack_tet8
+    d_xyz = ctx.upload(bg.xyz)
+    if args.layout == "tet8":
+        d_tet8 = ctx.upload(pack_tet8(bg.tetv, bg.adja))
+    else:
+        d_tetv, d_adja = ctx.upload(bg.tetv), ctx.upload(bg.adja)
     d_triv, d_adjt = ctx.upload(bg.triv), ctx.upload(bg.adjt)
     d_met = ctx.upload(met)
     d_f = [ctx.upload(f) for f in fields]
@@ -127,7 +143,10 @@ def main():
     d_hit = ctx.empty((new.np,), np.int8)
 
     def step():
-        ctx.set_background(d_xyz, d_tetv, d_adja, d_triv, d_adjt, w.hausd)
+        if args.layout == "tet8":
+            ctx.set_background_tet8(d_xyz, d_tet8, d_triv, d_adjt, w.hausd)
+        else:
+            ctx.set_background(d_xyz, d_tetv, d_adja, d_triv, d_adjt, w.hausd)
         ctx.set_solutions(d_met, d_f)
         ctx.locate_interp(d_qxyz, d_pc, d_mo, d_fo, d_elem, d_hit, sync=False)
 
@@ -184,6 +203,9 @@ def main():
             "located_points_per_gpu": npts, "K_doubles_per_vertex": w.K,
             "parallelism": f"one group per GPU x{world} (weak, no data-path collective)",
             "query_order": args.sort,
+            "locate": args.locate,
+            "tetra_layout": args.layout,
+            "volume_kernels": "fused" if args.fused else "walk+interp",
             "morton_binned": bool(st.sorted),
         },
         "gbps_algorithmic_step": round(B / (ms_per_step * 1e-3) / 1e9, 1),
@@ -194,7 +216,7 @@ def main():
         "locate_stats": {k: v for k, v in st.as_dict().items() if not k.startswith("ms_")},
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_vol",
+            "kernel": "k_vol_fused" if args.fused else "k_vol_walk + k_vol_interp (volume stage)",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

@@ -108,7 +108,8 @@ typedef struct {
                                    tetra for every query) instead of per-query walks; pays off
                                    only when the new mesh has many more points than the
                                    background has tetra */
-#define PMMG_HIP_OPT_SPLIT  8   /* volume walk and interpolation as two kernels (default: fused) */
+#define PMMG_HIP_OPT_FUSED  8   /* volume walk and interpolation in one kernel (default: two kernels,
+                                   the walk at higher occupancy, the interpolation in query order) */
 
 /* Create a context on HIP device `device`.  Returns NULL on failure. */
 pmmg_hip_ctx *pmmg_hip_create(int device, int options);
@@ -125,6 +126,18 @@ int pmmg_hip_set_background(pmmg_hip_ctx *ctx, int np, const double *xyz,
                             int ne, const int *tetv, const int *adja,
                             int nt, const int *triv, const int *adjt,
                             double hausd, int where);
+
+/* Same background with the tetrahedra as packed 32-byte records
+ *   tet8[8*ne] = {v0, v1, v2, v3, adja0, adja1, adja2, adja3} per tetra
+ * (MMG5_Tetra.v followed by the tetra's 4 adja codes 4*k+i).  This is the
+ * module's preferred HBM layout: a walk step reads one record (one cache
+ * line) instead of a tetv row plus an adja row.  A host shim builds it in the
+ * same pass that packs MMG5_Tetra.v.  In device mode tet8
+ * must be 16-byte aligned. */
+int pmmg_hip_set_background_tet8(pmmg_hip_ctx *ctx, int np, const double *xyz,
+                                 int ne, const int *tet8,
+                                 int nt, const int *triv, const int *adjt,
+                                 double hausd, int where);
 
 /* Background solutions: the metric (met_size 0 = none, 1 = iso, 6 = aniso,
  * storage m11,m12,m13,m22,m23,m33 as MMG5 stores it) and nfield fields of

@@ -39,6 +39,8 @@ HIP_API = {
     "pmmg_hip_destroy": (None, [c_void_p]),
     "pmmg_hip_set_background": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p,
                                         c_void_p, c_double, c_int]),
+    "pmmg_hip_set_background_tet8": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p,
+                                             c_double, c_int]),
     "pmmg_hip_set_solutions": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int]),
     "pmmg_hip_locate_interp": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                        c_void_p, P(HipStats), c_int]),

@@ -20,10 +20,15 @@ namespace pmmg {
 constexpr double kEps = 1.e-06;     // MMG5_EPS
 constexpr double kEpsD2 = 1.0e-200; // MMG5_EPSD2
 constexpr int kMaxSlot = 8;         // metric + up to 7 fields
-constexpr int kHist = 8;            // visited-element history of a walk
+constexpr int kHist = 4;            // visited-element history of a walk
 constexpr int kBlock = 256;
 constexpr int kFanMax = 64;
 
+// Background mesh.  Tetra rows are read through tetv_row / adja_row: either
+// two separate arrays (the reference's MMG5_Tetra.v and adja layouts,
+// tstride 1) or one packed 32-byte record per tetra {v[4], adja[4]}
+// (tetv = rec, adja = rec + 1, tstride 2), whose two halves share a cache
+// line, so a walk step costs one line request for the tetra instead of two.
 struct Bg {
   const double *xyz;
   const int4 *tetv;
@@ -31,8 +36,12 @@ struct Bg {
   const int *triv;
   const int *adjt;
   int np, ne, nt;
+  int tstride;
   double hausd;
 };
+
+__device__ __forceinline__ int4 tetv_row(const Bg &bg, int k) { return bg.tetv[(size_t)(k - 1) * bg.tstride]; }
+__device__ __forceinline__ int4 adja_row(const Bg &bg, int k) { return bg.adja[(size_t)(k - 1) * bg.tstride]; }
 
 // one solution array: code 1 = scalar, 3 = vector (both P1 iso
 // interpolation), 6 = symmetric tensor (inverse-tensor interpolation)
@@ -163,21 +172,40 @@ __device__ __forceinline__ double orvol4(const double *p0, const double *p1, con
          (p1[2] - p0[2]) * (ax * by - ay * bx);
 }
 
-// PMMG_barycoord3d_compute (barycoord_pmmg.c:238-257) on face normals recomputed
-// from the vertices (PMMG_precompute_faceAreas, locate_pmmg.c:107-119); the
-// reference's 96 B/tetra faceAreas array is never stored.  b[f] unsorted.
-__device__ __forceinline__ double tet_bary(const double *x, const double *p0, const double *p1, const double *p2,
-                                           const double *p3, double *b) {
+// Numerators of PMMG_barycoord3d_compute (barycoord_pmmg.c:238-257) on face
+// normals recomputed from the vertices (PMMG_precompute_faceAreas,
+// locate_pmmg.c:107-119; the reference's 96 B/tetra faceAreas array is never
+// stored): s[f] = (x - p_idir[f][0]) . n_f, so that bary[f] = -s[f] / vol.
+// Returns vol = MMG5_orvol.
+__device__ __forceinline__ double tet_dots(const double *x, const double *p0, const double *p1, const double *p2,
+                                           const double *p3, double *s) {
+  // sched_barrier: compute the faces one after the other.  Left alone, the
+  // scheduler interleaves all four for ILP and the walk kernels need ~100
+  // VGPRs (4 waves/SIMD); latency-bound walks gain more from occupancy.
   double vol = orvol4(p0, p1, p2, p3);
+  __builtin_amdgcn_sched_barrier(0);
   double n[3];
   nonunit_normal(p1, p2, p3, n); // face 0: idir {1,2,3}
-  b[0] = -((x[0] - p1[0]) * n[0] + (x[1] - p1[1]) * n[1] + (x[2] - p1[2]) * n[2]) / vol;
+  s[0] = (x[0] - p1[0]) * n[0] + (x[1] - p1[1]) * n[1] + (x[2] - p1[2]) * n[2];
+  __builtin_amdgcn_sched_barrier(0);
   nonunit_normal(p0, p3, p2, n); // face 1: idir {0,3,2}
-  b[1] = -((x[0] - p0[0]) * n[0] + (x[1] - p0[1]) * n[1] + (x[2] - p0[2]) * n[2]) / vol;
+  s[1] = (x[0] - p0[0]) * n[0] + (x[1] - p0[1]) * n[1] + (x[2] - p0[2]) * n[2];
+  __builtin_amdgcn_sched_barrier(0);
   nonunit_normal(p0, p1, p3, n); // face 2: idir {0,1,3}
-  b[2] = -((x[0] - p0[0]) * n[0] + (x[1] - p0[1]) * n[1] + (x[2] - p0[2]) * n[2]) / vol;
+  s[2] = (x[0] - p0[0]) * n[0] + (x[1] - p0[1]) * n[1] + (x[2] - p0[2]) * n[2];
+  __builtin_amdgcn_sched_barrier(0);
   nonunit_normal(p0, p2, p1, n); // face 3: idir {0,2,1}
-  b[3] = -((x[0] - p0[0]) * n[0] + (x[1] - p0[1]) * n[1] + (x[2] - p0[2]) * n[2]) / vol;
+  s[3] = (x[0] - p0[0]) * n[0] + (x[1] - p0[1]) * n[1] + (x[2] - p0[2]) * n[2];
+  return vol;
+}
+
+// PMMG_barycoord3d_compute: b[f] = -s[f] / vol, unsorted
+__device__ __forceinline__ double tet_bary(const double *x, const double *p0, const double *p1, const double *p2,
+                                           const double *p3, double *b) {
+  double s[4];
+  double vol = tet_dots(x, p0, p1, p2, p3, s);
+#pragma unroll
+  for (int f = 0; f < 4; f++) b[f] = -s[f] / vol;
   return vol;
 }
 

@@ -3,7 +3,7 @@
 //
 // Replaces, behind the C-ABI of include/parmmg_hip.h, the per-group body of
 // PMMG_interpMetricsAndFields (reference src/interpmesh_pmmg.c:477-741):
-//   PMMG_locatePointVol      src/locate_pmmg.c:786-883   -> k_vol_locate (one lane per query)
+//   PMMG_locatePointVol      src/locate_pmmg.c:786-883   -> step_vol / k_vol_walk, k_vol_fused
 //   PMMG_interp4bar_*        src/interpmesh_pmmg.c:206-270 -> k_vol_interp<slot layout>
 //   PMMG_locatePointBdy      src/locate_pmmg.c:587-723   -> k_bdy (locate + interpolate)
 //   exhaustive / closest     src/locate_pmmg.c:477-515, 737-770 -> k_*_exhaust*, k_*_finish
@@ -19,7 +19,7 @@
 //      is already spatially coherent, a stable class compaction     k_bin_*, DeviceSelect
 //   4. volume: lean walk kernel writing the located tetra per query,
 //      then an interpolation kernel specialised on the slot layout
-//      so that every row gather is issued before any math           k_vol_locate, k_vol_interp
+//      so that every row gather is issued before any math           k_vol_walk, k_vol_interp
 //   5. surface: tria walk + wedge/cone + interpolation              k_bdy
 //   6. queries whose walk got stuck / ran too long: brute-force
 //      scans with the reference's exhaustive semantics              k_*_exhaust*, k_*_finish
@@ -110,17 +110,23 @@ __global__ void k_frame_final(Frame *fr, int g, int gs, int gb) {
   }
 }
 
-// volume seeds: per cell, the sampled tetra whose first vertex is closest to
+// volume seeds: per cell, the sampled tetra whose centroid is closest to
 // the cell centre; key = (float(dist^2) bits << 32) | id -> deterministic min
 __global__ __launch_bounds__(kBlock) void k_seed_vol(Bg bg, const Frame *fr, unsigned long long *cell, int g,
                                                      long long nsamp) {
   for (long long s = blockIdx.x * (long long)blockDim.x + threadIdx.x; s < nsamp;
        s += (long long)gridDim.x * blockDim.x) {
     int k = 1 + (int)((s * (long long)bg.ne) / nsamp);
-    int v0 = bg.tetv[k - 1].x;
-    if (v0 <= 0) continue;
-    double p[3];
-    load_pt(bg.xyz, v0, p);
+    const int4 tv = tetv_row(bg, k);
+    if (tv.x <= 0) continue;
+    // tetra centroid (a cell's seed is the sampled tetra whose centroid is
+    // closest to the cell centre)
+    double p[3], a[3], b[3], e[3];
+    load_pt(bg.xyz, tv.x, p);
+    load_pt(bg.xyz, tv.y, a);
+    load_pt(bg.xyz, tv.z, b);
+    load_pt(bg.xyz, tv.w, e);
+    for (int d = 0; d < 3; d++) p[d] = 0.25 * (p[d] + a[d] + b[d] + e[d]);
     int c[3];
     float d2 = 0.f;
     for (int d = 0; d < 3; d++) {
@@ -149,16 +155,18 @@ __global__ __launch_bounds__(kBlock) void k_seed_srf(Bg bg, const Frame *fr, int
   }
 }
 
-__device__ __forceinline__ int seed_vol(const unsigned long long *cell, int g, const Frame *fr, const double *x) {
-  int ci = cell_coord(x[0], fr->lo[0], fr->inv_vol[0], g);
-  int cj = cell_coord(x[1], fr->lo[1], fr->inv_vol[1], g);
-  int ck = cell_coord(x[2], fr->lo[2], fr->inv_vol[2], g);
-  unsigned long long s = cell[ci + (size_t)g * (cj + (size_t)g * ck)];
-  if (s != ~0ULL) return (int)(unsigned)(s & 0xFFFFFFFFULL);
+// rare path of seed_vol (empty cell): lowest seed id in the shells of
+// radius 1 then 2 around the cell; kept out of line so the walk kernels do
+// not carry its registers
+__device__ __forceinline__ int seed_vol_ring(const unsigned long long *cell, int g, int ci, int cj, int ck) {
+#pragma unroll 1
   for (int r = 1; r <= 2; r++) {
     unsigned long long best = ~0ULL;
+#pragma unroll 1
     for (int dk = -r; dk <= r; dk++)
+#pragma unroll 1
       for (int dj = -r; dj <= r; dj++)
+#pragma unroll 1
         for (int di = -r; di <= r; di++) {
           if (max(abs(di), max(abs(dj), abs(dk))) != r) continue;
           int a = ci + di, b = cj + dj, c = ck + dk;
@@ -170,6 +178,15 @@ __device__ __forceinline__ int seed_vol(const unsigned long long *cell, int g, c
     if (best != ~0ULL) return (int)best;
   }
   return 1;
+}
+
+__device__ __forceinline__ int seed_vol(const unsigned long long *cell, int g, const Frame *fr, const double *x) {
+  int ci = cell_coord(x[0], fr->lo[0], fr->inv_vol[0], g);
+  int cj = cell_coord(x[1], fr->lo[1], fr->inv_vol[1], g);
+  int ck = cell_coord(x[2], fr->lo[2], fr->inv_vol[2], g);
+  unsigned long long s = cell[ci + (size_t)g * (cj + (size_t)g * ck)];
+  if (s != ~0ULL) return (int)(unsigned)(s & 0xFFFFFFFFULL);
+  return seed_vol_ring(cell, g, ci, cj, ck);
 }
 
 __device__ int seed_srf(const int *cell, int g, const Frame *fr, const double *x) {
@@ -315,6 +332,13 @@ __device__ __forceinline__ void wave_stats(BlockStats *bs, bool active, int hit,
   }
 }
 
+// per-wave sum of a counter into a BlockStats slot
+__device__ __forceinline__ void wave_count(BlockStats *bs, int slot, int v) {
+  unsigned int s = (unsigned)v;
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off);
+  if (__lane_id() == 0 && s) atomicAdd(&bs->cnt[slot], s);
+}
+
 // ---------------------------------------------------------------- volume
 
 // PMMG_locatePointVol (locate_pmmg.c:786-883) from a grid seed instead of the
@@ -322,100 +346,180 @@ __device__ __forceinline__ void wave_stats(BlockStats *bs, bool active, int hit,
 // accepting tetra, or 0 when the walk got stuck / exceeded maxstep (the query
 // then goes to the exhaustive kernels).
 //
-// Stepping through face f into k' = adja/4, the 3 vertices of f are shared:
-// their coordinates stay in registers and only the tetv/adja rows of k' and
-// its opposite vertex tetv[k'][adja%4] are fetched (5 loads per step instead
-// of 14).
-__device__ __forceinline__ int4 load_row_or_zero(const int4 *rows, int code) {
-  return code > 0 ? rows[(code >> 2) - 1] : make_int4(0, 0, 0, 0);
-}
-
-__device__ __forceinline__ void pick_pt(int id, const int4 &tv, const double (*p)[3], double *out) {
-  const int j = id == tv.x ? 0 : (id == tv.y ? 1 : (id == tv.z ? 2 : 3));
-#pragma unroll
-  for (int d = 0; d < 3; d++) out[d] = j == 0 ? p[0][d] : (j == 1 ? p[1][d] : (j == 2 ? p[2][d] : p[3][d]));
-}
-
-// the walk of one query; returns 1 found (k, tv, b = its barycentric
-// coordinates), 2 stuck, 3 over-long
-__device__ __forceinline__ int walk_vol(const Bg &bg, const unsigned long long *grid, int g, const Frame *fr,
-                                        const double *x, int maxstep, int &k, int4 &tv, double *b, int &steps) {
-  k = seed_vol(grid, g, fr, x);
-  tv = bg.tetv[k - 1];
-  int4 ad = bg.adja[k - 1];
-  double p[4][3];
+// One exact division per step.  The reference accepts tetra k iff
+// min_f bary[f] > -MMG5_EPS with bary[f] = -s[f]/vol (s = tet_dots).  IEEE
+// division is sign-symmetric and monotone, so for vol > 0
+//   min_f fl(-s[f]/vol) = -fl(max_f s[f] / vol)
+// (for vol < 0 with min_f s[f]): the acceptance decision is bit-identical to
+// the reference's while only one of its four divisions is evaluated.  The
+// face to step through is the reference's first sorted coordinate whose
+// neighbour exists and is unvisited, i.e. the eligible face of smallest
+// bary = largest sign(vol)*s (ties: lowest face index); quotients that round
+// to equal values may order differently than the reference's qsort, which
+// changes only the path of the walk, never which tetra accept (parity
+// classes of tests/parity.py).  Degenerate tetra (vol == 0) take the
+// reference's four divisions and ranking.
+//
+// Vertices are reloaded at every step (3 of the 4 rows are L1 hits: the
+// shared face) instead of carried over and permuted in registers: fewer live
+// registers, so more waves per SIMD hide the dependent gathers.
+__device__ __forceinline__ void load_tet_pts(const Bg &bg, const int4 &tv, double (*p)[3]) {
   load_pt(bg.xyz, tv.x, p[0]);
   load_pt(bg.xyz, tv.y, p[1]);
   load_pt(bg.xyz, tv.z, p[2]);
   load_pt(bg.xyz, tv.w, p[3]);
+}
+
+// One step of the walk at tetra k: the reference's acceptance test (exact,
+// one division, see above) and, when it fails, the face to leave through.
+// Returns 1 inside, 0 moved (k = neighbour, hist updated), 2 stuck.
+__device__ __forceinline__ int step_vol(const Bg &bg, const double *x, int &k, int *hist) {
+  const int4 tv = tetv_row(bg, k);
+  const int4 ad = adja_row(bg, k);
+  double p[4][3];
+  load_tet_pts(bg, tv, p);
+  double s[4];
+  const double vol = tet_dots(x, p[0], p[1], p[2], p[3], s);
+  double key[4]; // larger = more negative barycentric coordinate
+  bool inside;
+  if (vol > 0.0 || vol < 0.0) {
+    double sm;
+    if (vol > 0.0) {
+      sm = s[0];
+      sm = s[1] > sm ? s[1] : sm;
+      sm = s[2] > sm ? s[2] : sm;
+      sm = s[3] > sm ? s[3] : sm;
+    } else {
+      sm = s[0];
+      sm = s[1] < sm ? s[1] : sm;
+      sm = s[2] < sm ? s[2] : sm;
+      sm = s[3] < sm ? s[3] : sm;
+    }
+    inside = -(sm / vol) > -kEps;
+#pragma unroll
+    for (int f = 0; f < 4; f++) key[f] = vol > 0.0 ? s[f] : -s[f];
+  } else {
+    double b[4];
+#pragma unroll
+    for (int f = 0; f < 4; f++) b[f] = -s[f] / vol;
+    inside = min4(b) > -kEps;
+    int r[4];
+    ranks4(b, r);
+#pragma unroll
+    for (int f = 0; f < 4; f++) key[f] = (double)(3 - r[f]);
+  }
+  if (inside) return 1;
+  int f = -1;
+  double best = 0.0;
+#pragma unroll
+  for (int ff = 0; ff < 4; ff++) {
+    const int iel = sel4(ad, ff) >> 2;
+    bool vis = false;
+#pragma unroll
+    for (int h = 0; h < kHist; h++) vis = vis || (hist[h] == iel);
+    if (iel != 0 && !vis && (f < 0 || key[ff] > best)) { f = ff; best = key[ff]; }
+  }
+  if (f < 0) return 2;
+#pragma unroll
+  for (int h = kHist - 1; h > 0; h--) hist[h] = hist[h - 1];
+  hist[0] = k;
+  k = sel4(ad, f) >> 2;
+  return 0;
+}
+
+// the walk of one query; returns 1 found (k, tv = its vertices), 2 stuck,
+// 3 over-long
+__device__ __forceinline__ int walk_vol(const Bg &bg, const unsigned long long *grid, int g, const Frame *fr,
+                                        const double *x, int maxstep, int &k, int4 &tv, int &steps) {
+  k = seed_vol(grid, g, fr, x);
   int hist[kHist];
 #pragma unroll
   for (int h = 0; h < kHist; h++) hist[h] = 0;
   for (;;) {
     ++steps;
-    tet_bary(x, p[0], p[1], p[2], p[3], b);
-    if (min4(b) > -kEps) return 1;
-    int r[4];
-    ranks4(b, r);
-    int f = -1, nrank = 4;
-#pragma unroll
-    for (int ff = 0; ff < 4; ff++) {
-      int iel = sel4(ad, ff) >> 2;
-      bool vis = false;
-#pragma unroll
-      for (int h = 0; h < kHist; h++) vis = vis || (hist[h] == iel);
-      if (iel != 0 && !vis && r[ff] < nrank) { f = ff; nrank = r[ff]; }
+    const int r = step_vol(bg, x, k, hist);
+    if (r == 1) {
+      tv = tetv_row(bg, k);
+      return 1;
     }
-    if (f < 0) return 2;            // stuck -> exhaustive
-    if (steps >= maxstep) return 3; // over-long -> exhaustive
-    const int code = sel4(ad, f);
-    const int next = code >> 2, iopp = code & 3;
-    const int4 tn = bg.tetv[next - 1];
-    ad = bg.adja[next - 1];
-    double pn[3];
-    load_pt(bg.xyz, sel4(tn, iopp), pn);
-    double q[4][3];
-#pragma unroll
-    for (int l = 0; l < 4; l++) {
-      if (l == iopp) { q[l][0] = pn[0]; q[l][1] = pn[1]; q[l][2] = pn[2]; }
-      else pick_pt(sel4(tn, l), tv, p, q[l]);
-    }
-#pragma unroll
-    for (int l = 0; l < 4; l++)
-#pragma unroll
-      for (int d = 0; d < 3; d++) p[l][d] = q[l][d];
-#pragma unroll
-    for (int h = kHist - 1; h > 0; h--) hist[h] = hist[h - 1];
-    hist[0] = k;
-    k = next;
-    tv = tn;
+    if (r == 2) return 2;
+    if (steps >= maxstep) return 3;
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_vol_locate(Bg bg, const Frame *fr, const unsigned long long *grid, int g,
-                                                       const double *qxyz, const int *order, int *vloc, int *fb,
-                                                       DevStats *st, int maxstep) {
+// Volume walks, flattened per lane (split pipeline, default).
+//
+// A block owns kBlock*C consecutive queries of the processing order; lane l
+// of wave w walks queries base_w + j*64 + l, j = 0..C-1, one after the other.
+// Every loop iteration is ONE walk step for every live lane: a lane whose
+// query is located (or stuck) records it and starts its next query in the
+// same iteration, so the wave never idles waiting for its longest walk
+// (with one query per lane, each wave ran for the maximum of its 64 walks,
+// ~3x the mean).  The 64 lanes of a wave stay on 64 neighbouring queries,
+// so the wave's footprint in the background stays compact and L2-resident.
+// vloc[pos] = accepting tetra, 0 = stuck / over-long (-> exhaustive list).
+__global__ __launch_bounds__(kBlock) void k_vol_walk(Bg bg, const Frame *fr, const unsigned long long *grid, int g,
+                                                     const double *qxyz, const int *order, int *vloc, int *fb,
+                                                     DevStats *st, int maxstep, int C) {
   __shared__ BlockStats bs;
   bstats_init(&bs);
   __syncthreads();
   const int nvol = st->nvol;
-  const int stride = gridDim.x * blockDim.x;
-  const int iters = (nvol + stride - 1) / stride;
-  for (int it = 0; it < iters; it++) {
-    const int i = it * stride + xcd_block() * blockDim.x + threadIdx.x;
-    const bool active = i < nvol;
-    int status = 0, steps = 0, k = 0, ip = 0;
-    if (active) {
-      ip = order[i];
-      double x[3], b[4];
-      load_pt(qxyz, ip, x);
-      int4 tv;
-      status = walk_vol(bg, grid, g, fr, x, maxstep, k, tv, b, steps);
-      vloc[i] = status == 1 ? k : 0;
+  const int lb = xcd_block();
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long long wbase = ((long long)lb * (kBlock / 64) + w) * 64LL * C;
+  long long pos = wbase + lane;
+  int j = 0;
+  int nsteps = 0, nfound = 0, smax = 0;
+  bool live = pos < nvol;
+  double x[3];
+  int k = 0, steps = 0, ip = 0, ipn = 0;
+  int hist[kHist];
+  if (live) {
+    ip = order[pos];
+    ipn = (C > 1 && pos + 64 < nvol) ? order[pos + 64] : 0;
+    load_pt(qxyz, ip, x);
+    k = seed_vol(grid, g, fr, x);
+#pragma unroll
+    for (int h = 0; h < kHist; h++) hist[h] = 0;
+  }
+  while (live) {
+    ++steps;
+    const int r = step_vol(bg, x, k, hist);
+    const bool over = r == 0 && steps >= maxstep;
+    if (r != 0 || over) {
+      // query done: accepted (r == 1), stuck (2) or over-long
+      vloc[pos] = r == 1 ? k : 0;
+      if (r != 1) fb[atomicAdd(&st->nfb_vol, 1)] = ip;
+      nfound += r == 1;
+      nsteps += steps;
+      smax = steps > smax ? steps : smax;
+      steps = 0;
+      ++j;
+      pos += 64;
+      live = j < C && pos < nvol;
+      if (live) {
+        ip = ipn;
+        ipn = (j + 1 < C && pos + 64 < nvol) ? order[pos + 64] : 0;
+        load_pt(qxyz, ip, x);
+        k = seed_vol(grid, g, fr, x);
+#pragma unroll
+        for (int h = 0; h < kHist; h++) hist[h] = 0;
+      }
     }
-    int slot = wave_append(&st->nfb_vol, active && status != 1);
-    if (active && status != 1) fb[slot] = ip;
-    wave_stats(&bs, active, status == 1 ? PMMG_HIT_VOL_WALK : 0, steps);
+  }
+  wave_count(&bs, PMMG_HIT_VOL_WALK, nfound);
+  {
+    unsigned int s = (unsigned)nsteps, mx = (unsigned)smax;
+    for (int off = 32; off > 0; off >>= 1) {
+      s += __shfl_down(s, off);
+      unsigned o = __shfl_down(mx, off);
+      mx = o > mx ? o : mx;
+    }
+    if (__lane_id() == 0) {
+      if (s) atomicAdd(&bs.steps, (unsigned long long)s);
+      atomicMax(&bs.stepmax, mx);
+    }
   }
   __syncthreads();
   bstats_flush(&bs, st);
@@ -448,7 +552,7 @@ __global__ __launch_bounds__(kBlock) void k_vol_interp(Bg bg, const double *qxyz
     const int ip = order[i];
     double x[3], p0[3], p1[3], p2[3], p3[3], phi[4];
     load_pt(qxyz, ip, x);
-    const int4 tv = bg.tetv[k - 1];
+    const int4 tv = tetv_row(bg, k);
     load_pt(bg.xyz, tv.x, p0);
     load_pt(bg.xyz, tv.y, p1);
     load_pt(bg.xyz, tv.z, p2);
@@ -479,11 +583,13 @@ __global__ __launch_bounds__(kBlock) void k_vol_fused(Bg bg, const Frame *fr, co
     int status = 0, steps = 0, k = 0, ip = 0;
     if (active) {
       ip = order[i];
-      double x[3], b[4];
-      load_pt(qxyz, ip, x);
       int4 tv;
-      status = walk_vol(bg, grid, g, fr, x, maxstep, k, tv, b, steps);
+      double x[3], b[4], p[4][3];
+      load_pt(qxyz, ip, x);
+      status = walk_vol(bg, grid, g, fr, x, maxstep, k, tv, steps);
       if (status == 1) {
+        load_tet_pts(bg, tv, p);
+        tet_bary(x, p[0], p[1], p[2], p[3], b); // the reference's coordinates, exactly
         const int v[4] = {tv.x, tv.y, tv.z, tv.w};
         interp_vol_layout<C0, C1, C2, C3, C4, C5>(S, ip, v, b);
         if (elem_out) elem_out[ip - 1] = k;
@@ -546,7 +652,7 @@ __global__ __launch_bounds__(kBlock) void k_vol_scan(Bg bg, const Frame *fr, int
   unsigned long long tests = 0;
   for (long long kk = lo_k + (long long)bi * blockDim.x + threadIdx.x; kk < hi_k; kk += (long long)bpx * blockDim.x) {
     const int k = (int)kk + 1;
-    const int4 tv = bg.tetv[k - 1];
+    const int4 tv = tetv_row(bg, k);
     if (tv.x <= 0) continue;
     double p0[3], p1[3], p2[3], p3[3];
     load_pt(bg.xyz, tv.x, p0);
@@ -607,7 +713,7 @@ __global__ __launch_bounds__(kBlock) void k_vol_interp_scan(Bg bg, const double 
       if (k != INT_MAX) {
         double x[3], p0[3], p1[3], p2[3], p3[3], phi[4];
         load_pt(qs, i + 1, x);
-        const int4 tv = bg.tetv[k - 1];
+        const int4 tv = tetv_row(bg, k);
         load_pt(bg.xyz, tv.x, p0);
         load_pt(bg.xyz, tv.y, p1);
         load_pt(bg.xyz, tv.z, p2);
@@ -745,7 +851,7 @@ __global__ __launch_bounds__(kBlock) void k_vol_exhaust_accept(Bg bg, const doub
     for (int j = threadIdx.x; j < nq; j += blockDim.x) load_pt(qxyz, fb[q0 + j], sx[j]);
     __syncthreads();
     for (int k = 1 + blockIdx.x * blockDim.x + threadIdx.x; k <= bg.ne; k += gridDim.x * blockDim.x) {
-      int4 tv = bg.tetv[k - 1];
+      int4 tv = tetv_row(bg, k);
       if (tv.x <= 0) continue;
       double p0[3], p1[3], p2[3], p3[3];
       load_pt(bg.xyz, tv.x, p0);
@@ -795,7 +901,7 @@ __global__ __launch_bounds__(kBlock) void k_vol_exhaust_closest(Bg bg, const dou
     for (int j = 0; j < nq; j++) any = any || sneed[j];
     if (!any) continue;
     for (int k = 1 + blockIdx.x * blockDim.x + threadIdx.x; k <= bg.ne; k += gridDim.x * blockDim.x) {
-      int4 tv = bg.tetv[k - 1];
+      int4 tv = tetv_row(bg, k);
       if (tv.x <= 0) continue;
       double p0[3], p1[3], p2[3], p3[3];
       load_pt(bg.xyz, tv.x, p0);
@@ -826,7 +932,7 @@ __global__ __launch_bounds__(kBlock) void k_vol_finish(Bg bg, const double *qxyz
     if (best[j] != INT_MAX) { k = best[j]; hit = PMMG_HIT_VOL_EXHAUST; }
     else { k = cidx[j]; hit = PMMG_HIT_VOL_CLOSEST; }
     if (k == INT_MAX || k <= 0) continue;
-    int4 tv = bg.tetv[k - 1];
+    int4 tv = tetv_row(bg, k);
     double p[4][3], phi[4];
     load_pt(bg.xyz, tv.x, p[0]);
     load_pt(bg.xyz, tv.y, p[1]);
@@ -1006,11 +1112,13 @@ struct pmmg_hip_ctx {
   std::vector<DevBuf> h_f;
   hipEvent_t ev[8] = {};
   bool pending = false;
-  int tpc = 16;     // background tetra per volume seed cell
+  int tpc = 4;      // background tetra per volume seed cell
   int spc = 1;      // sampled tetra per seed cell
   int qpb = 8;      // queries per Morton bin (walk path)
   int qpc = 1;      // queries per scan cell (scan path)
-  int maxstep = 1 << 16;
+  int ncu = 256;     // compute units of the device
+  int chain = 0;     // queries per lane in k_vol_walk (0 = automatic)
+  int maxstep = 4096; // longer walks go to the exhaustive kernels (the reference caps at ne)
   int last_sorted = 0;
   int *h_small = nullptr; // pinned host words for the two small read-backs
 };
@@ -1097,6 +1205,12 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   c->qpb = env_int("PMMG_HIP_QPB", c->qpb);
   c->qpc = env_int("PMMG_HIP_QPC", c->qpc);
   c->maxstep = env_int("PMMG_HIP_MAXSTEP", c->maxstep);
+  c->chain = env_int("PMMG_HIP_CHAIN", c->chain);
+  {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+      c->ncu = prop.multiProcessorCount;
+  }
   return c;
 }
 
@@ -1120,11 +1234,14 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
 
 const char *pmmg_hip_last_error(pmmg_hip_ctx *c) { return c ? c->err : "null context"; }
 
-int pmmg_hip_set_background(pmmg_hip_ctx *c, int np, const double *xyz, int ne, const int *tetv, const int *adja,
-                            int nt, const int *triv, const int *adjt, double hausd, int where) {
+// shared body of the two background entry points: tet8 != NULL selects the
+// packed {v[4], adja[4]} records, else the separate tetv / adja arrays
+static int set_background_impl(pmmg_hip_ctx *c, int np, const double *xyz, int ne, const int *tetv, const int *adja,
+                               const int *tet8, int nt, const int *triv, const int *adjt, double hausd, int where) {
   if (!c) return 0;
   HIPCK(c, hipSetDevice(c->device));
-  if (np <= 0 || ne <= 0 || !xyz || !tetv || !adja || nt < 0 || (nt > 0 && (!triv || !adjt))) {
+  const bool packed = tet8 != nullptr;
+  if (np <= 0 || ne <= 0 || !xyz || (!packed && (!tetv || !adja)) || nt < 0 || (nt > 0 && (!triv || !adjt))) {
     set_err(c, "set_background: invalid arguments (np=%d ne=%d nt=%d)", np, ne, nt);
     return 0;
   }
@@ -1136,30 +1253,54 @@ int pmmg_hip_set_background(pmmg_hip_ctx *c, int np, const double *xyz, int ne, 
   c->bg.ne = ne;
   c->bg.nt = nt;
   c->bg.hausd = hausd;
+  c->bg.tstride = packed ? 2 : 1;
   if (where == PMMG_HIP_DEVICE) {
-    if (((uintptr_t)tetv & 15) || ((uintptr_t)adja & 15)) {
-      set_err(c, "set_background: device tetv/adja must be 16-byte aligned");
+    const void *t0 = packed ? (const void *)tet8 : (const void *)tetv;
+    if (((uintptr_t)t0 & 15) || (!packed && ((uintptr_t)adja & 15))) {
+      set_err(c, "set_background: device tetra arrays must be 16-byte aligned");
       return 0;
     }
     c->bg.xyz = xyz;
-    c->bg.tetv = reinterpret_cast<const int4 *>(tetv);
-    c->bg.adja = reinterpret_cast<const int4 *>(adja);
+    c->bg.tetv = reinterpret_cast<const int4 *>(packed ? tet8 : tetv);
+    c->bg.adja = reinterpret_cast<const int4 *>(packed ? tet8 + 4 : adja);
     c->bg.triv = triv;
     c->bg.adjt = adjt;
     return 1;
   }
   if (!upload(c, c->o_xyz, xyz, sizeof(double) * 3 * (size_t)np)) return 0;
-  if (!upload(c, c->o_tetv, tetv, sizeof(int) * 4 * (size_t)ne)) return 0;
-  if (!upload(c, c->o_adja, adja, sizeof(int) * 4 * (size_t)ne)) return 0;
+  if (packed) {
+    if (!upload(c, c->o_tetv, tet8, sizeof(int) * 8 * (size_t)ne)) return 0;
+  } else {
+    if (!upload(c, c->o_tetv, tetv, sizeof(int) * 4 * (size_t)ne)) return 0;
+    if (!upload(c, c->o_adja, adja, sizeof(int) * 4 * (size_t)ne)) return 0;
+  }
   if (!upload(c, c->o_triv, triv, sizeof(int) * 3 * (size_t)nt)) return 0;
   if (!upload(c, c->o_adjt, adjt, sizeof(int) * 3 * (size_t)nt)) return 0;
   HIPCK(c, hipStreamSynchronize(c->stream));
   c->bg.xyz = (const double *)c->o_xyz.p;
   c->bg.tetv = (const int4 *)c->o_tetv.p;
-  c->bg.adja = (const int4 *)c->o_adja.p;
+  c->bg.adja = packed ? (const int4 *)c->o_tetv.p + 1 : (const int4 *)c->o_adja.p;
   c->bg.triv = (const int *)c->o_triv.p;
   c->bg.adjt = (const int *)c->o_adjt.p;
   return 1;
+}
+
+int pmmg_hip_set_background(pmmg_hip_ctx *c, int np, const double *xyz, int ne, const int *tetv, const int *adja,
+                            int nt, const int *triv, const int *adjt, double hausd, int where) {
+  if (c && (!tetv || !adja)) {
+    set_err(c, "set_background: tetv / adja is NULL");
+    return 0;
+  }
+  return set_background_impl(c, np, xyz, ne, tetv, adja, nullptr, nt, triv, adjt, hausd, where);
+}
+
+int pmmg_hip_set_background_tet8(pmmg_hip_ctx *c, int np, const double *xyz, int ne, const int *tet8, int nt,
+                                 const int *triv, const int *adjt, double hausd, int where) {
+  if (c && !tet8) {
+    set_err(c, "set_background_tet8: tet8 is NULL");
+    return 0;
+  }
+  return set_background_impl(c, np, xyz, ne, nullptr, nullptr, tet8, nt, triv, adjt, hausd, where);
 }
 
 int pmmg_hip_set_solutions(pmmg_hip_ctx *c, int met_size, const double *met, int nfield, const int *field_size,
@@ -1419,9 +1560,14 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[2], s));
 
-  if (c->options & PMMG_HIP_OPT_SPLIT) {
-    hipLaunchKernelGGL(k_vol_locate, dim3(blocks_for(np_new, 1 << 30)), dim3(kBlock), 0, s, bg, fr, grid, g, xyz_new,
-                       order_v, (int *)c->vloc.p, (int *)c->fb_vol.p, st, c->maxstep);
+  if (!(c->options & PMMG_HIP_OPT_FUSED)) {
+    // C = 1 (one query per lane, lanes of a wave in lockstep on neighbouring
+    // queries) measured fastest: neighbouring walks share tetra and vertex
+    // lines inside each wave-instruction; desynchronised chains lose that
+    const int C = c->chain > 0 ? c->chain : 1;
+    const long long nblk = (np_new + (long long)kBlock * C - 1) / ((long long)kBlock * C);
+    hipLaunchKernelGGL(k_vol_walk, dim3((unsigned)nblk), dim3(kBlock), 0, s, bg, fr, grid, g, xyz_new, order_v,
+                       (int *)c->vloc.p, (int *)c->fb_vol.p, st, c->maxstep, C);
     HIPCK(c, hipEventRecord(c->ev[6], s));
     VolInterpFn interp = pick_layout(S).fn;
     hipLaunchKernelGGL(interp, dim3(blocks_for(np_new, 1 << 30)), dim3(kBlock), 0, s, bg, xyz_new, order_v,

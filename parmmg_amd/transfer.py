@@ -62,17 +62,24 @@ def device_count() -> int:
     return int(hip_lib().pmmg_hip_device_count())
 
 
+def pack_tet8(tetv: np.ndarray, adja: np.ndarray) -> np.ndarray:
+    """Packed tetra records {v0..v3, adja0..adja3} (include/parmmg_hip.h,
+    pmmg_hip_set_background_tet8): what a host shim builds while packing
+    MMG5_Tetra.v."""
+    return np.ascontiguousarray(np.hstack([np.asarray(tetv, np.int32), np.asarray(adja, np.int32)]))
+
+
 class TransferContext:
     """One ``pmmg_hip_ctx`` on a HIP device."""
 
-    def __init__(self, device: int = 0, sort: bool | None = None, scan: bool = False, split: bool = False):
+    def __init__(self, device: int = 0, sort: bool | None = None, scan: bool = False, fused: bool = False):
         """Volume points are located by per-query adjacency walks (default)
         or, with scan=True, by the tetra-centric scan.  sort=None picks the
         query order automatically (Morton-bin unless the numbering is
-        coherent); True / False force binning / input order.  split=True runs
-        the walk and the interpolation as two kernels."""
+        coherent); True / False force binning / input order.  fused=True runs
+        the walk and the interpolation as one kernel."""
         self.lib = hip_lib()
-        opts = (0 if sort is None else (2 if sort else 1)) | (4 if scan else 0) | (8 if split else 0)
+        opts = (0 if sort is None else (2 if sort else 1)) | (4 if scan else 0) | (8 if fused else 0)
         self.h = self.lib.pmmg_hip_create(int(device), opts)
         if not self.h:
             raise RuntimeError(f"pmmg_hip_create({device}) failed: no usable HIP device (the transfer step has "
@@ -128,6 +135,16 @@ class TransferContext:
         self._keep = [xyz, tetv, adja, triv, adjt]
         self._ck(self.lib.pmmg_hip_set_background(self.h, npt, _p(xyz), ne, _p(tetv), _p(adja), nt, _p(triv),
                                                   _p(adjt), float(hausd), where), "set_background")
+
+    def set_background_tet8(self, xyz, tet8, triv, adjt, hausd: float) -> None:
+        """Background with packed {v[4], adja[4]} tetra records (pack_tet8)."""
+        where = DEVICE if isinstance(xyz, DeviceArray) else HOST
+        npt, ne, nt = xyz.shape[0], tet8.shape[0], triv.shape[0]
+        if tet8.shape[1] != 8:
+            raise ValueError("tet8 must have 8 ints per tetra")
+        self._keep = [xyz, tet8, triv, adjt]
+        self._ck(self.lib.pmmg_hip_set_background_tet8(self.h, npt, _p(xyz), ne, _p(tet8), nt, _p(triv), _p(adjt),
+                                                       float(hausd), where), "set_background_tet8")
 
     def set_solutions(self, met, fields) -> None:
         fields = list(fields)

@@ -46,12 +46,16 @@ def make_case(kind=synth.CUBE, n_old=6, n_new=7, metric=synth.F_ANI,
     return case
 
 
-def run_gpu(case, sort=None, ctx=None, scan=False, split=False):
+def run_gpu(case, sort=None, ctx=None, scan=False, fused=False, tet8=False):
     bg, new = case["bg"], case["new"]
     own = ctx is None
-    ctx = ctx or TransferContext(0, sort=sort, scan=scan, split=split)
+    ctx = ctx or TransferContext(0, sort=sort, scan=scan, fused=fused)
     try:
-        ctx.set_background(bg.xyz, bg.tetv, bg.adja, bg.triv, bg.adjt, case["hausd"])
+        if tet8:
+            from parmmg_amd.transfer import pack_tet8
+            ctx.set_background_tet8(bg.xyz, pack_tet8(bg.tetv, bg.adja), bg.triv, bg.adjt, case["hausd"])
+        else:
+            ctx.set_background(bg.xyz, bg.tetv, bg.adja, bg.triv, bg.adjt, case["hausd"])
         ctx.set_solutions(case["met"], case["fields"])
         npn = new.np
         met_out = None if case["met"] is None else np.full((npn, case["met"].shape[1]), np.nan)

@@ -22,8 +22,9 @@ CASES = {
 }
 
 
-MODES = {"auto": {}, "morton": dict(sort=True), "nosort": dict(sort=False), "split": dict(split=True),
-         "scan": dict(scan=True)}
+MODES = {"auto": {}, "morton": dict(sort=True), "nosort": dict(sort=False), "fused": dict(fused=True),
+         "scan": dict(scan=True),
+         "tet8": dict(tet8=True), "tet8-scan": dict(tet8=True, scan=True)}
 
 
 @pytest.mark.gpu

@@ -66,11 +66,12 @@ def main(src, dst):
         wb = 1024.0 * sum(w) / len(w)
         pmc["kernels"][short(k)] = {"fetch_bytes": fb, "write_bytes": wb, "hbm_bytes": fb + wb,
                                     "fetch_raw_kib": sum(f) / len(f), "write_raw_kib": sum(w) / len(w)}
-    kv = [k for k in pmc["kernels"] if k.startswith("k_vol")]
+    # the volume stage: every k_vol* kernel of one call (walk + interpolation,
+    # or the fused kernel)
+    kv = sorted(k for k in pmc["kernels"] if k.startswith("k_vol") and "exhaust" not in k and "finish" not in k)
     if kv:
-        main_k = max(kv, key=lambda k: pmc["kernels"][k]["hbm_bytes"])
-        pmc["k_vol_kernel"] = main_k
-        pmc["k_vol_hbm_bytes_per_launch"] = pmc["kernels"][main_k]["hbm_bytes"]
+        pmc["k_vol_kernel"] = " + ".join(kv)
+        pmc["k_vol_hbm_bytes_per_launch"] = sum(pmc["kernels"][k]["hbm_bytes"] for k in kv)
     json.dump(pmc, open(os.path.join(dst, f"pmc_{pmc['workload']}.json"), "w"), indent=1)
     print(json.dumps({k: v for k, v in pmc.items() if k != "kernels"}, indent=1))
     for k, e in sorted(kern.items(), key=lambda kv: -kv[1]["total_ns"]):
