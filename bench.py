@@ -112,6 +112,8 @@ def main():
     ap.add_argument("--spc", type=int, default=0, help="sampled tetra per seed cell (0: module default)")
     ap.add_argument("--layout", default="tet8", choices=["tet8", "separate"],
                     help="HBM layout of the tetra: packed {v[4], adja[4]} records or separate tetv/adja arrays")
+    ap.add_argument("--solutions", default="separate", choices=["packed", "separate"],
+                    help="HBM layout of the metric/fields: packed per-vertex records or one array per solution")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -134,8 +136,13 @@ def main():
     else:
         d_tetv, d_adja = ctx.upload(bg.tetv), ctx.upload(bg.adja)
     d_triv, d_adjt = ctx.upload(bg.triv), ctx.upload(bg.adjt)
-    d_met = ctx.upload(met)
-    d_f = [ctx.upload(f) for f in fields]
+    from parmmg_amd.transfer import pack_solutions
+    if args.solutions == "packed":
+        rec, *recmeta = pack_solutions(met, fields)
+        d_rec = ctx.upload(rec)
+    else:
+        d_met = ctx.upload(met)
+        d_f = [ctx.upload(f) for f in fields]
     d_qxyz, d_pc = ctx.upload(new.xyz), ctx.upload(pclass)
     d_mo = ctx.empty((new.np, w.met_size), np.float64)
     d_fo = [ctx.empty((new.np, f.shape[1]), np.float64) for f in fields]
@@ -147,7 +154,10 @@ def main():
             ctx.set_background_tet8(d_xyz, d_tet8, d_triv, d_adjt, w.hausd)
         else:
             ctx.set_background(d_xyz, d_tetv, d_adja, d_triv, d_adjt, w.hausd)
-        ctx.set_solutions(d_met, d_f)
+        if args.solutions == "packed":
+            ctx.set_solutions_packed(d_rec, *recmeta)
+        else:
+            ctx.set_solutions(d_met, d_f)
         ctx.locate_interp(d_qxyz, d_pc, d_mo, d_fo, d_elem, d_hit, sync=False)
 
     log(f"[bench r{rank}] inputs resident in HBM; warmup {args.warmup} steps")
@@ -205,6 +215,7 @@ def main():
             "query_order": args.sort,
             "locate": args.locate,
             "tetra_layout": args.layout,
+            "solution_layout": args.solutions,
             "volume_kernels": "fused" if args.fused else "walk+interp",
             "morton_binned": bool(st.sorted),
         },

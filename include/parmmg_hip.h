@@ -148,6 +148,20 @@ int pmmg_hip_set_solutions(pmmg_hip_ctx *ctx, int met_size, const double *met,
                            int nfield, const int *field_size,
                            const double *const *fields, int where);
 
+/* Same solutions as packed per-vertex records (the module's preferred HBM
+ * layout: one vertex's metric and fields are one contiguous record, so the
+ * interpolation gathers one record per tetra vertex instead of one row per
+ * array):
+ *   rec[stride*np]   record of vertex v at rec + stride*(v-1); stride even,
+ *                    rec 16-byte aligned
+ *   met_off          first column of the metric (met_size columns)
+ *   field_off[j]     first column of field j (field_size[j] columns)
+ * Size-6 slots must start at even columns.  A host shim builds the records
+ * in the pass that copies met->m and field[j].m. */
+int pmmg_hip_set_solutions_packed(pmmg_hip_ctx *ctx, int met_size, int met_off,
+                                  int nfield, const int *field_size, const int *field_off,
+                                  const double *rec, int stride, int where);
+
 /* Locate every new point with pclass != PMMG_PT_SKIP and interpolate the
  * metric and fields into it.
  *   np_new         new-mesh vertices; xyz_new[3*np_new], pclass[np_new]

@@ -42,6 +42,8 @@ HIP_API = {
     "pmmg_hip_set_background_tet8": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p,
                                              c_double, c_int]),
     "pmmg_hip_set_solutions": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int]),
+    "pmmg_hip_set_solutions_packed": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int,
+                                              c_int]),
     "pmmg_hip_locate_interp": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                        c_void_p, P(HipStats), c_int]),
     "pmmg_hip_sync": (c_int, [c_void_p, P(HipStats)]),

@@ -45,10 +45,13 @@ __device__ __forceinline__ int4 adja_row(const Bg &bg, int k) { return bg.adja[(
 
 // one solution array: code 1 = scalar, 3 = vector (both P1 iso
 // interpolation), 6 = symmetric tensor (inverse-tensor interpolation)
+// `in` rows are `stride` doubles apart: the slot's own array (stride =
+// code) or its columns inside packed per-vertex records (stride = record size)
 struct Slot {
   const double *in;
   double *out;
   int code;
+  int stride;
 };
 
 struct Slots {
@@ -70,8 +73,24 @@ struct DevStats {
   int nvol, nbdy;
   int nfb_vol, nfb_bdy;
   int coherent;
-  int pad[2];
+  int ncont; // capped volume walks to continue (k_vol_walk_cont)
+  int pad;
 };
+
+// Statistics are accumulated into kStatParts partial records (block b ->
+// part b % kStatParts) placed after DevStats in the stats buffer and summed
+// on the host: one counter address hit by every workgroup serialises the
+// atomics at one L2 channel (a returning per-wave atomic on one address
+// measured +4 ms on cfg4).
+constexpr int kStatParts = 256;
+struct StatPart {
+  unsigned long long cnt[16];
+  unsigned long long steps;
+  unsigned long long stepmax;
+};
+__device__ __forceinline__ StatPart *stat_part(DevStats *st) {
+  return reinterpret_cast<StatPart *>(st + 1) + (blockIdx.x & (kStatParts - 1));
+}
 
 // ------------------------------------------------------------ small helpers
 
@@ -326,12 +345,13 @@ __device__ __forceinline__ void store6(double *p, const double *m) {
 // PMMG_interp{3,4}bar_iso (interpmesh_pmmg.c:125-149, 206-230):
 // out[j] = 0; out[j] += phi_i * old[v_i][j], i ascending
 template <int NV, int SZ>
-__device__ __forceinline__ void interp_iso(const double *in, const int *v, const double *phi, double *out) {
+__device__ __forceinline__ void interp_iso(const double *in, int stride, const int *v, const double *phi,
+                                           double *out) {
   double row[NV][SZ];
 #pragma unroll
   for (int i = 0; i < NV; i++)
 #pragma unroll
-    for (int j = 0; j < SZ; j++) row[i][j] = in[(size_t)SZ * (v[i] - 1) + j];
+    for (int j = 0; j < SZ; j++) row[i][j] = in[(size_t)stride * (v[i] - 1) + j];
   double acc[SZ];
 #pragma unroll
   for (int j = 0; j < SZ; j++) acc[j] = 0.0;
@@ -346,10 +366,11 @@ __device__ __forceinline__ void interp_iso(const double *in, const int *v, const
 // PMMG_interp{3,4}bar_ani (interpmesh_pmmg.c:166-190, 247-270):
 // M = invmat( sum_i phi_i invmat(M_i) ), row untouched if any inversion fails
 template <int NV>
-__device__ __forceinline__ void interp_ani(const double *in, const int *v, const double *phi, double *out) {
+__device__ __forceinline__ void interp_ani(const double *in, int stride, const int *v, const double *phi,
+                                           double *out) {
   double m[NV][6];
 #pragma unroll
-  for (int i = 0; i < NV; i++) load6(in + 6 * (size_t)(v[i] - 1), m[i]);
+  for (int i = 0; i < NV; i++) load6(in + (size_t)stride * (v[i] - 1), m[i]);
   double mint[6], mi[6];
   bool ok = true;
 #pragma unroll
@@ -364,8 +385,8 @@ __device__ __forceinline__ void interp_ani(const double *in, const int *v, const
 
 template <int NV, int CODE>
 __device__ __forceinline__ void interp_code(const Slot &sl, int ip, const int *v, const double *phi) {
-  if (CODE == 6) interp_ani<NV>(sl.in, v, phi, sl.out + 6 * (size_t)(ip - 1));
-  else interp_iso<NV, CODE>(sl.in, v, phi, sl.out + (size_t)CODE * (ip - 1));
+  if (CODE == 6) interp_ani<NV>(sl.in, sl.stride, v, phi, sl.out + 6 * (size_t)(ip - 1));
+  else interp_iso<NV, CODE>(sl.in, sl.stride, v, phi, sl.out + (size_t)CODE * (ip - 1));
 }
 
 template <int NV>
@@ -383,21 +404,21 @@ __device__ __forceinline__ void interp_edge(const Slot &sl, int ip, const int *v
   const double f0 = sel3d(phi[0], phi[1], phi[2], i0), f1 = sel3d(phi[0], phi[1], phi[2], i1);
   if (sl.code == 6) {
     double m[6], mi0[6], mi1[6], mint[6], r[6];
-    load6(sl.in + 6 * (size_t)(v0 - 1), m);
+    load6(sl.in + (size_t)sl.stride * (v0 - 1), m);
     bool ok = invmat(m, mi0);
-    load6(sl.in + 6 * (size_t)(v1 - 1), m);
+    load6(sl.in + (size_t)sl.stride * (v1 - 1), m);
     ok = invmat(m, mi1) && ok;
 #pragma unroll
     for (int s = 0; s < 6; s++) mint[s] = f0 * mi0[s] + f1 * mi1[s];
     if (invmat(mint, r) && ok) store6(sl.out + 6 * (size_t)(ip - 1), r);
   } else {
-    sl.out[ip - 1] = f0 * sl.in[v0 - 1] + f1 * sl.in[v1 - 1];
+    sl.out[ip - 1] = f0 * sl.in[(size_t)sl.stride * (v0 - 1)] + f1 * sl.in[(size_t)sl.stride * (v1 - 1)];
   }
 }
 
 __device__ __forceinline__ void copy_row(const Slot &sl, int ip, int vsrc) {
   double *out = sl.out + (size_t)sl.code * (ip - 1);
-  const double *in = sl.in + (size_t)sl.code * (vsrc - 1);
+  const double *in = sl.in + (size_t)sl.stride * (vsrc - 1);
   if (sl.code == 6) {
     double m[6];
     load6(in, m);

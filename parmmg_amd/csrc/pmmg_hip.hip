@@ -58,6 +58,10 @@ __global__ __launch_bounds__(kBlock) void k_reset(Frame *fr, DevStats *st, unsig
     for (size_t j = 0; j < sizeof(DevStats) / 4; j++) w[j] = 0u;
     if (keep_coherent) st->coherent = coh;
   }
+  {
+    unsigned long long *pw = reinterpret_cast<unsigned long long *>(st + 1);
+    for (long long j = tid; j < (long long)(kStatParts * sizeof(StatPart) / 8); j += nth) pw[j] = 0ULL;
+  }
   for (long long j = tid; j < ng; j += nth) grid[j] = ~0ULL;
   for (long long j = tid; j < nsg; j += nth) sgrid[j] = INT_MAX;
   for (long long j = tid; j < ncnt; j += nth) cnt[j] = 0;
@@ -113,20 +117,28 @@ __global__ void k_frame_final(Frame *fr, int g, int gs, int gb) {
 // volume seeds: per cell, the sampled tetra whose centroid is closest to
 // the cell centre; key = (float(dist^2) bits << 32) | id -> deterministic min
 __global__ __launch_bounds__(kBlock) void k_seed_vol(Bg bg, const Frame *fr, unsigned long long *cell, int g,
-                                                     long long nsamp) {
+                                                     long long nsamp, int mode) {
   for (long long s = blockIdx.x * (long long)blockDim.x + threadIdx.x; s < nsamp;
        s += (long long)gridDim.x * blockDim.x) {
     int k = 1 + (int)((s * (long long)bg.ne) / nsamp);
     const int4 tv = tetv_row(bg, k);
     if (tv.x <= 0) continue;
-    // tetra centroid (a cell's seed is the sampled tetra whose centroid is
-    // closest to the cell centre)
-    double p[3], a[3], b[3], e[3];
+    // representative point of the tetra: centroid (mode 0), midpoint of
+    // the edge v0-v3 (1), first vertex (2); a cell's seed is the sampled
+    // tetra whose point is closest to the cell centre
+    double p[3];
     load_pt(bg.xyz, tv.x, p);
-    load_pt(bg.xyz, tv.y, a);
-    load_pt(bg.xyz, tv.z, b);
-    load_pt(bg.xyz, tv.w, e);
-    for (int d = 0; d < 3; d++) p[d] = 0.25 * (p[d] + a[d] + b[d] + e[d]);
+    if (mode == 0) {
+      double a[3], b[3], e[3];
+      load_pt(bg.xyz, tv.y, a);
+      load_pt(bg.xyz, tv.z, b);
+      load_pt(bg.xyz, tv.w, e);
+      for (int d = 0; d < 3; d++) p[d] = 0.25 * (p[d] + a[d] + b[d] + e[d]);
+    } else if (mode == 1) {
+      double e[3];
+      load_pt(bg.xyz, tv.w, e);
+      for (int d = 0; d < 3; d++) p[d] = 0.5 * (p[d] + e[d]);
+    }
     int c[3];
     float d2 = 0.f;
     for (int d = 0; d < 3; d++) {
@@ -303,10 +315,11 @@ __device__ __forceinline__ void bstats_init(BlockStats *b) {
 }
 
 __device__ __forceinline__ void bstats_flush(BlockStats *b, DevStats *st) {
-  if (threadIdx.x < 16 && b->cnt[threadIdx.x]) atomicAdd(&st->cnt[threadIdx.x], (unsigned long long)b->cnt[threadIdx.x]);
+  StatPart *pt = stat_part(st);
+  if (threadIdx.x < 16 && b->cnt[threadIdx.x]) atomicAdd(&pt->cnt[threadIdx.x], (unsigned long long)b->cnt[threadIdx.x]);
   if (threadIdx.x == 0) {
-    if (b->steps) atomicAdd(&st->steps, b->steps);
-    atomicMax(&st->stepmax, b->stepmax);
+    if (b->steps) atomicAdd(&pt->steps, b->steps);
+    if (b->stepmax) atomicMax(&pt->stepmax, (unsigned long long)b->stepmax);
   }
 }
 
@@ -363,6 +376,12 @@ __device__ __forceinline__ void wave_count(BlockStats *bs, int slot, int v) {
 // Vertices are reloaded at every step (3 of the 4 rows are L1 hits: the
 // shared face) instead of carried over and permuted in registers: fewer live
 // registers, so more waves per SIMD hide the dependent gathers.
+__device__ __forceinline__ void pick_pt(int id, const int4 &tv, const double (*p)[3], double *out) {
+  const int j = id == tv.x ? 0 : (id == tv.y ? 1 : (id == tv.z ? 2 : 3));
+#pragma unroll
+  for (int d = 0; d < 3; d++) out[d] = j == 0 ? p[0][d] : (j == 1 ? p[1][d] : (j == 2 ? p[2][d] : p[3][d]));
+}
+
 __device__ __forceinline__ void load_tet_pts(const Bg &bg, const int4 &tv, double (*p)[3]) {
   load_pt(bg.xyz, tv.x, p[0]);
   load_pt(bg.xyz, tv.y, p[1]);
@@ -447,79 +466,109 @@ __device__ __forceinline__ int walk_vol(const Bg &bg, const unsigned long long *
   }
 }
 
-// Volume walks, flattened per lane (split pipeline, default).
+// Volume walks (default pipeline: k_vol_walk [+ k_vol_walk_cont], then
+// k_vol_interp).
 //
-// A block owns kBlock*C consecutive queries of the processing order; lane l
-// of wave w walks queries base_w + j*64 + l, j = 0..C-1, one after the other.
-// Every loop iteration is ONE walk step for every live lane: a lane whose
-// query is located (or stuck) records it and starts its next query in the
-// same iteration, so the wave never idles waiting for its longest walk
-// (with one query per lane, each wave ran for the maximum of its 64 walks,
-// ~3x the mean).  The 64 lanes of a wave stay on 64 neighbouring queries,
-// so the wave's footprint in the background stays compact and L2-resident.
-// vloc[pos] = accepting tetra, 0 = stuck / over-long (-> exhaustive list).
+// One query per lane, the 64 lanes of a wave on 64 consecutive queries of
+// the processing order: neighbouring walks run in lockstep through the same
+// tetra, so their tetra records and vertex rows share cache lines inside
+// each wave-instruction (flattened per-lane chains that desynchronise the
+// lanes, and walks carrying the shared face's vertices in registers, both
+// measured slower).  vloc[i] = accepting tetra, 0 = stuck / over-long (the
+// query then goes to the exhaustive kernels).
+//
+// A wave runs as long as its longest walk, so the first pass caps walks at
+// `cap` steps (mean ~4 with the seed grid): walks still going are compacted
+// into a continuation list {position, current tetra} and finished by
+// k_vol_walk_cont with full waves.  This removes most of the idle-lane
+// iterations (without the cap ~75% of the lane-iterations of a wave were
+// idle, waiting for its slowest walk).
+
+// walk from tetra k for at most `limit` more steps: 1 found (k), 2 stuck,
+// 3 limit reached (k = current tetra)
+__device__ __forceinline__ int walk_core(const Bg &bg, const double *x, int &k, int &steps, int limit) {
+  int hist[kHist];
+#pragma unroll
+  for (int h = 0; h < kHist; h++) hist[h] = 0;
+  for (int n = 0;; n++) {
+    if (n >= limit) return 3;
+    ++steps;
+    const int r = step_vol(bg, x, k, hist);
+    if (r == 1) return 1;
+    if (r == 2) return 2;
+  }
+}
+
+struct ContEntry {
+  int ip; // query
+  int k;  // tetra the capped walk stopped at
+};
+
+// order == nullptr: the queries are taken in input order (i = ip - 1) and
+// the volume points selected here (no compaction pass; the idle lanes of
+// surface / skipped points cost little next to the walks).  Otherwise the
+// queries are order[0 .. st->nvol).  vloc is indexed by ip - 1.
 __global__ __launch_bounds__(kBlock) void k_vol_walk(Bg bg, const Frame *fr, const unsigned long long *grid, int g,
-                                                     const double *qxyz, const int *order, int *vloc, int *fb,
-                                                     DevStats *st, int maxstep, int C) {
+                                                     const double *qxyz, const uint8_t *pclass, const int *order,
+                                                     int np, int *vloc, int *fb, ContEntry *cont, DevStats *st,
+                                                     int cap, int maxstep) {
   __shared__ BlockStats bs;
   bstats_init(&bs);
   __syncthreads();
-  const int nvol = st->nvol;
-  const int lb = xcd_block();
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const long long wbase = ((long long)lb * (kBlock / 64) + w) * 64LL * C;
-  long long pos = wbase + lane;
-  int j = 0;
-  int nsteps = 0, nfound = 0, smax = 0;
-  bool live = pos < nvol;
-  double x[3];
-  int k = 0, steps = 0, ip = 0, ipn = 0;
-  int hist[kHist];
-  if (live) {
-    ip = order[pos];
-    ipn = (C > 1 && pos + 64 < nvol) ? order[pos + 64] : 0;
+  const int i = xcd_block() * blockDim.x + threadIdx.x;
+  bool active;
+  int ip = 0;
+  if (order) {
+    active = i < st->nvol;
+    if (active) ip = order[i];
+  } else {
+    active = i < np && pclass[i] == PMMG_PT_VOL;
+    ip = i + 1;
+  }
+  int status = 0, steps = 0, k = 0;
+  if (active) {
+    double x[3];
     load_pt(qxyz, ip, x);
     k = seed_vol(grid, g, fr, x);
-#pragma unroll
-    for (int h = 0; h < kHist; h++) hist[h] = 0;
+    status = walk_core(bg, x, k, steps, cap < maxstep ? cap : maxstep);
+    if (status == 3 && steps < maxstep) status = 4; // -> continuation list
+    vloc[ip - 1] = status == 1 ? k : 0;
   }
-  while (live) {
-    ++steps;
-    const int r = step_vol(bg, x, k, hist);
-    const bool over = r == 0 && steps >= maxstep;
-    if (r != 0 || over) {
-      // query done: accepted (r == 1), stuck (2) or over-long
-      vloc[pos] = r == 1 ? k : 0;
-      if (r != 1) fb[atomicAdd(&st->nfb_vol, 1)] = ip;
-      nfound += r == 1;
-      nsteps += steps;
-      smax = steps > smax ? steps : smax;
-      steps = 0;
-      ++j;
-      pos += 64;
-      live = j < C && pos < nvol;
-      if (live) {
-        ip = ipn;
-        ipn = (j + 1 < C && pos + 64 < nvol) ? order[pos + 64] : 0;
-        load_pt(qxyz, ip, x);
-        k = seed_vol(grid, g, fr, x);
-#pragma unroll
-        for (int h = 0; h < kHist; h++) hist[h] = 0;
-      }
+  const bool fail = active && (status == 2 || status == 3);
+  const int slot = wave_append(&st->nfb_vol, fail);
+  if (fail) fb[slot] = ip;
+  const int cslot = wave_append(&st->ncont, active && status == 4);
+  if (active && status == 4) cont[cslot] = ContEntry{ip, k};
+  wave_stats(&bs, active, status == 1 ? PMMG_HIT_VOL_WALK : 0, steps);
+  __syncthreads();
+  bstats_flush(&bs, st);
+}
+
+// the capped walks, continued from where they stopped (fresh visited
+// history; the step count continues)
+__global__ __launch_bounds__(kBlock) void k_vol_walk_cont(Bg bg, const double *qxyz, int *vloc, int *fb,
+                                                          const ContEntry *cont, DevStats *st, int cap, int maxstep) {
+  __shared__ BlockStats bs;
+  bstats_init(&bs);
+  __syncthreads();
+  const XcdChunk ch = xcd_chunk(st->ncont);
+  for (int it = 0; it < ch.iters; it++) {
+    const long long j = ch.start + it * ch.stride;
+    const bool active = j < ch.hi;
+    int status = 0, steps = cap, ip = 0;
+    if (active) {
+      const ContEntry e = cont[j];
+      ip = e.ip;
+      double x[3];
+      load_pt(qxyz, ip, x);
+      int k = e.k;
+      status = walk_core(bg, x, k, steps, maxstep - cap);
+      vloc[ip - 1] = status == 1 ? k : 0;
     }
-  }
-  wave_count(&bs, PMMG_HIT_VOL_WALK, nfound);
-  {
-    unsigned int s = (unsigned)nsteps, mx = (unsigned)smax;
-    for (int off = 32; off > 0; off >>= 1) {
-      s += __shfl_down(s, off);
-      unsigned o = __shfl_down(mx, off);
-      mx = o > mx ? o : mx;
-    }
-    if (__lane_id() == 0) {
-      if (s) atomicAdd(&bs.steps, (unsigned long long)s);
-      atomicMax(&bs.stepmax, mx);
-    }
+    const bool fail = active && status != 1;
+    const int slot = wave_append(&st->nfb_vol, fail);
+    if (fail) fb[slot] = ip;
+    wave_stats(&bs, active, status == 1 ? PMMG_HIT_VOL_WALK : 0, active ? steps - cap : 0);
   }
   __syncthreads();
   bstats_flush(&bs, st);
@@ -542,14 +591,16 @@ __device__ __forceinline__ void interp_vol_layout(const Slots &S, int ip, const 
   }
 }
 
+// interpolation of the located volume queries, in input order (coalesced
+// output rows; vloc by ip - 1)
 template <int C0, int C1, int C2, int C3, int C4, int C5>
-__global__ __launch_bounds__(kBlock) void k_vol_interp(Bg bg, const double *qxyz, const int *order, const int *vloc,
-                                                       Slots S, int *elem_out, int8_t *hit_out, const DevStats *st) {
-  const int nvol = st->nvol;
-  for (int i = xcd_block() * blockDim.x + threadIdx.x; i < nvol; i += gridDim.x * blockDim.x) {
+__global__ __launch_bounds__(kBlock) void k_vol_interp(Bg bg, const double *qxyz, const uint8_t *pclass, int np,
+                                                       const int *vloc, Slots S, int *elem_out, int8_t *hit_out) {
+  for (int i = xcd_block() * blockDim.x + threadIdx.x; i < np; i += gridDim.x * blockDim.x) {
+    if (pclass[i] != PMMG_PT_VOL) continue;
     const int k = vloc[i];
     if (k == 0) continue;
-    const int ip = order[i];
+    const int ip = i + 1;
     double x[3], p0[3], p1[3], p2[3], p3[3], phi[4];
     load_pt(qxyz, ip, x);
     const int4 tv = tetv_row(bg, k);
@@ -687,7 +738,7 @@ __global__ __launch_bounds__(kBlock) void k_vol_scan(Bg bg, const Frame *fr, int
       }
   }
   for (int o = 32; o > 0; o >>= 1) tests += __shfl_down(tests, o);
-  if (__lane_id() == 0 && tests) atomicAdd(&st->steps, tests);
+  if (__lane_id() == 0 && tests) atomicAdd(&stat_part(st)->steps, tests);
 }
 
 // interpolation of the scanned queries (sorted positions, coordinates read
@@ -732,7 +783,7 @@ __global__ __launch_bounds__(kBlock) void k_vol_interp_scan(Bg bg, const double 
     if (__lane_id() == 0 && okm) atomicAdd(&nloc, (unsigned)__popcll(okm));
   }
   __syncthreads();
-  if (threadIdx.x == 0 && nloc) atomicAdd(&st->cnt[PMMG_HIT_VOL_SCAN], (unsigned long long)nloc);
+  if (threadIdx.x == 0 && nloc) atomicAdd(&stat_part(st)->cnt[PMMG_HIT_VOL_SCAN], (unsigned long long)nloc);
 }
 
 // ---------------------------------------------------------------- surface
@@ -944,7 +995,7 @@ __global__ __launch_bounds__(kBlock) void k_vol_finish(Bg bg, const double *qxyz
     for (int s = 0; s < S.n; s++) interp_dyn<4>(S.s[s], ip, v, phi);
     if (elem_out) elem_out[ip - 1] = k;
     if (hit_out) hit_out[ip - 1] = (int8_t)hit;
-    atomicAdd(&st->cnt[hit], 1ULL);
+    atomicAdd(&stat_part(st)->cnt[hit], 1ULL);
   }
 }
 
@@ -1026,7 +1077,7 @@ __global__ __launch_bounds__(kBlock) void k_bdy_finish(Bg bg, const double *qxyz
     interp_bdy(S, ip, t.v, phi, -1, -1);
     if (elem_out) elem_out[ip - 1] = k;
     if (hit_out) hit_out[ip - 1] = (int8_t)hit;
-    atomicAdd(&st->cnt[hit], 1ULL);
+    atomicAdd(&stat_part(st)->cnt[hit], 1ULL);
   }
 }
 
@@ -1041,7 +1092,7 @@ __global__ void k_fallback_init(int *a, int *b, unsigned long long *c, const int
 
 // ---------------------------------------------------------------- layout dispatch
 
-typedef void (*VolInterpFn)(Bg, const double *, const int *, const int *, Slots, int *, int8_t *, const DevStats *);
+typedef void (*VolInterpFn)(Bg, const double *, const uint8_t *, int, const int *, Slots, int *, int8_t *);
 typedef void (*ScanInterpFn)(Bg, const double *, const int *, const int *, Slots, int *, int8_t *, int *, DevStats *);
 typedef void (*FusedFn)(Bg, const Frame *, const unsigned long long *, int, const double *, const int *, Slots, int *,
                         int8_t *, int *, DevStats *, int);
@@ -1099,6 +1150,8 @@ struct pmmg_hip_ctx {
   int met_size = 0;
   int nfield = 0;
   std::vector<int> fsize;
+  std::vector<int> fstride; // input row strides (= sizes, or the packed record size)
+  int met_stride = 0;
   std::vector<const double *> fin;
   const double *met = nullptr;
   // owned copies for PMMG_HIP_HOST inputs
@@ -1106,20 +1159,25 @@ struct pmmg_hip_ctx {
   std::vector<DevBuf> o_f;
   // work buffers
   DevBuf frame, stats, grid, sgrid, cnt, off, binrank, order_v, order_b, vloc, scan_tmp, qs;
+  DevBuf cont;
   DevBuf fb_vol, fb_bdy, best, ckey, cidx, bbest, bckey, bcidx;
   // host-mode staging
   DevBuf h_xyz, h_cls, h_met, h_elem, h_hit;
   std::vector<DevBuf> h_f;
   hipEvent_t ev[8] = {};
   bool pending = false;
-  int tpc = 4;      // background tetra per volume seed cell
-  int spc = 1;      // sampled tetra per seed cell
+  int tpc = 8;      // background tetra per volume seed cell
+  int spc = 2;      // sampled tetra per seed cell
+  int seed_mode = 0; // seed point of a sampled tetra: 0 centroid, 1 edge v0-v3 midpoint, 2 first vertex
   int qpb = 8;      // queries per Morton bin (walk path)
   int qpc = 1;      // queries per scan cell (scan path)
   int ncu = 256;     // compute units of the device
-  int chain = 0;     // queries per lane in k_vol_walk (0 = automatic)
+  int cap = 1 << 30; // first-pass walk cap (k_vol_walk); capped walks continue in k_vol_walk_cont.
+                     // Off by default: the continuation walks lose the lockstep
+                     // line sharing of neighbouring queries and measured slower
   int maxstep = 4096; // longer walks go to the exhaustive kernels (the reference caps at ne)
   int last_sorted = 0;
+  int count_nvol = 0; // nvol not counted on the device (derived from the walk statistics)
   int *h_small = nullptr; // pinned host words for the two small read-backs
 };
 
@@ -1202,10 +1260,11 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   }
   c->tpc = env_int("PMMG_HIP_TPC", c->tpc);
   c->spc = env_int("PMMG_HIP_SPC", c->spc);
+  if (getenv("PMMG_HIP_SEEDMODE")) c->seed_mode = atoi(getenv("PMMG_HIP_SEEDMODE"));
   c->qpb = env_int("PMMG_HIP_QPB", c->qpb);
   c->qpc = env_int("PMMG_HIP_QPC", c->qpc);
   c->maxstep = env_int("PMMG_HIP_MAXSTEP", c->maxstep);
-  c->chain = env_int("PMMG_HIP_CHAIN", c->chain);
+  c->cap = env_int("PMMG_HIP_CAP", c->cap);
   {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
@@ -1218,7 +1277,7 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
-  DevBuf *bufs[] = {&c->o_xyz, &c->o_tetv, &c->o_adja, &c->o_triv, &c->o_adjt, &c->o_met, &c->frame, &c->stats,
+  DevBuf *bufs[] = {&c->cont, &c->o_xyz, &c->o_tetv, &c->o_adja, &c->o_triv, &c->o_adjt, &c->o_met, &c->frame, &c->stats,
                     &c->grid, &c->sgrid, &c->cnt, &c->off, &c->binrank, &c->order_v, &c->order_b, &c->vloc, &c->qs,
                     &c->scan_tmp, &c->fb_vol, &c->fb_bdy, &c->best, &c->ckey, &c->cidx, &c->bbest, &c->bckey,
                     &c->bcidx, &c->h_xyz, &c->h_cls, &c->h_met, &c->h_elem, &c->h_hit};
@@ -1332,8 +1391,10 @@ int pmmg_hip_set_solutions(pmmg_hip_ctx *c, int met_size, const double *met, int
     return 0;
   }
   c->met_size = met_size;
+  c->met_stride = met_size;
   c->nfield = nfield;
   c->fsize.assign(field_size, field_size + nfield);
+  c->fstride.assign(field_size, field_size + nfield);
   c->fin.resize(nfield);
   if (where == PMMG_HIP_DEVICE) {
     c->met = met;
@@ -1350,6 +1411,59 @@ int pmmg_hip_set_solutions(pmmg_hip_ctx *c, int met_size, const double *met, int
     c->fin[j] = (const double *)c->o_f[j].p;
   }
   HIPCK(c, hipStreamSynchronize(c->stream));
+  return 1;
+}
+
+int pmmg_hip_set_solutions_packed(pmmg_hip_ctx *c, int met_size, int met_off, int nfield, const int *field_size,
+                                  const int *field_off, const double *rec, int stride, int where) {
+  if (!c) return 0;
+  HIPCK(c, hipSetDevice(c->device));
+  if (met_size != 0 && met_size != 1 && met_size != 6) {
+    set_err(c, "set_solutions_packed: metric size %d (expected 0, 1 or 6)", met_size);
+    return 0;
+  }
+  if (nfield < 0 || nfield + (met_size ? 1 : 0) > kMaxSlot) {
+    set_err(c, "set_solutions_packed: %d fields exceed the %d-slot limit", nfield, kMaxSlot);
+    return 0;
+  }
+  const size_t np = (size_t)c->bg.np;
+  if (np == 0) {
+    set_err(c, "set_solutions_packed: call pmmg_hip_set_background first");
+    return 0;
+  }
+  if (!rec || stride <= 0 || (stride & 1) || ((uintptr_t)rec & 15)) {
+    set_err(c, "set_solutions_packed: rec must be 16-byte aligned with an even stride (got %d)", stride);
+    return 0;
+  }
+  // every column range inside the record; tensors 16-byte aligned (double2 loads)
+  auto bad = [&](int size, int off) { return off < 0 || off + size > stride || (size == 6 && (off & 1)); };
+  if (met_size && bad(met_size, met_off)) {
+    set_err(c, "set_solutions_packed: metric columns [%d, %d) do not fit / are misaligned", met_off,
+            met_off + met_size);
+    return 0;
+  }
+  for (int j = 0; j < nfield; j++) {
+    if (!field_size || !field_off || !(field_size[j] == 1 || field_size[j] == 3 || field_size[j] == 6) ||
+        bad(field_size[j], field_off[j])) {
+      set_err(c, "set_solutions_packed: field %d (size %d, offset %d) invalid", j, field_size ? field_size[j] : -1,
+              field_off ? field_off[j] : -1);
+      return 0;
+    }
+  }
+  const double *base = rec;
+  if (where != PMMG_HIP_DEVICE) {
+    if (!upload(c, c->o_met, rec, sizeof(double) * (size_t)stride * np)) return 0;
+    HIPCK(c, hipStreamSynchronize(c->stream));
+    base = (const double *)c->o_met.p;
+  }
+  c->met_size = met_size;
+  c->met_stride = stride;
+  c->met = met_size ? base + met_off : nullptr;
+  c->nfield = nfield;
+  c->fsize.assign(field_size, field_size + nfield);
+  c->fstride.assign(nfield, stride);
+  c->fin.resize(nfield);
+  for (int j = 0; j < nfield; j++) c->fin[j] = base + field_off[j];
   return 1;
 }
 
@@ -1480,11 +1594,11 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   S.has_met = c->met_size ? 1 : 0;
   if (c->met_size) {
     if (!met_out) { set_err(c, "locate_interp: met_out is NULL"); return 0; }
-    S.s[S.n++] = Slot{c->met, met_out, c->met_size};
+    S.s[S.n++] = Slot{c->met, met_out, c->met_size, c->met_stride};
   }
   for (int j = 0; j < c->nfield; j++) {
     if (!fields_out || !fields_out[j]) { set_err(c, "locate_interp: fields_out[%d] is NULL", j); return 0; }
-    S.s[S.n++] = Slot{c->fin[j], fields_out[j], c->fsize[j]};
+    S.s[S.n++] = Slot{c->fin[j], fields_out[j], c->fsize[j], c->fstride[j]};
   }
   const int g = grid_dim(bg.ne, c->tpc, 1024);
   const int gs = bg.nt > 0 ? grid_dim(bg.nt, 2, 512) : 1;
@@ -1492,9 +1606,9 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   while (bb < 10 && (1LL << (3 * bb)) * c->qpb < (long long)np_new) bb++;
   const int gb = 1 << bb, nbins = 1 << (3 * bb);
   const size_t nq = (size_t)np_new;
-  if (!ensure(c, c->frame, sizeof(Frame)) || !ensure(c, c->stats, sizeof(DevStats)) ||
+  if (!ensure(c, c->frame, sizeof(Frame)) || !ensure(c, c->stats, sizeof(DevStats) + kStatParts * sizeof(StatPart)) ||
       !ensure(c, c->grid, 8 * (size_t)g * g * g) || !ensure(c, c->sgrid, 4 * (size_t)gs * gs * gs) ||
-      !ensure(c, c->order_v, 4 * nq) || !ensure(c, c->order_b, 4 * nq) || !ensure(c, c->vloc, 4 * nq) ||
+      !ensure(c, c->order_v, 4 * nq) || !ensure(c, c->cont, 8 * nq) || !ensure(c, c->order_b, 4 * nq) || !ensure(c, c->vloc, 4 * nq) ||
       !ensure(c, c->fb_vol, 4 * nq) || !ensure(c, c->fb_bdy, 4 * nq) || !ensure(c, c->best, 4 * nq) ||
       !ensure(c, c->ckey, 8 * nq) || !ensure(c, c->cidx, 4 * nq) || !ensure(c, c->bbest, 4 * nq) ||
       !ensure(c, c->bckey, 8 * nq) || !ensure(c, c->bcidx, 4 * nq))
@@ -1532,7 +1646,8 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   hipLaunchKernelGGL(k_frame_final, dim3(1), dim3(1), 0, s, fr, g, gs, gb);
   long long nsamp = (long long)c->spc * ng;
   if (nsamp > bg.ne) nsamp = bg.ne;
-  hipLaunchKernelGGL(k_seed_vol, dim3(blocks_for(nsamp, 8192)), dim3(kBlock), 0, s, bg, fr, grid, g, nsamp);
+  hipLaunchKernelGGL(k_seed_vol, dim3(blocks_for(nsamp, 8192)), dim3(kBlock), 0, s, bg, fr, grid, g, nsamp,
+                     c->seed_mode);
   if (bg.nt > 0) hipLaunchKernelGGL(k_seed_srf, dim3(blocks_for(bg.nt, 4096)), dim3(kBlock), 0, s, bg, fr, sgrid, gs);
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[1], s));
@@ -1548,30 +1663,33 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
                        (const int2 *)c->binrank.p, (const int *)c->off.p, nbins, order_v, order_b);
     hipLaunchKernelGGL(k_bin_total, dim3(1), dim3(1), 0, s, (const int *)c->off.p, (const int *)c->cnt.p, nbins, st);
   } else {
+    // stable class compaction: the surface list always; the volume list only
+    // for the fused kernel (k_vol_walk selects volume points itself)
     hipcub::CountingInputIterator<int> ids(1);
     size_t tb = 0;
     HIPCK(c, hipcub::DeviceSelect::If(nullptr, tb, ids, order_v, &st->nvol, (int64_t)np_new, IsClass{pclass, 1}, s));
     if (!ensure(c, c->scan_tmp, tb)) return 0;
-    HIPCK(c, hipcub::DeviceSelect::If(c->scan_tmp.p, tb, ids, order_v, &st->nvol, (int64_t)np_new,
-                                      IsClass{pclass, PMMG_PT_VOL}, s));
+    if (c->options & PMMG_HIP_OPT_FUSED)
+      HIPCK(c, hipcub::DeviceSelect::If(c->scan_tmp.p, tb, ids, order_v, &st->nvol, (int64_t)np_new,
+                                        IsClass{pclass, PMMG_PT_VOL}, s));
     HIPCK(c, hipcub::DeviceSelect::If(c->scan_tmp.p, tb, ids, order_b, &st->nbdy, (int64_t)np_new,
                                       IsClass{pclass, PMMG_PT_BDY}, s));
   }
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[2], s));
+  c->count_nvol = !sorted && !(c->options & PMMG_HIP_OPT_FUSED);
 
   if (!(c->options & PMMG_HIP_OPT_FUSED)) {
-    // C = 1 (one query per lane, lanes of a wave in lockstep on neighbouring
-    // queries) measured fastest: neighbouring walks share tetra and vertex
-    // lines inside each wave-instruction; desynchronised chains lose that
-    const int C = c->chain > 0 ? c->chain : 1;
-    const long long nblk = (np_new + (long long)kBlock * C - 1) / ((long long)kBlock * C);
-    hipLaunchKernelGGL(k_vol_walk, dim3((unsigned)nblk), dim3(kBlock), 0, s, bg, fr, grid, g, xyz_new, order_v,
-                       (int *)c->vloc.p, (int *)c->fb_vol.p, st, c->maxstep, C);
+    hipLaunchKernelGGL(k_vol_walk, dim3(blocks_for(np_new, 1 << 30)), dim3(kBlock), 0, s, bg, fr, grid, g, xyz_new,
+                       pclass, sorted ? (const int *)order_v : nullptr, np_new, (int *)c->vloc.p, (int *)c->fb_vol.p,
+                       (ContEntry *)c->cont.p, st, c->cap, c->maxstep);
+    if (c->cap < c->maxstep) // continuation pass only when capping is enabled
+      hipLaunchKernelGGL(k_vol_walk_cont, dim3(8 * 256), dim3(kBlock), 0, s, bg, xyz_new, (int *)c->vloc.p,
+                         (int *)c->fb_vol.p, (const ContEntry *)c->cont.p, st, c->cap, c->maxstep);
     HIPCK(c, hipEventRecord(c->ev[6], s));
     VolInterpFn interp = pick_layout(S).fn;
-    hipLaunchKernelGGL(interp, dim3(blocks_for(np_new, 1 << 30)), dim3(kBlock), 0, s, bg, xyz_new, order_v,
-                       (const int *)c->vloc.p, S, elem_out, hit_out, st);
+    hipLaunchKernelGGL(interp, dim3(blocks_for(np_new, 1 << 30)), dim3(kBlock), 0, s, bg, xyz_new, pclass, np_new,
+                       (const int *)c->vloc.p, S, elem_out, hit_out);
   } else {
     FusedFn fused = pick_layout(S).ffn;
     hipLaunchKernelGGL(fused, dim3(blocks_for(np_new, 1 << 30)), dim3(kBlock), 0, s, bg, fr, grid, g, xyz_new,
@@ -1595,9 +1713,17 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
 
 static int collect_stats(pmmg_hip_ctx *c, pmmg_hip_stats *out) {
   DevStats h;
+  std::vector<StatPart> parts(kStatParts);
   HIPCK(c, hipMemcpy(&h, c->stats.p, sizeof(DevStats), hipMemcpyDeviceToHost));
+  HIPCK(c, hipMemcpy(parts.data(), (const DevStats *)c->stats.p + 1, kStatParts * sizeof(StatPart),
+                     hipMemcpyDeviceToHost));
+  for (const StatPart &pt : parts) {
+    for (int j = 0; j < 16; j++) h.cnt[j] += pt.cnt[j];
+    h.steps += pt.steps;
+    if (pt.stepmax > h.stepmax) h.stepmax = (unsigned)pt.stepmax;
+  }
   memset(out, 0, sizeof(*out));
-  out->nvol = h.nvol;
+  out->nvol = c->count_nvol ? (int64_t)h.cnt[PMMG_HIT_VOL_WALK] + h.nfb_vol : h.nvol;
   out->nbdy = h.nbdy;
   out->nvol_walk = (int64_t)h.cnt[PMMG_HIT_VOL_WALK];
   out->nvol_exhaust = (int64_t)h.cnt[PMMG_HIT_VOL_EXHAUST];

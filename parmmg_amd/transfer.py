@@ -69,6 +69,26 @@ def pack_tet8(tetv: np.ndarray, adja: np.ndarray) -> np.ndarray:
     return np.ascontiguousarray(np.hstack([np.asarray(tetv, np.int32), np.asarray(adja, np.int32)]))
 
 
+def pack_solutions(met, fields):
+    """Packed per-vertex records of the metric and fields
+    (pmmg_hip_set_solutions_packed): size-6 slots first (even columns), then
+    size-3, then size-1, the record padded to an even number of doubles.
+    Returns (rec, met_size, met_off, field_sizes, field_offs)."""
+    slots = ([("m", met)] if met is not None else []) + [(j, f) for j, f in enumerate(fields)]
+    order = sorted(slots, key=lambda s: -s[1].shape[1])  # stable: 6, 3, 1
+    off, col = {}, 0
+    for key, a in order:
+        off[key] = col
+        col += a.shape[1]
+    stride = col + (col & 1)
+    npt = (met if met is not None else fields[0]).shape[0]
+    rec = np.zeros((npt, max(stride, 2)), np.float64)
+    for key, a in slots:
+        rec[:, off[key]:off[key] + a.shape[1]] = a
+    msize = 0 if met is None else met.shape[1]
+    return (rec, msize, off.get("m", 0), [f.shape[1] for f in fields], [off[j] for j in range(len(fields))])
+
+
 class TransferContext:
     """One ``pmmg_hip_ctx`` on a HIP device."""
 
@@ -155,6 +175,16 @@ class TransferContext:
         self._sol_keep = [met, fields, sizes, ptrs]
         self._ck(self.lib.pmmg_hip_set_solutions(self.h, msize, _p(met), len(fields), sizes, ptrs, where),
                  "set_solutions")
+
+    def set_solutions_packed(self, rec, met_size: int, met_off: int, field_sizes, field_offs) -> None:
+        """Solutions as packed per-vertex records (pack_solutions)."""
+        where = DEVICE if isinstance(rec, DeviceArray) else HOST
+        nf = len(field_sizes)
+        sizes = (ctypes.c_int * max(1, nf))(*[int(x) for x in field_sizes])
+        offs = (ctypes.c_int * max(1, nf))(*[int(x) for x in field_offs])
+        self._sol_keep = [rec, sizes, offs]
+        self._ck(self.lib.pmmg_hip_set_solutions_packed(self.h, int(met_size), int(met_off), nf, sizes, offs, _p(rec),
+                                                        int(rec.shape[1]), where), "set_solutions_packed")
 
     def locate_interp(self, xyz_new, pclass, met_out, fields_out, elem_out=None, hit_out=None,
                       sync: bool = True) -> HipStats | None:

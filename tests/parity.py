@@ -46,7 +46,7 @@ def make_case(kind=synth.CUBE, n_old=6, n_new=7, metric=synth.F_ANI,
     return case
 
 
-def run_gpu(case, sort=None, ctx=None, scan=False, fused=False, tet8=False):
+def run_gpu(case, sort=None, ctx=None, scan=False, fused=False, tet8=False, packed=False):
     bg, new = case["bg"], case["new"]
     own = ctx is None
     ctx = ctx or TransferContext(0, sort=sort, scan=scan, fused=fused)
@@ -56,7 +56,12 @@ def run_gpu(case, sort=None, ctx=None, scan=False, fused=False, tet8=False):
             ctx.set_background_tet8(bg.xyz, pack_tet8(bg.tetv, bg.adja), bg.triv, bg.adjt, case["hausd"])
         else:
             ctx.set_background(bg.xyz, bg.tetv, bg.adja, bg.triv, bg.adjt, case["hausd"])
-        ctx.set_solutions(case["met"], case["fields"])
+        if packed:
+            from parmmg_amd.transfer import pack_solutions
+            rec, ms, mo, fs, fo = pack_solutions(case["met"], case["fields"])
+            ctx.set_solutions_packed(rec, ms, mo, fs, fo)
+        else:
+            ctx.set_solutions(case["met"], case["fields"])
         npn = new.np
         met_out = None if case["met"] is None else np.full((npn, case["met"].shape[1]), np.nan)
         f_out = [np.full((npn, f.shape[1]), np.nan) for f in case["fields"]]

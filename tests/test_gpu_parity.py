@@ -24,7 +24,8 @@ CASES = {
 
 MODES = {"auto": {}, "morton": dict(sort=True), "nosort": dict(sort=False), "fused": dict(fused=True),
          "scan": dict(scan=True),
-         "tet8": dict(tet8=True), "tet8-scan": dict(tet8=True, scan=True)}
+         "tet8": dict(tet8=True), "tet8-scan": dict(tet8=True, scan=True),
+         "packed": dict(tet8=True, packed=True), "packed-fused-morton": dict(tet8=True, packed=True, fused=True, sort=True)}
 
 
 @pytest.mark.gpu

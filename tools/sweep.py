@@ -32,27 +32,30 @@ def main():
     fields = [synth.solution(f, bg.xyz) for f in w.fields]
     pc = synth.classes(new)
     base = TransferContext(0)
-    from parmmg_amd.transfer import pack_tet8
+    from parmmg_amd.transfer import pack_solutions, pack_tet8
+    rec, *recmeta = pack_solutions(met, fields)
     d = dict(xyz=base.upload(bg.xyz), tetv=base.upload(bg.tetv), adja=base.upload(bg.adja),
-             tet8=base.upload(pack_tet8(bg.tetv, bg.adja)),
+             tet8=base.upload(pack_tet8(bg.tetv, bg.adja)), rec=base.upload(rec), recmeta=recmeta,
              triv=base.upload(bg.triv), adjt=base.upload(bg.adjt), met=base.upload(met),
              f=[base.upload(f) for f in fields], q=base.upload(new.xyz), pc=base.upload(pc),
              mo=base.empty((new.np, w.met_size), np.float64),
              fo=[base.empty((new.np, f.shape[1]), np.float64) for f in fields],
              el=base.empty((new.np,), np.int32), hit=base.empty((new.np,), np.int8))
     variants = []
-    tet8s = set()
+    tet8s, packeds = set(), set()
     if args.variants:
         # "chain=16,sort=1;chain=0" -> TransferContext keyword sets (sort: 1 on, 0 off)
         for spec in args.variants.split(";"):
             kw = {}
-            for name in ("TPC", "SPC", "QPB", "MAXSTEP", "CHAIN"):
+            for name in ("TPC", "SPC", "QPB", "MAXSTEP", "CAP", "SEEDMODE"):
                 os.environ.pop("PMMG_HIP_" + name, None)
             for item in filter(None, spec.split(",")):
                 k, v = item.split("=")
                 if k == "tet8":
                     tet8s.add(spec)
-                elif k in ("tpc", "spc", "qpb", "maxstep", "chain"):
+                elif k == "packed":
+                    packeds.add(spec)
+                elif k in ("tpc", "spc", "qpb", "maxstep", "cap", "seedmode"):
                     os.environ["PMMG_HIP_" + k.upper()] = v  # read by pmmg_hip_create
                 else:
                     kw[k] = bool(int(v)) if k in ("sort", "fused", "scan") else int(v)
@@ -72,7 +75,10 @@ def main():
                     ctx.set_background_tet8(d["xyz"], d["tet8"], d["triv"], d["adjt"], w.hausd)
                 else:
                     ctx.set_background(d["xyz"], d["tetv"], d["adja"], d["triv"], d["adjt"], w.hausd)
-                ctx.set_solutions(d["met"], d["f"])
+                if key[0] in packeds:
+                    ctx.set_solutions_packed(d["rec"], *d["recmeta"])
+                else:
+                    ctx.set_solutions(d["met"], d["f"])
                 ctx.locate_interp(d["q"], d["pc"], d["mo"], d["fo"], d["el"], d["hit"], sync=False)
                 st = ctx.sync()
                 if s > 0:
