@@ -392,7 +392,15 @@ __device__ __forceinline__ void load_tet_pts(const Bg &bg, const int4 &tv, doubl
 // One step of the walk at tetra k: the reference's acceptance test (exact,
 // one division, see above) and, when it fails, the face to leave through.
 // Returns 1 inside, 0 moved (k = neighbour, hist updated), 2 stuck.
-__device__ __forceinline__ int step_vol(const Bg &bg, const double *x, int &k, int *hist) {
+// On acceptance, loc (when given) receives the tetra's vertex ids and the
+// reference's barycentric coordinates -s[f]/vol (PMMG_barycoord3d_compute,
+// PMMG_barycoord_get: unsorted), bit-identical to tet_bary.
+struct VolLoc {
+  int4 v;
+  double phi[4];
+};
+
+__device__ __forceinline__ int step_vol(const Bg &bg, const double *x, int &k, int *hist, VolLoc *loc = nullptr) {
   const int4 tv = tetv_row(bg, k);
   const int4 ad = adja_row(bg, k);
   double p[4][3];
@@ -427,7 +435,14 @@ __device__ __forceinline__ int step_vol(const Bg &bg, const double *x, int &k, i
 #pragma unroll
     for (int f = 0; f < 4; f++) key[f] = (double)(3 - r[f]);
   }
-  if (inside) return 1;
+  if (inside) {
+    if (loc) {
+      loc->v = tv;
+#pragma unroll
+      for (int f = 0; f < 4; f++) loc->phi[f] = -s[f] / vol;
+    }
+    return 1;
+  }
   int f = -1;
   double best = 0.0;
 #pragma unroll
@@ -486,14 +501,15 @@ __device__ __forceinline__ int walk_vol(const Bg &bg, const unsigned long long *
 
 // walk from tetra k for at most `limit` more steps: 1 found (k), 2 stuck,
 // 3 limit reached (k = current tetra)
-__device__ __forceinline__ int walk_core(const Bg &bg, const double *x, int &k, int &steps, int limit) {
+__device__ __forceinline__ int walk_core(const Bg &bg, const double *x, int &k, int &steps, int limit,
+                                         VolLoc *loc = nullptr) {
   int hist[kHist];
 #pragma unroll
   for (int h = 0; h < kHist; h++) hist[h] = 0;
   for (int n = 0;; n++) {
     if (n >= limit) return 3;
     ++steps;
-    const int r = step_vol(bg, x, k, hist);
+    const int r = step_vol(bg, x, k, hist, loc);
     if (r == 1) return 1;
     if (r == 2) return 2;
   }
@@ -510,8 +526,8 @@ struct ContEntry {
 // queries are order[0 .. st->nvol).  vloc is indexed by ip - 1.
 __global__ __launch_bounds__(kBlock) void k_vol_walk(Bg bg, const Frame *fr, const unsigned long long *grid, int g,
                                                      const double *qxyz, const uint8_t *pclass, const int *order,
-                                                     int np, int *vloc, int *fb, ContEntry *cont, DevStats *st,
-                                                     int cap, int maxstep) {
+                                                     int np, int *vloc, VolLoc *vrec, int *fb, ContEntry *cont,
+                                                     DevStats *st, int cap, int maxstep) {
   __shared__ BlockStats bs;
   bstats_init(&bs);
   __syncthreads();
@@ -530,9 +546,11 @@ __global__ __launch_bounds__(kBlock) void k_vol_walk(Bg bg, const Frame *fr, con
     double x[3];
     load_pt(qxyz, ip, x);
     k = seed_vol(grid, g, fr, x);
-    status = walk_core(bg, x, k, steps, cap < maxstep ? cap : maxstep);
+    VolLoc loc;
+    status = walk_core(bg, x, k, steps, cap < maxstep ? cap : maxstep, &loc);
     if (status == 3 && steps < maxstep) status = 4; // -> continuation list
     vloc[ip - 1] = status == 1 ? k : 0;
+    if (status == 1) vrec[ip - 1] = loc;
   }
   const bool fail = active && (status == 2 || status == 3);
   const int slot = wave_append(&st->nfb_vol, fail);
@@ -546,7 +564,7 @@ __global__ __launch_bounds__(kBlock) void k_vol_walk(Bg bg, const Frame *fr, con
 
 // the capped walks, continued from where they stopped (fresh visited
 // history; the step count continues)
-__global__ __launch_bounds__(kBlock) void k_vol_walk_cont(Bg bg, const double *qxyz, int *vloc, int *fb,
+__global__ __launch_bounds__(kBlock) void k_vol_walk_cont(Bg bg, const double *qxyz, int *vloc, VolLoc *vrec, int *fb,
                                                           const ContEntry *cont, DevStats *st, int cap, int maxstep) {
   __shared__ BlockStats bs;
   bstats_init(&bs);
@@ -562,8 +580,10 @@ __global__ __launch_bounds__(kBlock) void k_vol_walk_cont(Bg bg, const double *q
       double x[3];
       load_pt(qxyz, ip, x);
       int k = e.k;
-      status = walk_core(bg, x, k, steps, maxstep - cap);
+      VolLoc loc;
+      status = walk_core(bg, x, k, steps, maxstep - cap, &loc);
       vloc[ip - 1] = status == 1 ? k : 0;
+      if (status == 1) vrec[ip - 1] = loc;
     }
     const bool fail = active && status != 1;
     const int slot = wave_append(&st->nfb_vol, fail);
@@ -592,25 +612,20 @@ __device__ __forceinline__ void interp_vol_layout(const Slots &S, int ip, const 
 }
 
 // interpolation of the located volume queries, in input order (coalesced
-// output rows; vloc by ip - 1)
+// output rows; vloc / vrec by ip - 1).  The walk left the tetra's vertex ids
+// and the exact barycentric coordinates in vrec (one coalesced 48-byte read
+// instead of re-gathering the query, the tetra and its 4 vertices).
 template <int C0, int C1, int C2, int C3, int C4, int C5>
-__global__ __launch_bounds__(kBlock) void k_vol_interp(Bg bg, const double *qxyz, const uint8_t *pclass, int np,
-                                                       const int *vloc, Slots S, int *elem_out, int8_t *hit_out) {
+__global__ __launch_bounds__(kBlock) void k_vol_interp(const uint8_t *pclass, int np, const int *vloc,
+                                                       const VolLoc *vrec, Slots S, int *elem_out, int8_t *hit_out) {
   for (int i = xcd_block() * blockDim.x + threadIdx.x; i < np; i += gridDim.x * blockDim.x) {
     if (pclass[i] != PMMG_PT_VOL) continue;
     const int k = vloc[i];
     if (k == 0) continue;
     const int ip = i + 1;
-    double x[3], p0[3], p1[3], p2[3], p3[3], phi[4];
-    load_pt(qxyz, ip, x);
-    const int4 tv = tetv_row(bg, k);
-    load_pt(bg.xyz, tv.x, p0);
-    load_pt(bg.xyz, tv.y, p1);
-    load_pt(bg.xyz, tv.z, p2);
-    load_pt(bg.xyz, tv.w, p3);
-    tet_bary(x, p0, p1, p2, p3, phi);
-    const int v[4] = {tv.x, tv.y, tv.z, tv.w};
-    interp_vol_layout<C0, C1, C2, C3, C4, C5>(S, ip, v, phi);
+    const VolLoc loc = vrec[i];
+    const int v[4] = {loc.v.x, loc.v.y, loc.v.z, loc.v.w};
+    interp_vol_layout<C0, C1, C2, C3, C4, C5>(S, ip, v, loc.phi);
     if (elem_out) elem_out[ip - 1] = k;
     if (hit_out) hit_out[ip - 1] = PMMG_HIT_VOL_WALK;
   }
@@ -1092,7 +1107,7 @@ __global__ void k_fallback_init(int *a, int *b, unsigned long long *c, const int
 
 // ---------------------------------------------------------------- layout dispatch
 
-typedef void (*VolInterpFn)(Bg, const double *, const uint8_t *, int, const int *, Slots, int *, int8_t *);
+typedef void (*VolInterpFn)(const uint8_t *, int, const int *, const VolLoc *, Slots, int *, int8_t *);
 typedef void (*ScanInterpFn)(Bg, const double *, const int *, const int *, Slots, int *, int8_t *, int *, DevStats *);
 typedef void (*FusedFn)(Bg, const Frame *, const unsigned long long *, int, const double *, const int *, Slots, int *,
                         int8_t *, int *, DevStats *, int);
@@ -1159,7 +1174,7 @@ struct pmmg_hip_ctx {
   std::vector<DevBuf> o_f;
   // work buffers
   DevBuf frame, stats, grid, sgrid, cnt, off, binrank, order_v, order_b, vloc, scan_tmp, qs;
-  DevBuf cont;
+  DevBuf cont, vrec;
   DevBuf fb_vol, fb_bdy, best, ckey, cidx, bbest, bckey, bcidx;
   // host-mode staging
   DevBuf h_xyz, h_cls, h_met, h_elem, h_hit;
@@ -1277,7 +1292,7 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
-  DevBuf *bufs[] = {&c->cont, &c->o_xyz, &c->o_tetv, &c->o_adja, &c->o_triv, &c->o_adjt, &c->o_met, &c->frame, &c->stats,
+  DevBuf *bufs[] = {&c->cont, &c->vrec, &c->o_xyz, &c->o_tetv, &c->o_adja, &c->o_triv, &c->o_adjt, &c->o_met, &c->frame, &c->stats,
                     &c->grid, &c->sgrid, &c->cnt, &c->off, &c->binrank, &c->order_v, &c->order_b, &c->vloc, &c->qs,
                     &c->scan_tmp, &c->fb_vol, &c->fb_bdy, &c->best, &c->ckey, &c->cidx, &c->bbest, &c->bckey,
                     &c->bcidx, &c->h_xyz, &c->h_cls, &c->h_met, &c->h_elem, &c->h_hit};
@@ -1608,7 +1623,8 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   const size_t nq = (size_t)np_new;
   if (!ensure(c, c->frame, sizeof(Frame)) || !ensure(c, c->stats, sizeof(DevStats) + kStatParts * sizeof(StatPart)) ||
       !ensure(c, c->grid, 8 * (size_t)g * g * g) || !ensure(c, c->sgrid, 4 * (size_t)gs * gs * gs) ||
-      !ensure(c, c->order_v, 4 * nq) || !ensure(c, c->cont, 8 * nq) || !ensure(c, c->order_b, 4 * nq) || !ensure(c, c->vloc, 4 * nq) ||
+      !ensure(c, c->order_v, 4 * nq) || !ensure(c, c->cont, 8 * nq) ||
+      !ensure(c, c->vrec, sizeof(VolLoc) * nq) || !ensure(c, c->order_b, 4 * nq) || !ensure(c, c->vloc, 4 * nq) ||
       !ensure(c, c->fb_vol, 4 * nq) || !ensure(c, c->fb_bdy, 4 * nq) || !ensure(c, c->best, 4 * nq) ||
       !ensure(c, c->ckey, 8 * nq) || !ensure(c, c->cidx, 4 * nq) || !ensure(c, c->bbest, 4 * nq) ||
       !ensure(c, c->bckey, 8 * nq) || !ensure(c, c->bcidx, 4 * nq))
@@ -1681,15 +1697,17 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
 
   if (!(c->options & PMMG_HIP_OPT_FUSED)) {
     hipLaunchKernelGGL(k_vol_walk, dim3(blocks_for(np_new, 1 << 30)), dim3(kBlock), 0, s, bg, fr, grid, g, xyz_new,
-                       pclass, sorted ? (const int *)order_v : nullptr, np_new, (int *)c->vloc.p, (int *)c->fb_vol.p,
-                       (ContEntry *)c->cont.p, st, c->cap, c->maxstep);
+                       pclass, sorted ? (const int *)order_v : nullptr, np_new, (int *)c->vloc.p,
+                       (VolLoc *)c->vrec.p, (int *)c->fb_vol.p, (ContEntry *)c->cont.p, st, c->cap, c->maxstep);
     if (c->cap < c->maxstep) // continuation pass only when capping is enabled
-      hipLaunchKernelGGL(k_vol_walk_cont, dim3(8 * 256), dim3(kBlock), 0, s, bg, xyz_new, (int *)c->vloc.p,
-                         (int *)c->fb_vol.p, (const ContEntry *)c->cont.p, st, c->cap, c->maxstep);
+      hipLaunchKernelGGL(k_vol_walk_cont, dim3(8 * blocks_for((np_new + 7) / 8, 1 << 20)), dim3(kBlock), 0, s, bg,
+                         xyz_new, (int *)c->vloc.p,
+                         (VolLoc *)c->vrec.p, (int *)c->fb_vol.p, (const ContEntry *)c->cont.p, st, c->cap,
+                         c->maxstep);
     HIPCK(c, hipEventRecord(c->ev[6], s));
     VolInterpFn interp = pick_layout(S).fn;
-    hipLaunchKernelGGL(interp, dim3(blocks_for(np_new, 1 << 30)), dim3(kBlock), 0, s, bg, xyz_new, pclass, np_new,
-                       (const int *)c->vloc.p, S, elem_out, hit_out);
+    hipLaunchKernelGGL(interp, dim3(blocks_for(np_new, 1 << 30)), dim3(kBlock), 0, s, pclass, np_new,
+                       (const int *)c->vloc.p, (const VolLoc *)c->vrec.p, S, elem_out, hit_out);
   } else {
     FusedFn fused = pick_layout(S).ffn;
     hipLaunchKernelGGL(fused, dim3(blocks_for(np_new, 1 << 30)), dim3(kBlock), 0, s, bg, fr, grid, g, xyz_new,
