@@ -67,30 +67,33 @@ def pmc_traffic(workload: str):
 
 
 def cpu_baseline(w, bg, new, met, fields, pclass, budget_s: float):
-    """The oracle (C port of the reference path, 1 thread) on a bounded sample:
-    the full per-iteration precompute (faceAreas, triaNormals, nodeTrias, as the
-    reference's tim=2 timer includes it, src/libparmmg1.c:823-836) plus
-    locate+interpolate of new points in lattice order (the reference's warm
-    start kept) until `budget_s` seconds are used; the full-step time is the
-    precompute plus the sampled per-point time times all points."""
+    """The oracle (C restatement of the reference path) as `threads` parallel
+    workers on this host's cores, each a sequential reference run (warm start,
+    private visited flags) over a contiguous range of the new points, like one
+    MPI rank per group: the per-iteration precompute (faceAreas, triaNormals,
+    nodeTrias, which the reference's tim=2 timer includes,
+    src/libparmmg1.c:823-836) split over the threads, then locate+interpolate
+    until `budget_s` seconds are used; the full-step time is the precompute
+    plus the measured rate extrapolated to all points."""
     from oracle import oracle as O
 
+    threads = int(os.environ.get("PMMG_CPU_THREADS", "0")) or min(16, os.cpu_count() or 1)
     B = O.Background(bg, met, fields, w.hausd)
     order = np.arange(1, new.np + 1, dtype=np.int32)
-    r = O.run(B, new.xyz, pclass, order, budget_s=budget_s)
-    s = int(r["nvisited"])
+    r = O.run(B, new.xyz, pclass, order, budget_s=budget_s, threads=threads)
     t_pre, t_loc = r["t_precompute"], r["t_locate"]
-    nproc = int((pclass[:s] != 0).sum())
+    nproc = int((r["hit"] != 0).sum())
     ntot = int((pclass != 0).sum())
     t_full = t_pre + t_loc * ntot / max(nproc, 1)
     return {
         "value": round(ntot / t_full / 1e6, 4),
         "unit": "Mpts/s",
-        "cores": 1,
+        "cores": threads,
         "kind": "port",
-        "sample": f"oracle (C restatement of the reference path, 1 thread) on {w.name}: full precompute over "
-                  f"{bg.ne} tets ({t_pre:.2f}s) + locate/interp of the first {s} new points in lattice order "
-                  f"({t_loc:.2f}s, time-bounded), per-point rate extrapolated to all {ntot} points",
+        "sample": f"oracle (C restatement of the reference path) as {threads} threads, one contiguous range of "
+                  f"new points each (like MPI ranks), on {w.name}: precompute over {bg.ne} tets ({t_pre:.2f}s) + "
+                  f"locate/interp of {nproc} of {ntot} points ({t_loc:.2f}s, time-bounded), rate extrapolated "
+                  f"to all points",
         "t_precompute_s": round(t_pre, 3),
         "t_sample_s": round(t_loc, 3),
         "sample_points": nproc,

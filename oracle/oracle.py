@@ -53,6 +53,8 @@ def lib():
         L.orc_interp_mesh.restype = ci
         L.orc_interp_mesh_budget.argtypes = [vp, vp, vp, ci, cd, vp]
         L.orc_interp_mesh_budget.restype = ci
+        L.orc_interp_mesh_mt.argtypes = [vp, vp, vp, ci, ci, cd, vp]
+        L.orc_interp_mesh_mt.restype = ci
         L.orc_eval_in_element.argtypes = [vp, vp, ci, ci, ci, ci, vp, vp]
         L.orc_eval_in_element.restype = ci
         L.orc_tetra_minbary.argtypes = [vp, ci, vp]
@@ -97,10 +99,11 @@ class Background:
         return ctypes.byref(self.s)
 
 
-def run(bg: Background, xyz_new, pclass, visit, mode=MODE_FAITHFUL, budget_s: float = 0.0):
+def run(bg: Background, xyz_new, pclass, visit, mode=MODE_FAITHFUL, budget_s: float = 0.0, threads: int = 0):
     """Sequential reference-order run.  Returns dict of per-point arrays.
     With budget_s > 0 the locate+interp phase stops after about that many
-    seconds; out["nvisited"] is the number of visit entries processed."""
+    seconds; out["nvisited"] is the number of visit entries processed.
+    threads > 0: the threaded driver (visit[] split into `threads` ranges)."""
     xyz_new = np.ascontiguousarray(xyz_new, np.float64)
     pclass = np.ascontiguousarray(pclass, np.uint8)
     visit = np.ascontiguousarray(visit, np.int32)
@@ -116,7 +119,12 @@ def run(bg: Background, xyz_new, pclass, visit, mode=MODE_FAITHFUL, budget_s: fl
              _p(out["minbary"]), _p(out["steps"]))
     q = _Q(npn, _p(xyz_new), _p(pclass), visit.shape[0], _p(visit))
     timing = (ctypes.c_double * 2)()
-    nv = lib().orc_interp_mesh_budget(bg.ref, ctypes.byref(q), ctypes.byref(o), int(mode), float(budget_s), timing)
+    if threads > 0:
+        nv = lib().orc_interp_mesh_mt(bg.ref, ctypes.byref(q), ctypes.byref(o), int(mode), int(threads),
+                                      float(budget_s), timing)
+    else:
+        nv = lib().orc_interp_mesh_budget(bg.ref, ctypes.byref(q), ctypes.byref(o), int(mode), float(budget_s),
+                                          timing)
     if nv < 0:
         raise RuntimeError("oracle run failed")
     out["nvisited"] = nv

@@ -13,6 +13,7 @@
  */
 #define _POSIX_C_SOURCE 199309L
 #include "pmmg_oracle.h"
+#include <pthread.h>
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -591,18 +592,18 @@ int orc_interp_mesh(const orc_background *bg, const orc_queries *q, orc_outputs 
   return orc_interp_mesh_budget(bg, q, out, mode, 0.0, timing) >= 0;
 }
 
-int orc_interp_mesh_budget(const orc_background *bg, const orc_queries *q, orc_outputs *out, int mode,
-                           double budget_s, double *timing) {
-  orc_state S;
-  double t0 = now_s();
-  if (!state_init(&S, bg, mode)) { state_free(&S); return -1; }
-  double t1 = now_s();
+/* The visit loop of PMMG_interpMetricsAndFields_mesh (interpmesh_pmmg.c:535-643)
+ * over visit[v0, v1), warm start carried from point to point; stops early once
+ * `deadline` (now_s() clock, <= 0: none) has passed.  Returns the visit
+ * entries processed. */
+static int visit_range(orc_state *S, const orc_queries *q, orc_outputs *out, int v0, int v1, double deadline) {
+  const orc_background *bg = S->bg;
   int itet = 1, itria = 1; /* interpmesh_pmmg.c:529 */
   int nf = bg->nfield;
   double **frow = (double **)malloc(sizeof(double *) * (nf > 0 ? nf : 1));
-  int v = 0;
-  for (; v < q->nvisit; v++) {
-    if (budget_s > 0.0 && (v & 255) == 0 && v > 0 && now_s() - t1 > budget_s) break;
+  int v = v0;
+  for (; v < v1; v++) {
+    if (deadline > 0.0 && ((v - v0) & 255) == 0 && v > v0 && now_s() > deadline) break;
     int ip = q->visit[v];
     if (ip < 1 || ip > q->np) continue;
     int cls = q->pclass[ip - 1];
@@ -616,13 +617,13 @@ int orc_interp_mesh_budget(const orc_background *bg, const orc_queries *q, orc_o
     double mb = 0.0;
     if (cls == 2) {
       int edge, vertex;
-      hit = locate_bdy(&S, x, b, &itria, &edge, &vertex, &steps);
+      hit = locate_bdy(S, x, b, &itria, &edge, &vertex, &steps);
       elem = itria;
       loc = (vertex != ORC_UNSET) ? vertex : edge;
       mb = b[0].val;
       apply_bdy(bg, elem, b, edge, vertex, mrow, frow);
     } else {
-      hit = locate_vol(&S, x, b, &itet, &steps);
+      hit = locate_vol(S, x, b, &itet, &steps);
       elem = itet;
       mb = b[0].val;
       apply_vol(bg, elem, b, mrow, frow);
@@ -633,11 +634,139 @@ int orc_interp_mesh_budget(const orc_background *bg, const orc_queries *q, orc_o
     if (out->minbary) out->minbary[ip - 1] = mb;
     if (out->steps) out->steps[ip - 1] = steps;
   }
-  double t2 = now_s();
   free(frow);
+  return v - v0;
+}
+
+int orc_interp_mesh_budget(const orc_background *bg, const orc_queries *q, orc_outputs *out, int mode,
+                           double budget_s, double *timing) {
+  orc_state S;
+  double t0 = now_s();
+  if (!state_init(&S, bg, mode)) { state_free(&S); return -1; }
+  double t1 = now_s();
+  int n = visit_range(&S, q, out, 0, q->nvisit, budget_s > 0.0 ? t1 + budget_s : 0.0);
+  double t2 = now_s();
   state_free(&S);
   if (timing) { timing[0] = t1 - t0; timing[1] = t2 - t1; }
-  return v;
+  return n;
+}
+
+/* ---------------- threaded driver (CPU baseline) ---------------- */
+
+typedef struct {
+  orc_state S;            /* shared precompute, private visited flags */
+  const orc_queries *q;
+  orc_outputs *out;
+  int v0, v1, done;
+  int k0, k1;             /* precompute range (tetra) */
+  double deadline;
+} orc_job;
+
+static void *job_precompute(void *arg) {
+  orc_job *J = (orc_job *)arg;
+  for (int k = J->k0; k < J->k1; k++) J->S.qual[k] = tet_geom(J->S.bg, k, J->S.farea + 12 * (size_t)k);
+  return NULL;
+}
+
+static void *job_visit(void *arg) {
+  orc_job *J = (orc_job *)arg;
+  J->done = visit_range(&J->S, J->q, J->out, J->v0, J->v1, J->deadline);
+  return NULL;
+}
+
+int orc_interp_mesh_mt(const orc_background *bg, const orc_queries *q, orc_outputs *out, int mode, int nthreads,
+                       double budget_s, double *timing) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  orc_state S0;
+  double t0 = now_s();
+  /* the precompute of state_init with the per-tetra part (faceAreas, the
+   * dominant O(ne) stream) split over the threads */
+  memset(&S0, 0, sizeof(S0));
+  S0.bg = bg;
+  S0.mode = mode;
+  size_t ne = (size_t)bg->ne, nt = (size_t)bg->nt, np = (size_t)bg->np;
+  S0.qual = (double *)malloc(sizeof(double) * (ne + 1));
+  S0.farea = (double *)malloc(sizeof(double) * 12 * (ne + 1));
+  S0.tqual = (double *)malloc(sizeof(double) * (nt + 1));
+  S0.tnorm = (double *)malloc(sizeof(double) * 3 * (nt + 1));
+  S0.tflag = (int *)calloc(ne + 1, sizeof(int));
+  S0.trflag = (int *)calloc(nt + 1, sizeof(int));
+  S0.pflag = (int *)calloc(np + 1, sizeof(int));
+  S0.ntoff = (int *)calloc(np + 2, sizeof(int));
+  S0.ntlist = (int *)malloc(sizeof(int) * (np + 3 * nt + 1));
+  orc_job *J = (orc_job *)calloc((size_t)nthreads, sizeof(orc_job));
+  pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+  int ok = S0.qual && S0.farea && S0.tqual && S0.tnorm && S0.tflag && S0.trflag && S0.pflag && S0.ntoff &&
+           S0.ntlist && J && th;
+  if (ok) {
+    for (int t = 0; t < nthreads; t++) {
+      J[t].S = S0;
+      J[t].k0 = 1 + (int)((ne * (size_t)t) / (size_t)nthreads);
+      J[t].k1 = 1 + (int)((ne * (size_t)(t + 1)) / (size_t)nthreads);
+      pthread_create(&th[t], NULL, job_precompute, &J[t]);
+    }
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    for (size_t k = 1; k <= nt; k++) S0.tqual[k] = tria_geom(bg, (int)k, S0.tnorm + 3 * k);
+    for (size_t k = 1; k <= nt; k++)
+      for (int l = 0; l < 3; l++) S0.pflag[TRIV(bg, k, l)]++;
+    int off = 0;
+    for (size_t ip = 1; ip <= np; ip++) {
+      S0.ntoff[ip] = off;
+      if (S0.pflag[ip]) {
+        S0.ntlist[off] = 0;
+        off += S0.pflag[ip] + 1;
+      }
+    }
+    for (size_t k = 1; k <= nt; k++)
+      for (int l = 0; l < 3; l++) {
+        int ip = TRIV(bg, k, l);
+        int *cc = &S0.ntlist[S0.ntoff[ip]];
+        cc[1 + cc[0]] = (int)k;
+        cc[0]++;
+      }
+  }
+  double t1 = now_s();
+  int total = 0;
+  if (ok) {
+    /* one contiguous visit range per thread (as one MPI rank per group),
+     * each with private visited flags */
+    for (int t = 0; t < nthreads && ok; t++) {
+      J[t].S = S0;
+      J[t].S.base = 0;
+      if (t > 0) {
+        J[t].S.tflag = (int *)calloc(ne + 1, sizeof(int));
+        J[t].S.trflag = (int *)calloc(nt + 1, sizeof(int));
+        J[t].S.pflag = (int *)malloc(sizeof(int) * (np + 1));
+        ok = J[t].S.tflag && J[t].S.trflag && J[t].S.pflag;
+        if (J[t].S.pflag) memcpy(J[t].S.pflag, S0.pflag, sizeof(int) * (np + 1));
+      }
+      J[t].q = q;
+      J[t].out = out;
+      J[t].v0 = (int)(((size_t)q->nvisit * (size_t)t) / (size_t)nthreads);
+      J[t].v1 = (int)(((size_t)q->nvisit * (size_t)(t + 1)) / (size_t)nthreads);
+    }
+    t1 = now_s();
+    for (int t = 0; t < nthreads && ok; t++) {
+      J[t].deadline = budget_s > 0.0 ? t1 + budget_s : 0.0;
+      pthread_create(&th[t], NULL, job_visit, &J[t]);
+    }
+    for (int t = 0; t < nthreads && ok; t++) {
+      pthread_join(th[t], NULL);
+      total += J[t].done;
+    }
+  }
+  double t2 = now_s();
+  for (int t = 1; J && t < nthreads; t++) {
+    free(J[t].S.tflag);
+    free(J[t].S.trflag);
+    free(J[t].S.pflag);
+  }
+  state_free(&S0);
+  free(J);
+  free(th);
+  if (timing) { timing[0] = t1 - t0; timing[1] = t2 - t1; }
+  return ok ? total : -1;
 }
 
 /* ---------------- element-wise checkers ---------------- */

@@ -86,6 +86,15 @@ int orc_interp_mesh(const orc_background *bg, const orc_queries *q, orc_outputs 
 int orc_interp_mesh_budget(const orc_background *bg, const orc_queries *q, orc_outputs *out,
                            int mode, double budget_s, double *timing);
 
+/* Threaded CPU baseline: the precompute's per-tetra stream split over
+ * nthreads, then nthreads contiguous ranges of visit[] processed in parallel
+ * (each as its own sequential reference run with warm start and private
+ * visited flags, like one MPI rank per group), each stopping after budget_s
+ * seconds (<= 0: none).  Returns the visit entries processed in total (the
+ * ranges' prefixes), or -1.  timing[0] precompute, timing[1] locate wall. */
+int orc_interp_mesh_mt(const orc_background *bg, const orc_queries *q, orc_outputs *out,
+                       int mode, int nthreads, double budget_s, double *timing);
+
 /* Re-evaluate one query in a given element / hit kind (as the GPU reports
  * it) with the reference arithmetic, writing the interpolated values into
  * met_row / field_rows (rows of the point, not whole arrays).  Used to check

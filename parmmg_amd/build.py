@@ -85,8 +85,8 @@ def build_oracle(force: bool = False) -> str:
     deps = [src, os.path.join(ORACLE, "pmmg_oracle.h"), __file__]
     if force or _stale(ORACLE_SO, deps):
         # -ffp-contract=off: keep the reference's rounding (no FMA contraction)
-        _run(["gcc", "-O2", "-std=c99", "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wextra", "-fPIC",
-              "-shared", "-o", ORACLE_SO, src, "-lm"])
+        _run(["gcc", "-O2", "-std=gnu99", "-pthread", "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wextra",
+              "-fPIC", "-shared", "-o", ORACLE_SO, src, "-lm", "-lpthread"])
     return ORACLE_SO
 
 

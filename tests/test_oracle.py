@@ -170,3 +170,29 @@ def test_faithful_vs_fresh_cone_state():
     rr = O.run(B, new.xyz, pc, synth.visit_order(new), O.MODE_FRESH)
     diff = rr["hit"] != rf["hit"]
     assert (~diff | np.isin(rf["hit"], [7, 8]) | np.isin(rr["hit"], [7, 8])).all()
+
+
+def test_threaded_driver_matches_sequential():
+    """orc_interp_mesh_mt (CPU baseline) = sequential runs over ranges: every
+    point is processed, and where both runs pick the same element the values
+    are bit-identical (warm starts differ per range, so near-face points may
+    legitimately land in another accepting element)."""
+    from parmmg_amd import synth
+
+    bg = synth.lattice(synth.CUBE, 6)
+    new = synth.lattice(synth.CUBE, 7, jitter=0.2, with_trias=False)
+    met = synth.solution(synth.F_ANI, bg.xyz)
+    fields = [synth.solution(synth.F_SCALAR, bg.xyz), synth.solution(synth.F_TENSOR, bg.xyz)]
+    B = O.Background(bg, met, fields, 0.01)
+    pc = synth.classes(new)
+    order = np.arange(1, new.np + 1, dtype=np.int32)
+    seq = O.run(B, new.xyz, pc, order)
+    mt = O.run(B, new.xyz, pc, order, threads=4)
+    act = pc != 0
+    assert mt["nvisited"] == new.np
+    assert ((mt["hit"] != 0) == act).all()
+    same = act & (seq["elem"] == mt["elem"]) & (seq["hit"] == mt["hit"])
+    assert same.sum() > 0.95 * act.sum()
+    np.testing.assert_array_equal(seq["met"][same], mt["met"][same])
+    for a, b in zip(seq["fields"], mt["fields"]):
+        np.testing.assert_array_equal(a[same], b[same])
