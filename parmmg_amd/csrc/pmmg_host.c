@@ -93,10 +93,16 @@ int pmmg_interp_metrics_and_fields(pmmg_hip_ctx *ctx, int ngrp, const pmmg_old_g
     }
     if (!ismet && o->nfield == 0) continue; /* nothing to do */
     uint8_t *pclass = (uint8_t *)malloc((size_t)g->np + 1);
-    if (!pclass) { ier = 0; continue; }
+    /* the module's HBM layout of the tetra: packed {v[4], adja[4]} records */
+    int *tet8 = (int *)malloc(sizeof(int) * 8 * (size_t)(o->ne > 0 ? o->ne : 1));
+    if (!pclass || !tet8) { free(pclass); free(tet8); ier = 0; continue; }
+    for (int64_t k = 0; k < o->ne; k++) {
+      memcpy(tet8 + 8 * k, o->tetv + 4 * k, 4 * sizeof(int));
+      memcpy(tet8 + 8 * k + 4, o->adja + 4 * k, 4 * sizeof(int));
+    }
     pmmg_classify_points(g, pclass);
-    int ok = pmmg_hip_set_background(ctx, o->np, o->xyz, o->ne, o->tetv, o->adja, o->nt, o->triv, o->adjt,
-                                     o->hausd, PMMG_HIP_HOST) &&
+    int ok = pmmg_hip_set_background_tet8(ctx, o->np, o->xyz, o->ne, tet8, o->nt, o->triv, o->adjt, o->hausd,
+                                          PMMG_HIP_HOST) &&
              pmmg_hip_set_solutions(ctx, ismet ? o->met_size : 0, ismet ? o->met : NULL, o->nfield,
                                     o->field_size, o->field, PMMG_HIP_HOST);
     pmmg_hip_stats st;
@@ -106,6 +112,7 @@ int pmmg_interp_metrics_and_fields(pmmg_hip_ctx *ctx, int ngrp, const pmmg_old_g
     if (ok && stats) stats_add(stats, &st);
     if (!ok) ier = 0;
     free(pclass);
+    free(tet8);
   }
   return ier;
 }
