@@ -116,39 +116,73 @@ __global__ void k_frame_final(Frame *fr, int g, int gs, int gb) {
 
 // volume seeds: per cell, the sampled tetra whose centroid is closest to
 // the cell centre; key = (float(dist^2) bits << 32) | id -> deterministic min
+// Samples are taken in runs of R consecutive tetra (R = 4: one 128-byte line
+// of packed tetra records), nsamp / R runs evenly spaced over the tetra: the
+// sampling cost is the lines it reads, and 4 samples per line quadruple the
+// samples for the same traffic.  Lanes of a run that land in the same cell
+// combine their keys first (one atomic per cell and run).
 __global__ __launch_bounds__(kBlock) void k_seed_vol(Bg bg, const Frame *fr, unsigned long long *cell, int g,
-                                                     long long nsamp, int mode) {
-  for (long long s = blockIdx.x * (long long)blockDim.x + threadIdx.x; s < nsamp;
-       s += (long long)gridDim.x * blockDim.x) {
-    int k = 1 + (int)((s * (long long)bg.ne) / nsamp);
-    const int4 tv = tetv_row(bg, k);
-    if (tv.x <= 0) continue;
-    // representative point of the tetra: centroid (mode 0), midpoint of
-    // the edge v0-v3 (1), first vertex (2); a cell's seed is the sampled
-    // tetra whose point is closest to the cell centre
-    double p[3];
-    load_pt(bg.xyz, tv.x, p);
-    if (mode == 0) {
-      double a[3], b[3], e[3];
-      load_pt(bg.xyz, tv.y, a);
-      load_pt(bg.xyz, tv.z, b);
-      load_pt(bg.xyz, tv.w, e);
-      for (int d = 0; d < 3; d++) p[d] = 0.25 * (p[d] + a[d] + b[d] + e[d]);
-    } else if (mode == 1) {
-      double e[3];
-      load_pt(bg.xyz, tv.w, e);
-      for (int d = 0; d < 3; d++) p[d] = 0.5 * (p[d] + e[d]);
+                                                     long long nsamp, int mode, int R) {
+  const long long nruns = (nsamp + R - 1) / R;
+  const long long quads = bg.ne / 4;
+  const long long nthreads = nruns * R;
+  for (long long s0 = blockIdx.x * (long long)blockDim.x; s0 < nthreads; s0 += (long long)gridDim.x * blockDim.x) {
+    const long long s = s0 + threadIdx.x;
+    const long long run = s / R;
+    const int r = (int)(s % R);
+    // run start aligned to a 4-tetra boundary (a cache line of tet8 records)
+    const long long base = 4 * ((run * quads) / (nruns > 0 ? nruns : 1));
+    const int k = (int)(1 + base + r);
+    bool ok = s < nthreads && k <= bg.ne;
+    int4 tv = make_int4(0, 0, 0, 0);
+    if (ok) {
+      tv = tetv_row(bg, k);
+      ok = tv.x > 0;
     }
-    int c[3];
-    float d2 = 0.f;
-    for (int d = 0; d < 3; d++) {
-      c[d] = cell_coord(p[d], fr->lo[d], fr->inv_vol[d], g);
-      double ctr = fr->lo[d] + (c[d] + 0.5) / (fr->inv_vol[d] > 0.0 ? fr->inv_vol[d] : 1.0);
-      float dd = (float)(p[d] - ctr);
-      d2 += dd * dd;
+    unsigned long long key = ~0ULL;
+    long long ci = -1;
+    if (ok) {
+      // representative point of the tetra: centroid (mode 0), midpoint of
+      // the edge v0-v3 (1), first vertex (2); a cell's seed is the sampled
+      // tetra whose point is closest to the cell centre
+      double p[3];
+      load_pt(bg.xyz, tv.x, p);
+      if (mode == 0) {
+        double a[3], b[3], e[3];
+        load_pt(bg.xyz, tv.y, a);
+        load_pt(bg.xyz, tv.z, b);
+        load_pt(bg.xyz, tv.w, e);
+        for (int d = 0; d < 3; d++) p[d] = 0.25 * (p[d] + a[d] + b[d] + e[d]);
+      } else if (mode == 1) {
+        double e[3];
+        load_pt(bg.xyz, tv.w, e);
+        for (int d = 0; d < 3; d++) p[d] = 0.5 * (p[d] + e[d]);
+      }
+      int c[3];
+      float d2 = 0.f;
+      for (int d = 0; d < 3; d++) {
+        c[d] = cell_coord(p[d], fr->lo[d], fr->inv_vol[d], g);
+        double ctr = fr->lo[d] + (c[d] + 0.5) / (fr->inv_vol[d] > 0.0 ? fr->inv_vol[d] : 1.0);
+        float dd = (float)(p[d] - ctr);
+        d2 += dd * dd;
+      }
+      key = ((unsigned long long)__float_as_uint(d2) << 32) | (unsigned)k;
+      ci = c[0] + (long long)g * (c[1] + (long long)g * c[2]);
     }
-    unsigned long long key = ((unsigned long long)__float_as_uint(d2) << 32) | (unsigned)k;
-    atomicMin(&cell[c[0] + (size_t)g * (c[1] + (size_t)g * c[2])], key);
+    // combine within the run (R lanes, R divides 64): the first lane of each
+    // distinct cell issues the atomic with the run's minimum for that cell
+    const int lane = __lane_id(), g0 = lane - r;
+    bool leader = ci >= 0;
+    unsigned long long best = key;
+    for (int o = 0; o < R; o++) {
+      const long long co = __shfl(ci, g0 + o);
+      const unsigned long long ko = __shfl(key, g0 + o);
+      if (co == ci && ci >= 0) {
+        best = ko < best ? ko : best;
+        if (o < r) leader = false;
+      }
+    }
+    if (leader) atomicMin(&cell[ci], best);
   }
 }
 
@@ -1182,8 +1216,9 @@ struct pmmg_hip_ctx {
   hipEvent_t ev[8] = {};
   bool pending = false;
   int tpc = 8;      // background tetra per volume seed cell
-  int spc = 2;      // sampled tetra per seed cell
+  int spc = 4;      // sampled tetra per seed cell
   int seed_mode = 0; // seed point of a sampled tetra: 0 centroid, 1 edge v0-v3 midpoint, 2 first vertex
+  int seed_run = 4;  // consecutive tetra per sample run (1, 2, 4, 8)
   int qpb = 8;      // queries per Morton bin (walk path)
   int qpc = 1;      // queries per scan cell (scan path)
   int ncu = 256;     // compute units of the device
@@ -1276,6 +1311,8 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   c->tpc = env_int("PMMG_HIP_TPC", c->tpc);
   c->spc = env_int("PMMG_HIP_SPC", c->spc);
   if (getenv("PMMG_HIP_SEEDMODE")) c->seed_mode = atoi(getenv("PMMG_HIP_SEEDMODE"));
+  c->seed_run = env_int("PMMG_HIP_SEEDRUN", c->seed_run);
+  if (c->seed_run != 1 && c->seed_run != 2 && c->seed_run != 4 && c->seed_run != 8) c->seed_run = 4;
   c->qpb = env_int("PMMG_HIP_QPB", c->qpb);
   c->qpc = env_int("PMMG_HIP_QPC", c->qpc);
   c->maxstep = env_int("PMMG_HIP_MAXSTEP", c->maxstep);
@@ -1663,7 +1700,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   long long nsamp = (long long)c->spc * ng;
   if (nsamp > bg.ne) nsamp = bg.ne;
   hipLaunchKernelGGL(k_seed_vol, dim3(blocks_for(nsamp, 8192)), dim3(kBlock), 0, s, bg, fr, grid, g, nsamp,
-                     c->seed_mode);
+                     c->seed_mode, c->seed_run);
   if (bg.nt > 0) hipLaunchKernelGGL(k_seed_srf, dim3(blocks_for(bg.nt, 4096)), dim3(kBlock), 0, s, bg, fr, sgrid, gs);
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[1], s));
