@@ -1,0 +1,152 @@
+"""Edge cases and full-size properties of the HIP module (runs on the MI355X).
+
+Full-size checks follow tests/parity.py's contract through size-independent
+properties (the oracle cannot replay 4M points in seconds): every point
+processed, affine fields reproduced exactly by the P1 interpolation (bit
+tolerance 1e-13 absolute), a constant SPD tensor reproduced by the
+inverse-tensor interpolation, acceptance and values of a random sample
+checked against the oracle, and determinism across runs.
+"""
+import numpy as np
+import pytest
+
+from parity import check, make_case, run_gpu
+from parmmg_amd import configs, synth
+from parmmg_amd.transfer import TransferContext, pack_solutions, pack_tet8
+
+C = synth.CUBE
+
+
+@pytest.mark.gpu
+def test_zero_new_points():
+    case = make_case(kind=C, n_old=4, n_new=3, with_ref=False)
+    with TransferContext(0) as ctx:
+        bg = case["bg"]
+        ctx.set_background(bg.xyz, bg.tetv, bg.adja, bg.triv, bg.adjt, case["hausd"])
+        ctx.set_solutions(case["met"], case["fields"])
+        st = ctx.locate_interp(np.zeros((0, 3)), np.zeros(0, np.uint8), np.zeros((0, 6)),
+                               [np.zeros((0, f.shape[1])) for f in case["fields"]])
+        assert st.nvol == 0 and st.nbdy == 0
+
+
+@pytest.mark.gpu
+def test_all_points_skipped():
+    case = make_case(kind=C, n_old=4, n_new=5, with_ref=False)
+    case["pclass"][:] = 0
+    gpu = run_gpu(case)
+    assert (gpu["hit"] == 0).all() and np.isnan(gpu["met"]).all()
+
+
+@pytest.mark.gpu
+def test_background_without_trias_volume_only():
+    """nt = 0 is allowed when no surface query is submitted."""
+    import dataclasses
+
+    case = make_case(kind=C, n_old=5, n_new=6)
+    case["pclass"] = np.where(case["pclass"] == 2, 0, case["pclass"]).astype(np.uint8)
+    bg_notri = dataclasses.replace(case["bg"], triv=np.zeros((0, 3), np.int32), adjt=np.zeros((0, 3), np.int32))
+    gpu = run_gpu(dict(case, bg=bg_notri))
+    rep = check(case, gpu)
+    assert rep["n"] == int((case["pclass"] == 1).sum())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fields", [
+    (synth.F_VECTOR, synth.F_SCALAR, synth.F_TENSOR, synth.F_VECTOR),                 # generic layout path
+    (synth.F_SCALAR,) * 7,                                                              # metric + 7 fields (slot limit)
+])
+def test_unusual_slot_layouts(fields):
+    case = make_case(kind=C, n_old=5, n_new=6, metric=synth.F_ISO, fields=fields)
+    for kw in ({}, dict(packed=True, tet8=True)):
+        gpu = run_gpu(case, **kw)
+        rep = check(case, gpu)
+        assert rep["class_i"] == rep["class_i_same"]
+
+
+@pytest.mark.gpu
+def test_too_many_fields_rejected():
+    case = make_case(kind=C, n_old=3, n_new=3, metric=synth.F_ISO, fields=(synth.F_SCALAR,) * 8, with_ref=False)
+    with TransferContext(0) as ctx:
+        bg = case["bg"]
+        ctx.set_background(bg.xyz, bg.tetv, bg.adja, bg.triv, bg.adjt, case["hausd"])
+        with pytest.raises(RuntimeError):
+            ctx.set_solutions(case["met"], case["fields"])
+
+
+def _full_size(w, seed=synth.SEED):
+    bg = synth.lattice(w.kind, w.n_old)
+    new = synth.lattice(w.kind, w.n_new, jitter=w.jitter_new, seed=seed)
+    met = synth.solution(w.metric, bg.xyz)
+    fields = [synth.solution(f, bg.xyz) for f in (synth.F_AFFINE, synth.F_AFFINE_VEC, synth.F_CONST_TENSOR)]
+    pc = synth.classes(new)
+    return bg, new, met, fields, pc
+
+
+def _run_dev(ctx, bg, new, met, fields, pc, hausd, packed=False):
+    d = dict(xyz=ctx.upload(bg.xyz), tet8=ctx.upload(pack_tet8(bg.tetv, bg.adja)), triv=ctx.upload(bg.triv),
+             adjt=ctx.upload(bg.adjt), q=ctx.upload(new.xyz), pc=ctx.upload(pc))
+    ctx.set_background_tet8(d["xyz"], d["tet8"], d["triv"], d["adjt"], hausd)
+    if packed:
+        rec, *meta = pack_solutions(met, fields)
+        d["rec"] = ctx.upload(rec)
+        ctx.set_solutions_packed(d["rec"], *meta)
+    else:
+        d["met"], d["f"] = ctx.upload(met), [ctx.upload(f) for f in fields]
+        ctx.set_solutions(d["met"], d["f"])
+    mo = ctx.empty((new.np, met.shape[1]), np.float64)
+    fo = [ctx.empty((new.np, f.shape[1]), np.float64) for f in fields]
+    el, hit = ctx.empty((new.np,), np.int32), ctx.empty((new.np,), np.int8)
+    ctx.locate_interp(d["q"], d["pc"], mo, fo, el, hit, sync=False)
+    st = ctx.sync()
+    return mo.download(), [f.download() for f in fo], el.download(), hit.download(), st
+
+
+@pytest.mark.gpu
+def test_full_size_cfg3_properties():
+    """cfg3 (20.25M background tetra, 4.1M new points) with fields whose exact
+    answers are known: affine scalar and vector (P1 reproduces them), constant
+    SPD tensor (the inverse-tensor interpolation returns it)."""
+    w = configs.CFG3
+    bg, new, met, fields, pc = _full_size(w)
+    with TransferContext(0) as ctx:
+        mo, fo, el, hit, st = _run_dev(ctx, bg, new, met, fields, pc, w.hausd)
+        mo2, fo2, el2, hit2, _ = _run_dev(ctx, bg, new, met, fields, pc, w.hausd, packed=True)
+    act = pc != 0
+    assert ((hit & 15) != 0).sum() == act.sum()
+    assert ((hit & 15)[~act] == 0).all()
+    assert st.nvol_exhaust + st.nvol_closest < 0.001 * act.sum()
+    x = new.xyz
+    vol = pc == 1
+    np.testing.assert_allclose(fo[0][vol, 0], 1 + 2 * x[vol, 0] - 3 * x[vol, 1] + 0.5 * x[vol, 2], rtol=0,
+                               atol=1e-12)
+    vec = np.c_[x[:, 0] + x[:, 1], 2 * x[:, 1] - x[:, 2], 3 * x[:, 2] + x[:, 0] - 1]
+    np.testing.assert_allclose(fo[1][vol], vec[vol], rtol=0, atol=1e-12)
+    np.testing.assert_allclose(fo[2][act], np.tile([4.0, 1.0, 0.5, 3.0, 0.25, 2.0], (int(act.sum()), 1)),
+                               rtol=1e-12)
+    # metric: SPD, finite on every processed point
+    assert np.isfinite(mo[act]).all()
+    # packed records give bit-identical results (same kernels, same elements)
+    np.testing.assert_array_equal(el, el2)
+    np.testing.assert_array_equal(mo, mo2)
+    for a, b in zip(fo, fo2):
+        np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.gpu
+def test_full_size_cfg3_sample_against_oracle_and_determinism():
+    """A random sample of cfg3's points checked against the oracle (acceptance
+    of the chosen element + values bit-for-bit), and two runs bit-identical."""
+    from oracle import oracle as O
+
+    w = configs.CFG3
+    bg, new, met, fields, pc = _full_size(w)
+    fields = [synth.solution(f, bg.xyz) for f in w.fields]
+    with TransferContext(0) as ctx:
+        mo, fo, el, hit, st = _run_dev(ctx, bg, new, met, fields, pc, w.hausd)
+        mo2, fo2, el2, hit2, _ = _run_dev(ctx, bg, new, met, fields, pc, w.hausd)
+    np.testing.assert_array_equal(el, el2)
+    np.testing.assert_array_equal(hit, hit2)
+    np.testing.assert_array_equal(mo, mo2)
+    case = dict(B=O.Background(bg, met, fields, w.hausd), new=new, pclass=pc, met=met, fields=fields)
+    rep = check(case, dict(met=mo, fields=fo, elem=el, hit=hit), max_points=3000)
+    assert rep["n"] == 3000 and rep["maxrel"] <= 1e-12
