@@ -1205,6 +1205,9 @@ struct pmmg_hip_ctx {
   int device = 0;
   int options = 0;
   hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr; // surface branch, concurrent with the volume walk
+  bool bdy_on_s2 = false;
+  int two_streams = 1; // PMMG_HIP_STREAMS=1: everything on one stream
   char err[512] = {0};
   Bg bg{};
   int met_size = 0;
@@ -1218,13 +1221,13 @@ struct pmmg_hip_ctx {
   DevBuf o_xyz, o_tetv, o_adja, o_triv, o_adjt, o_met;
   std::vector<DevBuf> o_f;
   // work buffers
-  DevBuf frame, stats, grid, sgrid, cnt, off, binrank, order_v, order_b, vloc, scan_tmp, qs;
+  DevBuf frame, stats, grid, sgrid, cnt, off, binrank, order_v, order_b, vloc, scan_tmp, scan_tmp2, qs;
   DevBuf cont, vrec;
   DevBuf fb_vol, fb_bdy, best, ckey, cidx, bbest, bckey, bcidx;
   // host-mode staging
   DevBuf h_xyz, h_cls, h_met, h_elem, h_hit;
   std::vector<DevBuf> h_f;
-  hipEvent_t ev[8] = {};
+  hipEvent_t ev[10] = {};
   bool pending = false;
   int tpc = 8;      // background tetra per volume seed cell
   int spc = 4;      // sampled tetra per seed cell
@@ -1308,12 +1311,13 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   pmmg_hip_ctx *c = new pmmg_hip_ctx();
   c->device = device;
   c->options = options;
-  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
     fprintf(stderr, "[parmmg_hip] cannot initialise device %d\n", device);
     delete c;
     return nullptr;
   }
-  for (int i = 0; i < 8; i++) (void)hipEventCreate(&c->ev[i]);
+  for (int i = 0; i < 10; i++) (void)hipEventCreate(&c->ev[i]);
   if (hipHostMalloc((void **)&c->h_small, 64, hipHostMallocDefault) != hipSuccess) {
     fprintf(stderr, "[parmmg_hip] cannot allocate pinned host memory\n");
     delete c;
@@ -1323,6 +1327,7 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   c->spc = env_int("PMMG_HIP_SPC", c->spc);
   if (getenv("PMMG_HIP_SEEDMODE")) c->seed_mode = atoi(getenv("PMMG_HIP_SEEDMODE"));
   c->seed_run = env_int("PMMG_HIP_SEEDRUN", c->seed_run);
+  c->two_streams = env_int("PMMG_HIP_STREAMS", 2) >= 2;
   if (c->seed_run != 1 && c->seed_run != 2 && c->seed_run != 4 && c->seed_run != 8) c->seed_run = 4;
   c->qpb = env_int("PMMG_HIP_QPB", c->qpb);
   c->qpc = env_int("PMMG_HIP_QPC", c->qpc);
@@ -1342,13 +1347,14 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   (void)hipStreamSynchronize(c->stream);
   DevBuf *bufs[] = {&c->cont, &c->vrec, &c->o_xyz, &c->o_tetv, &c->o_adja, &c->o_triv, &c->o_adjt, &c->o_met, &c->frame, &c->stats,
                     &c->grid, &c->sgrid, &c->cnt, &c->off, &c->binrank, &c->order_v, &c->order_b, &c->vloc, &c->qs,
-                    &c->scan_tmp, &c->fb_vol, &c->fb_bdy, &c->best, &c->ckey, &c->cidx, &c->bbest, &c->bckey,
+                    &c->scan_tmp, &c->scan_tmp2, &c->fb_vol, &c->fb_bdy, &c->best, &c->ckey, &c->cidx, &c->bbest, &c->bckey,
                     &c->bcidx, &c->h_xyz, &c->h_cls, &c->h_met, &c->h_elem, &c->h_hit};
   for (DevBuf *b : bufs) release(*b);
   for (auto &b : c->o_f) release(b);
   for (auto &b : c->h_f) release(b);
-  for (int i = 0; i < 8; i++)
+  for (int i = 0; i < 10; i++)
     if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
+  if (c->stream2) (void)hipStreamDestroy(c->stream2);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->h_small) (void)hipHostFree(c->h_small);
   delete c;
@@ -1635,11 +1641,16 @@ static int run_scan(pmmg_hip_ctx *c, const Slots &S, int np_new, const double *x
                      (const int *)order_v, (const int *)res, S, elem_out, hit_out, (int *)c->fb_vol.p, st);
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[3], s));
+  const hipStream_t sb = s; // the scan path keeps everything on one stream
+  c->bdy_on_s2 = false;
+  HIPCK(c, hipEventRecord(c->ev[8], sb));
   if (bg.nt > 0) {
-    hipLaunchKernelGGL(k_bdy, dim3(8 * blocks_for((np_new + 7) / 8, 256)), dim3(kBlock), 0, s, bg, fr, sgrid, gs,
+    hipLaunchKernelGGL(k_bdy, dim3(8 * blocks_for((np_new + 7) / 8, 256)), dim3(kBlock), 0, sb, bg, fr, sgrid, gs,
                        xyz_new, order_b, S, elem_out, hit_out, (int *)c->fb_bdy.p, st, c->maxstep);
     HIPCK(c, hipGetLastError());
   }
+  HIPCK(c, hipEventRecord(c->ev[9], sb));
+  if (c->bdy_on_s2) HIPCK(c, hipStreamWaitEvent(s, c->ev[9], 0));
   HIPCK(c, hipEventRecord(c->ev[4], s));
   if (!launch_fallbacks(c, S, xyz_new, elem_out, hit_out)) return 0;
   HIPCK(c, hipEventRecord(c->ev[5], s));
@@ -1708,11 +1719,20 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
                      sorted ? (int *)c->cnt.p : nullptr, sorted ? 2LL * nbins : 0LL, 1);
   hipLaunchKernelGGL(k_bbox, dim3(blocks_for(bg.np, 1024)), dim3(kBlock), 0, s, bg.xyz, bg.np, fr);
   hipLaunchKernelGGL(k_frame_final, dim3(1), dim3(1), 0, s, fr, g, gs, gb);
+  // The surface branch (tria seeds, surface list, k_bdy) only needs the
+  // frame: on the input-order path it runs on a second stream, concurrently
+  // with the volume seeds and walks (joined before the fallbacks).
+  const hipStream_t sb = (!sorted && bg.nt > 0 && c->two_streams) ? c->stream2 : s;
+  c->bdy_on_s2 = sb != s;
+  if (c->bdy_on_s2) {
+    HIPCK(c, hipEventRecord(c->ev[7], s));
+    HIPCK(c, hipStreamWaitEvent(sb, c->ev[7], 0));
+  }
+  if (bg.nt > 0) hipLaunchKernelGGL(k_seed_srf, dim3(blocks_for(bg.nt, 4096)), dim3(kBlock), 0, sb, bg, fr, sgrid, gs);
   long long nsamp = (long long)c->spc * ng;
   if (nsamp > bg.ne) nsamp = bg.ne;
   hipLaunchKernelGGL(k_seed_vol, dim3(blocks_for(nsamp, 8192)), dim3(kBlock), 0, s, bg, fr, grid, g, nsamp,
                      c->seed_mode, c->seed_run);
-  if (bg.nt > 0) hipLaunchKernelGGL(k_seed_srf, dim3(blocks_for(bg.nt, 4096)), dim3(kBlock), 0, s, bg, fr, sgrid, gs);
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[1], s));
 
@@ -1727,17 +1747,18 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
                        (const int2 *)c->binrank.p, (const int *)c->off.p, nbins, order_v, order_b);
     hipLaunchKernelGGL(k_bin_total, dim3(1), dim3(1), 0, s, (const int *)c->off.p, (const int *)c->cnt.p, nbins, st);
   } else {
-    // stable class compaction: the surface list always; the volume list only
-    // for the fused kernel (k_vol_walk selects volume points itself)
+    // stable class compaction: the surface list always (on the surface
+    // branch's stream); the volume list only for the fused kernel
+    // (k_vol_walk selects volume points itself)
     hipcub::CountingInputIterator<int> ids(1);
     size_t tb = 0;
     HIPCK(c, hipcub::DeviceSelect::If(nullptr, tb, ids, order_v, &st->nvol, (int64_t)np_new, IsClass{pclass, 1}, s));
-    if (!ensure(c, c->scan_tmp, tb)) return 0;
+    if (!ensure(c, c->scan_tmp, tb) || !ensure(c, c->scan_tmp2, tb)) return 0;
     if (c->options & PMMG_HIP_OPT_FUSED)
       HIPCK(c, hipcub::DeviceSelect::If(c->scan_tmp.p, tb, ids, order_v, &st->nvol, (int64_t)np_new,
                                         IsClass{pclass, PMMG_PT_VOL}, s));
-    HIPCK(c, hipcub::DeviceSelect::If(c->scan_tmp.p, tb, ids, order_b, &st->nbdy, (int64_t)np_new,
-                                      IsClass{pclass, PMMG_PT_BDY}, s));
+    HIPCK(c, hipcub::DeviceSelect::If(c->scan_tmp2.p, tb, ids, order_b, &st->nbdy, (int64_t)np_new,
+                                      IsClass{pclass, PMMG_PT_BDY}, sb));
   }
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[2], s));
@@ -1764,11 +1785,14 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   }
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[3], s));
+  HIPCK(c, hipEventRecord(c->ev[8], sb));
   if (bg.nt > 0) {
-    hipLaunchKernelGGL(k_bdy, dim3(8 * blocks_for((np_new + 7) / 8, 256)), dim3(kBlock), 0, s, bg, fr, sgrid, gs,
+    hipLaunchKernelGGL(k_bdy, dim3(8 * blocks_for((np_new + 7) / 8, 256)), dim3(kBlock), 0, sb, bg, fr, sgrid, gs,
                        xyz_new, order_b, S, elem_out, hit_out, (int *)c->fb_bdy.p, st, c->maxstep);
     HIPCK(c, hipGetLastError());
   }
+  HIPCK(c, hipEventRecord(c->ev[9], sb));
+  if (c->bdy_on_s2) HIPCK(c, hipStreamWaitEvent(s, c->ev[9], 0));
   HIPCK(c, hipEventRecord(c->ev[4], s));
 
   if (!launch_fallbacks(c, S, xyz_new, elem_out, hit_out)) return 0;
@@ -1815,8 +1839,8 @@ static int collect_stats(pmmg_hip_ctx *c, pmmg_hip_stats *out) {
   out->ms_vol = ms;
   HIPCK(c, hipEventElapsedTime(&ms, c->ev[2], c->ev[6]));
   out->ms_vol_locate = ms;
-  HIPCK(c, hipEventElapsedTime(&ms, c->ev[3], c->ev[4]));
-  out->ms_bdy = ms;
+  HIPCK(c, hipEventElapsedTime(&ms, c->ev[8], c->ev[9]));
+  out->ms_bdy = ms; // on the surface stream when it ran concurrently
   HIPCK(c, hipEventElapsedTime(&ms, c->ev[4], c->ev[5]));
   out->ms_fallback = ms;
   HIPCK(c, hipEventElapsedTime(&ms, c->ev[0], c->ev[5]));
