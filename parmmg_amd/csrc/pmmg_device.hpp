@@ -333,11 +333,19 @@ __device__ __forceinline__ void load6(const double *p, double *m) {
   m[0] = a.x; m[1] = a.y; m[2] = b.x; m[3] = b.y; m[4] = c.x; m[5] = c.y;
 }
 
+// Output rows are written once and never re-read by the step: non-temporal
+// stores keep them from displacing the gathered background rows in L2.
+typedef double ntd2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void nt_store(double *p, double v) { __builtin_nontemporal_store(v, p); }
+__device__ __forceinline__ void nt_store2(double *p, double a, double b) {
+  ntd2 v = {a, b};
+  __builtin_nontemporal_store(v, reinterpret_cast<ntd2 *>(p));
+}
+
 __device__ __forceinline__ void store6(double *p, const double *m) {
-  double2 *q = reinterpret_cast<double2 *>(p);
-  q[0] = make_double2(m[0], m[1]);
-  q[1] = make_double2(m[2], m[3]);
-  q[2] = make_double2(m[4], m[5]);
+  nt_store2(p, m[0], m[1]);
+  nt_store2(p + 2, m[2], m[3]);
+  nt_store2(p + 4, m[4], m[5]);
 }
 
 // ------------------------------------------------------------ interpolators
@@ -360,7 +368,7 @@ __device__ __forceinline__ void interp_iso(const double *in, int stride, const i
 #pragma unroll
     for (int j = 0; j < SZ; j++) acc[j] += phi[i] * row[i][j];
 #pragma unroll
-  for (int j = 0; j < SZ; j++) out[j] = acc[j];
+  for (int j = 0; j < SZ; j++) nt_store(out + j, acc[j]);
 }
 
 // PMMG_interp{3,4}bar_ani (interpmesh_pmmg.c:166-190, 247-270):

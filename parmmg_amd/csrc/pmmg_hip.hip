@@ -434,6 +434,26 @@ struct VolLoc {
   double phi[4];
 };
 
+// vrec rows stream out of the walk and back into the interpolation once:
+// non-temporal 16-byte pieces
+typedef int nti4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void vrec_store(VolLoc *dst, const VolLoc &l) {
+  nti4 a = {l.v.x, l.v.y, l.v.z, l.v.w};
+  __builtin_nontemporal_store(a, reinterpret_cast<nti4 *>(dst));
+  double *p = reinterpret_cast<double *>(dst) + 2;
+  nt_store2(p, l.phi[0], l.phi[1]);
+  nt_store2(p + 2, l.phi[2], l.phi[3]);
+}
+__device__ __forceinline__ VolLoc vrec_load(const VolLoc *src) {
+  VolLoc l;
+  const nti4 a = __builtin_nontemporal_load(reinterpret_cast<const nti4 *>(src));
+  l.v = make_int4(a.x, a.y, a.z, a.w);
+  const ntd2 *p = reinterpret_cast<const ntd2 *>(src) + 1;
+  const ntd2 b = __builtin_nontemporal_load(p), c = __builtin_nontemporal_load(p + 1);
+  l.phi[0] = b.x; l.phi[1] = b.y; l.phi[2] = c.x; l.phi[3] = c.y;
+  return l;
+}
+
 __device__ __forceinline__ int step_vol(const Bg &bg, const double *x, int &k, int *hist, VolLoc *loc = nullptr) {
   const int4 tv = tetv_row(bg, k);
   const int4 ad = adja_row(bg, k);
@@ -583,8 +603,8 @@ __global__ __launch_bounds__(kBlock) void k_vol_walk(Bg bg, const Frame *fr, con
     VolLoc loc;
     status = walk_core(bg, x, k, steps, cap < maxstep ? cap : maxstep, &loc);
     if (status == 3 && steps < maxstep) status = 4; // -> continuation list
-    vloc[ip - 1] = status == 1 ? k : 0;
-    if (status == 1) vrec[ip - 1] = loc;
+    __builtin_nontemporal_store(status == 1 ? k : 0, vloc + ip - 1);
+    if (status == 1) vrec_store(vrec + ip - 1, loc);
   }
   const bool fail = active && (status == 2 || status == 3);
   const int slot = wave_append(&st->nfb_vol, fail);
@@ -653,15 +673,15 @@ template <int C0, int C1, int C2, int C3, int C4, int C5>
 __global__ __launch_bounds__(kBlock) void k_vol_interp(const uint8_t *pclass, int np, const int *vloc,
                                                        const VolLoc *vrec, Slots S, int *elem_out, int8_t *hit_out) {
   for (int i = xcd_block() * blockDim.x + threadIdx.x; i < np; i += gridDim.x * blockDim.x) {
-    if (pclass[i] != PMMG_PT_VOL) continue;
-    const int k = vloc[i];
+    if (__builtin_nontemporal_load(pclass + i) != PMMG_PT_VOL) continue;
+    const int k = __builtin_nontemporal_load(vloc + i);
     if (k == 0) continue;
     const int ip = i + 1;
-    const VolLoc loc = vrec[i];
+    const VolLoc loc = vrec_load(vrec + i);
     const int v[4] = {loc.v.x, loc.v.y, loc.v.z, loc.v.w};
     interp_vol_layout<C0, C1, C2, C3, C4, C5>(S, ip, v, loc.phi);
-    if (elem_out) elem_out[ip - 1] = k;
-    if (hit_out) hit_out[ip - 1] = PMMG_HIT_VOL_WALK;
+    if (elem_out) __builtin_nontemporal_store(k, elem_out + ip - 1);
+    if (hit_out) __builtin_nontemporal_store((int8_t)PMMG_HIT_VOL_WALK, hit_out + ip - 1);
   }
 }
 
