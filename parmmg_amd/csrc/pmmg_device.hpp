@@ -116,6 +116,13 @@ __device__ __forceinline__ void load_pt(const double *xyz, int v, double *p) {
   p[2] = q[2];
 }
 
+__device__ __forceinline__ void load_pt_nt(const double *xyz, int v, double *p) {
+  const double *q = xyz + 3 * (size_t)(v - 1);
+  p[0] = __builtin_nontemporal_load(q);
+  p[1] = __builtin_nontemporal_load(q + 1);
+  p[2] = __builtin_nontemporal_load(q + 2);
+}
+
 __device__ __forceinline__ int wave_append(int *counter, bool pred) {
   unsigned long long m = __ballot(pred);
   if (m == 0ULL) return -1;
@@ -336,6 +343,7 @@ __device__ __forceinline__ void load6(const double *p, double *m) {
 // Output rows are written once and never re-read by the step: non-temporal
 // stores keep them from displacing the gathered background rows in L2.
 typedef double ntd2 __attribute__((ext_vector_type(2)));
+typedef int nti4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void nt_store(double *p, double v) { __builtin_nontemporal_store(v, p); }
 __device__ __forceinline__ void nt_store2(double *p, double a, double b) {
   ntd2 v = {a, b};

@@ -136,7 +136,9 @@ __global__ __launch_bounds__(kBlock) void k_seed_vol(Bg bg, const Frame *fr, uns
     bool ok = s < nthreads && k <= bg.ne;
     int4 tv = make_int4(0, 0, 0, 0);
     if (ok) {
-      tv = tetv_row(bg, k);
+      // sampled records stream through once: non-temporal
+      const nti4 r = __builtin_nontemporal_load(reinterpret_cast<const nti4 *>(bg.tetv + (size_t)(k - 1) * bg.tstride));
+      tv = make_int4(r.x, r.y, r.z, r.w);
       ok = tv.x > 0;
     }
     unsigned long long key = ~0ULL;
@@ -436,7 +438,6 @@ struct VolLoc {
 
 // vrec rows stream out of the walk and back into the interpolation once:
 // non-temporal 16-byte pieces
-typedef int nti4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void vrec_store(VolLoc *dst, const VolLoc &l) {
   nti4 a = {l.v.x, l.v.y, l.v.z, l.v.w};
   __builtin_nontemporal_store(a, reinterpret_cast<nti4 *>(dst));
@@ -598,7 +599,7 @@ __global__ __launch_bounds__(kBlock) void k_vol_walk(Bg bg, const Frame *fr, con
   int status = 0, steps = 0, k = 0;
   if (active) {
     double x[3];
-    load_pt(qxyz, ip, x);
+    load_pt_nt(qxyz, ip, x); // streamed once: non-temporal
     k = seed_vol(grid, g, fr, x);
     VolLoc loc;
     status = walk_core(bg, x, k, steps, cap < maxstep ? cap : maxstep, &loc);
