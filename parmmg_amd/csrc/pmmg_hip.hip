@@ -1229,6 +1229,7 @@ struct pmmg_hip_ctx {
   hipStream_t stream2 = nullptr; // surface branch, concurrent with the volume walk
   bool bdy_on_s2 = false;
   int two_streams = 1; // PMMG_HIP_STREAMS=1: everything on one stream
+  int s2_start = 0;    // surface branch start: 0 after the frame, 1 after the volume seeds
   char err[512] = {0};
   Bg bg{};
   int met_size = 0;
@@ -1349,6 +1350,7 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   if (getenv("PMMG_HIP_SEEDMODE")) c->seed_mode = atoi(getenv("PMMG_HIP_SEEDMODE"));
   c->seed_run = env_int("PMMG_HIP_SEEDRUN", c->seed_run);
   c->two_streams = env_int("PMMG_HIP_STREAMS", 2) >= 2;
+  if (getenv("PMMG_HIP_S2START")) c->s2_start = atoi(getenv("PMMG_HIP_S2START"));
   if (c->seed_run != 1 && c->seed_run != 2 && c->seed_run != 4 && c->seed_run != 8) c->seed_run = 4;
   c->qpb = env_int("PMMG_HIP_QPB", c->qpb);
   c->qpc = env_int("PMMG_HIP_QPC", c->qpc);
@@ -1745,15 +1747,21 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   // with the volume seeds and walks (joined before the fallbacks).
   const hipStream_t sb = (!sorted && bg.nt > 0 && c->two_streams) ? c->stream2 : s;
   c->bdy_on_s2 = sb != s;
-  if (c->bdy_on_s2) {
+  // the surface branch starts after the frame (s2_start 0, default) or
+  // after the volume seeds (1); both measured within noise of each other
+  if (c->bdy_on_s2 && c->s2_start == 0) {
     HIPCK(c, hipEventRecord(c->ev[7], s));
     HIPCK(c, hipStreamWaitEvent(sb, c->ev[7], 0));
   }
-  if (bg.nt > 0) hipLaunchKernelGGL(k_seed_srf, dim3(blocks_for(bg.nt, 4096)), dim3(kBlock), 0, sb, bg, fr, sgrid, gs);
   long long nsamp = (long long)c->spc * ng;
   if (nsamp > bg.ne) nsamp = bg.ne;
   hipLaunchKernelGGL(k_seed_vol, dim3(blocks_for(nsamp, 8192)), dim3(kBlock), 0, s, bg, fr, grid, g, nsamp,
                      c->seed_mode, c->seed_run);
+  if (c->bdy_on_s2 && c->s2_start != 0) {
+    HIPCK(c, hipEventRecord(c->ev[7], s));
+    HIPCK(c, hipStreamWaitEvent(sb, c->ev[7], 0));
+  }
+  if (bg.nt > 0) hipLaunchKernelGGL(k_seed_srf, dim3(blocks_for(bg.nt, 4096)), dim3(kBlock), 0, sb, bg, fr, sgrid, gs);
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[1], s));
 
