@@ -360,30 +360,30 @@ __device__ __forceinline__ void store6(double *p, const double *m) {
 
 // PMMG_interp{3,4}bar_iso (interpmesh_pmmg.c:125-149, 206-230):
 // out[j] = 0; out[j] += phi_i * old[v_i][j], i ascending
+// PMMG_interp{3,4}bar_iso (interpmesh_pmmg.c:125-165, 206-246): the row
+// value acc = sum_i phi_i * row_i (accumulated from 0.0 in vertex order)
 template <int NV, int SZ>
-__device__ __forceinline__ void interp_iso(const double *in, int stride, const int *v, const double *phi,
-                                           double *out) {
+__device__ __forceinline__ void interp_iso_row(const double *in, int stride, const int *v, const double *phi,
+                                               double *acc) {
   double row[NV][SZ];
 #pragma unroll
   for (int i = 0; i < NV; i++)
 #pragma unroll
     for (int j = 0; j < SZ; j++) row[i][j] = in[(size_t)stride * (v[i] - 1) + j];
-  double acc[SZ];
 #pragma unroll
   for (int j = 0; j < SZ; j++) acc[j] = 0.0;
 #pragma unroll
   for (int i = 0; i < NV; i++)
 #pragma unroll
     for (int j = 0; j < SZ; j++) acc[j] += phi[i] * row[i][j];
-#pragma unroll
-  for (int j = 0; j < SZ; j++) nt_store(out + j, acc[j]);
 }
 
 // PMMG_interp{3,4}bar_ani (interpmesh_pmmg.c:166-190, 247-270):
-// M = invmat( sum_i phi_i invmat(M_i) ), row untouched if any inversion fails
+// M = invmat( sum_i phi_i invmat(M_i) ); false (row left untouched by the
+// reference) if any inversion fails
 template <int NV>
-__device__ __forceinline__ void interp_ani(const double *in, int stride, const int *v, const double *phi,
-                                           double *out) {
+__device__ __forceinline__ bool interp_ani_row(const double *in, int stride, const int *v, const double *phi,
+                                               double *r) {
   double m[NV][6];
 #pragma unroll
   for (int i = 0; i < NV; i++) load6(in + (size_t)stride * (v[i] - 1), m[i]);
@@ -395,14 +395,29 @@ __device__ __forceinline__ void interp_ani(const double *in, int stride, const i
 #pragma unroll
     for (int s = 0; s < 6; s++) mint[s] = (i == 0) ? phi[0] * mi[s] : mint[s] + phi[i] * mi[s];
   }
-  double r[6];
-  if (invmat(mint, r) && ok) store6(out, r);
+  return invmat(mint, r) && ok;
+}
+
+// the row of one slot: returns false when the reference leaves it untouched
+template <int NV, int CODE>
+__device__ __forceinline__ bool interp_row(const Slot &sl, const int *v, const double *phi, double *r) {
+  if constexpr (CODE == 6) return interp_ani_row<NV>(sl.in, sl.stride, v, phi, r);
+  else {
+    interp_iso_row<NV, CODE>(sl.in, sl.stride, v, phi, r);
+    return true;
+  }
 }
 
 template <int NV, int CODE>
 __device__ __forceinline__ void interp_code(const Slot &sl, int ip, const int *v, const double *phi) {
-  if (CODE == 6) interp_ani<NV>(sl.in, sl.stride, v, phi, sl.out + 6 * (size_t)(ip - 1));
-  else interp_iso<NV, CODE>(sl.in, sl.stride, v, phi, sl.out + (size_t)CODE * (ip - 1));
+  double r[CODE];
+  if (!interp_row<NV, CODE>(sl, v, phi, r)) return;
+  double *out = sl.out + (size_t)CODE * (ip - 1);
+  if constexpr (CODE == 6) store6(out, r);
+  else {
+#pragma unroll
+    for (int j = 0; j < CODE; j++) nt_store(out + j, r[j]);
+  }
 }
 
 template <int NV>

@@ -16,7 +16,7 @@
 //      deterministic); surface seed grid: tria centroids           k_seed_vol, k_seed_srf
 //   3. query order: Morton binning of the queries per class
 //      (count / exclusive scan / scatter), or, when the input order
-//      is already spatially coherent, a stable class compaction     k_bin_*, DeviceSelect
+//      is already spatially coherent, a stable class compaction     k_bin_*, k_cls_*
 //   4. volume: lean walk kernel writing the located tetra per query,
 //      then an interpolation kernel specialised on the slot layout
 //      so that every row gather is issued before any math           k_vol_walk, k_vol_interp
@@ -122,18 +122,24 @@ __global__ void k_frame_final(Frame *fr, int g, int gs, int gb) {
 // samples for the same traffic.  Lanes of a run that land in the same cell
 // combine their keys first (one atomic per cell and run).
 __global__ __launch_bounds__(kBlock) void k_seed_vol(Bg bg, const Frame *fr, unsigned long long *cell, int g,
-                                                     long long nsamp, int mode, int R) {
+                                                     long long nsamp, int mode, int R, int atom) {
   const long long nruns = (nsamp + R - 1) / R;
   const long long quads = bg.ne / 4;
   const long long nthreads = nruns * R;
-  for (long long s0 = blockIdx.x * (long long)blockDim.x; s0 < nthreads; s0 += (long long)gridDim.x * blockDim.x) {
+  // XCD-aware: the blocks of XCD x (blockIdx % 8; gridDim is a multiple of
+  // 8) sweep one contiguous eighth of the samples, so the vertex rows shared
+  // by neighbouring tetra are fetched into one L2, not eight
+  const long long per = (nthreads + 8LL * kBlock - 1) / (8LL * kBlock) * kBlock;
+  const long long lo = (blockIdx.x & 7) * per, hi = lo + per < nthreads ? lo + per : nthreads;
+  const long long bstride = (long long)(gridDim.x >> 3) * blockDim.x;
+  for (long long s0 = lo + (blockIdx.x >> 3) * (long long)blockDim.x; s0 < hi; s0 += bstride) {
     const long long s = s0 + threadIdx.x;
     const long long run = s / R;
     const int r = (int)(s % R);
     // run start aligned to a 4-tetra boundary (a cache line of tet8 records)
     const long long base = 4 * ((run * quads) / (nruns > 0 ? nruns : 1));
     const int k = (int)(1 + base + r);
-    bool ok = s < nthreads && k <= bg.ne;
+    bool ok = s < hi && k <= bg.ne;
     int4 tv = make_int4(0, 0, 0, 0);
     if (ok) {
       // sampled records stream through once: non-temporal
@@ -184,7 +190,10 @@ __global__ __launch_bounds__(kBlock) void k_seed_vol(Bg bg, const Frame *fr, uns
         if (o < r) leader = false;
       }
     }
-    if (leader) atomicMin(&cell[ci], best);
+    if (leader) {
+      if (atom) atomicMin(&cell[ci], best);
+      else cell[ci] = best; // timing experiment only (racy)
+    }
   }
 }
 
@@ -331,11 +340,86 @@ __global__ void k_bin_total(const int *off, const int *cnt, int nbins, DevStats 
   st->nbdy = off[2 * nbins - 1] + cnt[2 * nbins - 1] - off[nbins];
 }
 
-struct IsClass {
-  const uint8_t *pclass;
-  int c;
-  __host__ __device__ __forceinline__ bool operator()(const int &ip) const { return pclass[ip - 1] == c; }
-};
+
+// Stable class compaction (the surface list): out = the ids ip (1-based) with
+// pclass[ip-1] == cls, in input order; *count = their number.  Three passes
+// over the 1-byte classes (count per block, scan of the block counts,
+// scatter): ~3 reads of np bytes, no global atomics.  Each block owns
+// kClsChunk consecutive points, kClsItems per thread.
+constexpr int kClsItems = 16, kClsChunk = kBlock * kClsItems;
+
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  const int lane = __lane_id();
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(v, o);
+    if (lane >= o) v += u;
+  }
+  return v;
+}
+
+// exclusive scan of one int per thread over the block; returns the prefix
+// and the block total in *tot
+__device__ __forceinline__ int block_excl_scan(int v, int *tot) {
+  __shared__ int wsum[kBlock / 64];
+  const int inc = wave_incl_scan(v);
+  const int w = threadIdx.x >> 6;
+  if (__lane_id() == 63) wsum[w] = inc;
+  __syncthreads();
+  int pre = 0, all = 0;
+#pragma unroll
+  for (int j = 0; j < kBlock / 64; j++) {
+    pre += j < w ? wsum[j] : 0;
+    all += wsum[j];
+  }
+  __syncthreads();
+  *tot = all;
+  return pre + inc - v;
+}
+
+__device__ __forceinline__ unsigned cls_bits(const uint8_t *pclass, long long np, long long i0, int cls) {
+  unsigned m = 0;
+#pragma unroll
+  for (int j = 0; j < kClsItems; j++) {
+    const long long i = i0 + j;
+    m |= (i < np && pclass[i] == cls) ? (1u << j) : 0u;
+  }
+  return m;
+}
+
+__global__ __launch_bounds__(kBlock) void k_cls_count(const uint8_t *pclass, long long np, int cls, int *bcnt) {
+  const long long i0 = (long long)blockIdx.x * kClsChunk + (long long)threadIdx.x * kClsItems;
+  int tot;
+  block_excl_scan(__popc(cls_bits(pclass, np, i0, cls)), &tot);
+  if (threadIdx.x == 0) bcnt[blockIdx.x] = tot;
+}
+
+// one block: bcnt[0..nb) -> exclusive offsets in place, total -> *count
+__global__ __launch_bounds__(kBlock) void k_cls_scan(int *bcnt, int nb, int *count) {
+  int carry = 0;
+  for (int b0 = 0; b0 < nb; b0 += kBlock) {
+    const int b = b0 + threadIdx.x;
+    const int v = b < nb ? bcnt[b] : 0;
+    int tot;
+    const int pre = block_excl_scan(v, &tot);
+    if (b < nb) bcnt[b] = carry + pre;
+    carry += tot;
+  }
+  if (threadIdx.x == 0) *count = carry;
+}
+
+__global__ __launch_bounds__(kBlock) void k_cls_scatter(const uint8_t *pclass, long long np, int cls,
+                                                        const int *boff, int *out) {
+  const long long i0 = (long long)blockIdx.x * kClsChunk + (long long)threadIdx.x * kClsItems;
+  unsigned m = cls_bits(pclass, np, i0, cls);
+  int tot;
+  int pos = boff[blockIdx.x] + block_excl_scan(__popc(m), &tot);
+  while (m) {
+    const int j = __ffs(m) - 1;
+    m &= m - 1;
+    out[pos++] = (int)(i0 + j + 1);
+  }
+}
 
 // ---------------------------------------------------------------- stats
 
@@ -436,22 +520,34 @@ struct VolLoc {
   double phi[4];
 };
 
-// vrec rows stream out of the walk and back into the interpolation once:
-// non-temporal 16-byte pieces
-__device__ __forceinline__ void vrec_store(VolLoc *dst, const VolLoc &l) {
-  nti4 a = {l.v.x, l.v.y, l.v.z, l.v.w};
-  __builtin_nontemporal_store(a, reinterpret_cast<nti4 *>(dst));
-  double *p = reinterpret_cast<double *>(dst) + 2;
-  nt_store2(p, l.phi[0], l.phi[1]);
-  nt_store2(p + 2, l.phi[2], l.phi[3]);
+// vrec: the walk's result per query, read back once by the interpolation.
+// Stored as three arrays (vertex ids int4, phi0..1, phi2..3) so that a
+// wave-instruction writes / reads 1 KiB contiguously (whole cache lines);
+// non-temporal: streamed once each way.
+struct VRec {
+  nti4 *v;
+  ntd2 *a, *b;
+};
+__host__ __device__ inline VRec vrec_arrays(void *base, size_t nq) {
+  VRec r;
+  r.v = reinterpret_cast<nti4 *>(base);
+  r.a = reinterpret_cast<ntd2 *>(r.v + nq);
+  r.b = r.a + nq;
+  return r;
 }
-__device__ __forceinline__ VolLoc vrec_load(const VolLoc *src) {
+__device__ __forceinline__ void vrec_store(const VRec &r, size_t i, const VolLoc &l) {
+  const nti4 v = {l.v.x, l.v.y, l.v.z, l.v.w};
+  const ntd2 a = {l.phi[0], l.phi[1]}, b = {l.phi[2], l.phi[3]};
+  __builtin_nontemporal_store(v, r.v + i);
+  __builtin_nontemporal_store(a, r.a + i);
+  __builtin_nontemporal_store(b, r.b + i);
+}
+__device__ __forceinline__ VolLoc vrec_load(const VRec &r, size_t i) {
   VolLoc l;
-  const nti4 a = __builtin_nontemporal_load(reinterpret_cast<const nti4 *>(src));
-  l.v = make_int4(a.x, a.y, a.z, a.w);
-  const ntd2 *p = reinterpret_cast<const ntd2 *>(src) + 1;
-  const ntd2 b = __builtin_nontemporal_load(p), c = __builtin_nontemporal_load(p + 1);
-  l.phi[0] = b.x; l.phi[1] = b.y; l.phi[2] = c.x; l.phi[3] = c.y;
+  const nti4 v = __builtin_nontemporal_load(r.v + i);
+  const ntd2 a = __builtin_nontemporal_load(r.a + i), b = __builtin_nontemporal_load(r.b + i);
+  l.v = make_int4(v.x, v.y, v.z, v.w);
+  l.phi[0] = a.x; l.phi[1] = a.y; l.phi[2] = b.x; l.phi[3] = b.y;
   return l;
 }
 
@@ -570,6 +666,246 @@ __device__ __forceinline__ int walk_core(const Bg &bg, const double *x, int &k, 
   }
 }
 
+// Walk that carries the 3 vertices of the crossed face in registers: a step
+// gathers the next tetra's record and only its opposite vertex (4 cache-line
+// lookups per step instead of 10: the texture path, ~2 cycles per distinct
+// line per wave-instruction, bounds the walk).  The carried vertices are
+// permuted into the new tetra's local order (the reference's arithmetic
+// order) with mask blends: a select chain over a register array is lowered
+// to scratch-memory indexing.
+__device__ __forceinline__ double blend4(double a, double b, double c, double d, long long m0, long long m1,
+                                         long long m2, long long m3) {
+  const long long r = (__double_as_longlong(a) & m0) | (__double_as_longlong(b) & m1) |
+                      (__double_as_longlong(c) & m2) | (__double_as_longlong(d) & m3);
+  return __longlong_as_double(r);
+}
+
+__device__ __forceinline__ int walk_core_carry(const Bg &bg, const double *x, int &k, int &steps, int limit,
+                                               VolLoc *loc) {
+  int hist[kHist];
+#pragma unroll
+  for (int h = 0; h < kHist; h++) hist[h] = 0;
+  int4 tv = tetv_row(bg, k), ad = adja_row(bg, k);
+  double p[4][3];
+  load_tet_pts(bg, tv, p);
+  for (int n = 0;; n++) {
+    if (n >= limit) return 3;
+    ++steps;
+    double s[4];
+    const double vol = tet_dots(x, p[0], p[1], p[2], p[3], s);
+    double key[4];
+    bool inside;
+    if (vol > 0.0 || vol < 0.0) {
+      double sm;
+      if (vol > 0.0) {
+        sm = s[0];
+        sm = s[1] > sm ? s[1] : sm;
+        sm = s[2] > sm ? s[2] : sm;
+        sm = s[3] > sm ? s[3] : sm;
+      } else {
+        sm = s[0];
+        sm = s[1] < sm ? s[1] : sm;
+        sm = s[2] < sm ? s[2] : sm;
+        sm = s[3] < sm ? s[3] : sm;
+      }
+      inside = -(sm / vol) > -kEps;
+#pragma unroll
+      for (int f = 0; f < 4; f++) key[f] = vol > 0.0 ? s[f] : -s[f];
+    } else {
+      double b[4];
+#pragma unroll
+      for (int f = 0; f < 4; f++) b[f] = -s[f] / vol;
+      inside = min4(b) > -kEps;
+      int r[4];
+      ranks4(b, r);
+#pragma unroll
+      for (int f = 0; f < 4; f++) key[f] = (double)(3 - r[f]);
+    }
+    if (inside) {
+      loc->v = tv;
+#pragma unroll
+      for (int f = 0; f < 4; f++) loc->phi[f] = -s[f] / vol;
+      return 1;
+    }
+    int f = -1;
+    double best = 0.0;
+#pragma unroll
+    for (int ff = 0; ff < 4; ff++) {
+      const int iel = sel4(ad, ff) >> 2;
+      bool vis = false;
+#pragma unroll
+      for (int h = 0; h < kHist; h++) vis = vis || (hist[h] == iel);
+      if (iel != 0 && !vis && (f < 0 || key[ff] > best)) { f = ff; best = key[ff]; }
+    }
+    if (f < 0) return 2;
+#pragma unroll
+    for (int h = kHist - 1; h > 0; h--) hist[h] = hist[h - 1];
+    hist[0] = k;
+    const int code = sel4(ad, f);
+    k = code >> 2;
+    const int iopp = code & 3;
+    const int4 tn = tetv_row(bg, k);
+    ad = adja_row(bg, k);
+    double pn[3];
+    load_pt(bg.xyz, sel4(tn, iopp), pn);
+    double q[4][3];
+#pragma unroll
+    for (int l = 0; l < 4; l++) {
+      const int id = sel4(tn, l);
+      const bool e1 = id == tv.y, e2 = id == tv.z, e3 = id == tv.w, en = l == iopp;
+#pragma unroll
+      for (int d = 0; d < 3; d++) {
+#if PMMG_CARRY_BLEND
+        const long long m0 = -(long long)(id == tv.x), m1 = -(long long)e1, m2 = -(long long)e2, m3 = -(long long)e3;
+        const long long mn = -(long long)en;
+        const double c = blend4(p[0][d], p[1][d], p[2][d], p[3][d], m0, m1, m2, m3);
+        q[l][d] = __longlong_as_double((__double_as_longlong(c) & ~mn) | (__double_as_longlong(pn[d]) & mn));
+#else
+        const double c = e1 ? p[1][d] : (e2 ? p[2][d] : (e3 ? p[3][d] : p[0][d]));
+        q[l][d] = en ? pn[d] : c;
+#endif
+      }
+    }
+#pragma unroll
+    for (int l = 0; l < 4; l++)
+#pragma unroll
+      for (int d = 0; d < 3; d++) p[l][d] = q[l][d];
+    tv = tn;
+  }
+}
+
+// Walk in slot order: the tetra's vertices stay in the registers ("slots")
+// they were loaded into, a step replaces only the slot of the vertex left
+// behind (one v_cndmask per dword), and the filter test runs on the slots'
+// order.  Its rounding differs from the reference's vertex order, so it only
+// nominates candidates (min barycentric > -kCandEps, a margin far above the
+// rounding of any non-degenerate tetra); every candidate is then re-evaluated
+// in the reference's order with the exact test (walk_exact), once per wave
+// when the lanes have all stopped (not inside the divergent step loop).  A
+// rejected candidate resumes its walk.  Acceptance and the coordinates are
+// therefore the reference's, bit for bit; only the path can differ (faces
+// are ranked by the slot-order keys), as with any walk start.
+constexpr double kCandEps = 8 * kEps;
+
+__device__ __forceinline__ int idx_in(int id, const int4 &t) {
+  return (id == t.y ? 1 : 0) + (id == t.z ? 2 : 0) + (id == t.w ? 3 : 0);
+}
+
+// the slots permuted into the tetra's local order: q[l] = p[j] with m_j == l
+__device__ __forceinline__ void slots_to_local(const double (*p)[3], const int4 &m, double (*q)[3]) {
+#pragma unroll
+  for (int l = 0; l < 4; l++) {
+    const long long m0 = -(long long)(m.x == l), m1 = -(long long)(m.y == l), m2 = -(long long)(m.z == l),
+                    m3 = -(long long)(m.w == l);
+#pragma unroll
+    for (int d = 0; d < 3; d++) q[l][d] = blend4(p[0][d], p[1][d], p[2][d], p[3][d], m0, m1, m2, m3);
+  }
+}
+
+__device__ __forceinline__ int walk_core_slot(const Bg &bg, const double *x, int &k, int &steps, int limit,
+                                              VolLoc *loc) {
+  int hist[kHist];
+#pragma unroll
+  for (int h = 0; h < kHist; h++) hist[h] = 0;
+  int4 ad = adja_row(bg, k);
+  int4 sid = tetv_row(bg, k);      // vertex id in slot j
+  double p[4][3];
+  load_tet_pts(bg, sid, p);
+  int4 m = make_int4(0, 1, 2, 3);  // local index (in tv / ad) of slot j
+  bool skip = false;               // the current tetra failed the exact test
+  int n = 0;
+  for (;;) {
+    int status = 0;
+    for (;;) {
+      if (n >= limit) { status = 3; break; }
+      ++n;
+      ++steps;
+      double s[4];
+      const double vol = tet_dots(x, p[0], p[1], p[2], p[3], s);
+      double key[4];
+      bool cand;
+      if (vol > 0.0 || vol < 0.0) {
+        double sm;
+        if (vol > 0.0) {
+          sm = s[0];
+          sm = s[1] > sm ? s[1] : sm;
+          sm = s[2] > sm ? s[2] : sm;
+          sm = s[3] > sm ? s[3] : sm;
+        } else {
+          sm = s[0];
+          sm = s[1] < sm ? s[1] : sm;
+          sm = s[2] < sm ? s[2] : sm;
+          sm = s[3] < sm ? s[3] : sm;
+        }
+        cand = -(sm / vol) > -kCandEps;
+#pragma unroll
+        for (int f = 0; f < 4; f++) key[f] = vol > 0.0 ? s[f] : -s[f];
+      } else { // degenerate in slot order: the exact test decides
+        cand = true;
+#pragma unroll
+        for (int f = 0; f < 4; f++) key[f] = s[f];
+      }
+      if (cand && !skip) { status = 1; break; }
+      skip = false;
+      int4 code;
+      code.x = sel4(ad, m.x);
+      code.y = sel4(ad, m.y);
+      code.z = sel4(ad, m.z);
+      code.w = sel4(ad, m.w);
+      int f = -1;
+      double best = 0.0;
+#pragma unroll
+      for (int ff = 0; ff < 4; ff++) {
+        const int iel = sel4(code, ff) >> 2;
+        bool vis = false;
+#pragma unroll
+        for (int h = 0; h < kHist; h++) vis = vis || (hist[h] == iel);
+        if (iel != 0 && !vis && (f < 0 || key[ff] > best)) { f = ff; best = key[ff]; }
+      }
+      if (f < 0) { status = 2; break; }
+#pragma unroll
+      for (int h = kHist - 1; h > 0; h--) hist[h] = hist[h - 1];
+      hist[0] = k;
+      const int c = sel4(code, f);
+      k = c >> 2;
+      const int iopp = c & 3;
+      const int4 tn = tetv_row(bg, k);
+      ad = adja_row(bg, k);
+      // (tn is dead after this step: the local order lives in m)
+      const int vn = sel4(tn, iopp);
+      double pn[3];
+      load_pt(bg.xyz, vn, pn);
+      m.x = f == 0 ? iopp : idx_in(sid.x, tn);
+      m.y = f == 1 ? iopp : idx_in(sid.y, tn);
+      m.z = f == 2 ? iopp : idx_in(sid.z, tn);
+      m.w = f == 3 ? iopp : idx_in(sid.w, tn);
+      sid.x = f == 0 ? vn : sid.x;
+      sid.y = f == 1 ? vn : sid.y;
+      sid.z = f == 2 ? vn : sid.z;
+      sid.w = f == 3 ? vn : sid.w;
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+#pragma unroll
+        for (int d = 0; d < 3; d++) p[j][d] = f == j ? pn[d] : p[j][d];
+    }
+    if (status != 1) return status;
+    // the reference's exact test, vertices in the tetra's own order
+    double q[4][3], s[4];
+    slots_to_local(p, m, q);
+    const double vol = tet_dots(x, q[0], q[1], q[2], q[3], s);
+    double b[4];
+#pragma unroll
+    for (int f = 0; f < 4; f++) b[f] = -s[f] / vol;
+    if (min4(b) > -kEps) {
+      loc->v = tetv_row(bg, k);
+#pragma unroll
+      for (int f = 0; f < 4; f++) loc->phi[f] = b[f];
+      return 1;
+    }
+    skip = true;
+  }
+}
+
 struct ContEntry {
   int ip; // query
   int k;  // tetra the capped walk stopped at
@@ -579,10 +915,13 @@ struct ContEntry {
 // the volume points selected here (no compaction pass; the idle lanes of
 // surface / skipped points cost little next to the walks).  Otherwise the
 // queries are order[0 .. st->nvol).  vloc is indexed by ip - 1.
-__global__ __launch_bounds__(kBlock) void k_vol_walk(Bg bg, const Frame *fr, const unsigned long long *grid, int g,
-                                                     const double *qxyz, const uint8_t *pclass, const int *order,
-                                                     int np, int *vloc, VolLoc *vrec, int *fb, ContEntry *cont,
-                                                     DevStats *st, int cap, int maxstep) {
+// CARRY selects walk_core_carry; MINW > 1 asks the compiler for that many
+// waves per SIMD (register budget 512 / MINW).
+template <int CARRY, int MINW>
+__global__ __launch_bounds__(kBlock, MINW) void k_vol_walk(Bg bg, const Frame *fr, const unsigned long long *grid,
+                                                           int g, const double *qxyz, const uint8_t *pclass,
+                                                           const int *order, int np, int *vloc, VRec vrec, int *fb,
+                                                           ContEntry *cont, DevStats *st, int cap, int maxstep) {
   __shared__ BlockStats bs;
   bstats_init(&bs);
   __syncthreads();
@@ -602,10 +941,13 @@ __global__ __launch_bounds__(kBlock) void k_vol_walk(Bg bg, const Frame *fr, con
     load_pt_nt(qxyz, ip, x); // streamed once: non-temporal
     k = seed_vol(grid, g, fr, x);
     VolLoc loc;
-    status = walk_core(bg, x, k, steps, cap < maxstep ? cap : maxstep, &loc);
+    const int lim = cap < maxstep ? cap : maxstep;
+    status = CARRY == 2   ? walk_core_slot(bg, x, k, steps, lim, &loc)
+             : CARRY == 1 ? walk_core_carry(bg, x, k, steps, lim, &loc)
+                          : walk_core(bg, x, k, steps, lim, &loc);
     if (status == 3 && steps < maxstep) status = 4; // -> continuation list
     __builtin_nontemporal_store(status == 1 ? k : 0, vloc + ip - 1);
-    if (status == 1) vrec_store(vrec + ip - 1, loc);
+    if (status == 1) vrec_store(vrec, ip - 1, loc);
   }
   const bool fail = active && (status == 2 || status == 3);
   const int slot = wave_append(&st->nfb_vol, fail);
@@ -619,7 +961,7 @@ __global__ __launch_bounds__(kBlock) void k_vol_walk(Bg bg, const Frame *fr, con
 
 // the capped walks, continued from where they stopped (fresh visited
 // history; the step count continues)
-__global__ __launch_bounds__(kBlock) void k_vol_walk_cont(Bg bg, const double *qxyz, int *vloc, VolLoc *vrec, int *fb,
+__global__ __launch_bounds__(kBlock) void k_vol_walk_cont(Bg bg, const double *qxyz, int *vloc, VRec vrec, int *fb,
                                                           const ContEntry *cont, DevStats *st, int cap, int maxstep) {
   __shared__ BlockStats bs;
   bstats_init(&bs);
@@ -638,7 +980,7 @@ __global__ __launch_bounds__(kBlock) void k_vol_walk_cont(Bg bg, const double *q
       VolLoc loc;
       status = walk_core(bg, x, k, steps, maxstep - cap, &loc);
       vloc[ip - 1] = status == 1 ? k : 0;
-      if (status == 1) vrec[ip - 1] = loc;
+      if (status == 1) vrec_store(vrec, ip - 1, loc);
     }
     const bool fail = active && status != 1;
     const int slot = wave_append(&st->nfb_vol, fail);
@@ -666,24 +1008,111 @@ __device__ __forceinline__ void interp_vol_layout(const Slots &S, int ip, const 
   }
 }
 
-// interpolation of the located volume queries, in input order (coalesced
-// output rows; vloc / vrec by ip - 1).  The walk left the tetra's vertex ids
-// and the exact barycentric coordinates in vrec (one coalesced 48-byte read
-// instead of re-gathering the query, the tetra and its 4 vertices).
-template <int C0, int C1, int C2, int C3, int C4, int C5>
-__global__ __launch_bounds__(kBlock) void k_vol_interp(const uint8_t *pclass, int np, const int *vloc,
-                                                       const VolLoc *vrec, Slots S, int *elem_out, int8_t *hit_out) {
-  for (int i = xcd_block() * blockDim.x + threadIdx.x; i < np; i += gridDim.x * blockDim.x) {
-    if (__builtin_nontemporal_load(pclass + i) != PMMG_PT_VOL) continue;
-    const int k = __builtin_nontemporal_load(vloc + i);
-    if (k == 0) continue;
-    const int ip = i + 1;
-    const VolLoc loc = vrec_load(vrec + i);
-    const int v[4] = {loc.v.x, loc.v.y, loc.v.z, loc.v.w};
-    interp_vol_layout<C0, C1, C2, C3, C4, C5>(S, ip, v, loc.phi);
-    if (elem_out) __builtin_nontemporal_store(k, elem_out + ip - 1);
-    if (hit_out) __builtin_nontemporal_store((int8_t)PMMG_HIT_VOL_WALK, hit_out + ip - 1);
+__device__ __forceinline__ void wait_lgkm() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// Output rows of one slot for the wave's 64 consecutive queries, written as
+// whole cache lines: each lane puts its row into a wave-private LDS image,
+// then lane l of store instruction t writes piece t*64+l of the image (16-byte
+// pieces for 6-double rows, 8-byte pieces for 3-double rows: every piece
+// inside one row), skipping the rows of `mask` bit 0 (other classes, failed
+// walks, failed inversions: the reference leaves those rows untouched, and
+// the surface kernel writes its own rows concurrently).  A lane storing its
+// own 48-byte row with three 16-byte stores instead writes partial lines in
+// every instruction; that cost ~1 ms of the 2 ms interpolation at cfg4.
+template <int C>
+__device__ __forceinline__ void wave_store_rows(double *out, const double *row, unsigned long long mask,
+                                                double *img) {
+  const int lane = __lane_id();
+  if constexpr (C == 1) {
+    if ((mask >> lane) & 1ULL) nt_store(out + lane, row[0]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < C; j++) img[C * lane + j] = row[j];
+    wait_lgkm();
+    if constexpr (C == 6) {
+      const ntd2 *src = reinterpret_cast<const ntd2 *>(img);
+#pragma unroll
+      for (int t = 0; t < 3; t++) {
+        const int p = 64 * t + lane; // 16-byte piece
+        if ((mask >> (p / 3)) & 1ULL) __builtin_nontemporal_store(src[p], reinterpret_cast<ntd2 *>(out) + p);
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < C; t++) {
+        const int p = 64 * t + lane; // 8-byte piece
+        if ((mask >> (p / C)) & 1ULL) nt_store(out + p, img[p]);
+      }
+    }
+    wait_lgkm(); // the image is reused by the next slot
   }
+}
+
+// one slot's row (C = 0: no slot)
+template <int C>
+struct SlotRow {
+  double r[C > 0 ? C : 1];
+  bool ok;
+  __device__ __forceinline__ void eval(const Slot &sl, bool act, const int *v, const double *phi) {
+    if constexpr (C > 0) ok = interp_row<4, C>(sl, v, phi, r) && act;
+  }
+  __device__ __forceinline__ void store(const Slot &sl, size_t i0, double *img) const {
+    if constexpr (C > 0) wave_store_rows<C>(sl.out + (size_t)C * i0, r, __ballot(ok), img);
+  }
+};
+
+// interpolation of the located volume queries, in input order; one lane per
+// query, one pass (the grid covers np).  vrec holds the walk's vertex ids and
+// exact barycentric coordinates (coalesced reads); the rows of every slot are
+// gathered before any math (slot layout = template: codes 1 / 3 / 6, 0 =
+// none; C0 < 0 = runtime layout, per-lane stores).
+template <int C0, int C1, int C2, int C3, int C4, int C5>
+__global__ __launch_bounds__(kBlock) void k_vol_interp(const uint8_t *pclass, int np, const int *vloc, VRec vrec,
+                                                       Slots S, int *elem_out, int8_t *hit_out) {
+  __shared__ double img_all[kBlock / 64][64 * 6];
+  double *img = img_all[threadIdx.x >> 6];
+  const int i = xcd_block() * blockDim.x + threadIdx.x;
+  bool act = i < np && __builtin_nontemporal_load(pclass + i) == PMMG_PT_VOL;
+  const int k = act ? __builtin_nontemporal_load(vloc + i) : 0;
+  act = act && k != 0;
+  if (!__any(act)) return;
+  VolLoc loc;
+  if (act) loc = vrec_load(vrec, i);
+  else { // idle lanes gather a valid row, never stored
+    loc.v = make_int4(1, 1, 1, 1);
+#pragma unroll
+    for (int f = 0; f < 4; f++) loc.phi[f] = 0.0;
+  }
+  const int v[4] = {loc.v.x, loc.v.y, loc.v.z, loc.v.w};
+  const int ip = i + 1;
+  if constexpr (C0 < 0) {
+    if (act)
+      for (int s = 0; s < S.n; s++) interp_dyn<4>(S.s[s], ip, v, loc.phi);
+  } else {
+    // every slot's rows are gathered and evaluated before the first store
+    // (the stores' LDS waits are compiler barriers)
+    SlotRow<C0> r0;
+    SlotRow<C1> r1;
+    SlotRow<C2> r2;
+    SlotRow<C3> r3;
+    SlotRow<C4> r4;
+    SlotRow<C5> r5;
+    r0.eval(S.s[0], act, v, loc.phi);
+    r1.eval(S.s[1], act, v, loc.phi);
+    r2.eval(S.s[2], act, v, loc.phi);
+    r3.eval(S.s[3], act, v, loc.phi);
+    r4.eval(S.s[4], act, v, loc.phi);
+    r5.eval(S.s[5], act, v, loc.phi);
+    const size_t i0 = (size_t)(i - __lane_id());
+    r0.store(S.s[0], i0, img);
+    r1.store(S.s[1], i0, img);
+    r2.store(S.s[2], i0, img);
+    r3.store(S.s[3], i0, img);
+    r4.store(S.s[4], i0, img);
+    r5.store(S.s[5], i0, img);
+  }
+  if (!act) return;
+  if (elem_out) __builtin_nontemporal_store(k, elem_out + ip - 1);
+  if (hit_out) __builtin_nontemporal_store((int8_t)PMMG_HIT_VOL_WALK, hit_out + ip - 1);
 }
 
 // walk + interpolation in one pass (default): the located tetra's vertex ids
@@ -1173,7 +1602,7 @@ __global__ void k_fallback_init(int *a, int *b, unsigned long long *c, const int
 
 // ---------------------------------------------------------------- layout dispatch
 
-typedef void (*VolInterpFn)(const uint8_t *, int, const int *, const VolLoc *, Slots, int *, int8_t *);
+typedef void (*VolInterpFn)(const uint8_t *, int, const int *, VRec, Slots, int *, int8_t *);
 typedef void (*ScanInterpFn)(Bg, const double *, const int *, const int *, Slots, int *, int8_t *, int *, DevStats *);
 typedef void (*FusedFn)(Bg, const Frame *, const unsigned long long *, int, const double *, const int *, Slots, int *,
                         int8_t *, int *, DevStats *, int);
@@ -1186,7 +1615,8 @@ struct LayoutEntry {
 };
 
 #define PMMG_LAYOUT(a, b, c, d, e, f)                                                                             \
-  {{a, b, c, d, e, f}, k_vol_interp<a, b, c, d, e, f>, k_vol_interp_scan<a, b, c, d, e, f>,                    \
+  {{a, b, c, d, e, f}, k_vol_interp<a, b, c, d, e, f>,                                                          \
+   k_vol_interp_scan<a, b, c, d, e, f>,                                                                         \
    k_vol_fused<a, b, c, d, e, f>}
 // common slot layouts (metric first): aniso metric + scalar/vector/tensor
 // (BASELINE cfg3/cfg4, libexamples cube-solphys.sol), iso metric + scalars
@@ -1229,6 +1659,8 @@ struct pmmg_hip_ctx {
   hipStream_t stream2 = nullptr; // surface branch, concurrent with the volume walk
   bool bdy_on_s2 = false;
   int two_streams = 1; // PMMG_HIP_STREAMS=1: everything on one stream
+  int carry = 1;       // walk carrying the crossed face's vertices (PMMG_HIP_CARRY)
+  int walkw = 0;       // >= 5: walk compiled for 5 waves per SIMD (PMMG_HIP_WALKW)
   int s2_start = 0;    // surface branch start: 0 after the frame, 1 after the volume seeds
   char err[512] = {0};
   Bg bg{};
@@ -1243,7 +1675,7 @@ struct pmmg_hip_ctx {
   DevBuf o_xyz, o_tetv, o_adja, o_triv, o_adjt, o_met;
   std::vector<DevBuf> o_f;
   // work buffers
-  DevBuf frame, stats, grid, sgrid, cnt, off, binrank, order_v, order_b, vloc, scan_tmp, scan_tmp2, qs;
+  DevBuf frame, stats, grid, sgrid, cnt, off, binrank, order_v, order_b, vloc, scan_tmp, qs, cls_cnt, cls_cnt2;
   DevBuf cont, vrec;
   DevBuf fb_vol, fb_bdy, best, ckey, cidx, bbest, bckey, bcidx;
   // host-mode staging
@@ -1255,6 +1687,8 @@ struct pmmg_hip_ctx {
   int spc = 4;      // sampled tetra per seed cell
   int seed_mode = 0; // seed point of a sampled tetra: 0 centroid, 1 edge v0-v3 midpoint, 2 first vertex
   int seed_run = 4;  // consecutive tetra per sample run (1, 2, 4, 8)
+  int seed_grid = 8192; // blocks of k_seed_vol (PMMG_HIP_SEEDGRID)
+  int seed_atom = 1;    // 0: racy plain stores (timing experiment, PMMG_HIP_SEEDATOM)
   int qpb = 8;      // queries per Morton bin (walk path)
   int qpc = 1;      // queries per scan cell (scan path)
   int ncu = 256;     // compute units of the device
@@ -1310,10 +1744,14 @@ static int upload(pmmg_hip_ctx *c, DevBuf &b, const void *src, size_t bytes) {
   return 1;
 }
 
-static int env_int(const char *name, int def) {
+static int env_int(const char *name, int def) { // positive values only
   const char *e = getenv(name);
   if (e && atoi(e) > 0) return atoi(e);
   return def;
+}
+static int env_flag(const char *name, int def) { // any integer, 0 included
+  const char *e = getenv(name);
+  return (e && *e) ? atoi(e) : def;
 }
 
 extern "C" {
@@ -1349,8 +1787,13 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   c->spc = env_int("PMMG_HIP_SPC", c->spc);
   if (getenv("PMMG_HIP_SEEDMODE")) c->seed_mode = atoi(getenv("PMMG_HIP_SEEDMODE"));
   c->seed_run = env_int("PMMG_HIP_SEEDRUN", c->seed_run);
+  c->seed_grid = env_int("PMMG_HIP_SEEDGRID", c->seed_grid);
+  c->seed_atom = env_flag("PMMG_HIP_SEEDATOM", c->seed_atom);
+  if (c->seed_grid < 8) c->seed_grid = 8;
   c->two_streams = env_int("PMMG_HIP_STREAMS", 2) >= 2;
   if (getenv("PMMG_HIP_S2START")) c->s2_start = atoi(getenv("PMMG_HIP_S2START"));
+  if (getenv("PMMG_HIP_CARRY")) c->carry = atoi(getenv("PMMG_HIP_CARRY"));
+  if (getenv("PMMG_HIP_WALKW")) c->walkw = atoi(getenv("PMMG_HIP_WALKW"));
   if (c->seed_run != 1 && c->seed_run != 2 && c->seed_run != 4 && c->seed_run != 8) c->seed_run = 4;
   c->qpb = env_int("PMMG_HIP_QPB", c->qpb);
   c->qpc = env_int("PMMG_HIP_QPC", c->qpc);
@@ -1370,7 +1813,7 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   (void)hipStreamSynchronize(c->stream);
   DevBuf *bufs[] = {&c->cont, &c->vrec, &c->o_xyz, &c->o_tetv, &c->o_adja, &c->o_triv, &c->o_adjt, &c->o_met, &c->frame, &c->stats,
                     &c->grid, &c->sgrid, &c->cnt, &c->off, &c->binrank, &c->order_v, &c->order_b, &c->vloc, &c->qs,
-                    &c->scan_tmp, &c->scan_tmp2, &c->fb_vol, &c->fb_bdy, &c->best, &c->ckey, &c->cidx, &c->bbest, &c->bckey,
+                    &c->scan_tmp, &c->cls_cnt, &c->cls_cnt2, &c->fb_vol, &c->fb_bdy, &c->best, &c->ckey, &c->cidx, &c->bbest, &c->bckey,
                     &c->bcidx, &c->h_xyz, &c->h_cls, &c->h_met, &c->h_elem, &c->h_hit};
   for (DevBuf *b : bufs) release(*b);
   for (auto &b : c->o_f) release(b);
@@ -1574,6 +2017,19 @@ static int blocks_for(long long n, int cap) {
   return (int)b;
 }
 
+// stable compaction of the points of class cls (k_cls_*); bcnt: a per-call
+// buffer of the context (one per stream that runs a compaction)
+static bool class_select(pmmg_hip_ctx *c, DevBuf &bcnt, const uint8_t *pclass, long long np, int cls, int *out,
+                         int *count, hipStream_t s) {
+  const long long nb = np > 0 ? (np + kClsChunk - 1) / kClsChunk : 1;
+  if (!ensure(c, bcnt, 4 * (size_t)nb)) return false;
+  int *bc = (int *)bcnt.p;
+  hipLaunchKernelGGL(k_cls_count, dim3((unsigned)nb), dim3(kBlock), 0, s, pclass, np, cls, bc);
+  hipLaunchKernelGGL(k_cls_scan, dim3(1), dim3(kBlock), 0, s, bc, (int)nb, count);
+  hipLaunchKernelGGL(k_cls_scatter, dim3((unsigned)nb), dim3(kBlock), 0, s, pclass, np, cls, (const int *)bc, out);
+  return true;
+}
+
 // fallbacks are rare: read the two counts back and launch only what is needed
 static int launch_fallbacks(pmmg_hip_ctx *c, const Slots &S, const double *xyz_new, int *elem_out, int8_t *hit_out) {
   const Bg &bg = c->bg;
@@ -1639,20 +2095,14 @@ static int run_scan(pmmg_hip_ctx *c, const Slots &S, int np_new, const double *x
 
   size_t tb = 0;
   HIPCK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (int *)c->cnt.p, (int *)c->off.p, (int)(ncells + 1), s));
-  size_t tb2 = 0;
-  hipcub::CountingInputIterator<int> ids(1);
-  HIPCK(c, hipcub::DeviceSelect::If(nullptr, tb2, ids, order_b, &st->nbdy, (int64_t)np_new,
-                                    IsClass{pclass, PMMG_PT_BDY}, s));
-  if (!ensure(c, c->scan_tmp, tb > tb2 ? tb : tb2)) return 0;
+  if (!ensure(c, c->scan_tmp, tb)) return 0;
   hipLaunchKernelGGL(k_qcount, dim3(blocks_for(np_new, 1 << 30)), dim3(kBlock), 0, s, xyz_new, pclass, np_new, fr, gq,
                      (int *)c->cnt.p, (int2 *)c->binrank.p);
   HIPCK(c, hipcub::DeviceScan::ExclusiveSum(c->scan_tmp.p, tb, (int *)c->cnt.p, (int *)c->off.p, (int)(ncells + 1), s));
   hipLaunchKernelGGL(k_qscatter, dim3(blocks_for(np_new, 1 << 30)), dim3(kBlock), 0, s, np_new, xyz_new,
                      (const int2 *)c->binrank.p, (const int *)c->off.p, order_v, (double *)c->qs.p, res);
   hipLaunchKernelGGL(k_qtotal, dim3(1), dim3(1), 0, s, (const int *)c->off.p, (int)ncells, st);
-  if (bg.nt > 0)
-    HIPCK(c, hipcub::DeviceSelect::If(c->scan_tmp.p, tb2, ids, order_b, &st->nbdy, (int64_t)np_new,
-                                      IsClass{pclass, PMMG_PT_BDY}, s));
+  if (bg.nt > 0 && !class_select(c, c->cls_cnt2, pclass, np_new, PMMG_PT_BDY, order_b, &st->nbdy, s)) return 0;
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[2], s));
 
@@ -1755,8 +2205,8 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   }
   long long nsamp = (long long)c->spc * ng;
   if (nsamp > bg.ne) nsamp = bg.ne;
-  hipLaunchKernelGGL(k_seed_vol, dim3(blocks_for(nsamp, 8192)), dim3(kBlock), 0, s, bg, fr, grid, g, nsamp,
-                     c->seed_mode, c->seed_run);
+  hipLaunchKernelGGL(k_seed_vol, dim3((blocks_for(nsamp, c->seed_grid) + 7) & ~7), dim3(kBlock), 0, s, bg, fr, grid, g, nsamp,
+                     c->seed_mode, c->seed_run, c->seed_atom);
   if (c->bdy_on_s2 && c->s2_start != 0) {
     HIPCK(c, hipEventRecord(c->ev[7], s));
     HIPCK(c, hipStreamWaitEvent(sb, c->ev[7], 0));
@@ -1779,33 +2229,32 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     // stable class compaction: the surface list always (on the surface
     // branch's stream); the volume list only for the fused kernel
     // (k_vol_walk selects volume points itself)
-    hipcub::CountingInputIterator<int> ids(1);
-    size_t tb = 0;
-    HIPCK(c, hipcub::DeviceSelect::If(nullptr, tb, ids, order_v, &st->nvol, (int64_t)np_new, IsClass{pclass, 1}, s));
-    if (!ensure(c, c->scan_tmp, tb) || !ensure(c, c->scan_tmp2, tb)) return 0;
-    if (c->options & PMMG_HIP_OPT_FUSED)
-      HIPCK(c, hipcub::DeviceSelect::If(c->scan_tmp.p, tb, ids, order_v, &st->nvol, (int64_t)np_new,
-                                        IsClass{pclass, PMMG_PT_VOL}, s));
-    HIPCK(c, hipcub::DeviceSelect::If(c->scan_tmp2.p, tb, ids, order_b, &st->nbdy, (int64_t)np_new,
-                                      IsClass{pclass, PMMG_PT_BDY}, sb));
+    if ((c->options & PMMG_HIP_OPT_FUSED) &&
+        !class_select(c, c->cls_cnt, pclass, np_new, PMMG_PT_VOL, order_v, &st->nvol, s))
+      return 0;
+    if (!class_select(c, c->cls_cnt2, pclass, np_new, PMMG_PT_BDY, order_b, &st->nbdy, sb)) return 0;
   }
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[2], s));
   c->count_nvol = !sorted && !(c->options & PMMG_HIP_OPT_FUSED);
 
   if (!(c->options & PMMG_HIP_OPT_FUSED)) {
-    hipLaunchKernelGGL(k_vol_walk, dim3(blocks_for(np_new, 1 << 30)), dim3(kBlock), 0, s, bg, fr, grid, g, xyz_new,
+    auto walk = c->carry == 2 ? (c->walkw >= 5 ? k_vol_walk<2, 5> : k_vol_walk<2, 1>)
+                : c->carry    ? (c->walkw >= 5 ? k_vol_walk<1, 5> : k_vol_walk<1, 1>)
+                              : (c->walkw >= 5 ? k_vol_walk<0, 5> : k_vol_walk<0, 1>);
+    hipLaunchKernelGGL(walk, dim3(blocks_for(np_new, 1 << 30)), dim3(kBlock), 0, s, bg, fr, grid, g, xyz_new,
                        pclass, sorted ? (const int *)order_v : nullptr, np_new, (int *)c->vloc.p,
-                       (VolLoc *)c->vrec.p, (int *)c->fb_vol.p, (ContEntry *)c->cont.p, st, c->cap, c->maxstep);
+                       vrec_arrays(c->vrec.p, (size_t)np_new), (int *)c->fb_vol.p, (ContEntry *)c->cont.p, st, c->cap,
+                       c->maxstep);
     if (c->cap < c->maxstep) // continuation pass only when capping is enabled
       hipLaunchKernelGGL(k_vol_walk_cont, dim3(8 * blocks_for((np_new + 7) / 8, 1 << 20)), dim3(kBlock), 0, s, bg,
                          xyz_new, (int *)c->vloc.p,
-                         (VolLoc *)c->vrec.p, (int *)c->fb_vol.p, (const ContEntry *)c->cont.p, st, c->cap,
+                         vrec_arrays(c->vrec.p, (size_t)np_new), (int *)c->fb_vol.p, (const ContEntry *)c->cont.p, st, c->cap,
                          c->maxstep);
     HIPCK(c, hipEventRecord(c->ev[6], s));
     VolInterpFn interp = pick_layout(S).fn;
     hipLaunchKernelGGL(interp, dim3(blocks_for(np_new, 1 << 30)), dim3(kBlock), 0, s, pclass, np_new,
-                       (const int *)c->vloc.p, (const VolLoc *)c->vrec.p, S, elem_out, hit_out);
+                       (const int *)c->vloc.p, vrec_arrays(c->vrec.p, (size_t)np_new), S, elem_out, hit_out);
   } else {
     FusedFn fused = pick_layout(S).ffn;
     hipLaunchKernelGGL(fused, dim3(blocks_for(np_new, 1 << 30)), dim3(kBlock), 0, s, bg, fr, grid, g, xyz_new,
