@@ -103,10 +103,15 @@ __device__ __forceinline__ double dunkey(unsigned long long k) {
   return __longlong_as_double((long long)u);
 }
 
+// Element i of a register tuple, branch-free: a ternary chain on i is turned
+// into a switch, i.e. divergent branches (exec-mask juggling per lane
+// pattern) in the walk loops.
+__device__ __forceinline__ unsigned bsel(unsigned a, unsigned b, unsigned bit) { return a ^ ((a ^ b) & (0u - bit)); }
 __device__ __forceinline__ int sel4(const int4 &a, int i) {
-  return i == 0 ? a.x : (i == 1 ? a.y : (i == 2 ? a.z : a.w));
+  const unsigned b0 = (unsigned)i & 1u, b1 = ((unsigned)i >> 1) & 1u;
+  return (int)bsel(bsel((unsigned)a.x, (unsigned)a.y, b0), bsel((unsigned)a.z, (unsigned)a.w, b0), b1);
 }
-__device__ __forceinline__ int sel3i(int a, int b, int c, int i) { return i == 0 ? a : (i == 1 ? b : c); }
+__device__ __forceinline__ int sel3i(int a, int b, int c, int i) { return sel4(make_int4(a, b, c, c), i); }
 __device__ __forceinline__ double sel3d(double a, double b, double c, int i) { return i == 0 ? a : (i == 1 ? b : c); }
 
 __device__ __forceinline__ void load_pt(const double *xyz, int v, double *p) {

@@ -673,12 +673,6 @@ __device__ __forceinline__ int walk_core(const Bg &bg, const double *x, int &k, 
 // permuted into the new tetra's local order (the reference's arithmetic
 // order) with mask blends: a select chain over a register array is lowered
 // to scratch-memory indexing.
-__device__ __forceinline__ double blend4(double a, double b, double c, double d, long long m0, long long m1,
-                                         long long m2, long long m3) {
-  const long long r = (__double_as_longlong(a) & m0) | (__double_as_longlong(b) & m1) |
-                      (__double_as_longlong(c) & m2) | (__double_as_longlong(d) & m3);
-  return __longlong_as_double(r);
-}
 
 __device__ __forceinline__ int walk_core_carry(const Bg &bg, const double *x, int &k, int &steps, int limit,
                                                VolLoc *loc) {
@@ -755,15 +749,8 @@ __device__ __forceinline__ int walk_core_carry(const Bg &bg, const double *x, in
       const bool e1 = id == tv.y, e2 = id == tv.z, e3 = id == tv.w, en = l == iopp;
 #pragma unroll
       for (int d = 0; d < 3; d++) {
-#if PMMG_CARRY_BLEND
-        const long long m0 = -(long long)(id == tv.x), m1 = -(long long)e1, m2 = -(long long)e2, m3 = -(long long)e3;
-        const long long mn = -(long long)en;
-        const double c = blend4(p[0][d], p[1][d], p[2][d], p[3][d], m0, m1, m2, m3);
-        q[l][d] = __longlong_as_double((__double_as_longlong(c) & ~mn) | (__double_as_longlong(pn[d]) & mn));
-#else
         const double c = e1 ? p[1][d] : (e2 ? p[2][d] : (e3 ? p[3][d] : p[0][d]));
         q[l][d] = en ? pn[d] : c;
-#endif
       }
     }
 #pragma unroll
@@ -774,135 +761,113 @@ __device__ __forceinline__ int walk_core_carry(const Bg &bg, const double *x, in
   }
 }
 
-// Walk in slot order: the tetra's vertices stay in the registers ("slots")
-// they were loaded into, a step replaces only the slot of the vertex left
-// behind (one v_cndmask per dword), and the filter test runs on the slots'
-// order.  Its rounding differs from the reference's vertex order, so it only
-// nominates candidates (min barycentric > -kCandEps, a margin far above the
-// rounding of any non-degenerate tetra); every candidate is then re-evaluated
-// in the reference's order with the exact test (walk_exact), once per wave
-// when the lanes have all stopped (not inside the divergent step loop).  A
-// rejected candidate resumes its walk.  Acceptance and the coordinates are
-// therefore the reference's, bit for bit; only the path can differ (faces
-// are ranked by the slot-order keys), as with any walk start.
-constexpr double kCandEps = 8 * kEps;
-
+// Walk with the tetra's vertex coordinates kept in LDS "slots" (per lane 4
+// slots x 3 doubles, lane-interleaved: conflict-free).  A step writes only
+// the new vertex into the slot of the vertex left behind and reads the four
+// slots back in the new tetra's local order (m = local -> slot), so the
+// reference's arithmetic order costs 12 LDS reads instead of ~100 register
+// selects, and no register copy of the previous tetra's points stays live.
 __device__ __forceinline__ int idx_in(int id, const int4 &t) {
   return (id == t.y ? 1 : 0) + (id == t.z ? 2 : 0) + (id == t.w ? 3 : 0);
 }
 
-// the slots permuted into the tetra's local order: q[l] = p[j] with m_j == l
-__device__ __forceinline__ void slots_to_local(const double (*p)[3], const int4 &m, double (*q)[3]) {
+struct LaneSlots { // this lane's view of the wave's slot image [slot][dim][64]
+  double *base;
+  __device__ __forceinline__ void put(int slot, const double *p) const {
 #pragma unroll
-  for (int l = 0; l < 4; l++) {
-    const long long m0 = -(long long)(m.x == l), m1 = -(long long)(m.y == l), m2 = -(long long)(m.z == l),
-                    m3 = -(long long)(m.w == l);
-#pragma unroll
-    for (int d = 0; d < 3; d++) q[l][d] = blend4(p[0][d], p[1][d], p[2][d], p[3][d], m0, m1, m2, m3);
+    for (int d = 0; d < 3; d++) base[(slot * 3 + d) * 64] = p[d];
   }
-}
+  __device__ __forceinline__ void get(int slot, double *p) const {
+#pragma unroll
+    for (int d = 0; d < 3; d++) p[d] = base[(slot * 3 + d) * 64];
+  }
+};
 
-__device__ __forceinline__ int walk_core_slot(const Bg &bg, const double *x, int &k, int &steps, int limit,
-                                              VolLoc *loc) {
+__device__ __forceinline__ int walk_core_lds(const Bg &bg, const double *x, int &k, int &steps, int limit,
+                                             VolLoc *loc, const LaneSlots &L) {
   int hist[kHist];
 #pragma unroll
   for (int h = 0; h < kHist; h++) hist[h] = 0;
-  int4 ad = adja_row(bg, k);
-  int4 sid = tetv_row(bg, k);      // vertex id in slot j
-  double p[4][3];
-  load_tet_pts(bg, sid, p);
-  int4 m = make_int4(0, 1, 2, 3);  // local index (in tv / ad) of slot j
-  bool skip = false;               // the current tetra failed the exact test
-  int n = 0;
-  for (;;) {
-    int status = 0;
-    for (;;) {
-      if (n >= limit) { status = 3; break; }
-      ++n;
-      ++steps;
-      double s[4];
-      const double vol = tet_dots(x, p[0], p[1], p[2], p[3], s);
-      double key[4];
-      bool cand;
-      if (vol > 0.0 || vol < 0.0) {
-        double sm;
-        if (vol > 0.0) {
-          sm = s[0];
-          sm = s[1] > sm ? s[1] : sm;
-          sm = s[2] > sm ? s[2] : sm;
-          sm = s[3] > sm ? s[3] : sm;
-        } else {
-          sm = s[0];
-          sm = s[1] < sm ? s[1] : sm;
-          sm = s[2] < sm ? s[2] : sm;
-          sm = s[3] < sm ? s[3] : sm;
-        }
-        cand = -(sm / vol) > -kCandEps;
+  int4 tv = tetv_row(bg, k), ad = adja_row(bg, k);
+  {
+    double p[4][3];
+    load_tet_pts(bg, tv, p);
 #pragma unroll
-        for (int f = 0; f < 4; f++) key[f] = vol > 0.0 ? s[f] : -s[f];
-      } else { // degenerate in slot order: the exact test decides
-        cand = true;
-#pragma unroll
-        for (int f = 0; f < 4; f++) key[f] = s[f];
+    for (int l = 0; l < 4; l++) L.put(l, p[l]);
+  }
+  int4 m = make_int4(0, 1, 2, 3); // slot of local vertex l
+  for (int n = 0;; n++) {
+    if (n >= limit) return 3;
+    ++steps;
+    double p[4][3];
+    L.get(m.x, p[0]);
+    L.get(m.y, p[1]);
+    L.get(m.z, p[2]);
+    L.get(m.w, p[3]);
+    double s[4];
+    const double vol = tet_dots(x, p[0], p[1], p[2], p[3], s);
+    double key[4];
+    bool inside;
+    if (vol > 0.0 || vol < 0.0) {
+      double sm;
+      if (vol > 0.0) {
+        sm = s[0];
+        sm = s[1] > sm ? s[1] : sm;
+        sm = s[2] > sm ? s[2] : sm;
+        sm = s[3] > sm ? s[3] : sm;
+      } else {
+        sm = s[0];
+        sm = s[1] < sm ? s[1] : sm;
+        sm = s[2] < sm ? s[2] : sm;
+        sm = s[3] < sm ? s[3] : sm;
       }
-      if (cand && !skip) { status = 1; break; }
-      skip = false;
-      int4 code;
-      code.x = sel4(ad, m.x);
-      code.y = sel4(ad, m.y);
-      code.z = sel4(ad, m.z);
-      code.w = sel4(ad, m.w);
-      int f = -1;
-      double best = 0.0;
+      inside = -(sm / vol) > -kEps;
 #pragma unroll
-      for (int ff = 0; ff < 4; ff++) {
-        const int iel = sel4(code, ff) >> 2;
-        bool vis = false;
+      for (int f = 0; f < 4; f++) key[f] = vol > 0.0 ? s[f] : -s[f];
+    } else { // degenerate: the reference's four divisions; any face order
+      double b[4];
 #pragma unroll
-        for (int h = 0; h < kHist; h++) vis = vis || (hist[h] == iel);
-        if (iel != 0 && !vis && (f < 0 || key[ff] > best)) { f = ff; best = key[ff]; }
-      }
-      if (f < 0) { status = 2; break; }
+      for (int f = 0; f < 4; f++) b[f] = -s[f] / vol;
+      inside = min4(b) > -kEps;
 #pragma unroll
-      for (int h = kHist - 1; h > 0; h--) hist[h] = hist[h - 1];
-      hist[0] = k;
-      const int c = sel4(code, f);
-      k = c >> 2;
-      const int iopp = c & 3;
-      const int4 tn = tetv_row(bg, k);
-      ad = adja_row(bg, k);
-      // (tn is dead after this step: the local order lives in m)
-      const int vn = sel4(tn, iopp);
-      double pn[3];
-      load_pt(bg.xyz, vn, pn);
-      m.x = f == 0 ? iopp : idx_in(sid.x, tn);
-      m.y = f == 1 ? iopp : idx_in(sid.y, tn);
-      m.z = f == 2 ? iopp : idx_in(sid.z, tn);
-      m.w = f == 3 ? iopp : idx_in(sid.w, tn);
-      sid.x = f == 0 ? vn : sid.x;
-      sid.y = f == 1 ? vn : sid.y;
-      sid.z = f == 2 ? vn : sid.z;
-      sid.w = f == 3 ? vn : sid.w;
-#pragma unroll
-      for (int j = 0; j < 4; j++)
-#pragma unroll
-        for (int d = 0; d < 3; d++) p[j][d] = f == j ? pn[d] : p[j][d];
+      for (int f = 0; f < 4; f++) key[f] = s[f];
     }
-    if (status != 1) return status;
-    // the reference's exact test, vertices in the tetra's own order
-    double q[4][3], s[4];
-    slots_to_local(p, m, q);
-    const double vol = tet_dots(x, q[0], q[1], q[2], q[3], s);
-    double b[4];
+    if (inside) {
+      loc->v = tv;
 #pragma unroll
-    for (int f = 0; f < 4; f++) b[f] = -s[f] / vol;
-    if (min4(b) > -kEps) {
-      loc->v = tetv_row(bg, k);
-#pragma unroll
-      for (int f = 0; f < 4; f++) loc->phi[f] = b[f];
+      for (int f = 0; f < 4; f++) loc->phi[f] = -s[f] / vol;
       return 1;
     }
-    skip = true;
+    int f = -1;
+    double best = 0.0;
+#pragma unroll
+    for (int ff = 0; ff < 4; ff++) {
+      const int iel = sel4(ad, ff) >> 2;
+      bool vis = false;
+#pragma unroll
+      for (int h = 0; h < kHist; h++) vis = vis || (hist[h] == iel);
+      if (iel != 0 && !vis && (f < 0 || key[ff] > best)) { f = ff; best = key[ff]; }
+    }
+    if (f < 0) return 2;
+#pragma unroll
+    for (int h = kHist - 1; h > 0; h--) hist[h] = hist[h - 1];
+    hist[0] = k;
+    const int code = sel4(ad, f);
+    k = code >> 2;
+    const int iopp = code & 3;
+    const int4 tn = tetv_row(bg, k);
+    ad = adja_row(bg, k);
+    double pn[3];
+    load_pt(bg.xyz, sel4(tn, iopp), pn);
+    const int sf = sel4(m, f); // slot of the vertex left behind
+    int4 mn; // branch-free (a ternary with a costly arm becomes a divergent branch)
+    mn.x = (int)bsel((unsigned)sel4(m, idx_in(tn.x, tv)), (unsigned)sf, iopp == 0);
+    mn.y = (int)bsel((unsigned)sel4(m, idx_in(tn.y, tv)), (unsigned)sf, iopp == 1);
+    mn.z = (int)bsel((unsigned)sel4(m, idx_in(tn.z, tv)), (unsigned)sf, iopp == 2);
+    mn.w = (int)bsel((unsigned)sel4(m, idx_in(tn.w, tv)), (unsigned)sf, iopp == 3);
+    L.put(sf, pn);
+    m = mn;
+    tv = tn;
   }
 }
 
@@ -923,6 +888,8 @@ __global__ __launch_bounds__(kBlock, MINW) void k_vol_walk(Bg bg, const Frame *f
                                                            const int *order, int np, int *vloc, VRec vrec, int *fb,
                                                            ContEntry *cont, DevStats *st, int cap, int maxstep) {
   __shared__ BlockStats bs;
+  __shared__ double slot_img[CARRY == 2 ? kBlock / 64 : 1][CARRY == 2 ? 12 * 64 : 1];
+  const LaneSlots L{&slot_img[CARRY == 2 ? threadIdx.x >> 6 : 0][CARRY == 2 ? __lane_id() : 0]};
   bstats_init(&bs);
   __syncthreads();
   const int i = xcd_block() * blockDim.x + threadIdx.x;
@@ -942,7 +909,7 @@ __global__ __launch_bounds__(kBlock, MINW) void k_vol_walk(Bg bg, const Frame *f
     k = seed_vol(grid, g, fr, x);
     VolLoc loc;
     const int lim = cap < maxstep ? cap : maxstep;
-    status = CARRY == 2   ? walk_core_slot(bg, x, k, steps, lim, &loc)
+    status = CARRY == 2   ? walk_core_lds(bg, x, k, steps, lim, &loc, L)
              : CARRY == 1 ? walk_core_carry(bg, x, k, steps, lim, &loc)
                           : walk_core(bg, x, k, steps, lim, &loc);
     if (status == 3 && steps < maxstep) status = 4; // -> continuation list
@@ -1659,7 +1626,7 @@ struct pmmg_hip_ctx {
   hipStream_t stream2 = nullptr; // surface branch, concurrent with the volume walk
   bool bdy_on_s2 = false;
   int two_streams = 1; // PMMG_HIP_STREAMS=1: everything on one stream
-  int carry = 1;       // walk carrying the crossed face's vertices (PMMG_HIP_CARRY)
+  int carry = 2;       // 0 reload, 1 registers, 2 LDS slots (PMMG_HIP_CARRY)
   int walkw = 0;       // >= 5: walk compiled for 5 waves per SIMD (PMMG_HIP_WALKW)
   int s2_start = 0;    // surface branch start: 0 after the frame, 1 after the volume seeds
   char err[512] = {0};
