@@ -886,13 +886,14 @@ template <int CARRY, int MINW>
 __global__ __launch_bounds__(kBlock, MINW) void k_vol_walk(Bg bg, const Frame *fr, const unsigned long long *grid,
                                                            int g, const double *qxyz, const uint8_t *pclass,
                                                            const int *order, int np, int *vloc, VRec vrec, int *fb,
-                                                           ContEntry *cont, DevStats *st, int cap, int maxstep) {
+                                                           ContEntry *cont, DevStats *st, int cap, int maxstep,
+                                                           int i0) {
   __shared__ BlockStats bs;
   __shared__ double slot_img[CARRY == 2 ? kBlock / 64 : 1][CARRY == 2 ? 12 * 64 : 1];
   const LaneSlots L{&slot_img[CARRY == 2 ? threadIdx.x >> 6 : 0][CARRY == 2 ? __lane_id() : 0]};
   bstats_init(&bs);
   __syncthreads();
-  const int i = xcd_block() * blockDim.x + threadIdx.x;
+  const int i = i0 + xcd_block() * blockDim.x + threadIdx.x;
   bool active;
   int ip = 0;
   if (order) {
@@ -1034,10 +1035,10 @@ struct SlotRow {
 // none; C0 < 0 = runtime layout, per-lane stores).
 template <int C0, int C1, int C2, int C3, int C4, int C5>
 __global__ __launch_bounds__(kBlock) void k_vol_interp(const uint8_t *pclass, int np, const int *vloc, VRec vrec,
-                                                       Slots S, int *elem_out, int8_t *hit_out) {
+                                                       Slots S, int *elem_out, int8_t *hit_out, int i0) {
   __shared__ double img_all[kBlock / 64][64 * 6];
   double *img = img_all[threadIdx.x >> 6];
-  const int i = xcd_block() * blockDim.x + threadIdx.x;
+  const int i = i0 + xcd_block() * blockDim.x + threadIdx.x;
   bool act = i < np && __builtin_nontemporal_load(pclass + i) == PMMG_PT_VOL;
   const int k = act ? __builtin_nontemporal_load(vloc + i) : 0;
   act = act && k != 0;
@@ -1569,7 +1570,7 @@ __global__ void k_fallback_init(int *a, int *b, unsigned long long *c, const int
 
 // ---------------------------------------------------------------- layout dispatch
 
-typedef void (*VolInterpFn)(const uint8_t *, int, const int *, VRec, Slots, int *, int8_t *);
+typedef void (*VolInterpFn)(const uint8_t *, int, const int *, VRec, Slots, int *, int8_t *, int);
 typedef void (*ScanInterpFn)(Bg, const double *, const int *, const int *, Slots, int *, int8_t *, int *, DevStats *);
 typedef void (*FusedFn)(Bg, const Frame *, const unsigned long long *, int, const double *, const int *, Slots, int *,
                         int8_t *, int *, DevStats *, int);
@@ -1614,6 +1615,8 @@ const LayoutEntry &pick_layout(const Slots &S) {
 
 // ================================================================ host side
 
+constexpr int kMaxChunks = 16;
+
 struct DevBuf {
   void *p = nullptr;
   size_t cap = 0;
@@ -1624,6 +1627,9 @@ struct pmmg_hip_ctx {
   int options = 0;
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr; // surface branch, concurrent with the volume walk
+  hipStream_t stream3 = nullptr; // volume interpolation of chunk c, concurrent with the walk of chunk c+1
+  int chunks = 3;                // volume pipeline chunks (PMMG_HIP_CHUNKS)
+  hipEvent_t evc[kMaxChunks] = {};
   bool bdy_on_s2 = false;
   int two_streams = 1; // PMMG_HIP_STREAMS=1: everything on one stream
   int carry = 2;       // 0 reload, 1 registers, 2 LDS slots (PMMG_HIP_CARRY)
@@ -1739,12 +1745,14 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   c->device = device;
   c->options = options;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
+      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess) {
     fprintf(stderr, "[parmmg_hip] cannot initialise device %d\n", device);
     delete c;
     return nullptr;
   }
   for (int i = 0; i < 10; i++) (void)hipEventCreate(&c->ev[i]);
+  for (int i = 0; i < kMaxChunks; i++) (void)hipEventCreateWithFlags(&c->evc[i], hipEventDisableTiming);
   if (hipHostMalloc((void **)&c->h_small, 64, hipHostMallocDefault) != hipSuccess) {
     fprintf(stderr, "[parmmg_hip] cannot allocate pinned host memory\n");
     delete c;
@@ -1766,6 +1774,8 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   c->qpc = env_int("PMMG_HIP_QPC", c->qpc);
   c->maxstep = env_int("PMMG_HIP_MAXSTEP", c->maxstep);
   c->cap = env_int("PMMG_HIP_CAP", c->cap);
+  c->chunks = env_int("PMMG_HIP_CHUNKS", c->chunks);
+  if (c->chunks > kMaxChunks) c->chunks = kMaxChunks;
   {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
@@ -1787,6 +1797,9 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   for (auto &b : c->h_f) release(b);
   for (int i = 0; i < 10; i++)
     if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
+  for (int i = 0; i < kMaxChunks; i++)
+    if (c->evc[i]) (void)hipEventDestroy(c->evc[i]);
+  if (c->stream3) (void)hipStreamDestroy(c->stream3);
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->h_small) (void)hipHostFree(c->h_small);
@@ -2209,19 +2222,43 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     auto walk = c->carry == 2 ? (c->walkw >= 5 ? k_vol_walk<2, 5> : k_vol_walk<2, 1>)
                 : c->carry    ? (c->walkw >= 5 ? k_vol_walk<1, 5> : k_vol_walk<1, 1>)
                               : (c->walkw >= 5 ? k_vol_walk<0, 5> : k_vol_walk<0, 1>);
-    hipLaunchKernelGGL(walk, dim3(blocks_for(np_new, 1 << 30)), dim3(kBlock), 0, s, bg, fr, grid, g, xyz_new,
-                       pclass, sorted ? (const int *)order_v : nullptr, np_new, (int *)c->vloc.p,
-                       vrec_arrays(c->vrec.p, (size_t)np_new), (int *)c->fb_vol.p, (ContEntry *)c->cont.p, st, c->cap,
-                       c->maxstep);
-    if (c->cap < c->maxstep) // continuation pass only when capping is enabled
+    VolInterpFn interp = pick_layout(S).fn;
+    const VRec vr = vrec_arrays(c->vrec.p, (size_t)np_new);
+    // Pipelined volume stage: the queries are cut into `nch` contiguous
+    // chunks; the interpolation of chunk j (bandwidth-bound) runs on stream3
+    // while the walk of chunk j+1 (latency-bound) runs on the main stream, so
+    // the interpolation's traffic fills the walk's idle memory slots.  The
+    // input-order path only (the Morton-binned walk is indexed by bin order).
+    const bool capped = c->cap < c->maxstep;
+    const int nch = (!sorted && !capped && c->chunks > 1) ? c->chunks : 1;
+    const long long per = ((long long)np_new + nch - 1) / nch;
+    const int chunk = (int)((per + kBlock - 1) / kBlock * kBlock);
+    for (int j = 0; j < nch; j++) {
+      const int a = j * chunk, n = np_new - a < chunk ? np_new - a : chunk;
+      if (n <= 0) break;
+      const int np_j = nch > 1 ? a + n : np_new; // lanes at or past np_j are idle
+      hipLaunchKernelGGL(walk, dim3(blocks_for(n, 1 << 30)), dim3(kBlock), 0, s, bg, fr, grid, g, xyz_new, pclass,
+                         sorted ? (const int *)order_v : nullptr, np_j, (int *)c->vloc.p, vr, (int *)c->fb_vol.p,
+                         (ContEntry *)c->cont.p, st, c->cap, c->maxstep, a);
+      if (nch > 1) {
+        HIPCK(c, hipEventRecord(c->evc[j], s));
+        HIPCK(c, hipStreamWaitEvent(c->stream3, c->evc[j], 0));
+        hipLaunchKernelGGL(interp, dim3(blocks_for(n, 1 << 30)), dim3(kBlock), 0, c->stream3, pclass, np_j,
+                           (const int *)c->vloc.p, vr, S, elem_out, hit_out, a);
+      }
+    }
+    if (capped) // continuation pass only when capping is enabled
       hipLaunchKernelGGL(k_vol_walk_cont, dim3(8 * blocks_for((np_new + 7) / 8, 1 << 20)), dim3(kBlock), 0, s, bg,
-                         xyz_new, (int *)c->vloc.p,
-                         vrec_arrays(c->vrec.p, (size_t)np_new), (int *)c->fb_vol.p, (const ContEntry *)c->cont.p, st, c->cap,
+                         xyz_new, (int *)c->vloc.p, vr, (int *)c->fb_vol.p, (const ContEntry *)c->cont.p, st, c->cap,
                          c->maxstep);
     HIPCK(c, hipEventRecord(c->ev[6], s));
-    VolInterpFn interp = pick_layout(S).fn;
-    hipLaunchKernelGGL(interp, dim3(blocks_for(np_new, 1 << 30)), dim3(kBlock), 0, s, pclass, np_new,
-                       (const int *)c->vloc.p, vrec_arrays(c->vrec.p, (size_t)np_new), S, elem_out, hit_out);
+    if (nch > 1) {
+      HIPCK(c, hipEventRecord(c->evc[nch - 1], c->stream3));
+      HIPCK(c, hipStreamWaitEvent(s, c->evc[nch - 1], 0));
+    } else {
+      hipLaunchKernelGGL(interp, dim3(blocks_for(np_new, 1 << 30)), dim3(kBlock), 0, s, pclass, np_new,
+                         (const int *)c->vloc.p, vr, S, elem_out, hit_out, 0);
+    }
   } else {
     FusedFn fused = pick_layout(S).ffn;
     hipLaunchKernelGGL(fused, dim3(blocks_for(np_new, 1 << 30)), dim3(kBlock), 0, s, bg, fr, grid, g, xyz_new,
