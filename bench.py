@@ -100,6 +100,40 @@ def cpu_baseline(w, bg, new, met, fields, pclass, budget_s: float):
     }
 
 
+def snapshot_timing(ctx, bg, rank: int, reps: int = 3):
+    """Device background snapshot (PMMG_create_oldGrp's
+    adjacency / boundary trias / tria adjacency, pmmg_hip_build_*) timed on
+    its own, outside the transfer step: wall time of the synchronous calls
+    (scratch allocation included), median of `reps`, checked against the
+    host-built arrays the step uses."""
+    d_tetv = ctx.upload(bg.tetv)
+    times = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        adja, tet8 = ctx.build_adjacency(bg.np, d_tetv, adja=False, tet8=True)
+        t1 = time.perf_counter()
+        triv, adjt = ctx.build_boundary(bg.np, tet8=tet8)
+        t2 = time.perf_counter()
+        times.append((t1 - t0, t2 - t1))
+        ok = bool(np.array_equal(adjt.download(), bg.adjt))
+        if _ == reps - 1:
+            from parmmg_amd.transfer import pack_tet8
+            ok = ok and bool(np.array_equal(tet8.download(), pack_tet8(bg.tetv, bg.adja)))
+            ok = ok and bool(np.array_equal(triv.download(), bg.triv))
+        for a in (tet8, triv, adjt):
+            a.free()
+    d_tetv.free()
+    t_adj = float(np.median([t[0] for t in times]))
+    t_bdy = float(np.median([t[1] for t in times]))
+    # compulsory bytes: tetv in (16 B/tet), tet8 records out (32 B/tet)
+    b_adj = bg.ne * (16 + 32)
+    log(f"[bench r{rank}] snapshot: adjacency {1e3 * t_adj:.2f} ms, boundary {1e3 * t_bdy:.2f} ms, match={ok}")
+    return {"what": "pmmg_hip_build_adjacency (tet8 out) + pmmg_hip_build_boundary, not part of the step",
+            "ms_adjacency": round(1e3 * t_adj, 3), "ms_boundary": round(1e3 * t_bdy, 3),
+            "tets": bg.ne, "trias": bg.nt, "matches_host_builder": ok,
+            "adjacency_algorithmic_gbps": round(b_adj / t_adj / 1e9, 1)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -119,6 +153,8 @@ def main():
                     help="HBM layout of the metric/fields: packed per-vertex records or one array per solution")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-snapshot", action="store_true",
+                    help="skip the (separately reported) device background snapshot timing")
     args = ap.parse_args()
 
     ri = ranks.init("nccl")
@@ -242,6 +278,8 @@ def main():
             "algorithmic_bytes_per_point": round(per_pt, 2),
         },
     }
+    if not args.no_snapshot:
+        out["snapshot"] = snapshot_timing(ctx, bg, rank)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log(f"[bench r{rank}] cpu baseline (oracle) on a bounded sample")
         out["cpu_baseline"] = cpu_baseline(w, bg, new, met, fields, pclass, args.cpu_baseline_seconds)

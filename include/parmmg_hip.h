@@ -184,6 +184,34 @@ int pmmg_hip_locate_interp(pmmg_hip_ctx *ctx, int np_new, const double *xyz_new,
  * PMMG_HIP_DEVICE call.  Returns 1/0. */
 int pmmg_hip_sync(pmmg_hip_ctx *ctx, pmmg_hip_stats *stats);
 
+/* ---- Background snapshot on the device -------------------------------------
+ * ParMmg rebuilds the background's derived arrays on the host every
+ * iteration: PMMG_create_oldGrp (src/grpsplit_pmmg.c:207-418) copies the
+ * adjacency computed by MMG3D_hashTetra (src/libparmmg1.c:495,730), rebuilds
+ * the boundary trias (MMG5_chkBdryTria, :404) and hashes the tria adjacency
+ * (MMG3D_hashTria, :410).  These two entry points build the same arrays on
+ * the device from the connectivity, so the arrays pmmg_hip_set_background*
+ * consumes never take a host round trip.  All pointers are device memory on
+ * the context's device, 16-byte aligned; calls are synchronous. */
+
+/* Tetra adjacency of a conforming mesh from tetv[4*ne] (1-based vertex ids):
+ *   adja[4*ne]  (may be NULL)  4*k'+i' of the tetra sharing face i, 0 on the boundary
+ *   tet8[8*ne]  (may be NULL)  packed {v[4], adja[4]} records (set_background_tet8)
+ * Returns 0 (message in pmmg_hip_last_error) for ids outside [1, np], repeated
+ * ids in a tetra, or a face shared by more than two tetra. */
+int pmmg_hip_build_adjacency(pmmg_hip_ctx *ctx, int np, int ne, const int *tetv,
+                             int *adja, int *tet8);
+
+/* Boundary trias: the faces with no neighbour, in (tetra, face) order, with
+ * vertices v[MMG5_idir[i]] (outward for positively oriented tetra), and their
+ * adjacency adjt[3*nt] (3*t'+j' across edge j, 0 on borders and on edges of
+ * more than two trias).  Tetra from tet8 (packed records) when non-NULL, else
+ * from tetv + adja.  *nt receives the number of trias; when it exceeds `cap`
+ * nothing is written and 0 is returned.  adjt may be NULL. */
+int pmmg_hip_build_boundary(pmmg_hip_ctx *ctx, int np, int ne, const int *tet8,
+                            const int *tetv, const int *adja, int cap, int *nt,
+                            int *triv, int *adjt);
+
 /* Device memory helpers for callers that keep data resident (bench, shims
  * that reuse buffers across iterations). */
 void *pmmg_hip_malloc(pmmg_hip_ctx *ctx, int64_t bytes);

@@ -36,6 +36,7 @@
 #include <vector>
 
 #include "pmmg_device.hpp"
+#include "pmmg_snapshot.hpp"
 
 using namespace pmmg;
 
@@ -2393,6 +2394,46 @@ int pmmg_hip_locate_interp(pmmg_hip_ctx *c, int np_new, const double *xyz_new, c
   HIPCK(c, hipStreamSynchronize(c->stream));
   if (stats) return collect_stats(c, stats);
   return 1;
+}
+
+// ---- background snapshot (pmmg_snapshot.hip)
+
+static bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
+
+int pmmg_hip_build_adjacency(pmmg_hip_ctx *c, int np, int ne, const int *tetv, int *adja, int *tet8) {
+  if (!c) return 0;
+  HIPCK(c, hipSetDevice(c->device));
+  if (np <= 0 || ne <= 0 || !tetv || (!adja && !tet8)) {
+    set_err(c, "build_adjacency: invalid arguments (np=%d ne=%d)", np, ne);
+    return 0;
+  }
+  if (ne >= (1 << 29)) {
+    set_err(c, "build_adjacency: %d tetra exceed the 4*k+i adjacency encoding (2^29)", ne);
+    return 0;
+  }
+  if (!aligned16(tetv) || (adja && !aligned16(adja)) || (tet8 && !aligned16(tet8))) {
+    set_err(c, "build_adjacency: device arrays must be 16-byte aligned");
+    return 0;
+  }
+  return pmmg_snap_adjacency(c->stream, np, ne, tetv, adja, tet8, c->err, sizeof(c->err));
+}
+
+int pmmg_hip_build_boundary(pmmg_hip_ctx *c, int np, int ne, const int *tet8, const int *tetv, const int *adja,
+                            int cap, int *nt, int *triv, int *adjt) {
+  if (!c) return 0;
+  HIPCK(c, hipSetDevice(c->device));
+  const bool packed = tet8 != nullptr;
+  if (np <= 0 || ne <= 0 || !nt || (!packed && (!tetv || !adja)) || cap < 0 || (cap > 0 && !triv)) {
+    set_err(c, "build_boundary: invalid arguments (np=%d ne=%d cap=%d)", np, ne, cap);
+    return 0;
+  }
+  const int *t0 = packed ? tet8 : tetv, *a0 = packed ? tet8 + 4 : adja;
+  if (!aligned16(t0) || !aligned16(a0)) {
+    set_err(c, "build_boundary: device tetra arrays must be 16-byte aligned");
+    return 0;
+  }
+  return pmmg_snap_boundary(c->stream, np, ne, t0, packed ? 2 : 1, a0, packed ? 2 : 1, cap, nt, triv, adjt, c->err,
+                            sizeof(c->err));
 }
 
 void *pmmg_hip_malloc(pmmg_hip_ctx *c, int64_t bytes) {

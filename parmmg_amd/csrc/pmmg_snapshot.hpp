@@ -1,0 +1,15 @@
+// pmmg_snapshot.hpp — internal interface of pmmg_snapshot.hip (background
+// snapshot on the device); the C-ABI wrappers live in pmmg_hip.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+
+// adja[4*ne] (may be NULL) and/or tet8[8*ne] (may be NULL) from tetv[4*ne];
+// all device pointers, 16-byte aligned.  Returns 1, or 0 with msg set.
+int pmmg_snap_adjacency(hipStream_t s, int np, int ne, const int *tetv, int *adja, int *tet8, char *msg,
+                        size_t msglen);
+
+// boundary trias (faces with adja == 0) and their adjacency.  Tetra rows are
+// int4 rows `tstride` / `astride` int4s apart (1: separate arrays, 2: tet8).
+int pmmg_snap_boundary(hipStream_t s, int np, int ne, const int *tetv, int tstride, const int *adja, int astride,
+                       int cap, int *nt_out, int *triv, int *adjt, char *msg, size_t msglen);

@@ -166,6 +166,30 @@ class TransferContext:
         self._ck(self.lib.pmmg_hip_set_background_tet8(self.h, npt, _p(xyz), ne, _p(tet8), nt, _p(triv), _p(adjt),
                                                        float(hausd), where), "set_background_tet8")
 
+    # ------------------------------------------------------------------ background snapshot
+    def build_adjacency(self, npt: int, tetv: DeviceArray, adja: bool = True, tet8: bool = True):
+        """Device-side MMG3D_hashTetra: (adja, tet8) DeviceArrays (None when not requested)."""
+        ne = tetv.shape[0]
+        a = self.empty((ne, 4), np.int32) if adja else None
+        t = self.empty((ne, 8), np.int32) if tet8 else None
+        self._ck(self.lib.pmmg_hip_build_adjacency(self.h, int(npt), ne, _p(tetv), _p(a), _p(t)), "build_adjacency")
+        return a, t
+
+    def build_boundary(self, npt: int, tet8: DeviceArray | None = None, tetv: DeviceArray | None = None,
+                       adja: DeviceArray | None = None, adjt: bool = True):
+        """Device-side MMG5_chkBdryTria + MMG3D_hashTria: (triv, adjt) DeviceArrays of nt rows."""
+        ne = (tet8 if tet8 is not None else tetv).shape[0]
+        nt = ctypes.c_int(0)
+        # capacity 0: the call only counts (it fails when there are trias, with nt set)
+        self.lib.pmmg_hip_build_boundary(self.h, int(npt), ne, _p(tet8), _p(tetv), _p(adja), 0, ctypes.byref(nt),
+                                         None, None)
+        n = nt.value
+        triv = self.empty((n, 3), np.int32)
+        at = self.empty((n, 3), np.int32) if adjt else None
+        self._ck(self.lib.pmmg_hip_build_boundary(self.h, int(npt), ne, _p(tet8), _p(tetv), _p(adja), n,
+                                                  ctypes.byref(nt), _p(triv), _p(at)), "build_boundary")
+        return triv, at
+
     def set_solutions(self, met, fields) -> None:
         fields = list(fields)
         where = DEVICE if (isinstance(met, DeviceArray) or (fields and isinstance(fields[0], DeviceArray))) else HOST

@@ -1,0 +1,117 @@
+"""Background snapshot on the device (pmmg_hip_build_adjacency /
+pmmg_hip_build_boundary; reference PMMG_create_oldGrp, src/grpsplit_pmmg.c:207-418,
+with Mmg's MMG3D_hashTetra / MMG5_chkBdryTria / MMG3D_hashTria).
+
+The checker is the host builder of the synthetic meshes (pmmg_synth.c: tetra
+adjacency analytic from the lattice, boundary trias and their adjacency by
+sorted edge matching), which restates the same Mmg conventions independently
+of the GPU's bucket hashing.  Results must be bit-identical.  Mmg itself is not
+in the image, so the conventions are restated, not pinned.
+"""
+import numpy as np
+import pytest
+
+from parity import make_case, run_gpu
+from parmmg_amd import synth
+from parmmg_amd.transfer import TransferContext, pack_tet8
+
+
+def _snapshot(ctx, bg, use_tet8=True):
+    tetv = ctx.upload(bg.tetv)
+    adja, tet8 = ctx.build_adjacency(bg.np, tetv)
+    if use_tet8:
+        triv, adjt = ctx.build_boundary(bg.np, tet8=tet8)
+    else:
+        triv, adjt = ctx.build_boundary(bg.np, tetv=tetv, adja=adja)
+    return tetv, adja, tet8, triv, adjt
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,n", [(synth.CUBE, 1), (synth.CUBE, 5), (synth.SHELL, 8), (synth.SHELL, 12),
+                                    (synth.CUBE, 40)])
+@pytest.mark.parametrize("use_tet8", [True, False])
+def test_snapshot_matches_host_builder(kind, n, use_tet8):
+    bg = synth.lattice(kind, n)
+    with TransferContext(0) as ctx:
+        _, adja, tet8, triv, adjt = _snapshot(ctx, bg, use_tet8)
+        np.testing.assert_array_equal(adja.download(), bg.adja)
+        np.testing.assert_array_equal(tet8.download(), pack_tet8(bg.tetv, bg.adja))
+        assert triv.shape[0] == bg.nt
+        np.testing.assert_array_equal(triv.download(), bg.triv)
+        np.testing.assert_array_equal(adjt.download(), bg.adjt)
+
+
+@pytest.mark.gpu
+def test_snapshot_of_a_shuffled_numbering():
+    """Tetra order and vertex numbering are arbitrary: the adjacency of a
+    permuted mesh is the permuted adjacency."""
+    bg = synth.lattice(synth.SHELL, 8)
+    rng = np.random.default_rng(7)
+    pe = rng.permutation(bg.ne)          # new tetra j = old tetra pe[j]
+    pv = rng.permutation(bg.np) + 1      # old vertex v -> new id pv[v-1]
+    tetv = pv[bg.tetv[pe] - 1].astype(np.int32)
+    inv = np.empty_like(pe)
+    inv[pe] = np.arange(bg.ne)
+    old = bg.adja[pe]
+    k_old, i_old = old // 4, old % 4
+    expect = np.where(old > 0, 4 * (inv[np.maximum(k_old - 1, 0)] + 1) + i_old, 0).astype(np.int32)
+    with TransferContext(0) as ctx:
+        adja, _ = ctx.build_adjacency(bg.np, ctx.upload(np.ascontiguousarray(tetv)), tet8=False)
+        np.testing.assert_array_equal(adja.download(), expect)
+
+
+@pytest.mark.gpu
+def test_snapshot_rejects_invalid_connectivity():
+    bg = synth.lattice(synth.CUBE, 2)
+    with TransferContext(0) as ctx:
+        bad = bg.tetv.copy()
+        bad[3, 2] = bg.np + 5  # id out of range
+        with pytest.raises(RuntimeError, match="vertex ids"):
+            ctx.build_adjacency(bg.np, ctx.upload(bad))
+        bad = bg.tetv.copy()
+        bad[0, 1] = bad[0, 0]  # repeated id
+        with pytest.raises(RuntimeError, match="vertex ids"):
+            ctx.build_adjacency(bg.np, ctx.upload(bad))
+        # a third tetra on an interior face: non-manifold
+        k = int(np.nonzero((bg.adja > 0).all(axis=1))[0][0]) if (bg.adja > 0).all(axis=1).any() else 0
+        extra = np.concatenate([bg.tetv, bg.tetv[k:k + 1, [1, 0, 2, 3]]]).astype(np.int32)
+        with pytest.raises(RuntimeError, match="more than two"):
+            ctx.build_adjacency(bg.np, ctx.upload(np.ascontiguousarray(extra)))
+
+
+@pytest.mark.gpu
+def test_transfer_on_device_snapshot_is_identical():
+    """Locate + interpolate against the device-built background gives the
+    same outputs bit for bit as against the host-built arrays."""
+    case = make_case(kind=synth.SHELL, n_old=12, n_new=16, with_ref=False)
+    ref = run_gpu(case)
+    bg = case["bg"]
+    with TransferContext(0) as ctx:
+        xyz = ctx.upload(bg.xyz)
+        _, _, tet8, triv, adjt = _snapshot(ctx, bg)
+        ctx.set_background_tet8(xyz, tet8, triv, adjt, case["hausd"])
+        met = ctx.upload(case["met"])
+        fields = [ctx.upload(f) for f in case["fields"]]
+        ctx.set_solutions(met, fields)
+        q, pc = ctx.upload(case["new"].xyz), ctx.upload(case["pclass"])
+        mo = ctx.upload(np.full((q.shape[0], case["met"].shape[1]), np.nan))
+        fo = [ctx.upload(np.full((q.shape[0], f.shape[1]), np.nan)) for f in case["fields"]]
+        el, hit = ctx.empty((q.shape[0],), np.int32), ctx.empty((q.shape[0],), np.int8)
+        ctx.locate_interp(q, pc, mo, fo, el, hit)
+        np.testing.assert_array_equal(el.download(), ref["elem"])
+        np.testing.assert_array_equal(hit.download(), ref["hit"])
+        np.testing.assert_array_equal(mo.download(), ref["met"])
+        for a, b in zip(fo, ref["fields"]):
+            np.testing.assert_array_equal(a.download(), b)
+
+
+@pytest.mark.gpu
+def test_snapshot_full_size_cfg3():
+    """cfg3 background (20.25M tetra, 3.4M vertices): bit-exact against the
+    host builder."""
+    bg = synth.lattice(synth.CUBE, 150)
+    with TransferContext(0) as ctx:
+        _, adja, tet8, triv, adjt = _snapshot(ctx, bg)
+        assert np.array_equal(adja.download(), bg.adja)
+        assert np.array_equal(triv.download(), bg.triv)
+        assert np.array_equal(adjt.download(), bg.adjt)
