@@ -68,13 +68,18 @@ __global__ __launch_bounds__(kBlock) void k_reset(Frame *fr, DevStats *st, unsig
   for (long long j = tid; j < ncnt; j += nth) cnt[j] = 0;
 }
 
-__global__ __launch_bounds__(kBlock) void k_bbox(const double *xyz, int np, Frame *fr) {
+// bbox of every `stride`-th vertex (and the last one): the frame only sizes
+// the seed / bin grids, whose cell lookups clamp, so a sampled bbox costs at
+// most slightly longer walks for the few points outside it
+__global__ __launch_bounds__(kBlock) void k_bbox(const double *xyz, int np, Frame *fr, int stride) {
   __shared__ unsigned long long slo[3][kBlock / 64], shi[3][kBlock / 64];
   unsigned long long lo[3] = {~0ULL, ~0ULL, ~0ULL}, hi[3] = {0ULL, 0ULL, 0ULL};
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < np; i += gridDim.x * blockDim.x) {
+  const long long ns = ((long long)np + stride - 1) / stride + 1;
+  for (long long j = blockIdx.x * blockDim.x + threadIdx.x; j < ns; j += gridDim.x * blockDim.x) {
+    const long long i = j * stride < np ? j * stride : np - 1;
 #pragma unroll
     for (int d = 0; d < 3; d++) {
-      unsigned long long k = dkey(xyz[3 * (size_t)i + d]);
+      unsigned long long k = dkey(xyz[3 * i + d]);
       lo[d] = k < lo[d] ? k : lo[d];
       hi[d] = k > hi[d] ? k : hi[d];
     }
@@ -1629,6 +1634,7 @@ struct pmmg_hip_ctx {
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr; // surface branch, concurrent with the volume walk
   hipStream_t stream3 = nullptr; // volume interpolation of chunk c, concurrent with the walk of chunk c+1
+  int bbox_stride = 16; // frame from every 16th background vertex (PMMG_HIP_BBOXSTRIDE)
   int chunks = 3;                // volume pipeline chunks (PMMG_HIP_CHUNKS)
   hipEvent_t evc[kMaxChunks] = {};
   bool bdy_on_s2 = false;
@@ -1776,6 +1782,7 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   c->maxstep = env_int("PMMG_HIP_MAXSTEP", c->maxstep);
   c->cap = env_int("PMMG_HIP_CAP", c->cap);
   c->chunks = env_int("PMMG_HIP_CHUNKS", c->chunks);
+  c->bbox_stride = env_int("PMMG_HIP_BBOXSTRIDE", c->bbox_stride);
   if (c->chunks > kMaxChunks) c->chunks = kMaxChunks;
   {
     hipDeviceProp_t prop;
@@ -2068,7 +2075,8 @@ static int run_scan(pmmg_hip_ctx *c, const Slots &S, int np_new, const double *x
   const long long nsg = bg.nt > 0 ? (long long)gs * gs * gs : 0;
   hipLaunchKernelGGL(k_reset, dim3(blocks_for(ncells + 1 > nsg ? ncells + 1 : nsg, 2048)), dim3(kBlock), 0, s, fr, st,
                      (unsigned long long *)nullptr, 0LL, sgrid, nsg, (int *)c->cnt.p, ncells + 1, 0);
-  hipLaunchKernelGGL(k_bbox, dim3(blocks_for(bg.np, 1024)), dim3(kBlock), 0, s, bg.xyz, bg.np, fr);
+  hipLaunchKernelGGL(k_bbox, dim3(blocks_for(bg.np / c->bbox_stride + 1, 1024)), dim3(kBlock), 0, s, bg.xyz, bg.np, fr,
+                     c->bbox_stride);
   hipLaunchKernelGGL(k_frame_final, dim3(1), dim3(1), 0, s, fr, 1, gs, gq);
   if (bg.nt > 0) hipLaunchKernelGGL(k_seed_srf, dim3(blocks_for(bg.nt, 4096)), dim3(kBlock), 0, s, bg, fr, sgrid, gs);
   HIPCK(c, hipGetLastError());
@@ -2171,7 +2179,8 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   const long long ng = (long long)g * g * g, nsg = bg.nt > 0 ? (long long)gs * gs * gs : 0;
   hipLaunchKernelGGL(k_reset, dim3(blocks_for(ng, 2048)), dim3(kBlock), 0, s, fr, st, grid, ng, sgrid, nsg,
                      sorted ? (int *)c->cnt.p : nullptr, sorted ? 2LL * nbins : 0LL, 1);
-  hipLaunchKernelGGL(k_bbox, dim3(blocks_for(bg.np, 1024)), dim3(kBlock), 0, s, bg.xyz, bg.np, fr);
+  hipLaunchKernelGGL(k_bbox, dim3(blocks_for(bg.np / c->bbox_stride + 1, 1024)), dim3(kBlock), 0, s, bg.xyz, bg.np, fr,
+                     c->bbox_stride);
   hipLaunchKernelGGL(k_frame_final, dim3(1), dim3(1), 0, s, fr, g, gs, gb);
   // The surface branch (tria seeds, surface list, k_bdy) only needs the
   // frame: on the input-order path it runs on a second stream, concurrently
