@@ -100,6 +100,33 @@ def cpu_baseline(w, bg, new, met, fields, pclass, budget_s: float):
     }
 
 
+def allgather_timing(ri, d_mo, d_fo, d_elem, counts, mine, rank: int, reps: int = 3):
+    """Morton mode: collect every rank's located elements and interpolated
+    rows on every rank (ranks.allgather_rows: RCCL all_gather_into_tensor over
+    xGMI), timed on its own after the timed steps (reported
+    separately; ParMmg itself consumes the results per rank).  Checks that the
+    gathered element ids cover every processed point."""
+    import torch
+
+    rows = torch.cat([d_mo] + list(d_fo), dim=1)
+    elem = d_elem.view(-1, 1)
+    times = []
+    for _ in range(reps):
+        ranks.barrier(ri)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        g_rows = ranks.allgather_rows(ri, rows, counts)
+        g_elem = ranks.allgather_rows(ri, elem, counts)
+        torch.cuda.synchronize()
+        times.append(ranks.max_over_ranks(ri, time.perf_counter() - t0))
+    ok = bool((g_elem > 0).all().item()) and g_rows.shape[0] == sum(counts)
+    nbytes = sum(counts) * (rows.shape[1] * 8 + 4)
+    t = float(np.median(times))
+    log(f"[bench r{rank}] all-gather of {nbytes / 1e9:.2f} GB: {1e3 * t:.2f} ms, complete={ok}")
+    return {"what": "RCCL all-gather of {elem, K doubles} per point, not part of the step",
+            "ms": round(1e3 * t, 3), "bytes": int(nbytes), "gbps": round(nbytes / t / 1e9, 1), "complete": ok}
+
+
 def snapshot_timing(ctx, bg, rank: int, reps: int = 3):
     """Device background snapshot (PMMG_create_oldGrp's
     adjacency / boundary trias / tria adjacency, pmmg_hip_build_*) timed on
@@ -153,6 +180,10 @@ def main():
                     help="HBM layout of the metric/fields: packed per-vertex records or one array per solution")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--shard", default="group", choices=["group", "morton"],
+                    help="multi-GPU split: one group per rank (weak scaling, ParMmg's own sharding) or one problem "
+                         "cut into contiguous Morton ranges of the new points, background replicated, results "
+                         "all-gathered over RCCL after the timed steps (strong scaling, SURVEY.md 8(e))")
     ap.add_argument("--no-snapshot", action="store_true",
                     help="skip the (separately reported) device background snapshot timing")
     args = ap.parse_args()
@@ -161,7 +192,19 @@ def main():
     rank, world, local = ri.rank, ri.world, ri.local
 
     w = configs.SHORT[args.config]
-    bg, new, met, fields, pclass = build_workload(w, rank)
+    morton = args.shard == "morton"
+    # Morton mode: every rank builds the same problem and keeps its range
+    bg, new, met, fields, pclass = build_workload(w, 0 if morton else rank)
+    mine = None
+    if morton:
+        shards = ranks.morton_shards(new.xyz, pclass, world)
+        mine = shards[rank]
+        counts = [len(x) for x in shards]
+        q_xyz, q_pc = np.ascontiguousarray(new.xyz[mine]), np.ascontiguousarray(pclass[mine])
+        log(f"[bench r{rank}] Morton range {len(mine)} of {int((pclass != 0).sum())} points")
+    else:
+        q_xyz, q_pc = new.xyz, pclass
+    nq = q_xyz.shape[0]
 
     for name in ("tpc", "spc"):
         if getattr(args, name) > 0:
@@ -182,11 +225,19 @@ def main():
     else:
         d_met = ctx.upload(met)
         d_f = [ctx.upload(f) for f in fields]
-    d_qxyz, d_pc = ctx.upload(new.xyz), ctx.upload(pclass)
-    d_mo = ctx.empty((new.np, w.met_size), np.float64)
-    d_fo = [ctx.empty((new.np, f.shape[1]), np.float64) for f in fields]
-    d_elem = ctx.empty((new.np,), np.int32)
-    d_hit = ctx.empty((new.np,), np.int8)
+    d_qxyz, d_pc = ctx.upload(q_xyz), ctx.upload(q_pc)
+    if morton:
+        # outputs as torch tensors in HBM: the all-gather reads them in place
+        import torch
+        dev = torch.device("cuda", local)
+        d_mo = torch.empty((nq, w.met_size), dtype=torch.float64, device=dev)
+        d_fo = [torch.empty((nq, f.shape[1]), dtype=torch.float64, device=dev) for f in fields]
+        d_elem = torch.empty((nq,), dtype=torch.int32, device=dev)
+    else:
+        d_mo = ctx.empty((nq, w.met_size), np.float64)
+        d_fo = [ctx.empty((nq, f.shape[1]), np.float64) for f in fields]
+        d_elem = ctx.empty((nq,), np.int32)
+    d_hit = ctx.empty((nq,), np.int8)
 
     def step():
         if args.layout == "tet8":
@@ -223,6 +274,10 @@ def main():
 
     npts = int(st.nvol + st.nbdy)
     agg = ranks.aggregate(ri, npts, elapsed, args.steps)
+    gather = None
+    if morton:
+        gather = allgather_timing(ri, d_mo, d_fo, d_elem, counts, mine, rank)
+        npts = agg["points_per_step"]  # the whole problem: bytes per point below are per problem point
     ms_per_step = agg["ms_per_step"]
     value = agg["mpts_per_s"]
     (np_o, ne_o, _), (np_n, _, _) = w.counts()
@@ -241,7 +296,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if morton else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (Kuhn lattices, analytic metric/fields, splitmix64 jitter)",
@@ -250,7 +305,8 @@ def main():
             "description": w.description,
             "background_tets": ne_o, "background_verts": np_o, "new_points": np_n,
             "located_points_per_gpu": npts, "K_doubles_per_vertex": w.K,
-            "parallelism": f"one group per GPU x{world} (weak, no data-path collective)",
+            "parallelism": (f"Morton-range shards x{world}, replicated background, RCCL all-gather after the step"
+                            if morton else f"one group per GPU x{world} (weak, no data-path collective)"),
             "query_order": args.sort,
             "locate": args.locate,
             "tetra_layout": args.layout,
@@ -278,6 +334,8 @@ def main():
             "algorithmic_bytes_per_point": round(per_pt, 2),
         },
     }
+    if gather is not None:
+        out["allgather"] = gather
     if not args.no_snapshot:
         out["snapshot"] = snapshot_timing(ctx, bg, rank)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

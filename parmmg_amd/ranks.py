@@ -85,3 +85,64 @@ def aggregate(ri: RankInfo, points_this_rank: int, elapsed_s: float, steps: int)
     pts = sum_over_ranks(ri, points_this_rank)
     return {"elapsed_s": t, "points_per_step": int(pts), "ms_per_step": t / steps * 1e3,
             "mpts_per_s": pts / (t / steps) / 1e6}
+
+
+# ---------------------------------------------------------------- Morton-range sharding
+#
+# one transfer problem split over the GPUs of a node, each
+# GPU owning a contiguous Morton range of the new points (balanced by count)
+# against a replicated background; the located elements and interpolated rows
+# are then collected with an all-gather (RCCL over xGMI on the GPU box, gloo
+# in the CPU tests).  This is the strong-scaling alternative to the
+# one-group-per-rank default above.
+
+def _expand10(v):
+    import numpy as np
+
+    v = v.astype(np.uint32) & np.uint32(0x3FF)
+    v = (v | (v << np.uint32(16))) & np.uint32(0x030000FF)
+    v = (v | (v << np.uint32(8))) & np.uint32(0x0300F00F)
+    v = (v | (v << np.uint32(4))) & np.uint32(0x030C30C3)
+    v = (v | (v << np.uint32(2))) & np.uint32(0x09249249)
+    return v
+
+
+def morton_codes(xyz):
+    """30-bit Morton codes of points (10 bits per axis over their bbox)."""
+    import numpy as np
+
+    lo, hi = xyz.min(axis=0), xyz.max(axis=0)
+    ext = np.where(hi > lo, hi - lo, 1.0)
+    q = np.clip(((xyz - lo) / ext * 1024.0).astype(np.int64), 0, 1023)
+    return (_expand10(q[:, 0]) << np.uint32(2)) | (_expand10(q[:, 1]) << np.uint32(1)) | _expand10(q[:, 2])
+
+
+def morton_shards(xyz, pclass, world: int):
+    """0-based point indices of each rank: the processed points (pclass != 0)
+    in Morton order (stable), cut into `world` contiguous ranges whose sizes
+    differ by at most one.  Skipped points (MG_REQ, copied by the host) are
+    in no shard."""
+    import numpy as np
+
+    idx = np.nonzero(pclass != 0)[0]
+    order = idx[np.argsort(morton_codes(xyz[idx]), kind="stable")]
+    cuts = [len(order) * r // world for r in range(world + 1)]
+    return [order[cuts[r]:cuts[r + 1]] for r in range(world)]
+
+
+def allgather_rows(ri: RankInfo, rows, counts):
+    """All-gather of per-rank row blocks (torch tensors [n_r, C], same dtype
+    and C on every rank; counts[r] = n_r): padded to the largest block, one
+    all_gather_into_tensor, trimmed; returns the blocks concatenated in rank
+    order.  Single process: the rows themselves."""
+    if not ri.distributed:
+        return rows
+    import torch
+    import torch.distributed as dist
+
+    m = max(counts)
+    pad = torch.zeros((m,) + tuple(rows.shape[1:]), dtype=rows.dtype, device=rows.device)
+    pad[: rows.shape[0]] = rows
+    out = torch.empty((ri.world * m,) + tuple(rows.shape[1:]), dtype=rows.dtype, device=rows.device)
+    dist.all_gather_into_tensor(out, pad)
+    return torch.cat([out[r * m: r * m + counts[r]] for r in range(ri.world)])

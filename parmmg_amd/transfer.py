@@ -33,9 +33,17 @@ def _p(a):
         return None
     if isinstance(a, DeviceArray):
         return ctypes.c_void_p(a.ptr)
+    if getattr(a, "is_cuda", False):  # torch tensor in HBM (e.g. an all-gather buffer)
+        if not a.is_contiguous():
+            raise ValueError("device tensors passed to the C-ABI must be contiguous")
+        return ctypes.c_void_p(a.data_ptr())
     if not a.flags["C_CONTIGUOUS"]:
         raise ValueError("arrays passed to the C-ABI must be C-contiguous")
     return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _is_dev(a) -> bool:
+    return isinstance(a, DeviceArray) or bool(getattr(a, "is_cuda", False))
 
 
 @dataclass
@@ -150,7 +158,7 @@ class TransferContext:
 
     # ------------------------------------------------------------------ C-ABI
     def set_background(self, xyz, tetv, adja, triv, adjt, hausd: float) -> None:
-        where = DEVICE if isinstance(xyz, DeviceArray) else HOST
+        where = DEVICE if _is_dev(xyz) else HOST
         npt, ne, nt = xyz.shape[0], tetv.shape[0], triv.shape[0]
         self._keep = [xyz, tetv, adja, triv, adjt]
         self._ck(self.lib.pmmg_hip_set_background(self.h, npt, _p(xyz), ne, _p(tetv), _p(adja), nt, _p(triv),
@@ -158,7 +166,7 @@ class TransferContext:
 
     def set_background_tet8(self, xyz, tet8, triv, adjt, hausd: float) -> None:
         """Background with packed {v[4], adja[4]} tetra records (pack_tet8)."""
-        where = DEVICE if isinstance(xyz, DeviceArray) else HOST
+        where = DEVICE if _is_dev(xyz) else HOST
         npt, ne, nt = xyz.shape[0], tet8.shape[0], triv.shape[0]
         if tet8.shape[1] != 8:
             raise ValueError("tet8 must have 8 ints per tetra")
@@ -192,7 +200,7 @@ class TransferContext:
 
     def set_solutions(self, met, fields) -> None:
         fields = list(fields)
-        where = DEVICE if (isinstance(met, DeviceArray) or (fields and isinstance(fields[0], DeviceArray))) else HOST
+        where = DEVICE if (_is_dev(met) or (fields and _is_dev(fields[0]))) else HOST
         msize = 0 if met is None else int(met.shape[1])
         sizes = (ctypes.c_int * max(1, len(fields)))(*[int(f.shape[1]) for f in fields])
         ptrs = (ctypes.c_void_p * max(1, len(fields)))(*[_p(f) for f in fields])
@@ -202,7 +210,7 @@ class TransferContext:
 
     def set_solutions_packed(self, rec, met_size: int, met_off: int, field_sizes, field_offs) -> None:
         """Solutions as packed per-vertex records (pack_solutions)."""
-        where = DEVICE if isinstance(rec, DeviceArray) else HOST
+        where = DEVICE if _is_dev(rec) else HOST
         nf = len(field_sizes)
         sizes = (ctypes.c_int * max(1, nf))(*[int(x) for x in field_sizes])
         offs = (ctypes.c_int * max(1, nf))(*[int(x) for x in field_offs])
@@ -212,7 +220,7 @@ class TransferContext:
 
     def locate_interp(self, xyz_new, pclass, met_out, fields_out, elem_out=None, hit_out=None,
                       sync: bool = True) -> HipStats | None:
-        where = DEVICE if isinstance(xyz_new, DeviceArray) else HOST
+        where = DEVICE if _is_dev(xyz_new) else HOST
         fields_out = list(fields_out)
         ptrs = (ctypes.c_void_p * max(1, len(fields_out)))(*[_p(f) for f in fields_out])
         st = HipStats()

@@ -70,3 +70,55 @@ def test_bench_configs_fit_one_gpu():
         (np_o, ne_o, nt_o), (np_n, _, _) = w.counts()
         b = np_o * (24 + 8 * w.K) + ne_o * 32 + nt_o * 24 + np_n * (24 + 1 + 8 * w.K + 4 + 1)
         assert b < 200e9, (w.name, b)
+
+
+def test_morton_shards_partition_and_locality():
+    new = synth.lattice(synth.CUBE, 12, jitter=0.2, with_trias=False)
+    pclass = synth.classes(new, req_every=7)
+    for world in (1, 2, 3, 8):
+        sh = ranks.morton_shards(new.xyz, pclass, world)
+        allidx = np.concatenate(sh)
+        assert sorted(allidx.tolist()) == np.nonzero(pclass != 0)[0].tolist()  # every processed point once
+        sizes = [len(s) for s in sh]
+        assert max(sizes) - min(sizes) <= 1
+        codes = ranks.morton_codes(new.xyz[np.nonzero(pclass != 0)[0]])
+        cmin = [int(ranks.morton_codes(new.xyz)[s].min()) for s in sh]
+        assert cmin == sorted(cmin)  # contiguous Morton ranges in rank order
+        assert codes.dtype == np.uint32
+
+
+def _gather_worker(rank, world, port, q):
+    import torch
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    ri = ranks.init("gloo")
+    new = synth.lattice(synth.SHELL, 8, jitter=0.2, with_trias=False)  # same problem on every rank
+    pclass = synth.classes(new)
+    sh = ranks.morton_shards(new.xyz, pclass, world)
+    mine = sh[rank]
+    # stand-in for this rank's interpolated rows: a function of the point
+    rows = torch.from_numpy(np.concatenate([new.xyz[mine], mine[:, None].astype(np.float64)], axis=1))
+    got = ranks.allgather_rows(ri, rows, [len(s) for s in sh]).numpy()
+    q.put((rank, got))
+    ranks.finalize(ri)
+
+
+def test_gloo_two_ranks_morton_allgather():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    new = synth.lattice(synth.SHELL, 8, jitter=0.2, with_trias=False)
+    pclass = synth.classes(new)
+    order = np.concatenate(ranks.morton_shards(new.xyz, pclass, world))
+    for r in range(world):
+        got = out[r]
+        np.testing.assert_array_equal(got[:, 3].astype(np.int64), order)  # rank-order blocks
+        np.testing.assert_array_equal(got[:, :3], new.xyz[order])
