@@ -61,7 +61,7 @@ def pmc_traffic(workload: str):
     try:
         with open(paths[-1]) as f:
             d = json.load(f)
-        return d.get("k_vol_hbm_bytes_per_launch"), os.path.relpath(paths[-1], ROOT)
+        return d.get("k_vol_hbm_bytes_per_call", d.get("k_vol_hbm_bytes_per_launch")), os.path.relpath(paths[-1], ROOT)
     except Exception:
         return None, None
 
@@ -328,9 +328,13 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "traffic_unit": "bytes per launch (FETCH_SIZE x2 + WRITE_SIZE)",
+            "traffic_unit": "bytes per volume stage = all walk + interpolation launches of one call "
+                            "(FETCH_SIZE x2 + WRITE_SIZE)",
             "traffic_source": traffic_src,
-            "algorithmic_bytes_per_launch": round(kvol_bytes),
+            "algorithmic_bytes_per_stage": round(kvol_bytes),
+            "stage": "volume stage of one transfer call: the walk and interpolation launches of its query chunks "
+                     "(overlapping on two streams), timed by HIP events from the first walk to the last "
+                     "interpolation",
             "algorithmic_bytes_per_point": round(per_pt, 2),
         },
     }

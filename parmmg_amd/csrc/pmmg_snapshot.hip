@@ -53,58 +53,108 @@ __device__ __forceinline__ void face_ids(const int4 &t, int i, int &a, int &b, i
 // error bits
 constexpr int kErrIds = 1, kErrNonManifold = 2;
 
-__global__ __launch_bounds__(kB) void k_face_count(const int4 *tetv, int ne, int np, int *cnt, int *rank,
-                                                   int *err) {
-  const long long f = blockIdx.x * (long long)kB + threadIdx.x;
-  if (f >= 4LL * ne) return;
-  const int4 t = tetv[f >> 2];
-  int a, b, c;
-  face_ids(t, (int)(f & 3), a, b, c);
-  if (a < 1 || c > np || a == b || b == c) {
-    atomicOr(err, kErrIds);
-    rank[f] = -1;
-    return;
+// The faces of a tetra whose sorted vertices are s0 < s1 < s2 < s3: the
+// three faces containing s0 (opposite s1, s2, s3) share the bucket of s0, the
+// face opposite s0 is in the bucket of s1.  One atomic reserves the three
+// slots in s0's bucket, one the slot in s1's; one scan of s0's bucket serves
+// all three faces in the match.
+
+// local index (0..3) of the smallest and second smallest vertex of a tetra
+__device__ __forceinline__ void two_smallest(const int4 &t, int &i0, int &i1) {
+  int v[4] = {t.x, t.y, t.z, t.w};
+  i0 = 0;
+#pragma unroll
+  for (int i = 1; i < 4; i++) i0 = v[i] < v[i0] ? i : i0;
+  i1 = i0 == 0 ? 1 : 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) i1 = (i != i0 && v[i] < v[i1]) ? i : i1;
+}
+
+__device__ __forceinline__ bool tet_ids_ok(const int4 &t, int np) {
+  const int v[4] = {t.x, t.y, t.z, t.w};
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    ok = ok && v[i] >= 1 && v[i] <= np;
+#pragma unroll
+    for (int j = i + 1; j < 4; j++) ok = ok && v[i] != v[j];
   }
-  rank[f] = atomicAdd(&cnt[a - 1], 1);
+  return ok;
 }
 
-__global__ __launch_bounds__(kB) void k_face_scatter(const int4 *tetv, int ne, const int *off, const int *rank,
-                                                     int4 *bucket) {
-  const long long f = blockIdx.x * (long long)kB + threadIdx.x;
-  if (f >= 4LL * ne) return;
-  const int r = rank[f];
-  if (r < 0) return;
-  const int4 t = tetv[f >> 2];
-  int a, b, c;
-  face_ids(t, (int)(f & 3), a, b, c);
-  // code of this face in the reference encoding: 4*k + i with k 1-based
-  bucket[off[a - 1] + r] = make_int4(b, c, (int)(4 * ((f >> 2) + 1) + (f & 3)), 0);
-}
-
-// one thread per tetra: the 4 twins, one adjacency row (and one tet8 record)
-__global__ __launch_bounds__(kB) void k_face_match(const int4 *tetv, int ne, const int *off, const int *cnt,
-                                                   const int4 *bucket, int4 *adja, int4 *tet8, int *err) {
+// rank[k] = {slot of the s0 faces (3 consecutive), slot of the s1 face}
+__global__ __launch_bounds__(kB) void k_face_count(const int4 *tetv, int ne, int np, int *cnt, int2 *rank,
+                                                   int *err) {
   const int k = blockIdx.x * kB + threadIdx.x;
   if (k >= ne) return;
   const int4 t = tetv[k];
-  int code[4];
+  if (!tet_ids_ok(t, np)) {
+    atomicOr(err, kErrIds);
+    rank[k] = make_int2(-1, -1);
+    return;
+  }
+  int i0, i1;
+  two_smallest(t, i0, i1);
+  const int r0 = atomicAdd(&cnt[sel(t, i0) - 1], 3);
+  const int r1 = atomicAdd(&cnt[sel(t, i1) - 1], 1);
+  rank[k] = make_int2(r0, r1);
+}
+
+__global__ __launch_bounds__(kB) void k_face_scatter(const int4 *tetv, int ne, const int *off, const int2 *rank,
+                                                     int4 *bucket) {
+  const int k = blockIdx.x * kB + threadIdx.x;
+  if (k >= ne) return;
+  const int2 r = rank[k];
+  if (r.x < 0) return;
+  const int4 t = tetv[k];
+  int i0, i1;
+  two_smallest(t, i0, i1);
+  int n = 0;
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     int a, b, c;
     face_ids(t, i, a, b, c);
-    code[i] = 0;
-    if (a < 1) continue; // flagged by k_face_count
-    const int self = 4 * (k + 1) + i;
-    const int lo = off[a - 1], n = cnt[a - 1];
-    int found = 0;
-    for (int j = 0; j < n; j++) {
-      const int4 e = bucket[lo + j];
-      if (e.x == b && e.y == c && e.z != self) {
-        if (!found) code[i] = e.z;
-        found++;
+    // code of this face in the reference encoding: 4*k + i with k 1-based
+    const int4 e = make_int4(b, c, 4 * (k + 1) + i, 0);
+    if (i == i0) bucket[off[a - 1] + r.y] = e; // face opposite s0: bucket of s1
+    else bucket[off[a - 1] + r.x + n++] = e;
+  }
+}
+
+// one thread per tetra: the 4 twins, one adjacency row (and one tet8 record)
+__global__ __launch_bounds__(kB) void k_face_match(const int4 *tetv, int ne, int np, const int *off, const int *cnt,
+                                                   const int4 *bucket, int4 *adja, int4 *tet8, int *err) {
+  const int k = blockIdx.x * kB + threadIdx.x;
+  if (k >= ne) return;
+  const int4 t = tetv[k];
+  int code[4] = {0, 0, 0, 0};
+  if (tet_ids_ok(t, np)) { // invalid tetra were flagged by k_face_count
+    int i0, i1;
+    two_smallest(t, i0, i1);
+    int fb[4], fc[4], found[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      int a;
+      face_ids(t, i, a, fb[i], fc[i]);
+    }
+    // bucket of s0: the three faces other than i0; bucket of s1: face i0
+#pragma unroll
+    for (int pass = 0; pass < 2; pass++) {
+      const int v = pass == 0 ? sel(t, i0) : sel(t, i1);
+      const int lo = off[v - 1], n = cnt[v - 1];
+      for (int j = 0; j < n; j++) {
+        const int4 e = bucket[lo + j];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          if ((i == i0) != (pass == 1)) continue;
+          if (e.x == fb[i] && e.y == fc[i] && e.z != 4 * (k + 1) + i) {
+            if (!found[i]) code[i] = e.z;
+            found[i]++;
+          }
+        }
       }
     }
-    if (found > 1) atomicOr(err, kErrNonManifold);
+    if (found[0] > 1 || found[1] > 1 || found[2] > 1 || found[3] > 1) atomicOr(err, kErrNonManifold);
   }
   const int4 row = make_int4(code[0], code[1], code[2], code[3]);
   if (adja) adja[k] = row;
@@ -239,8 +289,8 @@ int pmmg_snap_adjacency(hipStream_t s, int np, int ne, const int *tetv, int *adj
                         size_t msglen) {
   Scratch S;
   const long long nf = 4LL * ne;
-  int *cnt = S.get<int>((size_t)np), *off = S.get<int>((size_t)np), *rank = S.get<int>((size_t)nf),
-      *err = S.get<int>(1);
+  int *cnt = S.get<int>((size_t)np), *off = S.get<int>((size_t)np), *err = S.get<int>(1);
+  int2 *rank = S.get<int2>((size_t)ne);
   int4 *bucket = S.get<int4>((size_t)nf);
   if (!cnt || !off || !rank || !err || !bucket) {
     snprintf(msg, msglen, "build_adjacency: out of device memory (%lld faces)", nf);
@@ -249,10 +299,10 @@ int pmmg_snap_adjacency(hipStream_t s, int np, int ne, const int *tetv, int *adj
   SCK(hipMemsetAsync(cnt, 0, sizeof(int) * (size_t)np, s));
   SCK(hipMemsetAsync(err, 0, sizeof(int), s));
   const int4 *tv = reinterpret_cast<const int4 *>(tetv);
-  hipLaunchKernelGGL(k_face_count, dim3(blocks(nf)), dim3(kB), 0, s, tv, ne, np, cnt, rank, err);
+  hipLaunchKernelGGL(k_face_count, dim3(blocks(ne)), dim3(kB), 0, s, tv, ne, np, cnt, rank, err);
   if (!exclusive_scan(S, cnt, off, np, s, msg, msglen)) return 0;
-  hipLaunchKernelGGL(k_face_scatter, dim3(blocks(nf)), dim3(kB), 0, s, tv, ne, off, rank, bucket);
-  hipLaunchKernelGGL(k_face_match, dim3(blocks(ne)), dim3(kB), 0, s, tv, ne, off, cnt, bucket,
+  hipLaunchKernelGGL(k_face_scatter, dim3(blocks(ne)), dim3(kB), 0, s, tv, ne, off, rank, bucket);
+  hipLaunchKernelGGL(k_face_match, dim3(blocks(ne)), dim3(kB), 0, s, tv, ne, np, off, cnt, bucket,
                      reinterpret_cast<int4 *>(adja), reinterpret_cast<int4 *>(tet8), err);
   SCK(hipGetLastError());
   int h_err = 0;
