@@ -64,6 +64,7 @@ struct Frame {
   unsigned long long key_lo[3], key_hi[3];
   double lo[3], ext[3];
   double inv_vol[3], inv_srf[3], inv_bin[3];
+  int seed8; // volume seed cells hold {quantised centroid, id}; a query picks the nearest of 8 cells
 };
 
 struct DevStats {

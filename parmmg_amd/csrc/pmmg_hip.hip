@@ -108,7 +108,8 @@ __global__ __launch_bounds__(kBlock) void k_bbox(const double *xyz, int np, Fram
   }
 }
 
-__global__ void k_frame_final(Frame *fr, int g, int gs, int gb) {
+__global__ void k_frame_final(Frame *fr, int g, int gs, int gb, int seed8) {
+  fr->seed8 = seed8;
   for (int d = 0; d < 3; d++) {
     double lo = dunkey(fr->key_lo[d]), hi = dunkey(fr->key_hi[d]);
     double ext = hi - lo;
@@ -173,14 +174,31 @@ __global__ __launch_bounds__(kBlock) void k_seed_vol(Bg bg, const Frame *fr, uns
         for (int d = 0; d < 3; d++) p[d] = 0.5 * (p[d] + e[d]);
       }
       int c[3];
-      float d2 = 0.f;
-      for (int d = 0; d < 3; d++) {
-        c[d] = cell_coord(p[d], fr->lo[d], fr->inv_vol[d], g);
-        double ctr = fr->lo[d] + (c[d] + 0.5) / (fr->inv_vol[d] > 0.0 ? fr->inv_vol[d] : 1.0);
-        float dd = (float)(p[d] - ctr);
-        d2 += dd * dd;
+      if (fr->seed8) {
+        // seed8 key: {8-bit distance^2 to the cell centre (cell units),
+        // 9-bit centroid offset per axis, 29-bit id}: the cell's minimum is
+        // also what the queries decode (no pass after the sampling)
+        unsigned long long off = 0;
+        float d2 = 0.f;
+        for (int d = 0; d < 3; d++) {
+          c[d] = cell_coord(p[d], fr->lo[d], fr->inv_vol[d], g);
+          float f = (float)((p[d] - fr->lo[d]) * fr->inv_vol[d] - c[d]);
+          f = f < 0.f ? 0.f : (f > 0.999f ? 0.999f : f);
+          off |= (unsigned long long)(unsigned)(f * 512.f) << (9 * d);
+          d2 += (f - 0.5f) * (f - 0.5f);
+        }
+        const unsigned q8 = d2 * 340.f < 255.f ? (unsigned)(d2 * 340.f) : 255u;
+        key = ((unsigned long long)q8 << 56) | (off << 29) | (unsigned)k;
+      } else {
+        float d2 = 0.f;
+        for (int d = 0; d < 3; d++) {
+          c[d] = cell_coord(p[d], fr->lo[d], fr->inv_vol[d], g);
+          double ctr = fr->lo[d] + (c[d] + 0.5) / (fr->inv_vol[d] > 0.0 ? fr->inv_vol[d] : 1.0);
+          float dd = (float)(p[d] - ctr);
+          d2 += dd * dd;
+        }
+        key = ((unsigned long long)__float_as_uint(d2) << 32) | (unsigned)k;
       }
-      key = ((unsigned long long)__float_as_uint(d2) << 32) | (unsigned)k;
       ci = c[0] + (long long)g * (c[1] + (long long)g * c[2]);
     }
     // combine within the run (R lanes, R divides 64): the first lane of each
@@ -221,7 +239,10 @@ __global__ __launch_bounds__(kBlock) void k_seed_srf(Bg bg, const Frame *fr, int
 // rare path of seed_vol (empty cell): lowest seed id in the shells of
 // radius 1 then 2 around the cell; kept out of line so the walk kernels do
 // not carry its registers
-__device__ __forceinline__ int seed_vol_ring(const unsigned long long *cell, int g, int ci, int cj, int ck) {
+constexpr unsigned long long kSeedIdMask = (1ULL << 29) - 1; // seed8 keys: ids below 2^29 (the adja encoding's limit)
+
+__device__ __forceinline__ int seed_vol_ring(const unsigned long long *cell, int g, int ci, int cj, int ck,
+                                             unsigned long long idmask) {
 #pragma unroll 1
   for (int r = 1; r <= 2; r++) {
     unsigned long long best = ~0ULL;
@@ -235,7 +256,7 @@ __device__ __forceinline__ int seed_vol_ring(const unsigned long long *cell, int
           int a = ci + di, b = cj + dj, c = ck + dk;
           if (a < 0 || b < 0 || c < 0 || a >= g || b >= g || c >= g) continue;
           unsigned long long v = cell[a + (size_t)g * (b + (size_t)g * c)];
-          unsigned long long id = v & 0xFFFFFFFFULL;
+          unsigned long long id = v & idmask;
           if (v != ~0ULL && id < best) best = id;
         }
     if (best != ~0ULL) return (int)best;
@@ -244,12 +265,47 @@ __device__ __forceinline__ int seed_vol_ring(const unsigned long long *cell, int
 }
 
 __device__ __forceinline__ int seed_vol(const unsigned long long *cell, int g, const Frame *fr, const double *x) {
-  int ci = cell_coord(x[0], fr->lo[0], fr->inv_vol[0], g);
-  int cj = cell_coord(x[1], fr->lo[1], fr->inv_vol[1], g);
-  int ck = cell_coord(x[2], fr->lo[2], fr->inv_vol[2], g);
-  unsigned long long s = cell[ci + (size_t)g * (cj + (size_t)g * ck)];
-  if (s != ~0ULL) return (int)(unsigned)(s & 0xFFFFFFFFULL);
-  return seed_vol_ring(cell, g, ci, cj, ck);
+  if (!fr->seed8) {
+    int ci = cell_coord(x[0], fr->lo[0], fr->inv_vol[0], g);
+    int cj = cell_coord(x[1], fr->lo[1], fr->inv_vol[1], g);
+    int ck = cell_coord(x[2], fr->lo[2], fr->inv_vol[2], g);
+    unsigned long long s = cell[ci + (size_t)g * (cj + (size_t)g * ck)];
+    if (s != ~0ULL) return (int)(unsigned)(s & 0xFFFFFFFFULL);
+    return seed_vol_ring(cell, g, ci, cj, ck, 0xFFFFFFFFULL);
+  }
+  // the query's position in cell units; candidate cells: its own and the 7
+  // neighbours of the octant it lies in; the seed whose (quantised) centroid
+  // is nearest wins (ties: lower id)
+  double t[3];
+  int c[3], o[3];
+#pragma unroll
+  for (int d = 0; d < 3; d++) {
+    t[d] = (x[d] - fr->lo[d]) * fr->inv_vol[d];
+    c[d] = cell_coord(x[d], fr->lo[d], fr->inv_vol[d], g);
+    const double f = t[d] - c[d];
+    o[d] = f < 0.5 ? (c[d] > 0 ? -1 : 0) : (c[d] < g - 1 ? 1 : 0);
+  }
+  unsigned long long v[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const int a = c[0] + ((j & 1) ? o[0] : 0), b = c[1] + ((j & 2) ? o[1] : 0), e = c[2] + ((j & 4) ? o[2] : 0);
+    v[j] = cell[a + (size_t)g * (b + (size_t)g * e)];
+  }
+  float best = 3.4e38f;
+  unsigned bid = 0xFFFFFFFFu;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    if (v[j] == ~0ULL) continue;
+    const int a = c[0] + ((j & 1) ? o[0] : 0), b = c[1] + ((j & 2) ? o[1] : 0), e = c[2] + ((j & 4) ? o[2] : 0);
+    const unsigned q = (unsigned)((v[j] >> 29) & 0x7FFFFFFULL), id = (unsigned)(v[j] & kSeedIdMask);
+    const float dx = (float)(t[0] - a) - ((q & 511u) + 0.5f) * (1.0f / 512.0f);
+    const float dy = (float)(t[1] - b) - (((q >> 9) & 511u) + 0.5f) * (1.0f / 512.0f);
+    const float dz = (float)(t[2] - e) - (((q >> 18) & 511u) + 0.5f) * (1.0f / 512.0f);
+    const float d2 = dx * dx + dy * dy + dz * dz;
+    if (d2 < best || (d2 == best && id < bid)) { best = d2; bid = id; }
+  }
+  if (bid != 0xFFFFFFFFu) return (int)bid;
+  return seed_vol_ring(cell, g, c[0], c[1], c[2], kSeedIdMask);
 }
 
 __device__ int seed_srf(const int *cell, int g, const Frame *fr, const double *x) {
@@ -383,8 +439,18 @@ __device__ __forceinline__ int block_excl_scan(int v, int *tot) {
   return pre + inc - v;
 }
 
+// bit j = (pclass[i0 + j] == cls); the 16 classes of a thread come in one
+// 16-byte load when the array is 16-byte aligned and the run is complete
+// (byte loads cost 16 instructions per wave and ran at ~130 GB/s)
 __device__ __forceinline__ unsigned cls_bits(const uint8_t *pclass, long long np, long long i0, int cls) {
   unsigned m = 0;
+  if (i0 + kClsItems <= np && ((uintptr_t)pclass & 15) == 0) {
+    const uint4 w = *reinterpret_cast<const uint4 *>(pclass + i0);
+    const unsigned words[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int j = 0; j < kClsItems; j++) m |= (((words[j >> 2] >> (8 * (j & 3))) & 0xFFu) == (unsigned)cls) ? (1u << j) : 0u;
+    return m;
+  }
 #pragma unroll
   for (int j = 0; j < kClsItems; j++) {
     const long long i = i0 + j;
@@ -1634,6 +1700,7 @@ struct pmmg_hip_ctx {
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr; // surface branch, concurrent with the volume walk
   hipStream_t stream3 = nullptr; // volume interpolation of chunk c, concurrent with the walk of chunk c+1
+  int seed8 = 1;        // queries pick the nearest of 8 cell seeds (PMMG_HIP_SEED8)
   int bbox_stride = 16; // frame from every 16th background vertex (PMMG_HIP_BBOXSTRIDE)
   int chunks = 3;                // volume pipeline chunks (PMMG_HIP_CHUNKS)
   hipEvent_t evc[kMaxChunks] = {};
@@ -1664,7 +1731,7 @@ struct pmmg_hip_ctx {
   hipEvent_t ev[10] = {};
   bool pending = false;
   int tpc = 8;      // background tetra per volume seed cell
-  int spc = 4;      // sampled tetra per seed cell
+  int spc = 1;      // sampled tetra per seed cell
   int seed_mode = 0; // seed point of a sampled tetra: 0 centroid, 1 edge v0-v3 midpoint, 2 first vertex
   int seed_run = 4;  // consecutive tetra per sample run (1, 2, 4, 8)
   int seed_grid = 8192; // blocks of k_seed_vol (PMMG_HIP_SEEDGRID)
@@ -1783,6 +1850,7 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   c->cap = env_int("PMMG_HIP_CAP", c->cap);
   c->chunks = env_int("PMMG_HIP_CHUNKS", c->chunks);
   c->bbox_stride = env_int("PMMG_HIP_BBOXSTRIDE", c->bbox_stride);
+  c->seed8 = env_flag("PMMG_HIP_SEED8", c->seed8);
   if (c->chunks > kMaxChunks) c->chunks = kMaxChunks;
   {
     hipDeviceProp_t prop;
@@ -2077,7 +2145,7 @@ static int run_scan(pmmg_hip_ctx *c, const Slots &S, int np_new, const double *x
                      (unsigned long long *)nullptr, 0LL, sgrid, nsg, (int *)c->cnt.p, ncells + 1, 0);
   hipLaunchKernelGGL(k_bbox, dim3(blocks_for(bg.np / c->bbox_stride + 1, 1024)), dim3(kBlock), 0, s, bg.xyz, bg.np, fr,
                      c->bbox_stride);
-  hipLaunchKernelGGL(k_frame_final, dim3(1), dim3(1), 0, s, fr, 1, gs, gq);
+  hipLaunchKernelGGL(k_frame_final, dim3(1), dim3(1), 0, s, fr, 1, gs, gq, 0);
   if (bg.nt > 0) hipLaunchKernelGGL(k_seed_srf, dim3(blocks_for(bg.nt, 4096)), dim3(kBlock), 0, s, bg, fr, sgrid, gs);
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[1], s));
@@ -2181,7 +2249,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
                      sorted ? (int *)c->cnt.p : nullptr, sorted ? 2LL * nbins : 0LL, 1);
   hipLaunchKernelGGL(k_bbox, dim3(blocks_for(bg.np / c->bbox_stride + 1, 1024)), dim3(kBlock), 0, s, bg.xyz, bg.np, fr,
                      c->bbox_stride);
-  hipLaunchKernelGGL(k_frame_final, dim3(1), dim3(1), 0, s, fr, g, gs, gb);
+  hipLaunchKernelGGL(k_frame_final, dim3(1), dim3(1), 0, s, fr, g, gs, gb, c->seed8);
   // The surface branch (tria seeds, surface list, k_bdy) only needs the
   // frame: on the input-order path it runs on a second stream, concurrently
   // with the volume seeds and walks (joined before the fallbacks).
