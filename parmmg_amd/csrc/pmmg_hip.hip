@@ -1155,6 +1155,130 @@ __global__ __launch_bounds__(kBlock) void k_vol_interp(const uint8_t *pclass, in
   if (hit_out) __builtin_nontemporal_store((int8_t)PMMG_HIT_VOL_WALK, hit_out + ip - 1);
 }
 
+// Cooperative row gathers (default interpolation).  The texture addresser
+// is the interpolation's bound (PMC: TA busy ~92% of the kernel): its cost
+// follows the distinct cache lines each wave-instruction touches, and a lane
+// gathering its own 48-byte rows in three 16-byte instructions touches every
+// row's lines three times, ~41 lines per instruction.  Here the 64 lanes of a
+// wave gather the 256 rows (64 queries x 4 vertices) of one 3- or 6-double
+// slot together: piece p = 64 t + lane of the slot's row image (16-byte pieces
+// for 6-double rows, 8-byte pieces for 3-double rows, 3 pieces per row) is
+// loaded by one lane, so a row's pieces share an instruction and every
+// instruction covers ~21 whole rows.  The image goes through LDS, each lane
+// reads its 4 rows back and evaluates the reference interpolator (same
+// arithmetic, same order) from them.  Scalar slots keep per-lane gathers.
+template <int C>
+__device__ __forceinline__ void coop_gather(const Slot &sl, const int *vid, double *img) {
+  const int lane = __lane_id();
+  if constexpr (C == 6) {
+    double2 b[12];
+#pragma unroll
+    for (int t = 0; t < 12; t++) {
+      const int p = 64 * t + lane, r = p / 3, k = p - 3 * r;
+      b[t] = *reinterpret_cast<const double2 *>(sl.in + (size_t)sl.stride * (vid[r] - 1) + 2 * k);
+    }
+#pragma unroll
+    for (int t = 0; t < 12; t++) reinterpret_cast<double2 *>(img)[64 * t + lane] = b[t];
+  } else {
+    double b[12];
+#pragma unroll
+    for (int t = 0; t < 12; t++) {
+      const int p = 64 * t + lane, r = p / 3, k = p - 3 * r;
+      b[t] = sl.in[(size_t)sl.stride * (vid[r] - 1) + k];
+    }
+#pragma unroll
+    for (int t = 0; t < 12; t++) img[64 * t + lane] = b[t];
+  }
+  wait_lgkm();
+  __builtin_amdgcn_wave_barrier();
+}
+
+// the row of one slot from the wave's row image (rows 4*lane .. 4*lane+3)
+template <int C>
+__device__ __forceinline__ bool coop_row(const double *img, const double *phi, double *r) {
+  const double *base = img + 4 * C * __lane_id();
+  if constexpr (C == 6) {
+    double m[4][6];
+#pragma unroll
+    for (int i = 0; i < 4; i++) load6(base + 6 * i, m[i]);
+    double mint[6], mi[6];
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      ok = invmat(m[i], mi) && ok;
+#pragma unroll
+      for (int q = 0; q < 6; q++) mint[q] = (i == 0) ? phi[0] * mi[q] : mint[q] + phi[i] * mi[q];
+    }
+    return invmat(mint, r) && ok;
+  } else {
+    double row[4][C];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int j = 0; j < C; j++) row[i][j] = base[C * i + j];
+#pragma unroll
+    for (int j = 0; j < C; j++) r[j] = 0.0;
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int j = 0; j < C; j++) r[j] += phi[i] * row[i][j];
+    return true;
+  }
+}
+
+template <int C>
+__device__ __forceinline__ void coop_slot(const Slot &sl, bool act, const int *v, const double *phi, const int *vid,
+                                          double *img, size_t i0) {
+  if constexpr (C > 0) {
+    double r[C];
+    bool ok;
+    if constexpr (C == 1) {
+      ok = interp_row<4, 1>(sl, v, phi, r) && act;
+    } else {
+      coop_gather<C>(sl, vid, img);
+      ok = coop_row<C>(img, phi, r) && act;
+      wait_lgkm();
+      __builtin_amdgcn_wave_barrier(); // every lane has read its rows: the image becomes the store image
+    }
+    wave_store_rows<C>(sl.out + (size_t)C * i0, r, __ballot(ok), img);
+  }
+}
+
+template <int C0, int C1, int C2, int C3, int C4, int C5>
+__global__ __launch_bounds__(kBlock) void k_vol_interp_coop(const uint8_t *pclass, int np, const int *vloc, VRec vrec,
+                                                            Slots S, int *elem_out, int8_t *hit_out, int i0q) {
+  __shared__ double img_all[kBlock / 64][256 * 6];
+  __shared__ int vid_all[kBlock / 64][256];
+  double *img = img_all[threadIdx.x >> 6];
+  int *vid = vid_all[threadIdx.x >> 6];
+  const int i = i0q + xcd_block() * blockDim.x + threadIdx.x;
+  bool act = i < np && __builtin_nontemporal_load(pclass + i) == PMMG_PT_VOL;
+  const int k = act ? __builtin_nontemporal_load(vloc + i) : 0;
+  act = act && k != 0;
+  if (!__any(act)) return;
+  VolLoc loc;
+  if (act) loc = vrec_load(vrec, i);
+  else { // idle lanes gather a valid row, never stored
+    loc.v = make_int4(1, 1, 1, 1);
+#pragma unroll
+    for (int f = 0; f < 4; f++) loc.phi[f] = 0.0;
+  }
+  const int v[4] = {loc.v.x, loc.v.y, loc.v.z, loc.v.w};
+  reinterpret_cast<int4 *>(vid)[__lane_id()] = loc.v;
+  wait_lgkm();
+  __builtin_amdgcn_wave_barrier();
+  const size_t w0 = (size_t)(i - __lane_id());
+  coop_slot<C0>(S.s[0], act, v, loc.phi, vid, img, w0);
+  coop_slot<C1>(S.s[1], act, v, loc.phi, vid, img, w0);
+  coop_slot<C2>(S.s[2], act, v, loc.phi, vid, img, w0);
+  coop_slot<C3>(S.s[3], act, v, loc.phi, vid, img, w0);
+  coop_slot<C4>(S.s[4], act, v, loc.phi, vid, img, w0);
+  coop_slot<C5>(S.s[5], act, v, loc.phi, vid, img, w0);
+  if (!act) return;
+  if (elem_out) __builtin_nontemporal_store(k, elem_out + i);
+  if (hit_out) __builtin_nontemporal_store((int8_t)PMMG_HIT_VOL_WALK, hit_out + i);
+}
+
 // walk + interpolation in one pass (default): the located tetra's vertex ids
 // and barycentric coordinates are still in registers for the row gathers
 template <int C0, int C1, int C2, int C3, int C4, int C5>
@@ -1650,12 +1774,13 @@ typedef void (*FusedFn)(Bg, const Frame *, const unsigned long long *, int, cons
 struct LayoutEntry {
   int c[6];
   VolInterpFn fn;
+  VolInterpFn cfn; // cooperative-gather variant (nullptr: runtime layout)
   ScanInterpFn sfn;
   FusedFn ffn;
 };
 
 #define PMMG_LAYOUT(a, b, c, d, e, f)                                                                             \
-  {{a, b, c, d, e, f}, k_vol_interp<a, b, c, d, e, f>,                                                          \
+  {{a, b, c, d, e, f}, k_vol_interp<a, b, c, d, e, f>, k_vol_interp_coop<a, b, c, d, e, f>,                     \
    k_vol_interp_scan<a, b, c, d, e, f>,                                                                         \
    k_vol_fused<a, b, c, d, e, f>}
 // common slot layouts (metric first): aniso metric + scalar/vector/tensor
@@ -1668,7 +1793,7 @@ const LayoutEntry kLayouts[] = {
 };
 #undef PMMG_LAYOUT
 
-const LayoutEntry kGeneric = {{-1, 0, 0, 0, 0, 0}, k_vol_interp<-1, 0, 0, 0, 0, 0>,
+const LayoutEntry kGeneric = {{-1, 0, 0, 0, 0, 0}, k_vol_interp<-1, 0, 0, 0, 0, 0>, nullptr,
                                k_vol_interp_scan<-1, 0, 0, 0, 0, 0>, k_vol_fused<-1, 0, 0, 0, 0, 0>};
 
 const LayoutEntry &pick_layout(const Slots &S) {
@@ -1700,6 +1825,7 @@ struct pmmg_hip_ctx {
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr; // surface branch, concurrent with the volume walk
   hipStream_t stream3 = nullptr; // volume interpolation of chunk c, concurrent with the walk of chunk c+1
+  int coop = 1;         // cooperative row gathers in the interpolation (PMMG_HIP_COOP)
   int seed8 = 1;        // queries pick the nearest of 8 cell seeds (PMMG_HIP_SEED8)
   int bbox_stride = 16; // frame from every 16th background vertex (PMMG_HIP_BBOXSTRIDE)
   int chunks = 3;                // volume pipeline chunks (PMMG_HIP_CHUNKS)
@@ -1851,6 +1977,7 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   c->chunks = env_int("PMMG_HIP_CHUNKS", c->chunks);
   c->bbox_stride = env_int("PMMG_HIP_BBOXSTRIDE", c->bbox_stride);
   c->seed8 = env_flag("PMMG_HIP_SEED8", c->seed8);
+  c->coop = env_flag("PMMG_HIP_COOP", c->coop);
   if (c->chunks > kMaxChunks) c->chunks = kMaxChunks;
   {
     hipDeviceProp_t prop;
@@ -2300,7 +2427,8 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     auto walk = c->carry == 2 ? (c->walkw >= 5 ? k_vol_walk<2, 5> : k_vol_walk<2, 1>)
                 : c->carry    ? (c->walkw >= 5 ? k_vol_walk<1, 5> : k_vol_walk<1, 1>)
                               : (c->walkw >= 5 ? k_vol_walk<0, 5> : k_vol_walk<0, 1>);
-    VolInterpFn interp = pick_layout(S).fn;
+    const LayoutEntry &lay = pick_layout(S);
+    VolInterpFn interp = (c->coop && lay.cfn) ? lay.cfn : lay.fn;
     const VRec vr = vrec_arrays(c->vrec.p, (size_t)np_new);
     // Pipelined volume stage: the queries are cut into `nch` contiguous
     // chunks; the interpolation of chunk j (bandwidth-bound) runs on stream3
