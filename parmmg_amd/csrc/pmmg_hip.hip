@@ -332,16 +332,32 @@ __device__ int seed_srf(const int *cell, int g, const Frame *fr, const double *x
 
 // ---------------------------------------------------------------- query order
 
-// Is the input numbering spatially coherent?  Mean distance between
-// consecutive points (sampled) against the mean spacing of np points in the
-// bbox of the sample; lattice / SCOTCH-renumbered meshes pass, shuffled
-// numberings fail.  Self-contained so it can run first and be read back early.
+// Is the input numbering spatially coherent?  Distances between consecutive
+// points at 4096 pseudo-random positions against the mean spacing h of np points
+// in the bbox of the sample: coherent when at least half of them are below
+// 4h (a median test: the jumps at the ends of lattice rows or of Mmg's local
+// numbering runs, which an evenly strided sample can hit in a fixed fraction
+// of its positions, do not count; a shuffled numbering has almost every
+// distance at the scale of the bbox).  Self-contained so it can run first and
+// be read back early.
 __global__ __launch_bounds__(kBlock) void k_coherence(const double *xyz, int np, DevStats *st) {
-  __shared__ double ssum[kBlock], slo[3][kBlock], shi[3][kBlock];
-  double acc = 0.0, lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
-  const int nsamp = 4096;
-  for (int s = threadIdx.x; s < nsamp; s += blockDim.x) {
-    long long i = ((long long)s * (np - 1)) / nsamp;
+  constexpr int nsamp = 4096, per = nsamp / kBlock;
+  __shared__ double slo[3][kBlock], shi[3][kBlock];
+  __shared__ double s_h;
+  __shared__ int s_near[kBlock];
+  double dist[per], lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+#pragma unroll
+  for (int q = 0; q < per; q++) {
+    const int smp = threadIdx.x + q * kBlock;
+    dist[q] = 0.0;
+    if (np < 2) continue;
+    // pseudo-random positions (splitmix64 of the sample index): an evenly
+    // strided sample can alias with the row length of a lattice numbering
+    unsigned long long z = (unsigned long long)smp * 0x9E3779B97F4A7C15ULL + 0x5EED2025ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    z ^= z >> 31;
+    const long long i = (long long)(z % (unsigned long long)(np - 1));
     double d2 = 0.0;
     for (int d = 0; d < 3; d++) {
       double a = xyz[3 * (size_t)i + d], b = xyz[3 * (size_t)(i + 1) + d];
@@ -350,21 +366,27 @@ __global__ __launch_bounds__(kBlock) void k_coherence(const double *xyz, int np,
       lo[d] = fmin(lo[d], a);
       hi[d] = fmax(hi[d], a);
     }
-    acc += sqrt(d2);
+    dist[q] = sqrt(d2);
   }
-  ssum[threadIdx.x] = acc;
   for (int d = 0; d < 3; d++) { slo[d][threadIdx.x] = lo[d]; shi[d][threadIdx.x] = hi[d]; }
   __syncthreads();
   if (threadIdx.x == 0) {
-    double tot = 0.0, L[3] = {1e300, 1e300, 1e300}, H[3] = {-1e300, -1e300, -1e300};
-    for (int j = 0; j < kBlock; j++) {
-      tot += ssum[j];
+    double L[3] = {1e300, 1e300, 1e300}, H[3] = {-1e300, -1e300, -1e300};
+    for (int j = 0; j < kBlock; j++)
       for (int d = 0; d < 3; d++) { L[d] = fmin(L[d], slo[d][j]); H[d] = fmax(H[d], shi[d][j]); }
-    }
-    double mean = tot / nsamp;
     double vol = fmax(H[0] - L[0], 1e-300) * fmax(H[1] - L[1], 1e-300) * fmax(H[2] - L[2], 1e-300);
-    double h = cbrt(vol / (double)(np > 1 ? np : 1));
-    st->coherent = (np > 1 && mean < 4.0 * h) ? 1 : 0;
+    s_h = cbrt(vol / (double)(np > 1 ? np : 1));
+  }
+  __syncthreads();
+  int near = 0;
+#pragma unroll
+  for (int q = 0; q < per; q++) near += dist[q] < 4.0 * s_h ? 1 : 0;
+  s_near[threadIdx.x] = near;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int tot = 0;
+    for (int j = 0; j < kBlock; j++) tot += s_near[j];
+    st->coherent = (np > 1 && 2 * tot >= nsamp) ? 1 : 0;
   }
 }
 

@@ -150,3 +150,25 @@ def test_full_size_cfg3_sample_against_oracle_and_determinism():
     case = dict(B=O.Background(bg, met, fields, w.hausd), new=new, pclass=pc, met=met, fields=fields)
     rep = check(case, dict(met=mo, fields=fo, elem=el, hit=hit), max_points=3000)
     assert rep["n"] == 3000 and rep["maxrel"] <= 1e-12
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [39, 63])
+def test_query_order_detection(n):
+    """Input order is kept for a lattice numbering whatever its row length
+    (n=63: 64^3 points, a row length an evenly strided sample would alias
+    with), and Morton binning is chosen for a shuffled numbering; results are
+    the same either way."""
+    case = make_case(kind=C, n_old=8, n_new=n, with_ref=False)
+    a = run_gpu(case)
+    assert a["stats"]["sorted"] == 0
+    rng = np.random.default_rng(3)
+    perm = rng.permutation(case["new"].np)
+    import dataclasses
+    shuf = dict(case)
+    shuf["new"] = dataclasses.replace(case["new"], xyz=np.ascontiguousarray(case["new"].xyz[perm]))
+    shuf["pclass"] = np.ascontiguousarray(case["pclass"][perm])
+    b = run_gpu(shuf)
+    assert b["stats"]["sorted"] == 1
+    np.testing.assert_array_equal(b["elem"], a["elem"][perm])
+    np.testing.assert_array_equal(b["met"], a["met"][perm])
