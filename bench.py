@@ -39,7 +39,8 @@ def log(*a):
 def build_workload(w: configs.Workload, rank: int):
     t0 = time.time()
     bg = synth.lattice(w.kind, w.n_old, jitter=0.0)
-    new = synth.lattice(w.kind, w.n_new, jitter=w.jitter_new, seed=synth.SEED + rank, with_trias=False)
+    new = synth.lattice(w.kind, w.n_new, jitter=w.jitter_new, seed=synth.SEED + rank, with_trias=False,
+                        with_tetra=False)
     met = synth.solution(w.metric, bg.xyz)
     fields = [synth.solution(f, bg.xyz) for f in w.fields]
     pclass = synth.classes(new)

@@ -1856,7 +1856,6 @@ struct pmmg_hip_ctx {
   int two_streams = 1; // PMMG_HIP_STREAMS=1: everything on one stream
   int carry = 2;       // 0 reload, 1 registers, 2 LDS slots (PMMG_HIP_CARRY)
   int walkw = 0;       // >= 5: walk compiled for 5 waves per SIMD (PMMG_HIP_WALKW)
-  int s2_start = 0;    // surface branch start: 0 after the frame, 1 after the volume seeds
   char err[512] = {0};
   Bg bg{};
   int met_size = 0;
@@ -1876,7 +1875,7 @@ struct pmmg_hip_ctx {
   // host-mode staging
   DevBuf h_xyz, h_cls, h_met, h_elem, h_hit;
   std::vector<DevBuf> h_f;
-  hipEvent_t ev[10] = {};
+  hipEvent_t ev[11] = {};
   bool pending = false;
   int tpc = 8;      // background tetra per volume seed cell
   int spc = 1;      // sampled tetra per seed cell
@@ -1973,7 +1972,7 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
     delete c;
     return nullptr;
   }
-  for (int i = 0; i < 10; i++) (void)hipEventCreate(&c->ev[i]);
+  for (int i = 0; i < 11; i++) (void)hipEventCreate(&c->ev[i]);
   for (int i = 0; i < kMaxChunks; i++) (void)hipEventCreateWithFlags(&c->evc[i], hipEventDisableTiming);
   if (hipHostMalloc((void **)&c->h_small, 64, hipHostMallocDefault) != hipSuccess) {
     fprintf(stderr, "[parmmg_hip] cannot allocate pinned host memory\n");
@@ -1988,7 +1987,6 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   c->seed_atom = env_flag("PMMG_HIP_SEEDATOM", c->seed_atom);
   if (c->seed_grid < 8) c->seed_grid = 8;
   c->two_streams = env_int("PMMG_HIP_STREAMS", 2) >= 2;
-  if (getenv("PMMG_HIP_S2START")) c->s2_start = atoi(getenv("PMMG_HIP_S2START"));
   if (getenv("PMMG_HIP_CARRY")) c->carry = atoi(getenv("PMMG_HIP_CARRY"));
   if (getenv("PMMG_HIP_WALKW")) c->walkw = atoi(getenv("PMMG_HIP_WALKW"));
   if (c->seed_run != 1 && c->seed_run != 2 && c->seed_run != 4 && c->seed_run != 8) c->seed_run = 4;
@@ -2020,7 +2018,7 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   for (DevBuf *b : bufs) release(*b);
   for (auto &b : c->o_f) release(b);
   for (auto &b : c->h_f) release(b);
-  for (int i = 0; i < 10; i++)
+  for (int i = 0; i < 11; i++)
     if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
   for (int i = 0; i < kMaxChunks; i++)
     if (c->evc[i]) (void)hipEventDestroy(c->evc[i]);
@@ -2376,48 +2374,49 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
 
   if (c->options & PMMG_HIP_OPT_SCAN) return run_scan(c, S, np_new, xyz_new, pclass, elem_out, hit_out, gs);
 
-  // query order decision first: a 4096-point sample, read back early (one
-  // small synchronisation) unless the caller forced the order
+  // Query order: a 4096-point coherence sample whose 4-byte result is read
+  // back while the device already builds the frame and the volume seeds (they
+  // do not depend on the order); the host waits on that copy only, so the
+  // GPU is not left idle across the decision.
   int sorted = 1;
   HIPCK(c, hipEventRecord(c->ev[0], s));
-  if (c->options & PMMG_HIP_OPT_NOSORT) {
-    sorted = 0;
-  } else if (!(c->options & PMMG_HIP_OPT_SORT)) {
+  const bool auto_order = !(c->options & (PMMG_HIP_OPT_NOSORT | PMMG_HIP_OPT_SORT));
+  if (c->options & PMMG_HIP_OPT_NOSORT) sorted = 0;
+  if (auto_order) {
     hipLaunchKernelGGL(k_coherence, dim3(1), dim3(kBlock), 0, s, xyz_new, np_new, st);
     HIPCK(c, hipMemcpyAsync(c->h_small, &st->coherent, sizeof(int), hipMemcpyDeviceToHost, s));
-    HIPCK(c, hipStreamSynchronize(s));
-    sorted = c->h_small[0] ? 0 : 1;
+    HIPCK(c, hipEventRecord(c->ev[10], s));
   }
-  c->last_sorted = sorted;
-  if (sorted && (!ensure(c, c->cnt, 4 * (size_t)2 * nbins) || !ensure(c, c->off, 4 * (size_t)2 * nbins) ||
-                 !ensure(c, c->binrank, 8 * nq)))
-    return 0;
 
   const long long ng = (long long)g * g * g, nsg = bg.nt > 0 ? (long long)gs * gs * gs : 0;
-  hipLaunchKernelGGL(k_reset, dim3(blocks_for(ng, 2048)), dim3(kBlock), 0, s, fr, st, grid, ng, sgrid, nsg,
-                     sorted ? (int *)c->cnt.p : nullptr, sorted ? 2LL * nbins : 0LL, 1);
+  hipLaunchKernelGGL(k_reset, dim3(blocks_for(ng, 2048)), dim3(kBlock), 0, s, fr, st, grid, ng, sgrid, nsg, nullptr,
+                     0LL, 1);
   hipLaunchKernelGGL(k_bbox, dim3(blocks_for(bg.np / c->bbox_stride + 1, 1024)), dim3(kBlock), 0, s, bg.xyz, bg.np, fr,
                      c->bbox_stride);
   hipLaunchKernelGGL(k_frame_final, dim3(1), dim3(1), 0, s, fr, g, gs, gb, c->seed8);
+  HIPCK(c, hipEventRecord(c->ev[7], s)); // frame ready: the surface branch may start
+  long long nsamp = (long long)c->spc * ng;
+  if (nsamp > bg.ne) nsamp = bg.ne;
+  hipLaunchKernelGGL(k_seed_vol, dim3((blocks_for(nsamp, c->seed_grid) + 7) & ~7), dim3(kBlock), 0, s, bg, fr, grid, g, nsamp,
+                     c->seed_mode, c->seed_run, c->seed_atom);
+  HIPCK(c, hipGetLastError());
+  if (auto_order) {
+    HIPCK(c, hipEventSynchronize(c->ev[10]));
+    sorted = c->h_small[0] ? 0 : 1;
+  }
+  c->last_sorted = sorted;
+  if (sorted) {
+    if (!ensure(c, c->cnt, 4 * (size_t)2 * nbins) || !ensure(c, c->off, 4 * (size_t)2 * nbins) ||
+        !ensure(c, c->binrank, 8 * nq))
+      return 0;
+    HIPCK(c, hipMemsetAsync(c->cnt.p, 0, 4 * (size_t)2 * nbins, s));
+  }
   // The surface branch (tria seeds, surface list, k_bdy) only needs the
   // frame: on the input-order path it runs on a second stream, concurrently
   // with the volume seeds and walks (joined before the fallbacks).
   const hipStream_t sb = (!sorted && bg.nt > 0 && c->two_streams) ? c->stream2 : s;
   c->bdy_on_s2 = sb != s;
-  // the surface branch starts after the frame (s2_start 0, default) or
-  // after the volume seeds (1); both measured within noise of each other
-  if (c->bdy_on_s2 && c->s2_start == 0) {
-    HIPCK(c, hipEventRecord(c->ev[7], s));
-    HIPCK(c, hipStreamWaitEvent(sb, c->ev[7], 0));
-  }
-  long long nsamp = (long long)c->spc * ng;
-  if (nsamp > bg.ne) nsamp = bg.ne;
-  hipLaunchKernelGGL(k_seed_vol, dim3((blocks_for(nsamp, c->seed_grid) + 7) & ~7), dim3(kBlock), 0, s, bg, fr, grid, g, nsamp,
-                     c->seed_mode, c->seed_run, c->seed_atom);
-  if (c->bdy_on_s2 && c->s2_start != 0) {
-    HIPCK(c, hipEventRecord(c->ev[7], s));
-    HIPCK(c, hipStreamWaitEvent(sb, c->ev[7], 0));
-  }
+  if (c->bdy_on_s2) HIPCK(c, hipStreamWaitEvent(sb, c->ev[7], 0));
   if (bg.nt > 0) hipLaunchKernelGGL(k_seed_srf, dim3(blocks_for(bg.nt, 4096)), dim3(kBlock), 0, sb, bg, fr, sgrid, gs);
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[1], s));

@@ -55,13 +55,19 @@ def counts(kind: int, n: int) -> tuple[int, int, int]:
     return int(out[0]), int(out[1]), int(out[2])
 
 
-def lattice(kind: int, n: int, jitter: float = 0.0, seed: int = SEED, with_trias: bool = True) -> Mesh:
+def lattice(kind: int, n: int, jitter: float = 0.0, seed: int = SEED, with_trias: bool = True,
+            with_tetra: bool = True) -> Mesh:
+    """with_tetra=False: vertices and boundary flags only (a new mesh whose
+    points are the queries; no connectivity is generated)."""
     lib = synth_lib()
     npt, ne, nt = counts(kind, n)
     xyz = np.empty((npt, 3), np.float64)
     isbdy = np.empty(npt, np.uint8)
     if not lib.synth_vertices(kind, n, float(jitter), seed, _ptr(xyz), _ptr(isbdy)):
         raise RuntimeError("synth_vertices failed")
+    if not with_tetra:
+        empty4 = np.zeros((0, 4), np.int32)
+        return Mesh(kind, n, xyz, empty4, empty4, np.zeros((0, 3), np.int32), np.zeros((0, 3), np.int32), isbdy)
     tetv = np.empty((ne, 4), np.int32)
     adja = np.empty((ne, 4), np.int32)
     if not lib.synth_tetra(kind, n, _ptr(tetv), _ptr(adja)):

@@ -115,3 +115,28 @@ def test_snapshot_full_size_cfg3():
         assert np.array_equal(adja.download(), bg.adja)
         assert np.array_equal(triv.download(), bg.triv)
         assert np.array_equal(adjt.download(), bg.adjt)
+
+
+@pytest.mark.gpu
+def test_outputs_in_torch_tensors():
+    """Device-mode outputs may be torch tensors in HBM (the Morton-sharded
+    bench all-gathers them in place): same results as numpy host mode."""
+    import torch
+    case = make_case(kind=synth.CUBE, n_old=6, n_new=9, with_ref=False)
+    ref = run_gpu(case)
+    bg = case["bg"]
+    dev = torch.device("cuda", 0)
+    with TransferContext(0) as ctx:
+        ctx.set_background(ctx.upload(bg.xyz), ctx.upload(bg.tetv), ctx.upload(bg.adja), ctx.upload(bg.triv),
+                           ctx.upload(bg.adjt), case["hausd"])
+        ctx.set_solutions(ctx.upload(case["met"]), [ctx.upload(f) for f in case["fields"]])
+        npn = case["new"].np
+        mo = torch.full((npn, case["met"].shape[1]), float("nan"), dtype=torch.float64, device=dev)
+        fo = [torch.full((npn, f.shape[1]), float("nan"), dtype=torch.float64, device=dev) for f in case["fields"]]
+        el = torch.zeros(npn, dtype=torch.int32, device=dev)
+        ctx.locate_interp(ctx.upload(case["new"].xyz), ctx.upload(case["pclass"]), mo, fo, el, None)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(el.cpu().numpy(), ref["elem"])
+        np.testing.assert_array_equal(mo.cpu().numpy(), ref["met"])
+        for a, b in zip(fo, ref["fields"]):
+            np.testing.assert_array_equal(a.cpu().numpy(), b)
