@@ -181,28 +181,52 @@ def main():
                     help="HBM layout of the metric/fields: packed per-vertex records or one array per solution")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--shard", default="group", choices=["group", "morton"],
-                    help="multi-GPU split: one group per rank (weak scaling, ParMmg's own sharding) or one problem "
+    ap.add_argument("--shard", default="group", choices=["group", "morton", "halo"],
+                    help="multi-GPU split: one group per rank (weak scaling, ParMmg's own sharding); one problem "
                          "cut into contiguous Morton ranges of the new points, background replicated, results "
-                         "all-gathered over RCCL after the timed steps (strong scaling, SURVEY.md 8(e))")
+                         "all-gathered over RCCL after the timed steps (morton); or Morton ranges against halo "
+                         "shards of the background, results kept per rank (halo; strong scaling, SURVEY.md 8(e))")
+    ap.add_argument("--halo", type=float, default=-1.0,
+                    help="halo mode: growth of the range box (< 0: in largest-tetra extents)")
     ap.add_argument("--no-snapshot", action="store_true",
                     help="skip the (separately reported) device background snapshot timing")
     args = ap.parse_args()
 
-    ri = ranks.init("nccl")
+    # PMMG_BENCH_BACKEND=gloo: host-side collectives, ranks share the visible
+    # GPUs round-robin (rehearsing several ranks on a one-GPU box)
+    backend = os.environ.get("PMMG_BENCH_BACKEND", "nccl")
+    ri = ranks.init(backend)
     rank, world, local = ri.rank, ri.world, ri.local
+    if backend != "nccl":
+        import torch
+        local = local % max(1, torch.cuda.device_count())
 
     w = configs.SHORT[args.config]
+    split = args.shard in ("morton", "halo")
     morton = args.shard == "morton"
-    # Morton mode: every rank builds the same problem and keeps its range
-    bg, new, met, fields, pclass = build_workload(w, 0 if morton else rank)
+    # Morton / halo mode: every rank builds the same problem and keeps its range
+    bg, new, met, fields, pclass = build_workload(w, 0 if split else rank)
+    ne_group = bg.ne
     mine = None
-    if morton:
+    halo_info = None
+    if split:
         shards = ranks.morton_shards(new.xyz, pclass, world)
         mine = shards[rank]
         counts = [len(x) for x in shards]
         q_xyz, q_pc = np.ascontiguousarray(new.xyz[mine]), np.ascontiguousarray(pclass[mine])
         log(f"[bench r{rank}] Morton range {len(mine)} of {int((pclass != 0).sum())} points")
+        if args.shard == "halo":
+            from parmmg_amd import shard
+            t_sh = time.time()
+            lo, hi = shard.range_box(q_xyz)
+            sh = shard.halo_shard(bg, lo, hi, args.halo)
+            bg, met, fields = sh.mesh, sh.rows(met), [sh.rows(f) for f in fields]
+            halo_info = {"what": "halo shard of the background around this rank's Morton range (rank 0)",
+                         "tets": bg.ne, "verts": bg.np, "trias": bg.nt, "halo": sh.halo,
+                         "tet_fraction_of_group": round(bg.ne / ne_group, 4),
+                         "build_s": round(time.time() - t_sh, 2)}
+            log(f"[bench r{rank}] halo shard: {bg.ne} of {ne_group} tets, {bg.np} verts, {bg.nt} trias "
+                f"(halo {sh.halo:.4g}) in {time.time() - t_sh:.1f}s")
     else:
         q_xyz, q_pc = new.xyz, pclass
     nq = q_xyz.shape[0]
@@ -278,6 +302,7 @@ def main():
     gather = None
     if morton:
         gather = allgather_timing(ri, d_mo, d_fo, d_elem, counts, mine, rank)
+    if split:
         npts = agg["points_per_step"]  # the whole problem: bytes per point below are per problem point
     ms_per_step = agg["ms_per_step"]
     value = agg["mpts_per_s"]
@@ -297,7 +322,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "strong" if morton else "weak",
+        "scaling": "strong" if split else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (Kuhn lattices, analytic metric/fields, splitmix64 jitter)",
@@ -307,7 +332,9 @@ def main():
             "background_tets": ne_o, "background_verts": np_o, "new_points": np_n,
             "located_points_per_gpu": npts, "K_doubles_per_vertex": w.K,
             "parallelism": (f"Morton-range shards x{world}, replicated background, RCCL all-gather after the step"
-                            if morton else f"one group per GPU x{world} (weak, no data-path collective)"),
+                            if morton else
+                            f"Morton-range shards x{world}, halo-sharded background, results kept per rank"
+                            if split else f"one group per GPU x{world} (weak, no data-path collective)"),
             "query_order": args.sort,
             "locate": args.locate,
             "tetra_layout": args.layout,
@@ -341,9 +368,11 @@ def main():
     }
     if gather is not None:
         out["allgather"] = gather
-    if not args.no_snapshot:
+    if halo_info is not None:
+        out["halo_shard"] = halo_info
+    if not args.no_snapshot and halo_info is None:  # (a shard's cut faces are no boundary trias)
         out["snapshot"] = snapshot_timing(ctx, bg, rank)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and halo_info is None:
         log(f"[bench r{rank}] cpu baseline (oracle) on a bounded sample")
         out["cpu_baseline"] = cpu_baseline(w, bg, new, met, fields, pclass, args.cpu_baseline_seconds)
     if rank == 0:

@@ -96,6 +96,16 @@ def synth_lib() -> ctypes.CDLL:
     return _load(_build.SYNTH_SO, SYNTH_API, "libpmmg_synth.so")
 
 
+HOST_API = {
+    "pmmg_max_tet_extent": (c_double, [c_int, c_void_p, c_int, c_void_p]),
+    "pmmg_shard_mark": (c_int, [c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_double, c_void_p,
+                                c_void_p, P(c_int64)]),
+    "pmmg_shard_fill": (c_int64, [c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
+                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                  c_void_p, c_void_p, c_void_p]),
+}
+
+
 def host_lib() -> ctypes.CDLL:
     hip_lib()  # resolve the dependency from the same directory first
-    return _load(_build.HOST_SO, {}, "libpmmg_host.so")
+    return _load(_build.HOST_SO, HOST_API, "libpmmg_host.so")

@@ -66,10 +66,11 @@ def build_hip(force: bool = False) -> str:
 
 def build_host(force: bool = False) -> str:
     src = os.path.join(CSRC, "pmmg_host.c")
-    deps = [src, os.path.join(CSRC, "pmmg_host.h"), os.path.join(INC, "parmmg_hip.h"), HIP_SO, __file__]
+    shard = os.path.join(CSRC, "pmmg_shard.c")
+    deps = [src, shard, os.path.join(CSRC, "pmmg_host.h"), os.path.join(INC, "parmmg_hip.h"), HIP_SO, __file__]
     if force or _stale(HOST_SO, deps):
         _run(["gcc", "-O2", "-std=c99", "-Wall", "-Wextra", "-fPIC", "-shared", f"-I{INC}", f"-I{CSRC}",
-              "-o", HOST_SO, src, f"-L{PKG}", "-lpmmg_hip", "-Wl,-rpath,$ORIGIN"])
+              "-o", HOST_SO, src, shard, f"-L{PKG}", "-lpmmg_hip", "-Wl,-rpath,$ORIGIN"])
     return HOST_SO
 
 

@@ -73,6 +73,30 @@ int pmmg_set_constant_metric(int np, int met_size, double hsiz, double *met);
 int pmmg_interp_metrics_and_fields(pmmg_hip_ctx *ctx, int ngrp, const pmmg_old_group *old, pmmg_new_group *grp,
                                    int input_met, double hsiz, pmmg_hip_stats *stats);
 
+/* ---- halo shards of a background group (pmmg_shard.c) ----
+ * All arrays in the "row r = entity r+1" layout of parmmg_hip.h. */
+
+/* Largest bounding-box side over the tetra (halo unit). */
+double pmmg_max_tet_extent(int np, const double *xyz, int ne, const int *tetv);
+
+/* Marks the tetra whose bounding box meets [box_lo - halo, box_hi + halo]
+ * (halo < 0: |halo| x pmmg_max_tet_extent) and their vertices:
+ * tet_map[ne] / vert_map[np] receive the 1-based local id in the shard or 0
+ * (ascending with the global id).  counts = {shard tetra, shard vertices}.
+ * Returns 1, or 0 on invalid input. */
+int pmmg_shard_mark(int np, const double *xyz, int ne, const int *tetv, const double box_lo[3],
+                    const double box_hi[3], double halo, int *tet_map, int *vert_map, int64_t counts[2]);
+
+/* Writes the shard: s_xyz[3*nv], s_tetv/s_adja[4*nk] (neighbours outside the
+ * shard -> 0), the boundary trias with all vertices in the shard
+ * s_triv/s_adjt (room for nt rows) and the 1-based global ids of the local
+ * tetra / vertices / trias (each optional).  Returns the shard's tria count,
+ * or -1 on invalid input. */
+int64_t pmmg_shard_fill(int np, const double *xyz, int ne, const int *tetv, const int *adja, int nt,
+                        const int *triv, const int *adjt, const int *tet_map, const int *vert_map,
+                        double *s_xyz, int *s_tetv, int *s_adja, int *s_triv, int *s_adjt, int *tet_gid,
+                        int *vert_gid, int *tria_gid);
+
 #ifdef __cplusplus
 }
 #endif

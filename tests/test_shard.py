@@ -1,0 +1,122 @@
+"""Halo-sharded background (parmmg_amd/shard.py, csrc/pmmg_shard.c).
+
+Each rank of a Morton split transfers its points against the halo shard of
+the background around its range; mapped back to group ids, the union of the
+ranks' results must satisfy the same parity contract (tests/parity.py) as a
+transfer against the whole group: identical tetra for class (i) points,
+accepted elements otherwise, reference values in the chosen element.
+The CPU cases run the oracle on the shards; the GPU case runs the HIP module.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from parity import check, make_case
+from parmmg_amd import ranks, shard, synth
+
+BDY_CODES = set(range(4, 12))
+
+
+def _shards(case, world, halo=shard.DEFAULT_HALO):
+    new, pc = case["new"], case["pclass"]
+    for mine in ranks.morton_shards(new.xyz, pc, world):
+        lo, hi = shard.range_box(new.xyz[mine])
+        yield mine, shard.halo_shard(case["bg"], lo, hi, halo)
+
+
+def _empty_result(case):
+    npn = case["new"].np
+    return dict(met=None if case["met"] is None else np.full((npn, case["met"].shape[1]), np.nan),
+                fields=[np.full((npn, f.shape[1]), np.nan) for f in case["fields"]],
+                elem=np.zeros(npn, np.int32), hit=np.zeros(npn, np.int8))
+
+
+def _scatter(full, mine, sh, met, fields, elem, hit):
+    code = hit.astype(np.int32) & 15
+    is_tria = np.isin(code, list(BDY_CODES))
+    full["elem"][mine] = sh.to_group_elem(elem, is_tria)
+    full["hit"][mine] = hit
+    if met is not None:
+        full["met"][mine] = met
+    for f, g in zip(full["fields"], fields):
+        f[mine] = g
+
+
+def test_shard_of_everything_is_the_group():
+    bg = synth.lattice(synth.SHELL, 8)
+    lo, hi = bg.xyz.min(axis=0), bg.xyz.max(axis=0)
+    sh = shard.halo_shard(bg, lo, hi, 0.0)
+    m = sh.mesh
+    for a, b in ((m.xyz, bg.xyz), (m.tetv, bg.tetv), (m.adja, bg.adja), (m.triv, bg.triv), (m.adjt, bg.adjt)):
+        assert np.array_equal(a, b)
+    assert np.array_equal(sh.tet_gid, np.arange(1, bg.ne + 1))
+
+
+@pytest.mark.parametrize("kind,n", [(synth.CUBE, 7), (synth.SHELL, 12)])
+def test_shard_structure(kind, n):
+    bg = synth.lattice(kind, n)
+    lo, hi = np.array([-0.1, -0.2, 0.0]), np.array([0.35, 0.3, 0.6])
+    sh = shard.halo_shard(bg, lo, hi)
+    m = sh.mesh
+    assert 0 < m.ne < bg.ne and np.all(np.diff(sh.tet_gid) > 0) and np.all(np.diff(sh.vert_gid) > 0)
+    # connectivity and coordinates are the group's, renumbered
+    assert np.array_equal(sh.vert_gid[m.tetv - 1], bg.tetv[sh.tet_gid - 1])
+    assert np.array_equal(m.xyz, bg.xyz[sh.vert_gid - 1])
+    assert np.array_equal(sh.vert_gid[m.triv - 1], bg.triv[sh.tria_gid - 1])
+    # adjacency: symmetric, the group's where the neighbour is kept, 0 across the cut
+    a = m.adja
+    k, f = np.nonzero(a > 0)
+    nb, nf = a[k, f] // 4 - 1, a[k, f] % 4
+    assert np.array_equal(a[nb, nf], 4 * (k + 1) + f)
+    assert np.array_equal(sh.tet_gid[nb], bg.adja[sh.tet_gid[k] - 1, f] // 4)
+    cut = (a == 0) & (bg.adja[sh.tet_gid - 1] > 0)
+    assert cut.any()
+    # every kept tetra meets the grown box; every tetra meeting the box is kept
+    box = lambda xyz, tv: (xyz[tv - 1].min(axis=1), xyz[tv - 1].max(axis=1))
+    tl, th = box(bg.xyz, bg.tetv)
+    meets = np.all((th >= lo - sh.halo) & (tl <= hi + sh.halo), axis=1)
+    assert np.array_equal(np.nonzero(meets)[0] + 1, sh.tet_gid)
+
+
+@pytest.mark.parametrize("kind,n_old,n_new,world", [(synth.CUBE, 6, 7, 2), (synth.CUBE, 5, 9, 3),
+                                                    (synth.SHELL, 8, 12, 2), (synth.SHELL, 8, 12, 4)])
+def test_halo_shards_oracle_parity(kind, n_old, n_new, world):
+    """Oracle on each rank's halo shard == contract of a transfer on the group."""
+    case = make_case(kind=kind, n_old=n_old, n_new=n_new)
+    full = _empty_result(case)
+    nshard = 0
+    for mine, sh in _shards(case, world):
+        B = O.Background(sh.mesh, None if case["met"] is None else sh.rows(case["met"]),
+                         [sh.rows(f) for f in case["fields"]], case["hausd"])
+        q = np.ascontiguousarray(case["new"].xyz[mine])
+        r = O.run(B, q, case["pclass"][mine], np.arange(1, len(mine) + 1, dtype=np.int32), O.MODE_FRESH)
+        hit = (r["hit"].astype(np.int32) | (np.maximum(r["loc"], 0).astype(np.int32) << 4)).astype(np.int8)
+        _scatter(full, mine, sh, r["met"], r["fields"], r["elem"], hit)
+        nshard += sh.mesh.ne
+    rep = check(case, full)
+    assert rep["n"] == int((case["pclass"] != 0).sum()) and rep["class_i"] == rep["class_i_same"] > 0
+    assert nshard < world * case["bg"].ne  # not replicas
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,n_old,n_new,world", [(synth.CUBE, 6, 7, 3), (synth.SHELL, 12, 16, 4)])
+def test_halo_shards_gpu_parity(kind, n_old, n_new, world):
+    from parmmg_amd.transfer import TransferContext
+
+    case = make_case(kind=kind, n_old=n_old, n_new=n_new)
+    full = _empty_result(case)
+    with TransferContext(0) as ctx:
+        for mine, sh in _shards(case, world):
+            m = sh.mesh
+            ctx.set_background(m.xyz, m.tetv, m.adja, m.triv, m.adjt, case["hausd"])
+            ctx.set_solutions(None if case["met"] is None else sh.rows(case["met"]),
+                              [sh.rows(f) for f in case["fields"]])
+            n = len(mine)
+            met = None if case["met"] is None else np.full((n, case["met"].shape[1]), np.nan)
+            fo = [np.full((n, f.shape[1]), np.nan) for f in case["fields"]]
+            elem, hit = np.zeros(n, np.int32), np.zeros(n, np.int8)
+            ctx.locate_interp(np.ascontiguousarray(case["new"].xyz[mine]), np.ascontiguousarray(case["pclass"][mine]),
+                              met, fo, elem, hit)
+            _scatter(full, mine, sh, met, fo, elem, hit)
+    rep = check(case, full)
+    assert rep["n"] == int((case["pclass"] != 0).sum()) and rep["class_i"] == rep["class_i_same"] > 0
