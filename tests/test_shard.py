@@ -120,3 +120,62 @@ def test_halo_shards_gpu_parity(kind, n_old, n_new, world):
             _scatter(full, mine, sh, met, fo, elem, hit)
     rep = check(case, full)
     assert rep["n"] == int((case["pclass"] != 0).sum()) and rep["class_i"] == rep["class_i_same"] > 0
+
+
+def _halo_worker(rank, world, port, q):
+    import os
+
+    import torch
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    ri = ranks.init("gloo")
+    case = make_case(kind=synth.SHELL, n_old=8, n_new=12, with_ref=False)  # the same problem on every rank
+    shards = ranks.morton_shards(case["new"].xyz, case["pclass"], world)
+    mine = shards[rank]
+    lo, hi = shard.range_box(case["new"].xyz[mine])
+    sh = shard.halo_shard(case["bg"], lo, hi)
+    B = O.Background(sh.mesh, sh.rows(case["met"]), [sh.rows(f) for f in case["fields"]], case["hausd"])
+    r = O.run(B, np.ascontiguousarray(case["new"].xyz[mine]), case["pclass"][mine],
+              np.arange(1, len(mine) + 1, dtype=np.int32), O.MODE_FRESH)
+    code = r["hit"].astype(np.int32)
+    gid = sh.to_group_elem(r["elem"], np.isin(code, list(BDY_CODES)))
+    hit = code | (np.maximum(r["loc"], 0).astype(np.int32) << 4)
+    rows = np.concatenate([gid[:, None], hit[:, None], r["met"]] + r["fields"], axis=1).astype(np.float64)
+    got = ranks.allgather_rows(ri, torch.from_numpy(rows), [len(s) for s in shards]).numpy()
+    q.put((rank, got, sh.mesh.ne))
+    ranks.finalize(ri)
+
+
+def test_gloo_two_ranks_halo_shards():
+    """world 2 (gloo): each rank transfers its Morton range against its own halo
+    shard; the gathered results meet the group's parity contract."""
+    import torch.multiprocessing as mp
+    from test_ranks import _free_port
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_halo_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {r: (g, ne) for r, g, ne in (q.get(timeout=120) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    case = make_case(kind=synth.SHELL, n_old=8, n_new=12)
+    assert np.array_equal(out[0][0], out[1][0])
+    assert all(ne < case["bg"].ne for _, ne in out.values())
+    order = np.concatenate(ranks.morton_shards(case["new"].xyz, case["pclass"], world))
+    got = out[0][0]
+    full = _empty_result(case)
+    full["elem"][order] = got[:, 0].astype(np.int32)
+    full["hit"][order] = got[:, 1].astype(np.int8)
+    c = 2
+    full["met"][order] = got[:, c:c + case["met"].shape[1]]
+    c += case["met"].shape[1]
+    for f in full["fields"]:
+        f[order] = got[:, c:c + f.shape[1]]
+        c += f.shape[1]
+    rep = check(case, full)
+    assert rep["n"] == len(order) and rep["class_i"] == rep["class_i_same"] > 0
