@@ -361,7 +361,7 @@ def main():
             "traffic_source": traffic_src,
             "algorithmic_bytes_per_stage": round(kvol_bytes),
             "stage": "volume stage of one transfer call: the walk and interpolation launches of its query chunks "
-                     "(overlapping on two streams), timed by HIP events from the first walk to the last "
+                     "(chunks overlap on two streams when PMMG_HIP_CHUNKS > 1), timed by HIP events from the first walk to the last "
                      "interpolation",
             "algorithmic_bytes_per_point": round(per_pt, 2),
         },

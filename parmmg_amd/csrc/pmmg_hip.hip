@@ -1266,6 +1266,88 @@ __device__ __forceinline__ void coop_slot(const Slot &sl, bool act, const int *v
   }
 }
 
+// Half-image variant (PMMG_HIP_COOP=2): a 6-double slot's 256 rows are
+// gathered in two passes of 128 rows (vertices 0-1, then 2-3 of the wave's 64
+// queries), so a wave's image is 768 doubles for every slot kind (6 KiB
+// instead of 12 KiB): LDS then admits 5 blocks per CU instead of 3.
+template <int PASS>
+__device__ __forceinline__ void coop_gather6_pair(const Slot &sl, const int *vid, double *img, double (*m)[6]) {
+  const int lane = __lane_id();
+  double2 b[6];
+#pragma unroll
+  for (int t = 0; t < 6; t++) {
+    const int p = 64 * t + lane, r = p / 3, k = p - 3 * r; // r in [0, 128): query r/2, vertex 2*PASS + r%2
+    const int v = vid[4 * (r >> 1) + 2 * PASS + (r & 1)];
+    b[t] = *reinterpret_cast<const double2 *>(sl.in + (size_t)sl.stride * (v - 1) + 2 * k);
+  }
+#pragma unroll
+  for (int t = 0; t < 6; t++) reinterpret_cast<double2 *>(img)[64 * t + lane] = b[t];
+  wait_lgkm();
+  __builtin_amdgcn_wave_barrier();
+  load6(img + 12 * lane, m[2 * PASS]);
+  load6(img + 12 * lane + 6, m[2 * PASS + 1]);
+  wait_lgkm();
+  __builtin_amdgcn_wave_barrier(); // every lane has read its rows: the image is free again
+}
+
+template <int C>
+__device__ __forceinline__ void coop_slot_half(const Slot &sl, bool act, const int *v, const double *phi,
+                                               const int *vid, double *img, size_t i0) {
+  if constexpr (C == 6) {
+    double m[4][6];
+    coop_gather6_pair<0>(sl, vid, img, m);
+    coop_gather6_pair<1>(sl, vid, img, m);
+    double mint[6], mi[6], r[6];
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < 4; i++) { // PMMG_interp4bar_ani, same order as coop_row<6>
+      ok = invmat(m[i], mi) && ok;
+#pragma unroll
+      for (int q = 0; q < 6; q++) mint[q] = (i == 0) ? phi[0] * mi[q] : mint[q] + phi[i] * mi[q];
+    }
+    ok = invmat(mint, r) && ok && act;
+    wave_store_rows<6>(sl.out + (size_t)6 * i0, r, __ballot(ok), img);
+  } else {
+    coop_slot<C>(sl, act, v, phi, vid, img, i0);
+  }
+}
+
+template <int C0, int C1, int C2, int C3, int C4, int C5>
+__global__ __launch_bounds__(kBlock) void k_vol_interp_coop_half(const uint8_t *pclass, int np, const int *vloc,
+                                                                 VRec vrec, Slots S, int *elem_out, int8_t *hit_out,
+                                                                 int i0q) {
+  __shared__ double img_all[kBlock / 64][256 * 3];
+  __shared__ int vid_all[kBlock / 64][256];
+  double *img = img_all[threadIdx.x >> 6];
+  int *vid = vid_all[threadIdx.x >> 6];
+  const int i = i0q + xcd_block() * blockDim.x + threadIdx.x;
+  bool act = i < np && __builtin_nontemporal_load(pclass + i) == PMMG_PT_VOL;
+  const int k = act ? __builtin_nontemporal_load(vloc + i) : 0;
+  act = act && k != 0;
+  if (!__any(act)) return;
+  VolLoc loc;
+  if (act) loc = vrec_load(vrec, i);
+  else { // idle lanes gather a valid row, never stored
+    loc.v = make_int4(1, 1, 1, 1);
+#pragma unroll
+    for (int f = 0; f < 4; f++) loc.phi[f] = 0.0;
+  }
+  const int v[4] = {loc.v.x, loc.v.y, loc.v.z, loc.v.w};
+  reinterpret_cast<int4 *>(vid)[__lane_id()] = loc.v;
+  wait_lgkm();
+  __builtin_amdgcn_wave_barrier();
+  const size_t w0 = (size_t)(i - __lane_id());
+  coop_slot_half<C0>(S.s[0], act, v, loc.phi, vid, img, w0);
+  coop_slot_half<C1>(S.s[1], act, v, loc.phi, vid, img, w0);
+  coop_slot_half<C2>(S.s[2], act, v, loc.phi, vid, img, w0);
+  coop_slot_half<C3>(S.s[3], act, v, loc.phi, vid, img, w0);
+  coop_slot_half<C4>(S.s[4], act, v, loc.phi, vid, img, w0);
+  coop_slot_half<C5>(S.s[5], act, v, loc.phi, vid, img, w0);
+  if (!act) return;
+  if (elem_out) __builtin_nontemporal_store(k, elem_out + i);
+  if (hit_out) __builtin_nontemporal_store((int8_t)PMMG_HIT_VOL_WALK, hit_out + i);
+}
+
 template <int C0, int C1, int C2, int C3, int C4, int C5>
 __global__ __launch_bounds__(kBlock) void k_vol_interp_coop(const uint8_t *pclass, int np, const int *vloc, VRec vrec,
                                                             Slots S, int *elem_out, int8_t *hit_out, int i0q) {
@@ -1797,12 +1879,14 @@ struct LayoutEntry {
   int c[6];
   VolInterpFn fn;
   VolInterpFn cfn; // cooperative-gather variant (nullptr: runtime layout)
+  VolInterpFn hfn; // cooperative gathers through a half-size image
   ScanInterpFn sfn;
   FusedFn ffn;
 };
 
 #define PMMG_LAYOUT(a, b, c, d, e, f)                                                                             \
   {{a, b, c, d, e, f}, k_vol_interp<a, b, c, d, e, f>, k_vol_interp_coop<a, b, c, d, e, f>,                     \
+   k_vol_interp_coop_half<a, b, c, d, e, f>,                                                                    \
    k_vol_interp_scan<a, b, c, d, e, f>,                                                                         \
    k_vol_fused<a, b, c, d, e, f>}
 // common slot layouts (metric first): aniso metric + scalar/vector/tensor
@@ -1815,7 +1899,7 @@ const LayoutEntry kLayouts[] = {
 };
 #undef PMMG_LAYOUT
 
-const LayoutEntry kGeneric = {{-1, 0, 0, 0, 0, 0}, k_vol_interp<-1, 0, 0, 0, 0, 0>, nullptr,
+const LayoutEntry kGeneric = {{-1, 0, 0, 0, 0, 0}, k_vol_interp<-1, 0, 0, 0, 0, 0>, nullptr, nullptr,
                                k_vol_interp_scan<-1, 0, 0, 0, 0, 0>, k_vol_fused<-1, 0, 0, 0, 0, 0>};
 
 const LayoutEntry &pick_layout(const Slots &S) {
@@ -1847,10 +1931,10 @@ struct pmmg_hip_ctx {
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr; // surface branch, concurrent with the volume walk
   hipStream_t stream3 = nullptr; // volume interpolation of chunk c, concurrent with the walk of chunk c+1
-  int coop = 1;         // cooperative row gathers in the interpolation (PMMG_HIP_COOP)
+  int coop = 2;         // row gathers: 0 per lane, 1 cooperative, 2 cooperative half image (PMMG_HIP_COOP)
   int seed8 = 1;        // queries pick the nearest of 8 cell seeds (PMMG_HIP_SEED8)
   int bbox_stride = 16; // frame from every 16th background vertex (PMMG_HIP_BBOXSTRIDE)
-  int chunks = 3;                // volume pipeline chunks (PMMG_HIP_CHUNKS)
+  int chunks = 1;                // volume pipeline chunks (PMMG_HIP_CHUNKS)
   hipEvent_t evc[kMaxChunks] = {};
   bool bdy_on_s2 = false;
   int two_streams = 1; // PMMG_HIP_STREAMS=1: everything on one stream
@@ -2449,7 +2533,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
                 : c->carry    ? (c->walkw >= 5 ? k_vol_walk<1, 5> : k_vol_walk<1, 1>)
                               : (c->walkw >= 5 ? k_vol_walk<0, 5> : k_vol_walk<0, 1>);
     const LayoutEntry &lay = pick_layout(S);
-    VolInterpFn interp = (c->coop && lay.cfn) ? lay.cfn : lay.fn;
+    VolInterpFn interp = (c->coop == 2 && lay.hfn) ? lay.hfn : (c->coop && lay.cfn) ? lay.cfn : lay.fn;
     const VRec vr = vrec_arrays(c->vrec.p, (size_t)np_new);
     // Pipelined volume stage: the queries are cut into `nch` contiguous
     // chunks; the interpolation of chunk j (bandwidth-bound) runs on stream3
