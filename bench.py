@@ -162,6 +162,32 @@ def snapshot_timing(ctx, bg, rank: int, reps: int = 3):
             "adjacency_algorithmic_gbps": round(b_adj / t_adj / 1e9, 1)}
 
 
+def quality_timing(ctx, w, d_qxyz, d_mo, rank: int, reps: int = 3):
+    """PMMG_tetraQual on the new mesh in the device-resident interpolated
+    metric (pmmg_hip_tetra_qual), timed on its own
+    after the step: wall time of the synchronous call, median of `reps`.
+    Compulsory bytes: 16 B tetv + 8 B qual per tetra, 24 + 8*met_size B per
+    vertex row."""
+    new_t = synth.lattice(w.kind, w.n_new, jitter=0.0, with_trias=False)  # connectivity only (same numbering)
+    d_tetv = ctx.upload(new_t.tetv)
+    ne = new_t.ne
+    del new_t
+    met = d_mo if w.met_size == 6 else None
+    times = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        qual, mn = ctx.tetra_qual(d_qxyz, d_tetv, met)
+        times.append(time.perf_counter() - t0)
+        qual.free()
+    d_tetv.free()
+    t = float(np.median(times))
+    nb = ne * (16 + 8) + d_qxyz.shape[0] * (24 + (8 * w.met_size if met is not None else 0))
+    log(f"[bench r{rank}] tetra quality of {ne} new tetra: {1e3 * t:.3f} ms, min {mn:.4f}")
+    return {"what": "pmmg_hip_tetra_qual (PMMG_tetraQual / MMG3D_tetraQual) in the interpolated metric, "
+                    "not part of the step", "tets": ne, "ms": round(1e3 * t, 3), "minqual": mn,
+            "algorithmic_gbps": round(nb / t / 1e9, 1)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -188,6 +214,8 @@ def main():
                          "shards of the background, results kept per rank (halo; strong scaling, SURVEY.md 8(e))")
     ap.add_argument("--halo", type=float, default=-1.0,
                     help="halo mode: growth of the range box (< 0: in largest-tetra extents)")
+    ap.add_argument("--no-quality", action="store_true",
+                    help="skip the (separately reported) tetra-quality timing of the new mesh")
     ap.add_argument("--no-snapshot", action="store_true",
                     help="skip the (separately reported) device background snapshot timing")
     args = ap.parse_args()
@@ -370,6 +398,11 @@ def main():
         out["allgather"] = gather
     if halo_info is not None:
         out["halo_shard"] = halo_info
+    if not args.no_quality and not split:
+        try:
+            out["tetra_qual"] = quality_timing(ctx, w, d_qxyz, d_mo, rank)
+        except Exception as e:  # reported, never fatal to the bench line
+            out["tetra_qual"] = {"error": str(e)}
     if not args.no_snapshot and halo_info is None:  # (a shard's cut faces are no boundary trias)
         out["snapshot"] = snapshot_timing(ctx, bg, rank)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and halo_info is None:

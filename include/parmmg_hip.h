@@ -212,6 +212,21 @@ int pmmg_hip_build_boundary(pmmg_hip_ctx *ctx, int np, int ne, const int *tet8,
                             const int *tetv, const int *adja, int cap, int *nt,
                             int *triv, int *adjt);
 
+/* Element quality in the interpolated metric:
+ * replaces MMG3D_tetraQual(mesh, met, 1) inside PMMG_tetraQual
+ * (src/quality_pmmg.c:720-733, called at src/libparmmg1.c:845).  Device
+ * pointers (the metric where pmmg_hip_locate_interp wrote it), synchronous:
+ *   qual[ne]   pt->qual of every tetra (Mmg's unscaled caltet value; 0 for
+ *              unused tetra, tetv row with v[0] <= 0)
+ *   *minqual   MMG3D_ALPHAD * min over used tetra (2 when none is used)
+ * met_size 0/1: geometric quality (MMG5_caltet_iso); 6: MMG5_caltet_ani with
+ * the metric averaged over the 4 vertices.  As in the reference, a caller
+ * treats *minqual == 0 as the "Quality computation problem" failure.
+ * Returns 1, or 0 on invalid arguments. */
+int pmmg_hip_tetra_qual(pmmg_hip_ctx *ctx, int np, const double *xyz, int ne,
+                        const int *tetv, int met_size, const double *met,
+                        double *qual, double *minqual);
+
 /* Device memory helpers for callers that keep data resident (bench, shims
  * that reuse buffers across iterations). */
 void *pmmg_hip_malloc(pmmg_hip_ctx *ctx, int64_t bytes);

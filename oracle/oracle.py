@@ -72,6 +72,8 @@ def lib():
         L.orc_cone_test.restype = ci
         L.orc_invmat.argtypes = [vp, vp]
         L.orc_invmat.restype = ci
+        L.orc_tetra_qual.argtypes = [ci, vp, ci, vp, ci, vp, vp]
+        L.orc_tetra_qual.restype = cd
         _lib = L
     return _lib
 
@@ -188,3 +190,14 @@ def invmat(m):
     mi = np.zeros(6)
     ok = lib().orc_invmat(_p(m), _p(mi))
     return bool(ok), mi
+
+
+def tetra_qual(xyz, tetv, met=None):
+    """MMG3D_tetraQual(mesh, met, 1) restated: (qual[ne], ALPHAD * min)."""
+    xyz = np.ascontiguousarray(xyz, np.float64)
+    tetv = np.ascontiguousarray(tetv, np.int32)
+    met = None if met is None else np.ascontiguousarray(met, np.float64)
+    qual = np.empty(tetv.shape[0], np.float64)
+    mn = lib().orc_tetra_qual(xyz.shape[0], _p(xyz), tetv.shape[0], _p(tetv), 0 if met is None else met.shape[1],
+                              _p(met), _p(qual))
+    return qual, mn

@@ -939,3 +939,83 @@ int orc_cone_test(const orc_background *bg, int k, int iloc, const double *x) {
   (void)any;
   return 1;
 }
+
+/* ---------------------------------------------------------------- tetra quality
+ * MMG3D_tetraQual / MMG5_caltet_iso / MMG5_caltet_ani (Mmg @889d408,
+ * src/mmg3d/quality_3d.c, restated; reached from PMMG_tetraQual,
+ * src/quality_pmmg.c:720-733).  Edges in the order ab, ac, ad, bc, bd, cd. */
+#define ORC_EPSD2  1.e-200 /* MMG5_EPSD2 */
+#define ORC_EPSOK  1.e-20  /* MMG5_EPSOK */
+#define ORC_ALPHAD 20.7846096908265 /* MMG3D_ALPHAD = 12 sqrt(3): a regular tetra has quality 1 */
+
+static void orc_edges(const double *p[4], double e[6][3]) {
+  static const int ea[6] = {0, 0, 0, 1, 1, 2}, eb[6] = {1, 2, 3, 2, 3, 3};
+  for (int i = 0; i < 6; i++)
+    for (int d = 0; d < 3; d++) e[i][d] = p[eb[i]][d] - p[ea[i]][d];
+}
+
+static double orc_vol6(double e[6][3]) {
+  /* (b-a) . ((c-a) x (d-a)) */
+  double v1 = e[1][1] * e[2][2] - e[1][2] * e[2][1];
+  double v2 = e[1][2] * e[2][0] - e[1][0] * e[2][2];
+  double v3 = e[1][0] * e[2][1] - e[1][1] * e[2][0];
+  return e[0][0] * v1 + e[0][1] * v2 + e[0][2] * v3;
+}
+
+static double orc_caltet_iso(const double *p[4]) {
+  double e[6][3];
+  orc_edges(p, e);
+  double vol = orc_vol6(e);
+  if (vol < ORC_EPSD2) return 0.0;
+  double rap = e[0][0] * e[0][0] + e[0][1] * e[0][1] + e[0][2] * e[0][2];
+  for (int i = 1; i < 6; i++) rap += e[i][0] * e[i][0] + e[i][1] * e[i][1] + e[i][2] * e[i][2];
+  if (rap < ORC_EPSD2) return 0.0;
+  rap = rap * sqrt(rap);
+  return vol / rap;
+}
+
+static double orc_caltet_ani(const double *p[4], const double *mm) {
+  double e[6][3], h[6];
+  orc_edges(p, e);
+  double vol = orc_vol6(e);
+  if (vol <= 0.0) return 0.0;
+  double det = mm[0] * (mm[3] * mm[5] - mm[4] * mm[4]) - mm[1] * (mm[1] * mm[5] - mm[2] * mm[4]) +
+               mm[2] * (mm[1] * mm[4] - mm[2] * mm[3]);
+  if (det < ORC_EPSOK) return 0.0;
+  det = sqrt(det) * vol;
+  for (int i = 0; i < 6; i++) {
+    const double x = e[i][0], y = e[i][1], z = e[i][2];
+    h[i] = mm[0] * x * x + mm[3] * y * y + mm[5] * z * z + 2.0 * (mm[1] * x * y + mm[2] * x * z + mm[4] * y * z);
+  }
+  double rap = h[0] + h[1] + h[2] + h[3] + h[4] + h[5];
+  double num = sqrt(rap) * rap;
+  return det / num;
+}
+
+double orc_tetra_qual(int np, const double *xyz, int ne, const int *tetv, int met_size, const double *met,
+                      double *qual) {
+  double minqual = 2.0 / ORC_ALPHAD;
+  (void)np;
+  for (int k = 0; k < ne; k++) {
+    const int *v = tetv + 4 * (int64_t)k;
+    if (v[0] <= 0) {
+      qual[k] = 0.0;
+      continue;
+    }
+    const double *p[4];
+    for (int i = 0; i < 4; i++) p[i] = xyz + 3 * (int64_t)(v[i] - 1);
+    double q;
+    if (met_size == 6) {
+      double mm[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+      for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 6; j++) mm[j] += met[6 * (int64_t)(v[i] - 1) + j];
+      for (int j = 0; j < 6; j++) mm[j] *= 0.25;
+      q = orc_caltet_ani(p, mm);
+    } else {
+      q = orc_caltet_iso(p);
+    }
+    qual[k] = q;
+    if (q < minqual) minqual = q;
+  }
+  return ORC_ALPHAD * minqual;
+}

@@ -128,6 +128,14 @@ int orc_cone_test(const orc_background *bg, int k, int iloc, const double *x);
 /* MMG5_invmat restated; exposed for unit tests. */
 int orc_invmat(const double *m, double *mi);
 
+/* MMG3D_tetraQual(mesh, met, 1) as PMMG_tetraQual calls it
+ * (src/quality_pmmg.c:720-733): qual[ne] = MMG5_caltet_iso (no aniso metric)
+ * or MMG5_caltet_ani (metric averaged over the vertices) of every tetra
+ * (0 for tetv rows with v[0] <= 0); returns MMG3D_ALPHAD * min.  Restated
+ * from Mmg's published source (unpinned). */
+double orc_tetra_qual(int np, const double *xyz, int ne, const int *tetv, int met_size, const double *met,
+                      double *qual);
+
 #ifdef __cplusplus
 }
 #endif

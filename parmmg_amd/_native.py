@@ -52,6 +52,8 @@ HIP_API = {
     "pmmg_hip_build_adjacency": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "pmmg_hip_build_boundary": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                                         c_void_p, c_void_p]),
+    "pmmg_hip_tetra_qual": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p,
+                                    P(c_double)]),
     "pmmg_hip_memcpy_h2d": (c_int, [c_void_p, c_void_p, c_void_p, c_int64]),
     "pmmg_hip_memcpy_d2h": (c_int, [c_void_p, c_void_p, c_void_p, c_int64]),
     "pmmg_hip_last_error": (c_char_p, [c_void_p]),

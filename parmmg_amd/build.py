@@ -56,11 +56,13 @@ def _stale(out: str, deps: list[str]) -> bool:
 def build_hip(force: bool = False) -> str:
     src = os.path.join(CSRC, "pmmg_hip.hip")
     snap = os.path.join(CSRC, "pmmg_snapshot.hip")
-    deps = [src, snap, os.path.join(CSRC, "pmmg_device.hpp"), os.path.join(CSRC, "pmmg_snapshot.hpp"),
+    qual = os.path.join(CSRC, "pmmg_quality.hip")
+    deps = [src, snap, qual, os.path.join(CSRC, "pmmg_device.hpp"), os.path.join(CSRC, "pmmg_snapshot.hpp"),
+            os.path.join(CSRC, "pmmg_quality.hpp"),
             os.path.join(INC, "parmmg_hip.h"), __file__]
     if force or _stale(HIP_SO, deps):
         _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
-              f"-I{INC}", "-o", HIP_SO, src, snap])
+              f"-I{INC}", "-o", HIP_SO, src, snap, qual])
     return HIP_SO
 
 

@@ -37,6 +37,7 @@
 
 #include "pmmg_device.hpp"
 #include "pmmg_snapshot.hpp"
+#include "pmmg_quality.hpp"
 
 using namespace pmmg;
 
@@ -1955,6 +1956,7 @@ struct pmmg_hip_ctx {
   // work buffers
   DevBuf frame, stats, grid, sgrid, cnt, off, binrank, order_v, order_b, vloc, scan_tmp, qs, cls_cnt, cls_cnt2;
   DevBuf cont, vrec;
+  DevBuf qmin; // tetra quality minimum (pmmg_hip_tetra_qual)
   DevBuf fb_vol, fb_bdy, best, ckey, cidx, bbest, bckey, bcidx;
   // host-mode staging
   DevBuf h_xyz, h_cls, h_met, h_elem, h_hit;
@@ -2098,7 +2100,7 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   DevBuf *bufs[] = {&c->cont, &c->vrec, &c->o_xyz, &c->o_tetv, &c->o_adja, &c->o_triv, &c->o_adjt, &c->o_met, &c->frame, &c->stats,
                     &c->grid, &c->sgrid, &c->cnt, &c->off, &c->binrank, &c->order_v, &c->order_b, &c->vloc, &c->qs,
                     &c->scan_tmp, &c->cls_cnt, &c->cls_cnt2, &c->fb_vol, &c->fb_bdy, &c->best, &c->ckey, &c->cidx, &c->bbest, &c->bckey,
-                    &c->bcidx, &c->h_xyz, &c->h_cls, &c->h_met, &c->h_elem, &c->h_hit};
+                    &c->bcidx, &c->h_xyz, &c->h_cls, &c->h_met, &c->h_elem, &c->h_hit, &c->qmin};
   for (DevBuf *b : bufs) release(*b);
   for (auto &b : c->o_f) release(b);
   for (auto &b : c->h_f) release(b);
@@ -2726,6 +2728,37 @@ int pmmg_hip_build_adjacency(pmmg_hip_ctx *c, int np, int ne, const int *tetv, i
     return 0;
   }
   return pmmg_snap_adjacency(c->stream, np, ne, tetv, adja, tet8, c->err, sizeof(c->err));
+}
+
+int pmmg_hip_tetra_qual(pmmg_hip_ctx *c, int np, const double *xyz, int ne, const int *tetv, int met_size,
+                        const double *met, double *qual, double *minqual) {
+  if (!c) return 0;
+  HIPCK(c, hipSetDevice(c->device));
+  if (np < 0 || ne < 0 || (ne > 0 && (!xyz || !tetv || !qual)) || !minqual ||
+      (met_size == 6 && ne > 0 && !met) || (met_size != 0 && met_size != 1 && met_size != 6)) {
+    set_err(c, "tetra_qual: invalid arguments (np=%d ne=%d met_size=%d)", np, ne, met_size);
+    return 0;
+  }
+  if (ne > 0 && !aligned16(tetv)) {
+    set_err(c, "tetra_qual: tetv must be 16-byte aligned");
+    return 0;
+  }
+  if (!ensure(c, c->qmin, sizeof(unsigned long long))) return 0;
+  unsigned long long bits = 0;
+  if (!pmmg_qual_tetra(c->stream, np, xyz, ne, tetv, met_size, met, qual, (unsigned long long *)c->qmin.p, &bits)) {
+    set_err(c, "tetra_qual: kernel launch or copy failed");
+    return 0;
+  }
+  // MMG3D_tetraQual: minqual starts at 2/ALPHAD, returns ALPHAD * minqual
+  const double alphad = 20.7846096908265; // MMG3D_ALPHAD = 12 sqrt(3): a regular tetra has quality 1
+  double mn = 2.0 / alphad;
+  if (bits != ~0ULL) {
+    double q;
+    memcpy(&q, &bits, sizeof q);
+    if (q < mn) mn = q;
+  }
+  *minqual = alphad * mn;
+  return 1;
 }
 
 int pmmg_hip_build_boundary(pmmg_hip_ctx *c, int np, int ne, const int *tet8, const int *tetv, const int *adja,

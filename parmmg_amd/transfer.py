@@ -230,6 +230,20 @@ class TransferContext:
                  "locate_interp")
         return st if (sync or where == HOST) else None
 
+    def tetra_qual(self, xyz, tetv, met=None, qual=None):
+        """PMMG_tetraQual's MMG3D_tetraQual(mesh, met, 1) on the device
+        (pmmg_hip_tetra_qual): device arrays (the metric where locate_interp
+        wrote it).  Returns (qual DeviceArray [ne], ALPHAD * min quality)."""
+        if not (_is_dev(xyz) and _is_dev(tetv) and (met is None or _is_dev(met))):
+            raise ValueError("tetra_qual takes device arrays")
+        ne = tetv.shape[0]
+        qual = qual if qual is not None else self.empty((ne,), np.float64)
+        mn = ctypes.c_double(0.0)
+        self._ck(self.lib.pmmg_hip_tetra_qual(self.h, xyz.shape[0], _p(xyz), ne, _p(tetv),
+                                              0 if met is None else int(met.shape[1]), _p(met), _p(qual),
+                                              ctypes.byref(mn)), "tetra_qual")
+        return qual, mn.value
+
     def sync(self) -> HipStats:
         st = HipStats()
         self._ck(self.lib.pmmg_hip_sync(self.h, ctypes.byref(st)), "sync")

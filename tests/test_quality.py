@@ -1,0 +1,95 @@
+"""Tetra quality in the interpolated metric:
+PMMG_tetraQual -> MMG3D_tetraQual(mesh, met, 1) (reference
+src/quality_pmmg.c:720-733, src/libparmmg1.c:845).  Mmg's caltet formulas are
+restated (parity unpinned at the Mmg boundary); the oracle is
+pinned by known answers: a regular tetra has quality 1, the aniso quality is
+invariant under uniform metric scaling and equals the iso quality of the
+tetra mapped by A for M = A^T A, flat and inverted tetra score 0.  The HIP
+kernel must match the oracle bit for bit."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from parmmg_amd import synth
+
+REG = np.array([[1, 1, 1], [-1, 1, -1], [1, -1, -1], [-1, -1, 1]], np.float64)  # positively oriented
+ONE = np.array([[1, 2, 3, 4]], np.int32)
+
+
+def _orient(p):
+    v = np.dot(p[1] - p[0], np.cross(p[2] - p[0], p[3] - p[0]))
+    return p if v > 0 else p[[0, 2, 1, 3]]
+
+
+def _sym6(M):
+    return np.array([M[0, 0], M[0, 1], M[0, 2], M[1, 1], M[1, 2], M[2, 2]])
+
+
+def test_regular_tetra_quality_one():
+    q, mn = O.tetra_qual(REG, ONE)
+    assert abs(mn - 1.0) < 1e-12
+    met = np.tile(_sym6(np.eye(3) * 7.5), (4, 1))
+    q2, mn2 = O.tetra_qual(REG, ONE, met)
+    assert abs(mn2 - 1.0) < 1e-12
+
+
+def test_aniso_equals_iso_of_mapped_tetra():
+    rng = np.random.default_rng(3)
+    for _ in range(50):
+        p = _orient(rng.normal(size=(4, 3)))
+        A = np.triu(rng.normal(size=(3, 3))) + 3 * np.eye(3)
+        M = A.T @ A
+        met = np.tile(_sym6(M), (4, 1))
+        _, qa = O.tetra_qual(p, ONE, met)
+        pa = p @ A.T
+        _, qi = O.tetra_qual(pa if np.linalg.det(A) > 0 else _orient(pa), ONE)
+        assert abs(qa - qi) <= 1e-10 * max(1.0, abs(qi))
+        _, qs = O.tetra_qual(p, ONE, 4.0 * met)  # uniform scaling of the metric
+        assert abs(qs - qa) <= 1e-12 * max(1.0, abs(qa))
+
+
+def test_degenerate_and_unused_tetra():
+    flat = REG.copy()
+    flat[3] = flat[1] + flat[2] - flat[0]  # exactly coplanar
+    q, mn = O.tetra_qual(flat, ONE)
+    assert q[0] == 0.0 and mn == 0.0
+    q, mn = O.tetra_qual(REG, ONE[:, [0, 2, 1, 3]])  # inverted
+    assert q[0] == 0.0 and mn == 0.0
+    q, mn = O.tetra_qual(REG, np.array([[0, 2, 3, 4]], np.int32))  # unused row (MG_EOK false)
+    assert q[0] == 0.0 and mn == 2.0  # MMG3D_tetraQual's start value 2/ALPHAD, scaled
+
+
+def test_lattice_quality_range():
+    m = synth.lattice(synth.CUBE, 4)
+    q, mn = O.tetra_qual(m.xyz, m.tetv)
+    assert 0 < mn < 1 and np.all(q > 0)
+    # Kuhn tetra are all congruent: one quality value
+    assert np.ptp(q) <= 1e-15 * q.max()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,n_old,n_new,metric", [(synth.CUBE, 6, 7, synth.F_ANI), (synth.SHELL, 8, 12, synth.F_ANI),
+                                                     (synth.CUBE, 6, 9, synth.F_ISO)])
+def test_tetra_qual_gpu_after_transfer(kind, n_old, n_new, metric):
+    """Transfer on the device, then the quality of the new mesh in the
+    device-resident interpolated metric: bit-identical to the oracle."""
+    from parmmg_amd.transfer import TransferContext
+
+    bg = synth.lattice(kind, n_old)
+    new = synth.lattice(kind, n_new, jitter=0.2)
+    met = synth.solution(metric, bg.xyz)
+    pc = synth.classes(new)
+    with TransferContext(0) as ctx:
+        d = dict(xyz=ctx.upload(bg.xyz), tetv=ctx.upload(bg.tetv), adja=ctx.upload(bg.adja),
+                 triv=ctx.upload(bg.triv), adjt=ctx.upload(bg.adjt), met=ctx.upload(met))
+        ctx.set_background(d["xyz"], d["tetv"], d["adja"], d["triv"], d["adjt"], 0.01)
+        ctx.set_solutions(d["met"], [])
+        q_xyz, q_pc, q_tetv = ctx.upload(new.xyz), ctx.upload(pc), ctx.upload(new.tetv)
+        mo = ctx.empty((new.np, met.shape[1]), np.float64)
+        ctx.locate_interp(q_xyz, q_pc, mo, [], sync=False)
+        ctx.sync()
+        qual, mn = ctx.tetra_qual(q_xyz, q_tetv, mo if met.shape[1] == 6 else None)
+        qual_h, met_h = qual.download(), mo.download()
+    q_ref, mn_ref = O.tetra_qual(new.xyz, new.tetv, met_h if met.shape[1] == 6 else None)
+    assert np.array_equal(qual_h, q_ref)
+    assert mn == mn_ref and 0 < mn <= 1.0
