@@ -92,4 +92,5 @@ def test_tetra_qual_gpu_after_transfer(kind, n_old, n_new, metric):
         qual_h, met_h = qual.download(), mo.download()
     q_ref, mn_ref = O.tetra_qual(new.xyz, new.tetv, met_h if met.shape[1] == 6 else None)
     assert np.array_equal(qual_h, q_ref)
-    assert mn == mn_ref and 0 < mn <= 1.0
+    # (jittered shell lattices hold a few flat / inverted tetra: quality 0)
+    assert mn == mn_ref and 0 <= mn <= 1.0 and (qual_h > 0).mean() > 0.9
