@@ -188,6 +188,35 @@ def quality_timing(ctx, w, d_qxyz, d_mo, rank: int, reps: int = 3):
             "algorithmic_gbps": round(nb / t / 1e9, 1)}
 
 
+def host_mode_timing(ctx, w, bg, met, fields, q_xyz, q_pc, rank: int, reps: int = 2):
+    """End-to-end rate with host buffers (PMMG_HIP_HOST: the background,
+    solutions and queries copied H2D and the outputs D2H inside the call, as a
+    shim that hands over MMG5 arrays without keeping them resident would),
+    reported beside the HBM-resident step, never as the bench value."""
+    from parmmg_amd.transfer import pack_tet8
+    tet8 = pack_tet8(bg.tetv, bg.adja)
+    nq = q_xyz.shape[0]
+    mo = np.empty((nq, w.met_size), np.float64)
+    fo = [np.empty((nq, f.shape[1]), np.float64) for f in fields]
+    elem, hit = np.empty(nq, np.int32), np.empty(nq, np.int8)
+    times = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        ctx.set_background_tet8(bg.xyz, tet8, bg.triv, bg.adjt, w.hausd)
+        ctx.set_solutions(met, fields)
+        st = ctx.locate_interp(q_xyz, q_pc, mo, fo, elem, hit)
+        times.append(time.perf_counter() - t0)
+    t = float(np.median(times))
+    nbytes = (bg.xyz.nbytes + tet8.nbytes + bg.triv.nbytes + bg.adjt.nbytes + met.nbytes + sum(f.nbytes for f in fields)
+              + q_xyz.nbytes + q_pc.nbytes + mo.nbytes + sum(f.nbytes for f in fo) + elem.nbytes + hit.nbytes)
+    npts = int(st.nvol + st.nbdy)
+    log(f"[bench r{rank}] host-buffer (PCIe-inclusive) call: {1e3 * t:.1f} ms, {nbytes / 1e9:.2f} GB moved")
+    return {"what": "one pmmg_hip_locate_interp with host (pageable) buffers: H2D of background, solutions and "
+                    "queries + the step + D2H of the outputs; not the bench value",
+            "ms": round(1e3 * t, 2), "mpts_per_s": round(npts / t / 1e6, 1), "bytes_moved": int(nbytes),
+            "pcie_gbps_effective": round(nbytes / t / 1e9, 1)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -214,6 +243,8 @@ def main():
                          "shards of the background, results kept per rank (halo; strong scaling, SURVEY.md 8(e))")
     ap.add_argument("--halo", type=float, default=-1.0,
                     help="halo mode: growth of the range box (< 0: in largest-tetra extents)")
+    ap.add_argument("--no-host-mode", action="store_true",
+                    help="skip the (separately reported) host-buffer, PCIe-inclusive call")
     ap.add_argument("--no-quality", action="store_true",
                     help="skip the (separately reported) tetra-quality timing of the new mesh")
     ap.add_argument("--no-snapshot", action="store_true",
@@ -398,6 +429,11 @@ def main():
         out["allgather"] = gather
     if halo_info is not None:
         out["halo_shard"] = halo_info
+    if not args.no_host_mode and world == 1 and args.solutions == "separate":
+        try:
+            out["host_mode"] = host_mode_timing(ctx, w, bg, met, fields, q_xyz, q_pc, rank)
+        except Exception as e:  # reported, never fatal to the bench line
+            out["host_mode"] = {"error": str(e)}
     if not args.no_quality and not split:
         try:
             out["tetra_qual"] = quality_timing(ctx, w, d_qxyz, d_mo, rank)
