@@ -977,14 +977,14 @@ struct ContEntry {
 // queries are order[0 .. st->nvol).  vloc is indexed by ip - 1.
 // CARRY selects walk_core_carry; MINW > 1 asks the compiler for that many
 // waves per SIMD (register budget 512 / MINW).
-template <int CARRY, int MINW>
-__global__ __launch_bounds__(kBlock, MINW) void k_vol_walk(Bg bg, const Frame *fr, const unsigned long long *grid,
+template <int CARRY, int MINW, int B = kBlock>
+__global__ __launch_bounds__(B, MINW) void k_vol_walk(Bg bg, const Frame *fr, const unsigned long long *grid,
                                                            int g, const double *qxyz, const uint8_t *pclass,
                                                            const int *order, int np, int *vloc, VRec vrec, int *fb,
                                                            ContEntry *cont, DevStats *st, int cap, int maxstep,
                                                            int i0) {
   __shared__ BlockStats bs;
-  __shared__ double slot_img[CARRY == 2 ? kBlock / 64 : 1][CARRY == 2 ? 12 * 64 : 1];
+  __shared__ double slot_img[CARRY == 2 ? B / 64 : 1][CARRY == 2 ? 12 * 64 : 1];
   const LaneSlots L{&slot_img[CARRY == 2 ? threadIdx.x >> 6 : 0][CARRY == 2 ? __lane_id() : 0]};
   bstats_init(&bs);
   __syncthreads();
@@ -1936,6 +1936,7 @@ struct pmmg_hip_ctx {
   int seed8 = 1;        // queries pick the nearest of 8 cell seeds (PMMG_HIP_SEED8)
   int bbox_stride = 16; // frame from every 16th background vertex (PMMG_HIP_BBOXSTRIDE)
   int chunks = 1;                // volume pipeline chunks (PMMG_HIP_CHUNKS)
+  int walkb = 64;                // walk block size, 64 or 256 (PMMG_HIP_WALKB)
   hipEvent_t evc[kMaxChunks] = {};
   bool bdy_on_s2 = false;
   int two_streams = 1; // PMMG_HIP_STREAMS=1: everything on one stream
@@ -2084,6 +2085,7 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   c->bbox_stride = env_int("PMMG_HIP_BBOXSTRIDE", c->bbox_stride);
   c->seed8 = env_flag("PMMG_HIP_SEED8", c->seed8);
   c->coop = env_flag("PMMG_HIP_COOP", c->coop);
+  c->walkb = env_int("PMMG_HIP_WALKB", c->walkb) == 256 ? 256 : 64;
   if (c->chunks > kMaxChunks) c->chunks = kMaxChunks;
   {
     hipDeviceProp_t prop;
@@ -2531,7 +2533,11 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   c->count_nvol = !sorted && !(c->options & PMMG_HIP_OPT_FUSED);
 
   if (!(c->options & PMMG_HIP_OPT_FUSED)) {
-    auto walk = c->carry == 2 ? (c->walkw >= 5 ? k_vol_walk<2, 5> : k_vol_walk<2, 1>)
+    // PMMG_HIP_WALKB=64: one-wave blocks (LDS slots then cap occupancy at
+    // 26 instead of 24 waves per CU)
+    const bool wb64 = c->carry == 2 && c->walkb == 64;
+    auto walk = wb64 ? k_vol_walk<2, 1, 64>
+                : c->carry == 2 ? (c->walkw >= 5 ? k_vol_walk<2, 5> : k_vol_walk<2, 1>)
                 : c->carry    ? (c->walkw >= 5 ? k_vol_walk<1, 5> : k_vol_walk<1, 1>)
                               : (c->walkw >= 5 ? k_vol_walk<0, 5> : k_vol_walk<0, 1>);
     const LayoutEntry &lay = pick_layout(S);
@@ -2550,7 +2556,8 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
       const int a = j * chunk, n = np_new - a < chunk ? np_new - a : chunk;
       if (n <= 0) break;
       const int np_j = nch > 1 ? a + n : np_new; // lanes at or past np_j are idle
-      hipLaunchKernelGGL(walk, dim3(blocks_for(n, 1 << 30)), dim3(kBlock), 0, s, bg, fr, grid, g, xyz_new, pclass,
+      hipLaunchKernelGGL(walk, dim3(wb64 ? (n + 63) / 64 : blocks_for(n, 1 << 30)), dim3(wb64 ? 64 : kBlock), 0, s,
+                         bg, fr, grid, g, xyz_new, pclass,
                          sorted ? (const int *)order_v : nullptr, np_j, (int *)c->vloc.p, vr, (int *)c->fb_vol.p,
                          (ContEntry *)c->cont.p, st, c->cap, c->maxstep, a);
       if (nch > 1) {

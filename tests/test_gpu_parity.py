@@ -133,3 +133,21 @@ def test_interp_gather_variants_identical(name, monkeypatch):
         for x, y in zip(([a["met"]] if a["met"] is not None else []) + a["fields"],
                         ([b["met"]] if b["met"] is not None else []) + b["fields"]):
             assert np.array_equal(x, y, equal_nan=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["cube-ani-6-7", "shell-iso-12-16"])
+def test_walk_block_sizes_identical(name, monkeypatch):
+    """One-wave walk blocks (PMMG_HIP_WALKB=64) locate and interpolate exactly
+    like the default 256-thread blocks."""
+    case = make_case(**CASES[name])
+    outs = {}
+    for wb in ("256", "64"):
+        monkeypatch.setenv("PMMG_HIP_WALKB", wb)  # read by pmmg_hip_create
+        outs[wb] = run_gpu(case, tet8=True)
+    rep = check(case, outs["64"])
+    assert rep["n"] == int((case["pclass"] != 0).sum()) and rep["class_i"] == rep["class_i_same"]
+    a, b = outs["256"], outs["64"]
+    assert np.array_equal(a["elem"], b["elem"]) and np.array_equal(a["hit"], b["hit"])
+    for x, y in zip([a["met"]] + a["fields"], [b["met"]] + b["fields"]):
+        assert np.array_equal(x, y, equal_nan=True)
