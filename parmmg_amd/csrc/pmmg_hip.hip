@@ -2043,6 +2043,16 @@ int pmmg_hip_device_count(void) {
   return n;
 }
 
+// The surface branch's stream: PMMG_HIP_S2PRIO=1 creates it with
+// the device's greatest priority, so its few blocks are dispatched ahead of
+// the walk's instead of after them.
+static bool create_stream2(pmmg_hip_ctx *c) {
+  int least = 0, greatest = 0;
+  if (env_flag("PMMG_HIP_S2PRIO", 0) && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+    return hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, greatest) == hipSuccess;
+  return hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) == hipSuccess;
+}
+
 pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   int n = pmmg_hip_device_count();
   if (n <= 0 || device < 0 || device >= n) {
@@ -2053,7 +2063,7 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   c->device = device;
   c->options = options;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
+      !create_stream2(c) ||
       hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess) {
     fprintf(stderr, "[parmmg_hip] cannot initialise device %d\n", device);
     delete c;
