@@ -1937,6 +1937,7 @@ struct pmmg_hip_ctx {
   int bbox_stride = 16; // frame from every 16th background vertex (PMMG_HIP_BBOXSTRIDE)
   int chunks = 1;                // volume pipeline chunks (PMMG_HIP_CHUNKS)
   int walkb = 64;                // walk block size, 64 or 256 (PMMG_HIP_WALKB)
+  int bdy_early = 0;             // surface kernel enqueued before the walk (PMMG_HIP_BDYEARLY)
   hipEvent_t evc[kMaxChunks] = {};
   bool bdy_on_s2 = false;
   int two_streams = 1; // PMMG_HIP_STREAMS=1: everything on one stream
@@ -2096,6 +2097,7 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   c->seed8 = env_flag("PMMG_HIP_SEED8", c->seed8);
   c->coop = env_flag("PMMG_HIP_COOP", c->coop);
   c->walkb = env_int("PMMG_HIP_WALKB", c->walkb) == 256 ? 256 : 64;
+  c->bdy_early = env_flag("PMMG_HIP_BDYEARLY", c->bdy_early);
   if (c->chunks > kMaxChunks) c->chunks = kMaxChunks;
   {
     hipDeviceProp_t prop;
@@ -2542,6 +2544,21 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   HIPCK(c, hipEventRecord(c->ev[2], s));
   c->count_nvol = !sorted && !(c->options & PMMG_HIP_OPT_FUSED);
 
+  // surface queries (k_bdy) on the surface branch's stream
+  auto launch_bdy = [&]() -> int {
+    HIPCK(c, hipEventRecord(c->ev[8], sb));
+    if (bg.nt > 0) {
+      hipLaunchKernelGGL(k_bdy, dim3(8 * blocks_for((np_new + 7) / 8, 256)), dim3(kBlock), 0, sb, bg, fr, sgrid, gs,
+                         xyz_new, order_b, S, elem_out, hit_out, (int *)c->fb_bdy.p, st, c->maxstep);
+      HIPCK(c, hipGetLastError());
+    }
+    HIPCK(c, hipEventRecord(c->ev[9], sb));
+    return 1;
+  };
+  // PMMG_HIP_BDYEARLY=1: enqueue k_bdy before the walk, so its blocks are
+  // dispatched ahead of the walk's instead of as the walk drains
+  if (c->bdy_on_s2 && c->bdy_early && !(c->options & PMMG_HIP_OPT_FUSED) && !launch_bdy()) return 0;
+
   if (!(c->options & PMMG_HIP_OPT_FUSED)) {
     // PMMG_HIP_WALKB=64: one-wave blocks (LDS slots then cap occupancy at
     // 26 instead of 24 waves per CU)
@@ -2597,13 +2614,8 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   }
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[3], s));
-  HIPCK(c, hipEventRecord(c->ev[8], sb));
-  if (bg.nt > 0) {
-    hipLaunchKernelGGL(k_bdy, dim3(8 * blocks_for((np_new + 7) / 8, 256)), dim3(kBlock), 0, sb, bg, fr, sgrid, gs,
-                       xyz_new, order_b, S, elem_out, hit_out, (int *)c->fb_bdy.p, st, c->maxstep);
-    HIPCK(c, hipGetLastError());
-  }
-  HIPCK(c, hipEventRecord(c->ev[9], sb));
+  const bool bdy_early = c->bdy_on_s2 && c->bdy_early && !(c->options & PMMG_HIP_OPT_FUSED);
+  if (!bdy_early && !launch_bdy()) return 0;
   if (c->bdy_on_s2) HIPCK(c, hipStreamWaitEvent(s, c->ev[9], 0));
   HIPCK(c, hipEventRecord(c->ev[4], s));
 

@@ -137,13 +137,15 @@ def test_interp_gather_variants_identical(name, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["cube-ani-6-7", "shell-iso-12-16"])
-def test_walk_block_sizes_identical(name, monkeypatch):
-    """One-wave walk blocks (PMMG_HIP_WALKB=64) locate and interpolate exactly
-    like the default 256-thread blocks."""
+@pytest.mark.parametrize("knob", ["PMMG_HIP_WALKB", "PMMG_HIP_BDYEARLY"])
+def test_walk_block_sizes_identical(name, knob, monkeypatch):
+    """One-wave walk blocks (PMMG_HIP_WALKB=64 vs 256) and the surface kernel
+    enqueued before the walk (PMMG_HIP_BDYEARLY=1 vs 0) locate and
+    interpolate exactly alike."""
     case = make_case(**CASES[name])
     outs = {}
-    for wb in ("256", "64"):
-        monkeypatch.setenv("PMMG_HIP_WALKB", wb)  # read by pmmg_hip_create
+    for wb, val in (("256", "256" if knob.endswith("WALKB") else "0"), ("64", "64" if knob.endswith("WALKB") else "1")):
+        monkeypatch.setenv(knob, val)  # read by pmmg_hip_create
         outs[wb] = run_gpu(case, tet8=True)
     rep = check(case, outs["64"])
     assert rep["n"] == int((case["pclass"] != 0).sum()) and rep["class_i"] == rep["class_i_same"]
