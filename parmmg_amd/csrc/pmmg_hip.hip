@@ -1313,12 +1313,11 @@ __device__ __forceinline__ void coop_slot_half(const Slot &sl, bool act, const i
   }
 }
 
-template <int C0, int C1, int C2, int C3, int C4, int C5>
-__global__ __launch_bounds__(kBlock) void k_vol_interp_coop_half(const uint8_t *pclass, int np, const int *vloc,
-                                                                 VRec vrec, Slots S, int *elem_out, int8_t *hit_out,
-                                                                 int i0q) {
-  __shared__ double img_all[kBlock / 64][256 * 3];
-  __shared__ int vid_all[kBlock / 64][256];
+template <int C0, int C1, int C2, int C3, int C4, int C5, int B = kBlock>
+__global__ __launch_bounds__(B) void k_vol_interp_coop_half(const uint8_t *pclass, int np, const int *vloc, VRec vrec,
+                                                            Slots S, int *elem_out, int8_t *hit_out, int i0q) {
+  __shared__ double img_all[B / 64][256 * 3];
+  __shared__ int vid_all[B / 64][256];
   double *img = img_all[threadIdx.x >> 6];
   int *vid = vid_all[threadIdx.x >> 6];
   const int i = i0q + xcd_block() * blockDim.x + threadIdx.x;
@@ -1881,13 +1880,14 @@ struct LayoutEntry {
   VolInterpFn fn;
   VolInterpFn cfn; // cooperative-gather variant (nullptr: runtime layout)
   VolInterpFn hfn; // cooperative gathers through a half-size image
+  VolInterpFn hfn64; // the same in one-wave blocks
   ScanInterpFn sfn;
   FusedFn ffn;
 };
 
 #define PMMG_LAYOUT(a, b, c, d, e, f)                                                                             \
   {{a, b, c, d, e, f}, k_vol_interp<a, b, c, d, e, f>, k_vol_interp_coop<a, b, c, d, e, f>,                     \
-   k_vol_interp_coop_half<a, b, c, d, e, f>,                                                                    \
+   k_vol_interp_coop_half<a, b, c, d, e, f>, k_vol_interp_coop_half<a, b, c, d, e, f, 64>,                      \
    k_vol_interp_scan<a, b, c, d, e, f>,                                                                         \
    k_vol_fused<a, b, c, d, e, f>}
 // common slot layouts (metric first): aniso metric + scalar/vector/tensor
@@ -1900,7 +1900,7 @@ const LayoutEntry kLayouts[] = {
 };
 #undef PMMG_LAYOUT
 
-const LayoutEntry kGeneric = {{-1, 0, 0, 0, 0, 0}, k_vol_interp<-1, 0, 0, 0, 0, 0>, nullptr, nullptr,
+const LayoutEntry kGeneric = {{-1, 0, 0, 0, 0, 0}, k_vol_interp<-1, 0, 0, 0, 0, 0>, nullptr, nullptr, nullptr,
                                k_vol_interp_scan<-1, 0, 0, 0, 0, 0>, k_vol_fused<-1, 0, 0, 0, 0, 0>};
 
 const LayoutEntry &pick_layout(const Slots &S) {
@@ -1938,6 +1938,7 @@ struct pmmg_hip_ctx {
   int chunks = 1;                // volume pipeline chunks (PMMG_HIP_CHUNKS)
   int walkb = 64;                // walk block size, 64 or 256 (PMMG_HIP_WALKB)
   int bdy_early = 0;             // surface kernel enqueued before the walk (PMMG_HIP_BDYEARLY)
+  int interpb = 256;             // half-image interpolation block size, 256 or 64 (PMMG_HIP_INTERPB)
   hipEvent_t evc[kMaxChunks] = {};
   bool bdy_on_s2 = false;
   int two_streams = 1; // PMMG_HIP_STREAMS=1: everything on one stream
@@ -2098,6 +2099,7 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   c->coop = env_flag("PMMG_HIP_COOP", c->coop);
   c->walkb = env_int("PMMG_HIP_WALKB", c->walkb) == 256 ? 256 : 64;
   c->bdy_early = env_flag("PMMG_HIP_BDYEARLY", c->bdy_early);
+  c->interpb = env_int("PMMG_HIP_INTERPB", c->interpb) == 64 ? 64 : 256;
   if (c->chunks > kMaxChunks) c->chunks = kMaxChunks;
   {
     hipDeviceProp_t prop;
@@ -2568,7 +2570,11 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
                 : c->carry    ? (c->walkw >= 5 ? k_vol_walk<1, 5> : k_vol_walk<1, 1>)
                               : (c->walkw >= 5 ? k_vol_walk<0, 5> : k_vol_walk<0, 1>);
     const LayoutEntry &lay = pick_layout(S);
-    VolInterpFn interp = (c->coop == 2 && lay.hfn) ? lay.hfn : (c->coop && lay.cfn) ? lay.cfn : lay.fn;
+    // PMMG_HIP_INTERPB=64: the half-image interpolation in one-wave blocks
+    const bool ib64 = c->coop == 2 && lay.hfn64 && c->interpb == 64;
+    VolInterpFn interp = ib64 ? lay.hfn64
+                         : (c->coop == 2 && lay.hfn) ? lay.hfn : (c->coop && lay.cfn) ? lay.cfn : lay.fn;
+    const int ib = ib64 ? 64 : kBlock;
     const VRec vr = vrec_arrays(c->vrec.p, (size_t)np_new);
     // Pipelined volume stage: the queries are cut into `nch` contiguous
     // chunks; the interpolation of chunk j (bandwidth-bound) runs on stream3
@@ -2590,7 +2596,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
       if (nch > 1) {
         HIPCK(c, hipEventRecord(c->evc[j], s));
         HIPCK(c, hipStreamWaitEvent(c->stream3, c->evc[j], 0));
-        hipLaunchKernelGGL(interp, dim3(blocks_for(n, 1 << 30)), dim3(kBlock), 0, c->stream3, pclass, np_j,
+        hipLaunchKernelGGL(interp, dim3((n + ib - 1) / ib), dim3(ib), 0, c->stream3, pclass, np_j,
                            (const int *)c->vloc.p, vr, S, elem_out, hit_out, a);
       }
     }
@@ -2603,7 +2609,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
       HIPCK(c, hipEventRecord(c->evc[nch - 1], c->stream3));
       HIPCK(c, hipStreamWaitEvent(s, c->evc[nch - 1], 0));
     } else {
-      hipLaunchKernelGGL(interp, dim3(blocks_for(np_new, 1 << 30)), dim3(kBlock), 0, s, pclass, np_new,
+      hipLaunchKernelGGL(interp, dim3((np_new + ib - 1) / ib), dim3(ib), 0, s, pclass, np_new,
                          (const int *)c->vloc.p, vr, S, elem_out, hit_out, 0);
     }
   } else {

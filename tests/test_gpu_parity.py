@@ -137,14 +137,15 @@ def test_interp_gather_variants_identical(name, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["cube-ani-6-7", "shell-iso-12-16"])
-@pytest.mark.parametrize("knob", ["PMMG_HIP_WALKB", "PMMG_HIP_BDYEARLY"])
+@pytest.mark.parametrize("knob", ["PMMG_HIP_WALKB", "PMMG_HIP_BDYEARLY", "PMMG_HIP_INTERPB"])
 def test_walk_block_sizes_identical(name, knob, monkeypatch):
     """One-wave walk blocks (PMMG_HIP_WALKB=64 vs 256) and the surface kernel
     enqueued before the walk (PMMG_HIP_BDYEARLY=1 vs 0) locate and
     interpolate exactly alike."""
     case = make_case(**CASES[name])
     outs = {}
-    for wb, val in (("256", "256" if knob.endswith("WALKB") else "0"), ("64", "64" if knob.endswith("WALKB") else "1")):
+    sized = knob.endswith("B") and not knob.endswith("EARLY")
+    for wb, val in (("256", "256" if sized else "0"), ("64", "64" if sized else "1")):
         monkeypatch.setenv(knob, val)  # read by pmmg_hip_create
         outs[wb] = run_gpu(case, tet8=True)
     rep = check(case, outs["64"])

@@ -47,7 +47,7 @@ def main():
         # "chain=16,sort=1;chain=0" -> TransferContext keyword sets (sort: 1 on, 0 off)
         for spec in args.variants.split(";"):
             kw = {}
-            for name in ("TPC", "SPC", "QPB", "MAXSTEP", "CAP", "SEEDMODE", "SEEDRUN", "STREAMS", "S2START", "CARRY", "WALKW", "SEEDGRID", "SEEDATOM", "RUNORDER", "CHUNKS", "BBOXSTRIDE", "SEED8", "COOP", "WALKB", "S2PRIO", "BDYEARLY"):
+            for name in ("TPC", "SPC", "QPB", "MAXSTEP", "CAP", "SEEDMODE", "SEEDRUN", "STREAMS", "S2START", "CARRY", "WALKW", "SEEDGRID", "SEEDATOM", "RUNORDER", "CHUNKS", "BBOXSTRIDE", "SEED8", "COOP", "WALKB", "S2PRIO", "BDYEARLY", "INTERPB"):
                 os.environ.pop("PMMG_HIP_" + name, None)
             for item in filter(None, spec.split(",")):
                 k, v = item.split("=")
@@ -55,7 +55,7 @@ def main():
                     tet8s.add(spec)
                 elif k == "packed":
                     packeds.add(spec)
-                elif k in ("tpc", "spc", "qpb", "maxstep", "cap", "seedmode", "seedrun", "streams", "s2start", "carry", "walkw", "seedgrid", "seedatom", "runorder", "chunks", "bboxstride", "seed8", "coop", "walkb", "s2prio", "bdyearly"):
+                elif k in ("tpc", "spc", "qpb", "maxstep", "cap", "seedmode", "seedrun", "streams", "s2start", "carry", "walkw", "seedgrid", "seedatom", "runorder", "chunks", "bboxstride", "seed8", "coop", "walkb", "s2prio", "bdyearly", "interpb"):
                     os.environ["PMMG_HIP_" + k.upper()] = v  # read by pmmg_hip_create
                 else:
                     kw[k] = bool(int(v)) if k in ("sort", "fused", "scan") else int(v)
