@@ -1,14 +1,25 @@
 """Benchmark of the old->new mesh transfer step (PMMG_interpMetricsAndFields).
 
-One step = one full pmmg_hip_locate_interp over one group: bbox + seed
-grids + Morton sort + volume/surface locate + metric/field interpolation +
+One step = one full pmmg_hip_locate_interp over one group: frame + seed
+grids + query order + volume/surface locate + metric/field interpolation +
 fallbacks, with every input already resident in HBM (device-mode C-ABI).
 
-Multi-GPU (torchrun, one process per GPU): every rank owns one group of the
-same size, exactly as ParMmg shards the step by group (the per-group work is
-independent, src/interpmesh_pmmg.c:690-730), so there is no collective in the
-data path and the scaling is weak.  `value` = points located+interpolated by
-all ranks / max-over-ranks step time.
+N = 1: the whole cfg4 group on one GPU.  N > 1 (torchrun, one process per
+GPU), default ``--shard halo``: every rank owns a contiguous Morton range of
+the new points against the halo shard of the background around that range
+(SURVEY.md §8(e)); the located elements and interpolated rows are collected
+with an RCCL all-gather after the timed steps (reported separately, outside
+the step: ParMmg consumes results per rank).  Strong scaling: `value` =
+points of the whole problem / max-over-ranks step time.  ``--shard morton``
+replicates the background instead; ``--shard group`` gives every rank its own
+group (weak scaling, ParMmg's per-group sharding).
+
+After the timed steps (rank 0, N = 1): the CPU baseline runs the oracle — a C
+restatement of the reference path — over ALL new points in the reference's
+visitation order on the host cores, and the GPU outputs of the last step are
+checked against that same run point by point (``parity``: class (i) identity,
+acceptance of every chosen element, values of the reference interpolator in
+it, bit-exact count and max relative error).
 
 Prints ONE JSON line (rank 0).
 """
@@ -26,10 +37,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from parmmg_amd import configs, ranks, synth  # noqa: E402
-from parmmg_amd.transfer import TransferContext  # noqa: E402
+from parmmg_amd.transfer import TransferContext, pack_tet8  # noqa: E402
 
 METRIC = "new-mesh points located+interpolated/sec (Mpts/s) and HBM GB/s, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+BOX_CPU_SHARE = 16     # host CPUs a one-GPU lease of the GPU pool gives a job
 
 
 def log(*a):
@@ -50,8 +62,8 @@ def build_workload(w: configs.Workload, rank: int):
 
 
 def pmc_traffic(workload: str):
-    """HBM bytes per launch of the dominant volume kernel from the newest
-    committed rocprofv3 PMC summary (profiles/rNN/pmc_<workload>.json, made by
+    """HBM bytes per call of the volume stage from the newest committed
+    rocprofv3 PMC summary (profiles/rNN*/pmc_<workload>.json, made by
     tools/prof_summary.py from FETCH_SIZE / WRITE_SIZE passes of this bench),
     or (None, None)."""
     import glob
@@ -62,51 +74,104 @@ def pmc_traffic(workload: str):
     try:
         with open(paths[-1]) as f:
             d = json.load(f)
-        return d.get("k_vol_hbm_bytes_per_call", d.get("k_vol_hbm_bytes_per_launch")), os.path.relpath(paths[-1], ROOT)
+        return d.get("k_vol_hbm_bytes_per_call"), os.path.relpath(paths[-1], ROOT)
     except Exception:
         return None, None
 
 
-def cpu_baseline(w, bg, new, met, fields, pclass, budget_s: float):
-    """The oracle (C restatement of the reference path) as `threads` parallel
-    workers on this host's cores, each a sequential reference run (warm start,
-    private visited flags) over a contiguous range of the new points, like one
-    MPI rank per group: the per-iteration precompute (faceAreas, triaNormals,
-    nodeTrias, which the reference's tim=2 timer includes,
-    src/libparmmg1.c:823-836) split over the threads, then locate+interpolate
-    until `budget_s` seconds are used; the full-step time is the precompute
-    plus the measured rate extrapolated to all points."""
+def host_cores() -> tuple[int, int]:
+    """(threads used, CPUs visible): the CPUs this process may run on, capped
+    at the pool's per-GPU share (a one-GPU box shows the whole machine)."""
+    try:
+        vis = len(os.sched_getaffinity(0))
+    except AttributeError:
+        vis = os.cpu_count() or 1
+    env = int(os.environ.get("PMMG_CPU_THREADS", "0"))
+    return (env or min(vis, BOX_CPU_SHARE)), vis
+
+
+def cpu_baseline(w, bg, met, fields, pclass, new, budget_s: float):
+    """The oracle (C restatement of the reference path) on this host's cores:
+    the per-iteration precompute (faceAreas, triaNormals, nodeTrias, inside
+    the reference's tim=2 timer, src/libparmmg1.c:823-836) split over the
+    threads, then ALL new points in the reference's visitation order (first
+    appearance in new-tetra order, src/interpmesh_pmmg.c:535-541) cut into one
+    contiguous range per thread, each a sequential reference run with warm
+    start and private visited flags (one MPI rank per group).  Returns the
+    report and the oracle's per-point outputs (the parity reference)."""
     from oracle import oracle as O
 
-    threads = int(os.environ.get("PMMG_CPU_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads, visible = host_cores()
+    t0 = time.time()
+    new_t = synth.lattice(w.kind, w.n_new, jitter=w.jitter_new, seed=synth.SEED, with_trias=False)
+    order = synth.visit_order(new_t)
+    del new_t
+    log(f"[bench] visit order of {order.shape[0]} points in {time.time() - t0:.1f}s; oracle on {threads} threads")
     B = O.Background(bg, met, fields, w.hausd)
-    order = np.arange(1, new.np + 1, dtype=np.int32)
     r = O.run(B, new.xyz, pclass, order, budget_s=budget_s, threads=threads)
     t_pre, t_loc = r["t_precompute"], r["t_locate"]
     nproc = int((r["hit"] != 0).sum())
     ntot = int((pclass != 0).sum())
     t_full = t_pre + t_loc * ntot / max(nproc, 1)
-    return {
+    frac = nproc / max(ntot, 1)
+    rep = {
         "value": round(ntot / t_full / 1e6, 4),
         "unit": "Mpts/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"oracle (C restatement of the reference path) as {threads} threads, one contiguous range of "
-                  f"new points each (like MPI ranks), on {w.name}: precompute over {bg.ne} tets ({t_pre:.2f}s) + "
-                  f"locate/interp of {nproc} of {ntot} points ({t_loc:.2f}s, time-bounded), rate extrapolated "
-                  f"to all points",
+        "sample": f"oracle (C restatement of the reference path) as {threads} threads ({visible} CPUs visible; "
+                  f"{BOX_CPU_SHARE} = the box's per-GPU CPU share), one contiguous range of the reference's "
+                  f"visitation order each (like MPI ranks), on {w.name}: precompute over {bg.ne} tets "
+                  f"({t_pre:.2f}s) + locate/interp of {nproc} of {ntot} points ({100 * frac:.1f}%, {t_loc:.2f}s)"
+                  + ("" if nproc == ntot else ", rate extrapolated to all points"),
         "t_precompute_s": round(t_pre, 3),
-        "t_sample_s": round(t_loc, 3),
-        "sample_points": nproc,
+        "t_locate_s": round(t_loc, 3),
+        "points_timed": nproc,
+        "points_total": ntot,
     }
+    return rep, B, r
 
 
-def allgather_timing(ri, d_mo, d_fo, d_elem, counts, mine, rank: int, reps: int = 3):
-    """Morton mode: collect every rank's located elements and interpolated
+def parity_report(B, new, pclass, gpu, ref) -> dict:
+    """The GPU outputs of the last step against the oracle run of the CPU
+    baseline, over every point the oracle processed (tests/parity.py
+    contract, oracle.check_batch)."""
+    from oracle import oracle as O
+
+    threads, _ = host_cores()
+    idx = np.nonzero(ref["hit"] != 0)[0].astype(np.int32)
+    t0 = time.time()
+    rep = O.check_batch(B, new.xyz, pclass, gpu["elem"], gpu["hit"], gpu["met"], gpu["fields"], idx=idx, ref=ref,
+                        threads=threads)
+    # points whose element and hit kind equal the oracle's must carry the
+    # oracle's own values bit for bit
+    same = (gpu["elem"][idx] == ref["elem"][idx]) & ((gpu["hit"][idx] & 15) == (ref["hit"][idx] & 15))
+    ident = np.ones(idx.shape[0], bool)
+    for a, b in zip(([gpu["met"]] if gpu["met"] is not None else []) + gpu["fields"],
+                    ([ref["met"]] if ref["met"] is not None else []) + ref["fields"]):
+        ident &= np.all((a[idx] == b[idx]) | (np.isnan(a[idx]) & np.isnan(b[idx])), axis=1)
+    out = {
+        "what": "GPU outputs of the timed step vs the oracle run of cpu_baseline, every point it processed",
+        "points": int(idx.shape[0]), "checked": rep["n"], "exact": rep["exact"],
+        "class_i": rep["class_i"], "class_i_same": rep["class_i_same"],
+        "accept_fail": rep["accept_fail"], "value_fail": rep["value_fail"], "unprocessed": rep["unprocessed"],
+        "maxrel": rep["maxrel"], "rel_tol": 1e-12,
+        "same_element_as_oracle": int(same.sum()),
+        "same_element_values_identical": int((same & ident).sum()),
+        "hits": rep["hits"],
+        "ok": bool(rep["accept_fail"] == 0 and rep["value_fail"] == 0 and rep["unprocessed"] == 0
+                   and rep["class_i"] == rep["class_i_same"] and rep["maxrel"] <= 1e-12
+                   and int((same & ~ident).sum()) == 0),
+        "check_s": round(time.time() - t0, 2),
+    }
+    return out
+
+
+def allgather_timing(ri, d_mo, d_fo, d_elem, counts, rank: int, reps: int = 3):
+    """Split modes: collect every rank's located elements and interpolated
     rows on every rank (ranks.allgather_rows: RCCL all_gather_into_tensor over
     xGMI), timed on its own after the timed steps (reported
-    separately; ParMmg itself consumes the results per rank).  Checks that the
-    gathered element ids cover every processed point."""
+    separately; ParMmg itself consumes the results per rank)."""
     import torch
 
     rows = torch.cat([d_mo] + list(d_fo), dim=1)
@@ -131,21 +196,20 @@ def allgather_timing(ri, d_mo, d_fo, d_elem, counts, mine, rank: int, reps: int 
 def snapshot_timing(ctx, bg, rank: int, reps: int = 3):
     """Device background snapshot (PMMG_create_oldGrp's
     adjacency / boundary trias / tria adjacency, pmmg_hip_build_*) timed on
-    its own, outside the transfer step: wall time of the synchronous calls
-    (scratch allocation included), median of `reps`, checked against the
-    host-built arrays the step uses."""
+    its own, outside the transfer step, checked against the host-built
+    arrays the step uses."""
     d_tetv = ctx.upload(bg.tetv)
     times = []
-    for _ in range(reps):
+    ok = True
+    for rep in range(reps):
         t0 = time.perf_counter()
         adja, tet8 = ctx.build_adjacency(bg.np, d_tetv, adja=False, tet8=True)
         t1 = time.perf_counter()
         triv, adjt = ctx.build_boundary(bg.np, tet8=tet8)
         t2 = time.perf_counter()
         times.append((t1 - t0, t2 - t1))
-        ok = bool(np.array_equal(adjt.download(), bg.adjt))
-        if _ == reps - 1:
-            from parmmg_amd.transfer import pack_tet8
+        ok = ok and bool(np.array_equal(adjt.download(), bg.adjt))
+        if rep == reps - 1:
             ok = ok and bool(np.array_equal(tet8.download(), pack_tet8(bg.tetv, bg.adja)))
             ok = ok and bool(np.array_equal(triv.download(), bg.triv))
         for a in (tet8, triv, adjt):
@@ -153,8 +217,7 @@ def snapshot_timing(ctx, bg, rank: int, reps: int = 3):
     d_tetv.free()
     t_adj = float(np.median([t[0] for t in times]))
     t_bdy = float(np.median([t[1] for t in times]))
-    # compulsory bytes: tetv in (16 B/tet), tet8 records out (32 B/tet)
-    b_adj = bg.ne * (16 + 32)
+    b_adj = bg.ne * (16 + 32)  # tetv in, tet8 records out
     log(f"[bench r{rank}] snapshot: adjacency {1e3 * t_adj:.2f} ms, boundary {1e3 * t_bdy:.2f} ms, match={ok}")
     return {"what": "pmmg_hip_build_adjacency (tet8 out) + pmmg_hip_build_boundary, not part of the step",
             "ms_adjacency": round(1e3 * t_adj, 3), "ms_boundary": round(1e3 * t_bdy, 3),
@@ -165,9 +228,7 @@ def snapshot_timing(ctx, bg, rank: int, reps: int = 3):
 def quality_timing(ctx, w, d_qxyz, d_mo, rank: int, reps: int = 3):
     """PMMG_tetraQual on the new mesh in the device-resident interpolated
     metric (pmmg_hip_tetra_qual), timed on its own
-    after the step: wall time of the synchronous call, median of `reps`.
-    Compulsory bytes: 16 B tetv + 8 B qual per tetra, 24 + 8*met_size B per
-    vertex row."""
+    after the step."""
     new_t = synth.lattice(w.kind, w.n_new, jitter=0.0, with_trias=False)  # connectivity only (same numbering)
     d_tetv = ctx.upload(new_t.tetv)
     ne = new_t.ne
@@ -189,32 +250,42 @@ def quality_timing(ctx, w, d_qxyz, d_mo, rank: int, reps: int = 3):
 
 
 def host_mode_timing(ctx, w, bg, met, fields, q_xyz, q_pc, rank: int, reps: int = 2):
-    """End-to-end rate with host buffers (PMMG_HIP_HOST: the background,
-    solutions and queries copied H2D and the outputs D2H inside the call, as a
-    shim that hands over MMG5 arrays without keeping them resident would),
-    reported beside the HBM-resident step, never as the bench value."""
-    from parmmg_amd.transfer import pack_tet8
-    tet8 = pack_tet8(bg.tetv, bg.adja)
+    """End-to-end rate with host buffers (PMMG_HIP_HOST), as the C host layer
+    runs a group inside ParMmg: the vertices and tetra vertex ids go up
+    through the context's pinned staging buffers, the adjacency and the
+    boundary trias are built on the device (PMMG_create_oldGrp's arrays, not
+    uploaded), then the solutions and queries go up, the step runs and the
+    rows it wrote come back.  Reported beside the HBM-resident step, never as
+    the bench value."""
     nq = q_xyz.shape[0]
     mo = np.empty((nq, w.met_size), np.float64)
     fo = [np.empty((nq, f.shape[1]), np.float64) for f in fields]
     elem, hit = np.empty(nq, np.int32), np.empty(nq, np.int8)
-    times = []
+    tb, ts, tl = [], [], []
     for _ in range(reps):
         t0 = time.perf_counter()
-        ctx.set_background_tet8(bg.xyz, tet8, bg.triv, bg.adjt, w.hausd)
+        ctx.set_background(bg.xyz, bg.tetv, None, None, None, w.hausd)
+        t1 = time.perf_counter()
         ctx.set_solutions(met, fields)
+        t2 = time.perf_counter()
         st = ctx.locate_interp(q_xyz, q_pc, mo, fo, elem, hit)
-        times.append(time.perf_counter() - t0)
-    t = float(np.median(times))
-    nbytes = (bg.xyz.nbytes + tet8.nbytes + bg.triv.nbytes + bg.adjt.nbytes + met.nbytes + sum(f.nbytes for f in fields)
-              + q_xyz.nbytes + q_pc.nbytes + mo.nbytes + sum(f.nbytes for f in fo) + elem.nbytes + hit.nbytes)
+        t3 = time.perf_counter()
+        tb.append(t1 - t0)
+        ts.append(t2 - t1)
+        tl.append(t3 - t2)
+    b, s_, l_ = (float(np.median(x)) for x in (tb, ts, tl))
+    t = b + s_ + l_
+    up = bg.xyz.nbytes + bg.tetv.nbytes + met.nbytes + sum(f.nbytes for f in fields) + q_xyz.nbytes + q_pc.nbytes
+    down = mo.nbytes + sum(f.nbytes for f in fo) + elem.nbytes + hit.nbytes
     npts = int(st.nvol + st.nbdy)
-    log(f"[bench r{rank}] host-buffer (PCIe-inclusive) call: {1e3 * t:.1f} ms, {nbytes / 1e9:.2f} GB moved")
-    return {"what": "one pmmg_hip_locate_interp with host (pageable) buffers: H2D of background, solutions and "
-                    "queries + the step + D2H of the outputs; not the bench value",
-            "ms": round(1e3 * t, 2), "mpts_per_s": round(npts / t / 1e6, 1), "bytes_moved": int(nbytes),
-            "pcie_gbps_effective": round(nbytes / t / 1e9, 1)}
+    log(f"[bench r{rank}] host-buffer (PCIe-inclusive) call: {1e3 * t:.1f} ms "
+        f"(background {1e3 * b:.1f}, solutions {1e3 * s_:.1f}, locate {1e3 * l_:.1f})")
+    return {"what": "one group through host buffers as the C host layer runs it: background (xyz + tetv up, "
+                    "adjacency and boundary trias built on the device), solutions up, queries up + the step + the "
+                    "written rows down; not the bench value",
+            "ms": round(1e3 * t, 2), "ms_background": round(1e3 * b, 2), "ms_solutions": round(1e3 * s_, 2),
+            "ms_locate_interp": round(1e3 * l_, 2), "mpts_per_s": round(npts / t / 1e6, 1),
+            "bytes_up": int(up), "bytes_down": int(down), "pcie_gbps_effective": round((up + down) / t / 1e9, 1)}
 
 
 def main():
@@ -224,25 +295,19 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="cfg4", choices=sorted(configs.SHORT))
     ap.add_argument("--sort", default="auto", choices=["auto", "on", "off"],
-                    help="query order: Morton binning (on), input order (off), or automatic")
-    ap.add_argument("--locate", default="walk", choices=["walk", "scan"],
-                    help="volume location: grid-seeded adjacency walks or the tetra-centric scan")
-    ap.add_argument("--fused", action="store_true", help="volume walk and interpolation as one kernel")
+                    help="query order: Morton binning (on), input order (off), or chosen on the device")
     ap.add_argument("--tpc", type=int, default=0, help="background tetra per volume seed cell (0: module default)")
-    ap.add_argument("--spc", type=int, default=0, help="sampled tetra per seed cell (0: module default)")
     ap.add_argument("--layout", default="tet8", choices=["tet8", "separate"],
                     help="HBM layout of the tetra: packed {v[4], adja[4]} records or separate tetv/adja arrays")
-    ap.add_argument("--solutions", default="separate", choices=["packed", "separate"],
-                    help="HBM layout of the metric/fields: packed per-vertex records or one array per solution")
-    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--shard", default="group", choices=["group", "morton", "halo"],
-                    help="multi-GPU split: one group per rank (weak scaling, ParMmg's own sharding); one problem "
-                         "cut into contiguous Morton ranges of the new points, background replicated, results "
-                         "all-gathered over RCCL after the timed steps (morton); or Morton ranges against halo "
-                         "shards of the background, results kept per rank (halo; strong scaling, SURVEY.md 8(e))")
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=90.0,
+                    help="cap of the CPU baseline's locate phase (it normally finishes every point first)")
+    ap.add_argument("--no-cpu-baseline", action="store_true", help="skip the CPU baseline (and the parity check)")
+    ap.add_argument("--shard", default="auto", choices=["auto", "group", "morton", "halo"],
+                    help="multi-GPU split (auto: halo for N > 1): Morton ranges of the new points against halo "
+                         "shards of the background (halo) or a replicated background (morton), results "
+                         "all-gathered over RCCL after the timed steps; or one group per rank (group, weak)")
     ap.add_argument("--halo", type=float, default=-1.0,
-                    help="halo mode: growth of the range box (< 0: in largest-tetra extents)")
+                    help="halo mode: growth of the range box (< 0: in largest-tetra extents, at least hausd)")
     ap.add_argument("--no-host-mode", action="store_true",
                     help="skip the (separately reported) host-buffer, PCIe-inclusive call")
     ap.add_argument("--no-quality", action="store_true",
@@ -259,26 +324,27 @@ def main():
     if backend != "nccl":
         import torch
         local = local % max(1, torch.cuda.device_count())
+    shard_mode = args.shard if args.shard != "auto" else ("halo" if world > 1 else "group")
 
     w = configs.SHORT[args.config]
-    split = args.shard in ("morton", "halo")
-    morton = args.shard == "morton"
-    # Morton / halo mode: every rank builds the same problem and keeps its range
+    split = shard_mode in ("morton", "halo")
+    # split modes: every rank builds the same problem and keeps its range
     bg, new, met, fields, pclass = build_workload(w, 0 if split else rank)
     ne_group = bg.ne
-    mine = None
+    counts = None
     halo_info = None
+    sh = None
     if split:
         shards = ranks.morton_shards(new.xyz, pclass, world)
         mine = shards[rank]
         counts = [len(x) for x in shards]
         q_xyz, q_pc = np.ascontiguousarray(new.xyz[mine]), np.ascontiguousarray(pclass[mine])
         log(f"[bench r{rank}] Morton range {len(mine)} of {int((pclass != 0).sum())} points")
-        if args.shard == "halo":
+        if shard_mode == "halo":
             from parmmg_amd import shard
             t_sh = time.time()
             lo, hi = shard.range_box(q_xyz)
-            sh = shard.halo_shard(bg, lo, hi, args.halo)
+            sh = shard.halo_shard(bg, lo, hi, args.halo, hausd=w.hausd)
             bg, met, fields = sh.mesh, sh.rows(met), [sh.rows(f) for f in fields]
             halo_info = {"what": "halo shard of the background around this rank's Morton range (rank 0)",
                          "tets": bg.ne, "verts": bg.np, "trias": bg.nt, "halo": sh.halo,
@@ -290,27 +356,19 @@ def main():
         q_xyz, q_pc = new.xyz, pclass
     nq = q_xyz.shape[0]
 
-    for name in ("tpc", "spc"):
-        if getattr(args, name) > 0:
-            os.environ["PMMG_HIP_" + name.upper()] = str(getattr(args, name))  # read by pmmg_hip_create
-    ctx = TransferContext(local, fused=args.fused, sort={"auto": None, "on": True, "off": False}[args.sort],
-                          scan=args.locate == "scan")
-    from parmmg_amd.transfer import pack_tet8
+    if args.tpc > 0:
+        os.environ["PMMG_HIP_TPC"] = str(args.tpc)  # read by pmmg_hip_create
+    ctx = TransferContext(local, sort={"auto": None, "on": True, "off": False}[args.sort])
     d_xyz = ctx.upload(bg.xyz)
     if args.layout == "tet8":
         d_tet8 = ctx.upload(pack_tet8(bg.tetv, bg.adja))
     else:
         d_tetv, d_adja = ctx.upload(bg.tetv), ctx.upload(bg.adja)
     d_triv, d_adjt = ctx.upload(bg.triv), ctx.upload(bg.adjt)
-    from parmmg_amd.transfer import pack_solutions
-    if args.solutions == "packed":
-        rec, *recmeta = pack_solutions(met, fields)
-        d_rec = ctx.upload(rec)
-    else:
-        d_met = ctx.upload(met)
-        d_f = [ctx.upload(f) for f in fields]
+    d_met = ctx.upload(met)
+    d_f = [ctx.upload(f) for f in fields]
     d_qxyz, d_pc = ctx.upload(q_xyz), ctx.upload(q_pc)
-    if morton:
+    if split:
         # outputs as torch tensors in HBM: the all-gather reads them in place
         import torch
         dev = torch.device("cuda", local)
@@ -328,10 +386,7 @@ def main():
             ctx.set_background_tet8(d_xyz, d_tet8, d_triv, d_adjt, w.hausd)
         else:
             ctx.set_background(d_xyz, d_tetv, d_adja, d_triv, d_adjt, w.hausd)
-        if args.solutions == "packed":
-            ctx.set_solutions_packed(d_rec, *recmeta)
-        else:
-            ctx.set_solutions(d_met, d_f)
+        ctx.set_solutions(d_met, d_f)
         ctx.locate_interp(d_qxyz, d_pc, d_mo, d_fo, d_elem, d_hit, sync=False)
 
     log(f"[bench r{rank}] inputs resident in HBM; warmup {args.warmup} steps")
@@ -343,14 +398,14 @@ def main():
     # timed region: barrier + device sync on both sides
     ranks.barrier(ri)
     ctx.sync()
-    ms_vol = []
-    ms_tot = []
+    ms_vol, ms_tot, ms_walk = [], [], []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
         st = ctx.sync()  # per-step event times of this step (sync adds no device work)
         ms_vol.append(st.ms_vol)
         ms_tot.append(st.ms_total)
+        ms_walk.append(st.ms_vol_locate)
     ranks.barrier(ri)
     ctx.sync()
     elapsed = time.perf_counter() - t0
@@ -359,9 +414,8 @@ def main():
     npts = int(st.nvol + st.nbdy)
     agg = ranks.aggregate(ri, npts, elapsed, args.steps)
     gather = None
-    if morton:
-        gather = allgather_timing(ri, d_mo, d_fo, d_elem, counts, mine, rank)
     if split:
+        gather = allgather_timing(ri, d_mo, d_fo, d_elem, counts, rank)
         npts = agg["points_per_step"]  # the whole problem: bytes per point below are per problem point
     ms_per_step = agg["ms_per_step"]
     value = agg["mpts_per_s"]
@@ -372,6 +426,7 @@ def main():
     kvol_bytes = per_pt * st.nvol
     achieved = kvol_bytes / (kvol_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(w.name)
+    steps_pp = st.steps_total / max(1, st.nvol + st.nbdy)
     out = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -389,39 +444,37 @@ def main():
             "workload": w.name,
             "description": w.description,
             "background_tets": ne_o, "background_verts": np_o, "new_points": np_n,
-            "located_points_per_gpu": npts, "K_doubles_per_vertex": w.K,
+            "located_points_per_step": npts, "K_doubles_per_vertex": w.K,
             "parallelism": (f"Morton-range shards x{world}, replicated background, RCCL all-gather after the step"
-                            if morton else
-                            f"Morton-range shards x{world}, halo-sharded background, results kept per rank"
-                            if split else f"one group per GPU x{world} (weak, no data-path collective)"),
+                            if shard_mode == "morton" else
+                            f"Morton-range shards x{world}, halo-sharded background, RCCL all-gather after the step"
+                            if shard_mode == "halo" else f"one group per GPU x{world} (weak, no data-path collective)"),
             "query_order": args.sort,
-            "locate": args.locate,
             "tetra_layout": args.layout,
-            "solution_layout": args.solutions,
-            "volume_kernels": "fused" if args.fused else "walk+interp",
             "morton_binned": bool(st.sorted),
         },
         "gbps_algorithmic_step": round(B / (ms_per_step * 1e-3) / 1e9, 1),
-        "device_ms": {"step_total": round(float(np.mean(ms_tot)), 4), "k_vol": round(kvol_ms, 4),
-                      "k_vol_locate": round(st.ms_vol_locate, 4),
-                      "prepare": round(st.ms_prepare, 4), "sort": round(st.ms_sort, 4),
-                      "k_bdy": round(st.ms_bdy, 4), "fallback": round(st.ms_fallback, 4)},
+        "device_ms": {"step_total": round(float(np.mean(ms_tot)), 4), "volume_stage": round(kvol_ms, 4),
+                      "walk": round(float(np.mean(ms_walk)), 4),
+                      "prepare": round(st.ms_prepare, 4), "order": round(st.ms_sort, 4),
+                      "k_bdy_stream": round(st.ms_bdy, 4), "fallback": round(st.ms_fallback, 4)},
         "locate_stats": {k: v for k, v in st.as_dict().items() if not k.startswith("ms_")},
+        "walk_steps_per_point": round(steps_pp, 3),
+        "lockstep_efficiency": round(st.steps_total / max(1, 64 * st.wave_iters), 3),
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_vol_fused" if args.fused else "k_vol_walk + k_vol_interp (volume stage)",
+            "kernel": "volume stage: k_vol_walk + k_vol_walk_exact + k_vol_interp",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "traffic_unit": "bytes per volume stage = all walk + interpolation launches of one call "
-                            "(FETCH_SIZE x2 + WRITE_SIZE)",
+            "traffic_unit": "bytes per volume stage (all walk + interpolation launches of one call; FETCH_SIZE "
+                            "calibrated per tools/calib, WRITE_SIZE)",
             "traffic_source": traffic_src,
             "algorithmic_bytes_per_stage": round(kvol_bytes),
-            "stage": "volume stage of one transfer call: the walk and interpolation launches of its query chunks "
-                     "(chunks overlap on two streams when PMMG_HIP_CHUNKS > 1), timed by HIP events from the first walk to the last "
-                     "interpolation",
+            "stage": "HIP events on the main stream from the end of the query order to the end of the "
+                     "interpolation (the surface kernel runs concurrently on a second stream)",
             "algorithmic_bytes_per_point": round(per_pt, 2),
         },
     }
@@ -429,11 +482,16 @@ def main():
         out["allgather"] = gather
     if halo_info is not None:
         out["halo_shard"] = halo_info
-    if not args.no_host_mode and world == 1 and args.solutions == "separate":
+    if not args.no_host_mode and world == 1:
         try:
             out["host_mode"] = host_mode_timing(ctx, w, bg, met, fields, q_xyz, q_pc, rank)
         except Exception as e:  # reported, never fatal to the bench line
             out["host_mode"] = {"error": str(e)}
+    gpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not split:
+        # outputs of the last timed step (the host-mode call used its own buffers)
+        gpu = {"elem": d_elem.download(), "hit": d_hit.download(), "met": d_mo.download(),
+               "fields": [f.download() for f in d_fo]}
     if not args.no_quality and not split:
         try:
             out["tetra_qual"] = quality_timing(ctx, w, d_qxyz, d_mo, rank)
@@ -441,12 +499,15 @@ def main():
             out["tetra_qual"] = {"error": str(e)}
     if not args.no_snapshot and halo_info is None:  # (a shard's cut faces are no boundary trias)
         out["snapshot"] = snapshot_timing(ctx, bg, rank)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and halo_info is None:
-        log(f"[bench r{rank}] cpu baseline (oracle) on a bounded sample")
-        out["cpu_baseline"] = cpu_baseline(w, bg, new, met, fields, pclass, args.cpu_baseline_seconds)
+    ctx.close()
+    if gpu is not None:
+        log(f"[bench r{rank}] cpu baseline (oracle) over all points")
+        out["cpu_baseline"], B_o, ref = cpu_baseline(w, bg, met, fields, pclass, new, args.cpu_baseline_seconds)
+        log(f"[bench r{rank}] parity of the GPU outputs against the oracle run")
+        out["parity"] = parity_report(B_o, new, pclass, gpu, ref)
+        log(f"[bench r{rank}] parity: {out['parity']}")
     if rank == 0:
         print(json.dumps(out), flush=True)
-    ctx.close()
     ranks.finalize(ri)
 
 

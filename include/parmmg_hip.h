@@ -29,11 +29,13 @@
  *    in tetv/triv are 1-based, adja holds 4*k'+i' (0 = boundary face,
  *    src/locate_pmmg.c:821), adjt holds 3*k'+i' (0 = surface border,
  *    src/locate_pmmg.c:635).
- *  - `where` = PMMG_HIP_HOST: pointers are host memory, calls copy and are
- *    synchronous.  `where` = PMMG_HIP_DEVICE: pointers are device memory on
+ *  - `where` = PMMG_HIP_HOST: pointers are host memory, calls copy (through
+ *    pinned staging buffers of the context) and are synchronous.  `where` = PMMG_HIP_DEVICE: pointers are device memory on
  *    the context's device; set_* calls only record the pointers (no copy) and
- *    pmmg_hip_locate_interp enqueues on the context stream (use
- *    pmmg_hip_sync before reading results or stats).
+ *    pmmg_hip_locate_interp only enqueues work on the context's streams (no
+ *    host synchronisation inside the call: every decision — query order,
+ *    fallback launches — is taken on the device); use pmmg_hip_sync before
+ *    reading results or stats.
  *  - The module is reentrant per context (the reference is not: it uses
  *    static warning flags and global function pointers).
  */
@@ -68,9 +70,6 @@ extern "C" {
 #define PMMG_HIT_BDY_EXHAUST  9  /* exhaustive tria scan: lowest-index accepted locate_pmmg.c:483-503 */
 #define PMMG_HIT_BDY_STALE   10  /* not located, re-evaluation accepted         locate_pmmg.c:505-509 */
 #define PMMG_HIT_BDY_CLOSEST 11  /* not located: closest tria, nearest vertex   locate_pmmg.c:511,681 */
-#define PMMG_HIT_VOL_SCAN    12  /* tetra-centric scan: lowest-index accepting tetra, i.e. the
-                                    reference's exhaustive semantics (locate_pmmg.c:743-762)
-                                    obtained for every query in one pass */
 
 #define PMMG_HIT_CODE(h) ((h) & 15)
 #define PMMG_HIT_LOC(h)  (((h) >> 4) & 3)
@@ -83,11 +82,13 @@ typedef struct {
   int64_t nvol;          /* volume queries */
   int64_t nbdy;          /* surface queries */
   int64_t nvol_walk, nvol_exhaust, nvol_closest;
-  int64_t nvol_scan;     /* volume queries located by the tetra-centric scan */
+  int64_t nvol_exact;    /* volume queries the fp32 filter walk handed to the exact (fp64) walk */
   int64_t nbdy_face, nbdy_edge, nbdy_vertex, nbdy_wedge, nbdy_cone;
   int64_t nbdy_exhaust, nbdy_stale, nbdy_closest;
   int64_t steps_total;   /* walk steps, volume + surface */
   int64_t stepmax;
+  int64_t wave_iters;    /* sum over wavefronts of their longest walk (lockstep cost; steps_total /
+                            (64 * wave_iters) = lockstep efficiency) */
   int64_t sorted;        /* 1 if the queries were Morton-binned, 0 if processed in input order */
   /* device time in milliseconds, measured with HIP events on the context stream */
   float ms_prepare;      /* bbox, seed grids, input-order coherence test */
@@ -100,16 +101,11 @@ typedef struct {
 } pmmg_hip_stats;
 
 /* Options (bit flags) for pmmg_hip_create.  Default: Morton-bin the queries
- * unless a sampled test finds the input numbering already spatially coherent
- * (mean distance between consecutive points < 4 mean spacings). */
+ * unless a sampled test on the device finds the input numbering already
+ * spatially coherent (median distance between consecutive points < 4 mean
+ * spacings). */
 #define PMMG_HIP_OPT_NOSORT 1   /* always process queries in input order */
 #define PMMG_HIP_OPT_SORT   2   /* always Morton-bin the queries */
-#define PMMG_HIP_OPT_SCAN   4   /* volume points by a tetra-centric scan (lowest-index accepting
-                                   tetra for every query) instead of per-query walks; pays off
-                                   only when the new mesh has many more points than the
-                                   background has tetra */
-#define PMMG_HIP_OPT_FUSED  8   /* volume walk and interpolation in one kernel (default: two kernels,
-                                   the walk at higher occupancy, the interpolation in query order) */
 
 /* Create a context on HIP device `device`.  Returns NULL on failure. */
 pmmg_hip_ctx *pmmg_hip_create(int device, int options);
@@ -121,7 +117,17 @@ void pmmg_hip_destroy(pmmg_hip_ctx *ctx);
  *   ne    tetrahedra, tetv[4*ne]     (MMG5_Tetra.v, packed), adja[4*ne] (= &mesh->adja[1])
  *   nt    boundary trias, triv[3*nt] (MMG5_Tria.v, packed),  adjt[3*nt] (= &mesh->adjt[1])
  *   hausd surface distance tolerance (oldMesh->info.hausd, src/locate_pmmg.c:253,315,363)
- * nt may be 0 (then no PMMG_PT_BDY query may be submitted). */
+ * What PMMG_create_oldGrp derives from the connectivity (src/grpsplit_pmmg.c:
+ * 350-415) may instead be built on the device:
+ *   adja == NULL            the tetra adjacency (MMG3D_hashTetra's result)
+ *   triv == NULL, nt < 0    the boundary trias, in (tetra, face) order oriented
+ *                           by MMG5_idir, and their adjacency (MMG5_chkBdryTria
+ *                           + MMG3D_hashTria for a single-material old mesh
+ *                           without input trias)
+ *   adjt == NULL, triv set  the tria adjacency (MMG3D_hashTria)
+ * In host mode this also spares the PCIe upload of those arrays (the
+ * adjacency is as large as the connectivity).  nt may be 0 (then no
+ * PMMG_PT_BDY query may be submitted). */
 int pmmg_hip_set_background(pmmg_hip_ctx *ctx, int np, const double *xyz,
                             int ne, const int *tetv, const int *adja,
                             int nt, const int *triv, const int *adjt,
@@ -143,24 +149,11 @@ int pmmg_hip_set_background_tet8(pmmg_hip_ctx *ctx, int np, const double *xyz,
  * storage m11,m12,m13,m22,m23,m33 as MMG5 stores it) and nfield fields of
  * size field_size[j] (1, 3 or 6; size 6 fields use the inverse-tensor
  * interpolation, src/interpmesh_pmmg.c:582-593,623-634).
- * met[met_size*np], fields[j][field_size[j]*np] (= sol->m + sol->size). */
+ * met[met_size*np], fields[j][field_size[j]*np] (= sol->m + sol->size).
+ * Device-mode size-6 arrays must be 16-byte aligned. */
 int pmmg_hip_set_solutions(pmmg_hip_ctx *ctx, int met_size, const double *met,
                            int nfield, const int *field_size,
                            const double *const *fields, int where);
-
-/* Same solutions as packed per-vertex records (the module's preferred HBM
- * layout: one vertex's metric and fields are one contiguous record, so the
- * interpolation gathers one record per tetra vertex instead of one row per
- * array):
- *   rec[stride*np]   record of vertex v at rec + stride*(v-1); stride even,
- *                    rec 16-byte aligned
- *   met_off          first column of the metric (met_size columns)
- *   field_off[j]     first column of field j (field_size[j] columns)
- * Size-6 slots must start at even columns.  A host shim builds the records
- * in the pass that copies met->m and field[j].m. */
-int pmmg_hip_set_solutions_packed(pmmg_hip_ctx *ctx, int met_size, int met_off,
-                                  int nfield, const int *field_size, const int *field_off,
-                                  const double *rec, int stride, int where);
 
 /* Locate every new point with pclass != PMMG_PT_SKIP and interpolate the
  * metric and fields into it.
@@ -202,15 +195,18 @@ int pmmg_hip_sync(pmmg_hip_ctx *ctx, pmmg_hip_stats *stats);
 int pmmg_hip_build_adjacency(pmmg_hip_ctx *ctx, int np, int ne, const int *tetv,
                              int *adja, int *tet8);
 
-/* Boundary trias: the faces with no neighbour, in (tetra, face) order, with
+/* Boundary trias: the faces with no neighbour — and, when tref[ne] (the
+ * tetra references, MMG5_Tetra.ref) is given, the faces towards a neighbour
+ * of smaller reference (MMG5_chkBdryTria's rule for a multi-material old mesh,
+ * restated from Mmg @889d408: unpinned) — in (tetra, face) order, with
  * vertices v[MMG5_idir[i]] (outward for positively oriented tetra), and their
  * adjacency adjt[3*nt] (3*t'+j' across edge j, 0 on borders and on edges of
  * more than two trias).  Tetra from tet8 (packed records) when non-NULL, else
  * from tetv + adja.  *nt receives the number of trias; when it exceeds `cap`
- * nothing is written and 0 is returned.  adjt may be NULL. */
+ * nothing is written and 0 is returned.  tref and adjt may be NULL. */
 int pmmg_hip_build_boundary(pmmg_hip_ctx *ctx, int np, int ne, const int *tet8,
-                            const int *tetv, const int *adja, int cap, int *nt,
-                            int *triv, int *adjt);
+                            const int *tetv, const int *adja, const int *tref,
+                            int cap, int *nt, int *triv, int *adjt);
 
 /* Element quality in the interpolated metric:
  * replaces MMG3D_tetraQual(mesh, met, 1) inside PMMG_tetraQual

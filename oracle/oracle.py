@@ -74,12 +74,26 @@ def lib():
         L.orc_invmat.restype = ci
         L.orc_tetra_qual.argtypes = [ci, vp, ci, vp, ci, vp, vp]
         L.orc_tetra_qual.restype = cd
+        L.orc_check_batch.argtypes = [vp, vp, vp, vp, ctypes.c_int64, vp, vp, vp, vp, vp, vp, vp, ci, cd, vp]
+        L.orc_check_batch.restype = ci
         _lib = L
     return _lib
 
 
 def _p(a):
     return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+class CheckReport(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int64), ("exact", ctypes.c_int64), ("class_i", ctypes.c_int64),
+                ("class_i_same", ctypes.c_int64), ("accept_fail", ctypes.c_int64), ("value_fail", ctypes.c_int64),
+                ("unprocessed", ctypes.c_int64), ("skipped_written", ctypes.c_int64), ("first_fail", ctypes.c_int64),
+                ("maxrel", ctypes.c_double), ("hits", ctypes.c_int64 * 16)]
+
+    def as_dict(self) -> dict:
+        d = {name: getattr(self, name) for name, _ in self._fields_ if name != "hits"}
+        d["hits"] = {h: int(self.hits[h]) for h in range(16) if self.hits[h]}
+        return d
 
 
 class Background:
@@ -183,6 +197,40 @@ def wedge_test(bg, k, l, x):
 
 def cone_test(bg, k, iloc, x):
     return lib().orc_cone_test(bg.ref, int(k), int(iloc), _p(np.ascontiguousarray(x, np.float64)))
+
+
+def check_batch(bg: Background, xyz, pclass, elem, hit, met_out, fields_out, idx=None, ref=None,
+                threads: int = 0, rel_tol: float = 1e-12) -> dict:
+    """The parity contract of tests/parity.py::check over many points in C
+    (orc_check_batch): acceptance of each point's element for its hit kind,
+    values of the reference interpolator in that element (bit-exact count,
+    max relative error), and with `ref` (an oracle run) class (i) identity.
+    idx: 0-based points to check (default: all)."""
+    xyz = np.ascontiguousarray(xyz, np.float64)
+    pclass = np.ascontiguousarray(pclass, np.uint8)
+    elem = np.ascontiguousarray(elem, np.int32)
+    hit = np.ascontiguousarray(hit, np.int8)
+    met_out = None if met_out is None else np.ascontiguousarray(met_out, np.float64)
+    fo = [np.ascontiguousarray(f, np.float64) for f in fields_out]
+    fpt = (ctypes.c_void_p * max(1, len(fo)))(*[_p(f) for f in fo])
+    if idx is None:
+        n = xyz.shape[0]
+    else:
+        idx = np.ascontiguousarray(idx, np.int32)
+        n = idx.shape[0]
+    r_elem = r_hit = r_mb = None
+    if ref is not None:
+        r_elem = np.ascontiguousarray(ref["elem"], np.int32)
+        r_hit = np.ascontiguousarray(ref["hit"], np.int8)
+        r_mb = np.ascontiguousarray(ref["minbary"], np.float64)
+    rep = CheckReport()
+    threads = threads or min(16, os.cpu_count() or 1)
+    ok = lib().orc_check_batch(bg.ref, _p(xyz), _p(pclass), _p(idx), int(n), _p(elem), _p(hit), _p(met_out),
+                               ctypes.cast(fpt, ctypes.c_void_p), _p(r_elem), _p(r_hit), _p(r_mb), int(threads),
+                               float(rel_tol), ctypes.byref(rep))
+    if not ok:
+        raise RuntimeError("orc_check_batch failed")
+    return rep.as_dict()
 
 
 def invmat(m):

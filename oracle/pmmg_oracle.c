@@ -27,7 +27,6 @@ static const int kIprv2[3] = {2, 0, 1};                                      /* 
 enum {
   HIT_NONE = 0, HIT_VOL_WALK, HIT_VOL_EXHAUST, HIT_VOL_CLOSEST, HIT_BDY_FACE, HIT_BDY_EDGE,
   HIT_BDY_VERTEX, HIT_BDY_WEDGE, HIT_BDY_CONE, HIT_BDY_EXHAUST, HIT_BDY_STALE, HIT_BDY_CLOSEST,
-  HIT_VOL_SCAN /* the module's tetra-centric scan: exhaustive semantics */
 };
 
 /* PMMG_barycoord, src/barycoord_pmmg.h:41-44 */
@@ -776,7 +775,7 @@ int orc_eval_in_element(const orc_background *bg, const double *x, int is_bdy, i
   bcoord b[4];
   if (!is_bdy) {
     if (elem < 1 || elem > bg->ne) return 0;
-    if (hit == HIT_VOL_WALK || hit == HIT_VOL_EXHAUST || hit == HIT_VOL_SCAN) {
+    if (hit == HIT_VOL_WALK || hit == HIT_VOL_EXHAUST) {
       double fa[12];
       double vol = tet_geom(bg, elem, fa);
       bc3d_evaluate(bg, elem, fa, vol, x, b);
@@ -940,11 +939,189 @@ int orc_cone_test(const orc_background *bg, int k, int iloc, const double *x) {
   return 1;
 }
 
+/* ---------------------------------------------------------------- batch parity check
+ * The contract of tests/parity.py::check (BASELINE.json north_star, SURVEY.md
+ * §8(a) row A1) for many points at once, over threads:
+ *  (ii)  the element each point was located in is accepted by the reference's
+ *        own test for its hit kind (walk / exhaustive / closest / tria /
+ *        wedge / cone / stale);
+ *  (iii) its values equal the reference interpolator evaluated in that
+ *        element (bitwise count + maximum relative error);
+ *  (i)   with a reference run given: points whose reference tetra has min
+ *        barycentric > EPS are located in the identical tetra. */
+static int same_bits(double a, double b) {
+  return (a == b) || (isnan(a) && isnan(b));
+}
+static double rel_err(double a, double b) {
+  if (isnan(a) && isnan(b)) return 0.0;
+  if (isnan(a) || isnan(b)) return INFINITY;
+  double d = fabs(a - b), s = fmax(fabs(a), fabs(b));
+  return s > 0.0 ? d / s : d;
+}
+
+typedef struct {
+  const orc_background *bg;
+  const double *xyz;
+  const uint8_t *pclass;
+  const int *idx;
+  int64_t i0, i1;
+  const int *elem;
+  const int8_t *hit;
+  const double *met_out;
+  const double *const *field_out;
+  const int *ref_elem;
+  const int8_t *ref_hit;
+  const double *ref_minbary;
+  double rel_tol;
+  orc_check_report rep;
+} chk_job;
+
+static void *job_check(void *arg) {
+  chk_job *J = (chk_job *)arg;
+  const orc_background *bg = J->bg;
+  orc_check_report *R = &J->rep;
+  int ms = bg->met_size, nf = bg->nfield;
+  double met_row[6], frow[64][6];
+  double *fptr[64];
+  for (int j = 0; j < nf && j < 64; j++) fptr[j] = frow[j];
+  for (int64_t t = J->i0; t < J->i1; t++) {
+    int64_t i = J->idx ? J->idx[t] : t;
+    int pc = J->pclass[i];
+    int h = J->hit[i] & 15, l = (J->hit[i] >> 4) & 3, k = J->elem[i];
+    if (pc == 0) {
+      if (h != 0) R->skipped_written++;
+      continue;
+    }
+    if (h == 0) {
+      R->unprocessed++;
+      if (R->first_fail < 0) R->first_fail = i;
+      continue;
+    }
+    R->hits[h]++;
+    const double *x = J->xyz + 3 * i;
+    int is_bdy = pc == 2, ok = 0;
+    switch (h) {
+      case HIT_VOL_WALK:
+        ok = !is_bdy && k >= 1 && k <= bg->ne && orc_tetra_minbary(bg, k, x) > -ORC_EPS;
+        break;
+      case HIT_VOL_EXHAUST:
+        ok = !is_bdy && k == orc_first_accepting_tetra(bg, x);
+        break;
+      case HIT_VOL_CLOSEST: {
+        int kb = orc_closest_tetra(bg, x);
+        ok = !is_bdy && orc_first_accepting_tetra(bg, x) == 0 && k >= 1 && k <= bg->ne &&
+             (k == kb || orc_closest_value(bg, k, x) == orc_closest_value(bg, kb, x));
+      } break;
+      case HIT_BDY_FACE: case HIT_BDY_EDGE: case HIT_BDY_VERTEX:
+        ok = is_bdy && k >= 1 && k <= bg->nt && orc_tria_accepts(bg, k, x, NULL);
+        break;
+      case HIT_BDY_WEDGE:
+        ok = is_bdy && k >= 1 && k <= bg->nt && in_wedge(bg, NULL, k, l, x, NULL) == 4;
+        break;
+      case HIT_BDY_CONE:
+        ok = is_bdy && k >= 1 && k <= bg->nt && orc_cone_test(bg, k, l, x) == 1;
+        break;
+      case HIT_BDY_EXHAUST:
+        ok = is_bdy && k == orc_first_accepting_tria(bg, x);
+        break;
+      case HIT_BDY_STALE: case HIT_BDY_CLOSEST:
+        ok = is_bdy && orc_first_accepting_tria(bg, x) == 0 && k == orc_closest_tria(bg, x);
+        break;
+      default:
+        ok = 0;
+    }
+    if (!ok) {
+      R->accept_fail++;
+      if (R->first_fail < 0) R->first_fail = i;
+      continue;
+    }
+    for (int c = 0; c < 6; c++) met_row[c] = NAN;
+    for (int j = 0; j < nf && j < 64; j++)
+      for (int c = 0; c < 6; c++) frow[j][c] = NAN;
+    if (!orc_eval_in_element(bg, x, is_bdy, k, h, l, ms ? met_row : NULL, fptr)) {
+      R->value_fail++;
+      if (R->first_fail < 0) R->first_fail = i;
+      continue;
+    }
+    int same = 1;
+    double rel = 0.0;
+    for (int c = 0; c < ms; c++) {
+      double g = J->met_out[(size_t)ms * i + c];
+      same = same && same_bits(g, met_row[c]);
+      rel = fmax(rel, rel_err(g, met_row[c]));
+    }
+    for (int j = 0; j < nf && j < 64; j++) {
+      int fs = bg->field_size[j];
+      for (int c = 0; c < fs; c++) {
+        double g = J->field_out[j][(size_t)fs * i + c];
+        same = same && same_bits(g, frow[j][c]);
+        rel = fmax(rel, rel_err(g, frow[j][c]));
+      }
+    }
+    R->n++;
+    R->exact += same;
+    if (rel > R->maxrel) R->maxrel = rel;
+    if (rel > J->rel_tol) {
+      R->value_fail++;
+      if (R->first_fail < 0) R->first_fail = i;
+    }
+    if (J->ref_elem && J->ref_hit) {
+      int rh = J->ref_hit[i] & 15;
+      double mb = J->ref_minbary ? J->ref_minbary[i] : 1.0;
+      if ((rh == HIT_VOL_WALK || rh == HIT_VOL_EXHAUST) && mb > ORC_EPS) {
+        R->class_i++;
+        if (J->ref_elem[i] == k) R->class_i_same++;
+        else if (R->first_fail < 0) R->first_fail = i;
+      }
+    }
+  }
+  return NULL;
+}
+
+int orc_check_batch(const orc_background *bg, const double *xyz, const uint8_t *pclass, const int *idx, int64_t n,
+                    const int *elem, const int8_t *hit, const double *met_out, const double *const *field_out,
+                    const int *ref_elem, const int8_t *ref_hit, const double *ref_minbary, int nthreads,
+                    double rel_tol, orc_check_report *rep) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  if (bg->nfield > 64) return 0;
+  chk_job *J = (chk_job *)calloc((size_t)nthreads, sizeof(chk_job));
+  pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+  if (!J || !th) {
+    free(J);
+    free(th);
+    return 0;
+  }
+  for (int t = 0; t < nthreads; t++) {
+    chk_job *j = &J[t];
+    j->bg = bg; j->xyz = xyz; j->pclass = pclass; j->idx = idx;
+    j->i0 = (n * t) / nthreads; j->i1 = (n * (t + 1)) / nthreads;
+    j->elem = elem; j->hit = hit; j->met_out = met_out; j->field_out = field_out;
+    j->ref_elem = ref_elem; j->ref_hit = ref_hit; j->ref_minbary = ref_minbary; j->rel_tol = rel_tol;
+    j->rep.first_fail = -1;
+    pthread_create(&th[t], NULL, job_check, j);
+  }
+  memset(rep, 0, sizeof(*rep));
+  rep->first_fail = -1;
+  for (int t = 0; t < nthreads; t++) {
+    pthread_join(th[t], NULL);
+    const orc_check_report *r = &J[t].rep;
+    rep->n += r->n; rep->exact += r->exact; rep->class_i += r->class_i; rep->class_i_same += r->class_i_same;
+    rep->accept_fail += r->accept_fail; rep->value_fail += r->value_fail; rep->unprocessed += r->unprocessed;
+    rep->skipped_written += r->skipped_written;
+    if (r->maxrel > rep->maxrel) rep->maxrel = r->maxrel;
+    for (int h = 0; h < 16; h++) rep->hits[h] += r->hits[h];
+    if (rep->first_fail < 0 && r->first_fail >= 0) rep->first_fail = r->first_fail;
+  }
+  free(J);
+  free(th);
+  return 1;
+}
+
 /* ---------------------------------------------------------------- tetra quality
  * MMG3D_tetraQual / MMG5_caltet_iso / MMG5_caltet_ani (Mmg @889d408,
  * src/mmg3d/quality_3d.c, restated; reached from PMMG_tetraQual,
  * src/quality_pmmg.c:720-733).  Edges in the order ab, ac, ad, bc, bd, cd. */
-#define ORC_EPSD2  1.e-200 /* MMG5_EPSD2 */
 #define ORC_EPSOK  1.e-20  /* MMG5_EPSOK */
 #define ORC_ALPHAD 20.7846096908265 /* MMG3D_ALPHAD = 12 sqrt(3): a regular tetra has quality 1 */
 

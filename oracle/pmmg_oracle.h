@@ -125,6 +125,29 @@ int orc_closest_tria(const orc_background *bg, const double *x);
 int orc_wedge_test(const orc_background *bg, int k, int l, const double *x);
 int orc_cone_test(const orc_background *bg, int k, int iloc, const double *x);
 
+/* Batch parity check (the contract of tests/parity.py::check) of a module's
+ * outputs over n points (idx[0..n) 0-based point ids, or all np points when
+ * idx is NULL and n == np), over nthreads threads.  ref_elem / ref_hit /
+ * ref_minbary: a reference run's per-point outputs (class (i) identity; may
+ * be NULL).  Returns 1 (report filled), 0 on invalid input. */
+typedef struct {
+  int64_t n;               /* points whose element was accepted and values evaluated */
+  int64_t exact;           /* of those, every value bit-identical */
+  int64_t class_i, class_i_same;
+  int64_t accept_fail;     /* element not accepted by the reference's test for its hit kind */
+  int64_t value_fail;      /* relative error above rel_tol (or not evaluable) */
+  int64_t unprocessed;     /* pclass != 0 but no hit code */
+  int64_t skipped_written; /* pclass == 0 but a hit code */
+  int64_t first_fail;      /* first failing point (0-based) or -1 */
+  double maxrel;
+  int64_t hits[16];
+} orc_check_report;
+
+int orc_check_batch(const orc_background *bg, const double *xyz, const uint8_t *pclass, const int *idx, int64_t n,
+                    const int *elem, const int8_t *hit, const double *met_out, const double *const *field_out,
+                    const int *ref_elem, const int8_t *ref_hit, const double *ref_minbary, int nthreads,
+                    double rel_tol, orc_check_report *rep);
+
 /* MMG5_invmat restated; exposed for unit tests. */
 int orc_invmat(const double *m, double *mi);
 

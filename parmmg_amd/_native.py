@@ -20,10 +20,10 @@ class HipStats(ctypes.Structure):
 
     _fields_ = [
         ("nvol", c_int64), ("nbdy", c_int64),
-        ("nvol_walk", c_int64), ("nvol_exhaust", c_int64), ("nvol_closest", c_int64), ("nvol_scan", c_int64),
+        ("nvol_walk", c_int64), ("nvol_exhaust", c_int64), ("nvol_closest", c_int64), ("nvol_exact", c_int64),
         ("nbdy_face", c_int64), ("nbdy_edge", c_int64), ("nbdy_vertex", c_int64), ("nbdy_wedge", c_int64),
         ("nbdy_cone", c_int64), ("nbdy_exhaust", c_int64), ("nbdy_stale", c_int64), ("nbdy_closest", c_int64),
-        ("steps_total", c_int64), ("stepmax", c_int64), ("sorted", c_int64),
+        ("steps_total", c_int64), ("stepmax", c_int64), ("wave_iters", c_int64), ("sorted", c_int64),
         ("ms_prepare", ctypes.c_float), ("ms_sort", ctypes.c_float), ("ms_vol", ctypes.c_float),
         ("ms_bdy", ctypes.c_float), ("ms_fallback", ctypes.c_float), ("ms_total", ctypes.c_float),
         ("ms_vol_locate", ctypes.c_float),
@@ -42,16 +42,14 @@ HIP_API = {
     "pmmg_hip_set_background_tet8": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p,
                                              c_double, c_int]),
     "pmmg_hip_set_solutions": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int]),
-    "pmmg_hip_set_solutions_packed": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int,
-                                              c_int]),
     "pmmg_hip_locate_interp": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                        c_void_p, P(HipStats), c_int]),
     "pmmg_hip_sync": (c_int, [c_void_p, P(HipStats)]),
     "pmmg_hip_malloc": (c_void_p, [c_void_p, c_int64]),
     "pmmg_hip_free": (c_int, [c_void_p, c_void_p]),
     "pmmg_hip_build_adjacency": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
-    "pmmg_hip_build_boundary": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
-                                        c_void_p, c_void_p]),
+    "pmmg_hip_build_boundary": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                                        c_void_p, c_void_p, c_void_p]),
     "pmmg_hip_tetra_qual": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p,
                                     P(c_double)]),
     "pmmg_hip_memcpy_h2d": (c_int, [c_void_p, c_void_p, c_void_p, c_int64]),
@@ -99,6 +97,10 @@ def synth_lib() -> ctypes.CDLL:
 
 
 HOST_API = {
+    "pmmg_classify_points": (c_int64, [c_void_p, c_void_p]),
+    "pmmg_copy_metrics_and_fields_point": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int]),
+    "pmmg_set_constant_metric": (c_int, [c_void_p]),
+    "pmmg_interp_metrics_and_fields": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, P(HipStats)]),
     "pmmg_max_tet_extent": (c_double, [c_int, c_void_p, c_int, c_void_p]),
     "pmmg_shard_mark": (c_int, [c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_double, c_void_p,
                                 c_void_p, P(c_int64)]),

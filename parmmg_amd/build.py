@@ -57,9 +57,9 @@ def build_hip(force: bool = False) -> str:
     src = os.path.join(CSRC, "pmmg_hip.hip")
     snap = os.path.join(CSRC, "pmmg_snapshot.hip")
     qual = os.path.join(CSRC, "pmmg_quality.hip")
-    deps = [src, snap, qual, os.path.join(CSRC, "pmmg_device.hpp"), os.path.join(CSRC, "pmmg_snapshot.hpp"),
-            os.path.join(CSRC, "pmmg_quality.hpp"),
-            os.path.join(INC, "parmmg_hip.h"), __file__]
+    deps = [src, snap, qual, os.path.join(INC, "parmmg_hip.h"), __file__] + [
+        os.path.join(CSRC, h) for h in ("pmmg_device.hpp", "pmmg_prep.hpp", "pmmg_vol.hpp", "pmmg_bdy.hpp",
+                                        "pmmg_fallback.hpp", "pmmg_snapshot.hpp", "pmmg_quality.hpp")]
     if force or _stale(HIP_SO, deps):
         _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
               f"-I{INC}", "-o", HIP_SO, src, snap, qual])

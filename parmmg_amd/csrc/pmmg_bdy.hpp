@@ -1,0 +1,132 @@
+// pmmg_bdy.hpp — surface (MG_BDY) points of the transfer step (included by
+// pmmg_hip.hip only): PMMG_locatePointBdy (locate_pmmg.c:587-723) with the
+// wedge / cone tests and the surface interpolation (interpmesh_pmmg.c:550-599).
+#pragma once
+
+#include "pmmg_prep.hpp"
+
+namespace pmmg {
+
+// one surface query; returns the hit code (0 = not located: exhaustive list)
+__device__ __forceinline__ int bdy_query(const Bg &bg, const Frame *fr, const int *sgrid, int gs, const double *qxyz,
+                                         int ip, const Slots &S, int *elem_out, int8_t *hit_out, int maxstep,
+                                         int &steps) {
+  int hit = 0;
+  double x[3];
+  load_pt(qxyz, ip, x);
+  int k = seed_srf(sgrid, gs, fr, x);
+  if (k == 0) return 0;
+  int hist[kHist];
+#pragma unroll
+  for (int h = 0; h < kHist; h++) hist[h] = 0;
+  int edge = -1, vertex = -1;
+  TriGeom t;
+  double phi[3];
+  for (;;) {
+    ++steps;
+    tri_load(bg, k, t);
+    double b[3];
+    double dist = tri_bary(x, t.p, t.q, t.n, b);
+    int r[3];
+    ranks3(b, r);
+    double bmin = b[0];
+    bmin = b[1] < bmin ? b[1] : bmin;
+    bmin = b[2] < bmin ? b[2] : bmin;
+    phi[0] = b[0];
+    phi[1] = b[1];
+    phi[2] = b[2];
+    // PMMG_locatePointInTria: inside and |dist| <= hausd
+    if (bmin > -kEps && !(fabs(dist) > bg.hausd)) {
+      // PMMG_barycoord_isBorder on the sorted coordinates
+      int f0 = r[0] == 0 ? 0 : (r[1] == 0 ? 1 : 2);
+      int f1 = r[0] == 1 ? 0 : (r[1] == 1 ? 1 : 2);
+      int f2 = r[0] == 2 ? 0 : (r[1] == 2 ? 1 : 2);
+      double b1 = sel3d(b[0], b[1], b[2], f1);
+      hit = PMMG_HIT_BDY_FACE;
+      if (bmin < kEps) {
+        if (b1 < kEps) {
+          vertex = f2;
+          hit = PMMG_HIT_BDY_VERTEX;
+        } else {
+          edge = f0;
+          hit = PMMG_HIT_BDY_EDGE;
+        }
+      }
+      break;
+    }
+    // step through the first edge (sorted order) whose neighbour exists; a
+    // visited neighbour triggers the wedge test of that edge and, outside
+    // it, the cone test of the wedge's end vertex (locate_pmmg.c:629-668)
+    const int *ad = bg.adjt + 3 * (size_t)(k - 1);
+    const int a0 = ad[0], a1 = ad[1], a2 = ad[2];
+    int next = 0;
+    bool done = false;
+    for (int j = 0; j < 3 && !done && next == 0; j++) {
+      int f = r[0] == j ? 0 : (r[1] == j ? 1 : 2);
+      int k1 = sel3i(a0, a1, a2, f) / 3;
+      if (!k1) continue;
+      bool vis = false;
+#pragma unroll
+      for (int h = 0; h < kHist; h++) vis = vis || (hist[h] == k1);
+      if (vis) {
+        double w[3];
+        int il = tri_wedge(bg.hausd, t, f, x, w);
+        if (il < 0) continue;
+        if (il == 4) {
+          phi[0] = w[0];
+          phi[1] = w[1];
+          phi[2] = w[2];
+          edge = f;
+          hit = PMMG_HIT_BDY_WEDGE;
+          done = true;
+        } else if (tri_cone(bg, k, il, t, x)) {
+          vertex = il;
+          hit = PMMG_HIT_BDY_CONE;
+          done = true;
+        }
+        continue;
+      }
+      next = k1;
+    }
+    if (done) break;
+    if (next == 0 || steps >= maxstep) { // -> exhaustive
+      hit = 0;
+      break;
+    }
+#pragma unroll
+    for (int h = kHist - 1; h > 0; h--) hist[h] = hist[h - 1];
+    hist[0] = k;
+    k = next;
+  }
+  if (hit) {
+    interp_bdy(S, ip, t.v, phi, edge, vertex);
+    if (elem_out) elem_out[ip - 1] = k;
+    if (hit_out) hit_out[ip - 1] = (int8_t)(hit | ((vertex >= 0 ? vertex : (edge >= 0 ? edge : 0)) << 4));
+  }
+  return hit;
+}
+
+__global__ __launch_bounds__(kBlock) void k_bdy(Bg bg, const Frame *fr, const int *sgrid, int gs, const double *qxyz,
+                                                const int *order, Slots S, int *elem_out, int8_t *hit_out, int *fb,
+                                                DevStats *st, int maxstep) {
+  __shared__ BlockStats bs;
+  bstats_init(&bs);
+  __syncthreads();
+  const XcdChunk ch = xcd_chunk(st->nbdy);
+  for (int it = 0; it < ch.iters; it++) {
+    const int i = (int)(ch.start + it * ch.stride);
+    const bool active = i < ch.hi;
+    int steps = 0, hit = 0, ip = 0;
+    if (active) {
+      ip = order[i];
+      hit = bdy_query(bg, fr, sgrid, gs, qxyz, ip, S, elem_out, hit_out, maxstep, steps);
+    }
+    int slot = wave_append(&st->nfb_bdy, active && hit == 0);
+    if (active && hit == 0) fb[slot] = ip;
+    wave_stats(&bs, active, hit, steps);
+  }
+  __syncthreads();
+  bstats_flush(&bs, st);
+}
+
+} // namespace pmmg

@@ -22,7 +22,6 @@ constexpr double kEpsD2 = 1.0e-200; // MMG5_EPSD2
 constexpr int kMaxSlot = 8;         // metric + up to 7 fields
 constexpr int kHist = 4;            // visited-element history of a walk
 constexpr int kBlock = 256;
-constexpr int kFanMax = 64;
 
 // Background mesh.  Tetra rows are read through tetv_row / adja_row: either
 // two separate arrays (the reference's MMG5_Tetra.v and adja layouts,
@@ -43,15 +42,13 @@ struct Bg {
 __device__ __forceinline__ int4 tetv_row(const Bg &bg, int k) { return bg.tetv[(size_t)(k - 1) * bg.tstride]; }
 __device__ __forceinline__ int4 adja_row(const Bg &bg, int k) { return bg.adja[(size_t)(k - 1) * bg.tstride]; }
 
-// one solution array: code 1 = scalar, 3 = vector (both P1 iso
-// interpolation), 6 = symmetric tensor (inverse-tensor interpolation)
-// `in` rows are `stride` doubles apart: the slot's own array (stride =
-// code) or its columns inside packed per-vertex records (stride = record size)
+// one solution array in the reference layout (row of vertex v at
+// in + code*(v-1)): code 1 = scalar, 3 = vector (both P1 iso interpolation),
+// 6 = symmetric tensor (inverse-tensor interpolation)
 struct Slot {
   const double *in;
   double *out;
   int code;
-  int stride;
 };
 
 struct Slots {
@@ -59,39 +56,6 @@ struct Slots {
   int n;
   int has_met; // slot 0 is the metric (boundary points treat it differently)
 };
-
-struct Frame {
-  unsigned long long key_lo[3], key_hi[3];
-  double lo[3], ext[3];
-  double inv_vol[3], inv_srf[3], inv_bin[3];
-  int seed8; // volume seed cells hold {quantised centroid, id}; a query picks the nearest of 8 cells
-};
-
-struct DevStats {
-  unsigned long long cnt[16];
-  unsigned long long steps;
-  unsigned int stepmax;
-  int nvol, nbdy;
-  int nfb_vol, nfb_bdy;
-  int coherent;
-  int ncont; // capped volume walks to continue (k_vol_walk_cont)
-  int pad;
-};
-
-// Statistics are accumulated into kStatParts partial records (block b ->
-// part b % kStatParts) placed after DevStats in the stats buffer and summed
-// on the host: one counter address hit by every workgroup serialises the
-// atomics at one L2 channel (a returning per-wave atomic on one address
-// measured +4 ms on cfg4).
-constexpr int kStatParts = 256;
-struct StatPart {
-  unsigned long long cnt[16];
-  unsigned long long steps;
-  unsigned long long stepmax;
-};
-__device__ __forceinline__ StatPart *stat_part(DevStats *st) {
-  return reinterpret_cast<StatPart *>(st + 1) + (blockIdx.x & (kStatParts - 1));
-}
 
 // ------------------------------------------------------------ small helpers
 
@@ -369,13 +333,12 @@ __device__ __forceinline__ void store6(double *p, const double *m) {
 // PMMG_interp{3,4}bar_iso (interpmesh_pmmg.c:125-165, 206-246): the row
 // value acc = sum_i phi_i * row_i (accumulated from 0.0 in vertex order)
 template <int NV, int SZ>
-__device__ __forceinline__ void interp_iso_row(const double *in, int stride, const int *v, const double *phi,
-                                               double *acc) {
+__device__ __forceinline__ void interp_iso_row(const double *in, const int *v, const double *phi, double *acc) {
   double row[NV][SZ];
 #pragma unroll
   for (int i = 0; i < NV; i++)
 #pragma unroll
-    for (int j = 0; j < SZ; j++) row[i][j] = in[(size_t)stride * (v[i] - 1) + j];
+    for (int j = 0; j < SZ; j++) row[i][j] = in[(size_t)SZ * (v[i] - 1) + j];
 #pragma unroll
   for (int j = 0; j < SZ; j++) acc[j] = 0.0;
 #pragma unroll
@@ -388,11 +351,10 @@ __device__ __forceinline__ void interp_iso_row(const double *in, int stride, con
 // M = invmat( sum_i phi_i invmat(M_i) ); false (row left untouched by the
 // reference) if any inversion fails
 template <int NV>
-__device__ __forceinline__ bool interp_ani_row(const double *in, int stride, const int *v, const double *phi,
-                                               double *r) {
+__device__ __forceinline__ bool interp_ani_row(const double *in, const int *v, const double *phi, double *r) {
   double m[NV][6];
 #pragma unroll
-  for (int i = 0; i < NV; i++) load6(in + (size_t)stride * (v[i] - 1), m[i]);
+  for (int i = 0; i < NV; i++) load6(in + (size_t)6 * (v[i] - 1), m[i]);
   double mint[6], mi[6];
   bool ok = true;
 #pragma unroll
@@ -407,9 +369,9 @@ __device__ __forceinline__ bool interp_ani_row(const double *in, int stride, con
 // the row of one slot: returns false when the reference leaves it untouched
 template <int NV, int CODE>
 __device__ __forceinline__ bool interp_row(const Slot &sl, const int *v, const double *phi, double *r) {
-  if constexpr (CODE == 6) return interp_ani_row<NV>(sl.in, sl.stride, v, phi, r);
+  if constexpr (CODE == 6) return interp_ani_row<NV>(sl.in, v, phi, r);
   else {
-    interp_iso_row<NV, CODE>(sl.in, sl.stride, v, phi, r);
+    interp_iso_row<NV, CODE>(sl.in, v, phi, r);
     return true;
   }
 }
@@ -441,21 +403,25 @@ __device__ __forceinline__ void interp_edge(const Slot &sl, int ip, const int *v
   const double f0 = sel3d(phi[0], phi[1], phi[2], i0), f1 = sel3d(phi[0], phi[1], phi[2], i1);
   if (sl.code == 6) {
     double m[6], mi0[6], mi1[6], mint[6], r[6];
-    load6(sl.in + (size_t)sl.stride * (v0 - 1), m);
+    load6(sl.in + (size_t)6 * (v0 - 1), m);
     bool ok = invmat(m, mi0);
-    load6(sl.in + (size_t)sl.stride * (v1 - 1), m);
+    load6(sl.in + (size_t)6 * (v1 - 1), m);
     ok = invmat(m, mi1) && ok;
 #pragma unroll
     for (int s = 0; s < 6; s++) mint[s] = f0 * mi0[s] + f1 * mi1[s];
     if (invmat(mint, r) && ok) store6(sl.out + 6 * (size_t)(ip - 1), r);
   } else {
-    sl.out[ip - 1] = f0 * sl.in[(size_t)sl.stride * (v0 - 1)] + f1 * sl.in[(size_t)sl.stride * (v1 - 1)];
+    // sizes 1 and 3 (a vertex / edge hit of the metric is size 1 or 6; the
+    // fields always go through interp3bar)
+    for (int j = 0; j < sl.code; j++)
+      sl.out[(size_t)sl.code * (ip - 1) + j] =
+          f0 * sl.in[(size_t)sl.code * (v0 - 1) + j] + f1 * sl.in[(size_t)sl.code * (v1 - 1) + j];
   }
 }
 
 __device__ __forceinline__ void copy_row(const Slot &sl, int ip, int vsrc) {
   double *out = sl.out + (size_t)sl.code * (ip - 1);
-  const double *in = sl.in + (size_t)sl.stride * (vsrc - 1);
+  const double *in = sl.in + (size_t)sl.code * (vsrc - 1);
   if (sl.code == 6) {
     double m[6];
     load6(in, m);
@@ -560,19 +526,50 @@ __device__ __forceinline__ int tri_wedge(double hausd, const TriGeom &t, int l, 
   return 4;
 }
 
-__device__ __forceinline__ bool cone_edge_ok(const double *xyz, int jp, const double *p0, const double *p) {
-  double p1[3], a[3], alpha = 0.0;
-  load_pt(xyz, jp, p1);
-  for (int d = 0; d < 3; d++) a[d] = p1[d] - p0[d];
-  for (int d = 0; d < 3; d++) alpha += a[d] * p[d];
-  return !(alpha > 0.0);
+// PMMG_locatePointInCone (locate_pmmg.c:209-270) with a fresh visited state
+// per query: x is in the shadow cone of vertex ip iff every surface edge
+// leaving ip (every other vertex of every tria of ip, the node->tria list of
+// PMMG_precompute_nodeTrias) makes a non-acute angle with x - p(ip), and
+// |x - p(ip)| <= hausd (tested inside the scan, as the reference does).
+// The reference skips neighbours flagged by earlier queries of the same
+// vertex (a state leak, :248-249; the oracle's ORC_MODE_FAITHFUL); here every
+// neighbour is tested.
+//
+// The trias of ip are reached by rotating through adjt around ip from tria k
+// in both directions.  When the rotation comes back to k the fan is complete
+// (a manifold vertex).  Otherwise (a border edge, a non-manifold edge — adjt
+// is 0 on edges of more than two trias — or a fan longer than kFanMax) the
+// test scans every tria for those containing ip: the exact node->tria list,
+// at O(nt) for the rare query that needs it, instead of building the list for
+// every vertex on every call.
+constexpr int kFanMax = 64;
+
+__device__ __forceinline__ int cone_tria(const Bg &bg, int tt, int ip, const double *p0, const double *p,
+                                         double dist) {
+  // 1 ok, 0 outside the cone
+  const int *tv = bg.triv + 3 * (size_t)(tt - 1);
+  for (int l = 0; l < 3; l++) {
+    const int jp = tv[l];
+    if (jp == ip) continue;
+    if (dist > bg.hausd) return 0;
+    double p1[3], e[3], alpha = 0.0;
+    load_pt(bg.xyz, jp, p1);
+    for (int d = 0; d < 3; d++) e[d] = p1[d] - p0[d];
+    for (int d = 0; d < 3; d++) alpha += e[d] * p[d];
+    if (alpha > 0.0) return 0;
+  }
+  return 1;
 }
 
-// PMMG_locatePointInCone (locate_pmmg.c:209-270) with a fresh visited state
-// per query: x is in the shadow cone of vertex ip iff |x-p(ip)| <= hausd and
-// every surface edge leaving ip makes a non-acute angle with x-p(ip).  The
-// vertex's trias are reached by rotating through adjt around ip (manifold
-// fan) instead of the reference's node->trias CSR; the edge set is the same.
+__device__ __noinline__ bool tri_cone_scan(const Bg &bg, int ip, const double *p0, const double *p, double dist) {
+  for (int tt = 1; tt <= bg.nt; tt++) {
+    const int *tv = bg.triv + 3 * (size_t)(tt - 1);
+    if (tv[0] <= 0 || (tv[0] != ip && tv[1] != ip && tv[2] != ip)) continue;
+    if (!cone_tria(bg, tt, ip, p0, p, dist)) return false;
+  }
+  return true;
+}
+
 __device__ __forceinline__ bool tri_cone(const Bg &bg, int k, int iloc, const TriGeom &t, const double *x) {
   const int ip = sel3i(t.v[0], t.v[1], t.v[2], iloc);
   double p0[3], p[3], dist = 0.0;
@@ -580,32 +577,20 @@ __device__ __forceinline__ bool tri_cone(const Bg &bg, int k, int iloc, const Tr
   for (int d = 0; d < 3; d++) p[d] = x[d] - p0[d];
   for (int d = 0; d < 3; d++) dist += p[d] * p[d];
   dist = sqrt(dist);
-  if (dist > bg.hausd) return false;
-  {
-    double q[3];
-    for (int o = 1; o <= 2; o++) {
-      int j = (iloc + o) % 3;
-      tri_pick(t, j, q);
-      double a[3], alpha = 0.0;
-      for (int d = 0; d < 3; d++) a[d] = q[d] - p0[d];
-      for (int d = 0; d < 3; d++) alpha += a[d] * p[d];
-      if (alpha > 0.0) return false;
-    }
-  }
+  if (!cone_tria(bg, k, ip, p0, p, dist)) return false;
   for (int dir = 0; dir < 2; dir++) {
     int tcur = k;
     int e = dir == 0 ? (iloc + 1) % 3 : (iloc + 2) % 3; // an edge of tcur incident to ip
-    for (int it = 0; it < kFanMax; it++) {
-      int code = bg.adjt[3 * (size_t)(tcur - 1) + e];
-      int tn = code / 3, en = code % 3;
-      if (tn == 0) break;
-      if (tn == k) return true;
+    for (int it = 0;; it++) {
+      if (it == kFanMax) return tri_cone_scan(bg, ip, p0, p, dist);
+      const int code = bg.adjt[3 * (size_t)(tcur - 1) + e];
+      const int tn = code / 3, en = code % 3;
+      if (tn == 0) return tri_cone_scan(bg, ip, p0, p, dist); // open or non-manifold fan
+      if (tn == k) return true;                                // the fan closed: every tria tested
+      if (!cone_tria(bg, tn, ip, p0, p, dist)) return false;
       const int *tvn = bg.triv + 3 * (size_t)(tn - 1);
-      int w0 = tvn[0], w1 = tvn[1], w2 = tvn[2];
-      int lvn = (w0 == ip) ? 0 : ((w1 == ip) ? 1 : 2);
-      int j1 = sel3i(w0, w1, w2, (lvn + 1) % 3), j2 = sel3i(w0, w1, w2, (lvn + 2) % 3);
-      if (!cone_edge_ok(bg.xyz, j1, p0, p) || !cone_edge_ok(bg.xyz, j2, p0, p)) return false;
-      int ea = (lvn + 1) % 3, eb = (lvn + 2) % 3;
+      const int lvn = (tvn[0] == ip) ? 0 : ((tvn[1] == ip) ? 1 : 2);
+      const int ea = (lvn + 1) % 3, eb = (lvn + 2) % 3;
       e = (ea == en) ? eb : ea;
       tcur = tn;
     }

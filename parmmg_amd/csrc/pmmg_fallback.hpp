@@ -1,0 +1,233 @@
+// pmmg_fallback.hpp — exhaustive searches with the reference's semantics
+// (included by pmmg_hip.hip only):
+//   volume:  PMMG_locatePoint_exhaustTetra (locate_pmmg.c:737-770): the
+//            lowest-index accepting tetra, else the closest tetra (argmin
+//            |bary_min| * vol, :453-458) and its nearest vertex
+//            (PMMG_barycoord3d_getClosest, barycoord_pmmg.c:371-404)
+//   surface: PMMG_locatePoint_exhaustTria (locate_pmmg.c:477-515): the
+//            lowest-index accepting tria, else the closest tria by centroid
+//            distance with the stale re-evaluation of :505-509
+// The query lists and their counts are produced on the device by the walks;
+// every kernel here reads the count itself and returns at once when its list
+// is empty, so the host launches them unconditionally (no read-back).
+#pragma once
+
+#include "pmmg_prep.hpp"
+
+namespace pmmg {
+
+constexpr int kQB = 128; // fallback queries staged in LDS per pass
+
+__global__ void k_fallback_init(int *best, int *cidx, unsigned long long *ckey, const int *count, int *bbest,
+                                int *bcidx, unsigned long long *bckey, const int *bcount) {
+  const int n = *count, nb = *bcount;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    best[i] = INT_MAX;
+    cidx[i] = INT_MAX;
+    ckey[i] = ~0ULL;
+  }
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += gridDim.x * blockDim.x) {
+    bbest[i] = INT_MAX;
+    bcidx[i] = INT_MAX;
+    bckey[i] = ~0ULL;
+  }
+}
+
+// lowest-index tetra accepting each fallback query (locate_pmmg.c:743-762)
+__global__ __launch_bounds__(kBlock) void k_vol_exhaust_accept(Bg bg, const double *qxyz, const int *fb,
+                                                               const DevStats *st, int *best) {
+  __shared__ double sx[kQB][3];
+  const int nfb = st->nfb_vol;
+  for (int q0 = 0; q0 < nfb; q0 += kQB) {
+    int nq = min(kQB, nfb - q0);
+    __syncthreads();
+    for (int j = threadIdx.x; j < nq; j += blockDim.x) load_pt(qxyz, fb[q0 + j], sx[j]);
+    __syncthreads();
+    for (int k = 1 + blockIdx.x * blockDim.x + threadIdx.x; k <= bg.ne; k += gridDim.x * blockDim.x) {
+      int4 tv = tetv_row(bg, k);
+      if (tv.x <= 0) continue;
+      double p0[3], p1[3], p2[3], p3[3];
+      load_pt(bg.xyz, tv.x, p0);
+      load_pt(bg.xyz, tv.y, p1);
+      load_pt(bg.xyz, tv.z, p2);
+      load_pt(bg.xyz, tv.w, p3);
+      double lo[3], hi[3];
+      for (int d = 0; d < 3; d++) {
+        lo[d] = fmin(fmin(p0[d], p1[d]), fmin(p2[d], p3[d]));
+        hi[d] = fmax(fmax(p0[d], p1[d]), fmax(p2[d], p3[d]));
+        // an accepted point has every barycentric coordinate > -EPS, so it
+        // lies inside the tetra's bbox inflated by 3 EPS of its extent
+        double pad = 8.0 * kEps * (hi[d] - lo[d]) + 1e-300;
+        lo[d] -= pad;
+        hi[d] += pad;
+      }
+      for (int j = 0; j < nq; j++) {
+        const double *x = sx[j];
+        if (x[0] < lo[0] || x[0] > hi[0] || x[1] < lo[1] || x[1] > hi[1] || x[2] < lo[2] || x[2] > hi[2]) continue;
+        if (best[q0 + j] <= k) continue;
+        double b[4];
+        tet_bary(x, p0, p1, p2, p3, b);
+        if (min4(b) > -kEps) atomicMin(&best[q0 + j], k);
+      }
+    }
+  }
+}
+
+// closest tetra of queries nobody accepts: argmin |bary_min| * vol
+// (locate_pmmg.c:453-458); pass 0 finds the minimum value, pass 1 the lowest
+// index reaching it
+__global__ __launch_bounds__(kBlock) void k_vol_exhaust_closest(Bg bg, const double *qxyz, const int *fb,
+                                                                const DevStats *st, const int *best,
+                                                                unsigned long long *ckey, int pass, int *cidx) {
+  __shared__ double sx[kQB][3];
+  __shared__ int sneed[kQB];
+  const int nfb = st->nfb_vol;
+  for (int q0 = 0; q0 < nfb; q0 += kQB) {
+    int nq = min(kQB, nfb - q0);
+    __syncthreads();
+    for (int j = threadIdx.x; j < nq; j += blockDim.x) {
+      load_pt(qxyz, fb[q0 + j], sx[j]);
+      sneed[j] = best[q0 + j] == INT_MAX;
+    }
+    __syncthreads();
+    bool any = false;
+    for (int j = 0; j < nq; j++) any = any || sneed[j];
+    if (!any) continue;
+    for (int k = 1 + blockIdx.x * blockDim.x + threadIdx.x; k <= bg.ne; k += gridDim.x * blockDim.x) {
+      int4 tv = tetv_row(bg, k);
+      if (tv.x <= 0) continue;
+      double p0[3], p1[3], p2[3], p3[3];
+      load_pt(bg.xyz, tv.x, p0);
+      load_pt(bg.xyz, tv.y, p1);
+      load_pt(bg.xyz, tv.z, p2);
+      load_pt(bg.xyz, tv.w, p3);
+      for (int j = 0; j < nq; j++) {
+        if (!sneed[j]) continue;
+        double b[4];
+        double vol = tet_bary(sx[j], p0, p1, p2, p3, b);
+        unsigned long long key = dkey(fabs(min4(b)) * vol);
+        if (pass == 0) atomicMin(&ckey[q0 + j], key);
+        else if (key == ckey[q0 + j]) atomicMin(&cidx[q0 + j], k);
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_vol_finish(Bg bg, const double *qxyz, const int *fb, DevStats *st,
+                                                       const int *best, const int *cidx, Slots S, int *elem_out,
+                                                       int8_t *hit_out) {
+  const int nfb = st->nfb_vol;
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nfb; j += gridDim.x * blockDim.x) {
+    int ip = fb[j];
+    double x[3];
+    load_pt(qxyz, ip, x);
+    int hit, k;
+    if (best[j] != INT_MAX) {
+      k = best[j];
+      hit = PMMG_HIT_VOL_EXHAUST;
+    } else {
+      k = cidx[j];
+      hit = PMMG_HIT_VOL_CLOSEST;
+    }
+    if (k == INT_MAX || k <= 0) continue;
+    int4 tv = tetv_row(bg, k);
+    double p[4][3], phi[4];
+    load_pt(bg.xyz, tv.x, p[0]);
+    load_pt(bg.xyz, tv.y, p[1]);
+    load_pt(bg.xyz, tv.z, p[2]);
+    load_pt(bg.xyz, tv.w, p[3]);
+    if (hit == PMMG_HIT_VOL_EXHAUST) tet_bary(x, p[0], p[1], p[2], p[3], phi);
+    else closest_vertex<4>(x, p, phi);
+    const int v[4] = {tv.x, tv.y, tv.z, tv.w};
+    for (int s = 0; s < S.n; s++) interp_dyn<4>(S.s[s], ip, v, phi);
+    if (elem_out) elem_out[ip - 1] = k;
+    if (hit_out) hit_out[ip - 1] = (int8_t)hit;
+    atomicAdd(&stat_part(st)->cnt[hit], 1ULL);
+  }
+}
+
+// surface: pass 0 lowest-index accepting tria (locate_pmmg.c:483-503), pass 1
+// minimum centroid distance, pass 2 lowest index reaching it (:400-416)
+__global__ __launch_bounds__(kBlock) void k_bdy_exhaust(Bg bg, const double *qxyz, const int *fb, const DevStats *st,
+                                                        int *best, unsigned long long *ckey, int pass, int *cidx) {
+  __shared__ double sx[kQB][3];
+  const int nfb = st->nfb_bdy;
+  for (int q0 = 0; q0 < nfb; q0 += kQB) {
+    int nq = min(kQB, nfb - q0);
+    __syncthreads();
+    for (int j = threadIdx.x; j < nq; j += blockDim.x) load_pt(qxyz, fb[q0 + j], sx[j]);
+    __syncthreads();
+    for (int k = 1 + blockIdx.x * blockDim.x + threadIdx.x; k <= bg.nt; k += gridDim.x * blockDim.x) {
+      if (bg.triv[3 * (size_t)(k - 1)] <= 0) continue;
+      TriGeom t;
+      tri_load(bg, k, t);
+      for (int j = 0; j < nq; j++) {
+        const double *x = sx[j];
+        if (pass == 0) {
+          if (best[q0 + j] <= k) continue;
+          double b[3];
+          double dist = tri_bary(x, t.p, t.q, t.n, b);
+          double bmin = fmin(b[0], fmin(b[1], b[2]));
+          if (bmin > -kEps && !(fabs(dist) > bg.hausd)) atomicMin(&best[q0 + j], k);
+        } else {
+          if (best[q0 + j] != INT_MAX) continue;
+          double d[3] = {x[0], x[1], x[2]};
+          for (int v = 0; v < 3; v++)
+            for (int c = 0; c < 3; c++) d[c] -= t.p[v][c] / 3.0;
+          double nrm = 0;
+          for (int c = 0; c < 3; c++) nrm += d[c] * d[c];
+          nrm = sqrt(nrm);
+          unsigned long long key = dkey(nrm);
+          if (pass == 1) atomicMin(&ckey[q0 + j], key);
+          else if (key == ckey[q0 + j]) atomicMin(&cidx[q0 + j], k);
+        }
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_bdy_finish(Bg bg, const double *qxyz, const int *fb, DevStats *st,
+                                                       const int *best, const int *cidx, Slots S, int *elem_out,
+                                                       int8_t *hit_out) {
+  const int nfb = st->nfb_bdy;
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nfb; j += gridDim.x * blockDim.x) {
+    int ip = fb[j];
+    double x[3];
+    load_pt(qxyz, ip, x);
+    int hit, k;
+    double phi[3];
+    TriGeom t;
+    if (best[j] != INT_MAX) {
+      k = best[j];
+      hit = PMMG_HIT_BDY_EXHAUST;
+      tri_load(bg, k, t);
+      tri_bary(x, t.p, t.q, t.n, phi);
+    } else {
+      k = cidx[j];
+      if (k == INT_MAX || k <= 0) continue;
+      tri_load(bg, k, t);
+      // stale re-evaluation (locate_pmmg.c:505-509): vertices and area of the
+      // last tria scanned (nt), normal of the closest one
+      TriGeom ts;
+      tri_load(bg, bg.nt, ts);
+      double b[3];
+      double dist = tri_bary(x, ts.p, ts.q, t.n, b);
+      double bmin = fmin(b[0], fmin(b[1], b[2]));
+      if (bmin > -kEps && !(fabs(dist) > bg.hausd)) {
+        hit = PMMG_HIT_BDY_STALE;
+        phi[0] = b[0];
+        phi[1] = b[1];
+        phi[2] = b[2];
+      } else {
+        hit = PMMG_HIT_BDY_CLOSEST;
+        closest_vertex<3>(x, t.p, phi);
+      }
+    }
+    interp_bdy(S, ip, t.v, phi, -1, -1);
+    if (elem_out) elem_out[ip - 1] = k;
+    if (hit_out) hit_out[ip - 1] = (int8_t)hit;
+    atomicAdd(&stat_part(st)->cnt[hit], 1ULL);
+  }
+}
+
+} // namespace pmmg

@@ -9,6 +9,8 @@
  *   - classifies new points in the reference's visitation loop
  *     (src/interpmesh_pmmg.c:535-550: invalid / MG_REQ skipped, MG_BDY to the
  *     surface path, the rest to the volume path),
+ *   - copies the solutions of frozen (MG_REQ) points
+ *     (PMMG_copyMetricsAndFields_point, src/interpmesh_pmmg.c:432-446),
  *   - and runs the HIP module (include/parmmg_hip.h) group by group.
  */
 #ifndef PMMG_HOST_H
@@ -26,13 +28,17 @@ extern "C" {
 #define PMMG_TAG_BDY (1 << 4)  /* MG_BDY */
 #define PMMG_TAG_NUL (1 << 14) /* MG_NUL: MG_VOK(p) == (p->tag < MG_NUL) */
 
+/* The background group (parmesh->old_listgrp[igrp] after PMMG_update_oldGrps,
+ * src/grpsplit_pmmg.c:1224).  Arrays in the "row r = entity r+1" layout. */
 typedef struct {
   int np, ne, nt;
-  const double *xyz;   /* 3*np */
-  const int *tetv;     /* 4*ne */
-  const int *adja;     /* 4*ne (= &mesh->adja[1]) */
-  const int *triv;     /* 3*nt */
-  const int *adjt;     /* 3*nt (= &mesh->adjt[1]) */
+  const double *xyz;   /* 3*np (MMG5_Point.c packed) */
+  const uint16_t *tag; /* np point tags (may be NULL: no MG_REQ copy) */
+  const int *tetv;     /* 4*ne (MMG5_Tetra.v packed) */
+  const int *adja;     /* 4*ne (= &mesh->adja[1]); NULL: built on the device (MMG3D_hashTetra's result) */
+  const int *triv;     /* 3*nt (MMG5_Tria.v packed); NULL with nt < 0: the boundary faces are built on
+                          the device (MMG5_chkBdryTria's single-material result) */
+  const int *adjt;     /* 3*nt (= &mesh->adjt[1]); NULL: built on the device (MMG3D_hashTria) */
   double hausd;        /* oldMesh->info.hausd */
   int met_size;        /* oldMet->size (0 if no metric) */
   const double *met;   /* met_size*np */
@@ -41,37 +47,50 @@ typedef struct {
   const double *const *field;
 } pmmg_old_group;
 
+/* The adapted group (parmesh->listgrp[igrp]). */
 typedef struct {
   int np, ne;
   const double *xyz;   /* 3*np */
   const uint16_t *tag; /* np, Mmg point tags */
   const int *tetv;     /* 4*ne, new tetra (MG_EOK: v[0] > 0) */
-  double *met;         /* met_size*np output (may be NULL when no metric) */
+  int met_size;        /* rows of met (0 = no metric array, 1 or 6) */
+  double *met;         /* met_size*np output */
   double *const *field;/* nfield outputs */
   int *elem;           /* optional np diagnostics */
   int8_t *hit;         /* optional np diagnostics */
+  double hsiz;         /* mesh->info.hsiz (> 0: constant metric, not interpolated) */
+  double hmin, hmax;   /* mesh->info.hmin / hmax: bounds of the constant size (<= 0: unset) */
+  int ani;             /* mesh->info.ani: the constant metric is a tensor (met_size 6) */
 } pmmg_new_group;
 
 /* Classification of the reference loop: pclass[np] receives PMMG_PT_*.
  * Returns the number of points to locate. */
 int64_t pmmg_classify_points(const pmmg_new_group *g, uint8_t *pclass);
 
-/* PMMG_copyMetricsAndFields_point (src/interpmesh_pmmg.c:432-446): copy the
- * solutions of MG_REQ points from the old group (optionally through
- * permNodGlob, 1-based).  Returns 1. */
-int pmmg_copy_required(const pmmg_old_group *old, const uint16_t *old_tag, pmmg_new_group *g,
-                       const int *permNodGlob, int copy_met);
+/* PMMG_copyMetricsAndFields_point (src/interpmesh_pmmg.c:432-446) ->
+ * PMMG_copySol_point (:311-358): the rows of the old group's valid MG_REQ
+ * points are copied into the new group, at the same index when
+ * `!renum || !permNodGlob`, else at permNodGlob[ip] (1-based, the SCOTCH
+ * renumbering, src/libparmmg1.c:692-715).  The metric only when
+ * input_met == 1 and hsiz <= 0 (PMMG_copyMetrics_point, :373-383); the
+ * fields always.  Returns 1, or 0 on invalid arguments / a target out of
+ * range. */
+int pmmg_copy_metrics_and_fields_point(const pmmg_old_group *old, pmmg_new_group *g, const int *permNodGlob,
+                                       int renum, int input_met);
 
-/* MMG3D_Set_constantSize's fill (hsiz > 0 branch): iso -> hsiz,
- * aniso -> diag(1/hsiz^2).  Returns 1. */
-int pmmg_set_constant_metric(int np, int met_size, double hsiz, double *met);
+/* MMG3D_Set_constantSize's fill (hsiz > 0 branch of the ismet logic,
+ * src/interpmesh_pmmg.c:501-505), restated from Mmg @889d408 (unpinned):
+ * MMG5_Compute_constantSize clamps hsiz to [hmin, hmax] (bounds <= 0 are
+ * unset), then every valid point gets hsiz (iso, info.ani == 0) or
+ * diag(1/hsiz^2) (aniso).  g->met_size must be 6 when g->ani, else 1.
+ * Returns 1, or 0 on a size mismatch. */
+int pmmg_set_constant_metric(pmmg_new_group *g);
 
 /* PMMG_interpMetricsAndFields over ngrp groups.
  *   input_met   parmesh->info.inputMet (1 = the user provided a metric)
- *   hsiz        mesh->info.hsiz (> 0: constant metric recomputed, not interpolated)
  * Returns 1 if every group succeeded, 0 otherwise (src/interpmesh_pmmg.c:689-741). */
 int pmmg_interp_metrics_and_fields(pmmg_hip_ctx *ctx, int ngrp, const pmmg_old_group *old, pmmg_new_group *grp,
-                                   int input_met, double hsiz, pmmg_hip_stats *stats);
+                                   int input_met, pmmg_hip_stats *stats);
 
 /* ---- halo shards of a background group (pmmg_shard.c) ----
  * All arrays in the "row r = entity r+1" layout of parmmg_hip.h. */

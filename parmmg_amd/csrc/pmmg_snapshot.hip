@@ -165,25 +165,37 @@ __global__ __launch_bounds__(kB) void k_face_match(const int4 *tetv, int ne, int
 }
 
 // ---- boundary trias
+//
+// A face is a boundary tria when it has no neighbour, or (with tetra
+// references, a multi-material mesh) when the neighbour's reference is
+// smaller than the tetra's: MMG5_chkBdryTria's rule for an old mesh without
+// input trias (adj == 0 || pt->ref > pt1->ref), restated from Mmg @889d408
+// (absent from the image: unpinned), each interface face emitted once, from
+// the tetra of the larger reference, oriented by MMG5_idir.
 
-__global__ __launch_bounds__(kB) void k_bdy_count(const int4 *adja, int astride, int ne, int *nb) {
-  const int k = blockIdx.x * kB + threadIdx.x;
-  if (k >= ne) return;
-  const int4 a = adja[(size_t)k * astride];
-  nb[k] = (a.x == 0) + (a.y == 0) + (a.z == 0) + (a.w == 0);
+__device__ __forceinline__ bool bdy_face(int code, int k, const int *tref) {
+  if (code == 0) return true;
+  return tref && tref[k] > tref[(code >> 2) - 1];
 }
 
-__global__ __launch_bounds__(kB) void k_bdy_write(const int4 *tetv, int tstride, const int4 *adja, int astride, int ne,
-                                                  const int *toff, int *triv) {
+__global__ __launch_bounds__(kB) void k_bdy_count(const int4 *adja, int astride, const int *tref, int ne, int *nb) {
   const int k = blockIdx.x * kB + threadIdx.x;
   if (k >= ne) return;
   const int4 a = adja[(size_t)k * astride];
-  if (a.x && a.y && a.z && a.w) return;
+  nb[k] = bdy_face(a.x, k, tref) + bdy_face(a.y, k, tref) + bdy_face(a.z, k, tref) + bdy_face(a.w, k, tref);
+}
+
+__global__ __launch_bounds__(kB) void k_bdy_write(const int4 *tetv, int tstride, const int4 *adja, int astride,
+                                                  const int *tref, int ne, const int *toff, int *triv) {
+  const int k = blockIdx.x * kB + threadIdx.x;
+  if (k >= ne) return;
+  const int4 a = adja[(size_t)k * astride];
+  if (!tref && a.x && a.y && a.z && a.w) return;
   const int4 t = tetv[(size_t)k * tstride];
   int pos = toff[k];
 #pragma unroll
   for (int i = 0; i < 4; i++) {
-    if (sel(a, i)) continue;
+    if (!bdy_face(sel(a, i), k, tref)) continue;
 #pragma unroll
     for (int l = 0; l < 3; l++) triv[3 * (size_t)pos + l] = sel(t, kIdirS[i][l]);
     pos++;
@@ -313,13 +325,41 @@ int pmmg_snap_adjacency(hipStream_t s, int np, int ne, const int *tetv, int *adj
   return 1;
 }
 
-int pmmg_snap_boundary(hipStream_t s, int np, int ne, const int *tetv, int tstride, const int *adja, int astride,
-                       int cap, int *nt_out, int *triv, int *adjt, char *msg, size_t msglen) {
+int pmmg_snap_tria_adjacency(hipStream_t s, int np, int nt, const int *triv, int *adjt, char *msg, size_t msglen) {
+  if (nt == 0) return 1;
   Scratch S;
-  int *nb = S.get<int>((size_t)ne), *toff = S.get<int>((size_t)ne), *err = S.get<int>(1);
-  if (!nb || !toff || !err) { snprintf(msg, msglen, "build_boundary: out of device memory"); return 0; }
+  const long long nedge = 3LL * nt;
+  int *cnt = S.get<int>((size_t)np), *off = S.get<int>((size_t)np), *rank = S.get<int>((size_t)nedge);
+  int2 *bucket = S.get<int2>((size_t)nedge);
+  int *err = S.get<int>(1);
+  if (!cnt || !off || !rank || !bucket || !err) {
+    snprintf(msg, msglen, "tria adjacency: out of device memory");
+    return 0;
+  }
+  SCK(hipMemsetAsync(cnt, 0, sizeof(int) * (size_t)np, s));
+  SCK(hipMemsetAsync(err, 0, sizeof(int), s));
+  hipLaunchKernelGGL(k_edge_count, dim3(blocks(nedge)), dim3(kB), 0, s, triv, nt, np, cnt, rank, err);
+  if (!exclusive_scan(S, cnt, off, np, s, msg, msglen)) return 0;
+  hipLaunchKernelGGL(k_edge_scatter, dim3(blocks(nedge)), dim3(kB), 0, s, triv, nt, off, rank, bucket);
+  hipLaunchKernelGGL(k_edge_match, dim3(blocks(nedge)), dim3(kB), 0, s, triv, nt, off, cnt, bucket, adjt);
+  SCK(hipGetLastError());
+  int h_err = 0;
+  SCK(hipMemcpyAsync(&h_err, err, sizeof(int), hipMemcpyDeviceToHost, s));
+  SCK(hipStreamSynchronize(s));
+  if (h_err) {
+    snprintf(msg, msglen, "tria adjacency: tria vertex ids out of [1, np]");
+    return 0;
+  }
+  return 1;
+}
+
+int pmmg_snap_boundary(hipStream_t s, int np, int ne, const int *tetv, int tstride, const int *adja, int astride,
+                       const int *tref, int cap, int *nt_out, int *triv, int *adjt, char *msg, size_t msglen) {
+  Scratch S;
+  int *nb = S.get<int>((size_t)ne), *toff = S.get<int>((size_t)ne);
+  if (!nb || !toff) { snprintf(msg, msglen, "build_boundary: out of device memory"); return 0; }
   const int4 *tv = reinterpret_cast<const int4 *>(tetv), *ad = reinterpret_cast<const int4 *>(adja);
-  hipLaunchKernelGGL(k_bdy_count, dim3(blocks(ne)), dim3(kB), 0, s, ad, astride, ne, nb);
+  hipLaunchKernelGGL(k_bdy_count, dim3(blocks(ne)), dim3(kB), 0, s, ad, astride, tref, ne, nb);
   if (!exclusive_scan(S, nb, toff, ne, s, msg, msglen)) return 0;
   int last[2] = {0, 0};
   SCK(hipMemcpyAsync(&last[0], toff + ne - 1, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -329,20 +369,9 @@ int pmmg_snap_boundary(hipStream_t s, int np, int ne, const int *tetv, int tstri
   *nt_out = nt;
   if (nt > cap) { snprintf(msg, msglen, "build_boundary: %d boundary trias exceed the capacity %d", nt, cap); return 0; }
   if (nt == 0) return 1;
-  hipLaunchKernelGGL(k_bdy_write, dim3(blocks(ne)), dim3(kB), 0, s, tv, tstride, ad, astride, ne, toff, triv);
-  if (adjt) {
-    const long long nedge = 3LL * nt;
-    int *cnt = S.get<int>((size_t)np), *off = S.get<int>((size_t)np), *rank = S.get<int>((size_t)nedge);
-    int2 *bucket = S.get<int2>((size_t)nedge);
-    if (!cnt || !off || !rank || !bucket) { snprintf(msg, msglen, "build_boundary: out of device memory"); return 0; }
-    SCK(hipMemsetAsync(cnt, 0, sizeof(int) * (size_t)np, s));
-    SCK(hipMemsetAsync(err, 0, sizeof(int), s));
-    hipLaunchKernelGGL(k_edge_count, dim3(blocks(nedge)), dim3(kB), 0, s, triv, nt, np, cnt, rank, err);
-    if (!exclusive_scan(S, cnt, off, np, s, msg, msglen)) return 0;
-    hipLaunchKernelGGL(k_edge_scatter, dim3(blocks(nedge)), dim3(kB), 0, s, triv, nt, off, rank, bucket);
-    hipLaunchKernelGGL(k_edge_match, dim3(blocks(nedge)), dim3(kB), 0, s, triv, nt, off, cnt, bucket, adjt);
-  }
+  hipLaunchKernelGGL(k_bdy_write, dim3(blocks(ne)), dim3(kB), 0, s, tv, tstride, ad, astride, tref, ne, toff, triv);
   SCK(hipGetLastError());
+  if (adjt && !pmmg_snap_tria_adjacency(s, np, nt, triv, adjt, msg, msglen)) return 0;
   SCK(hipStreamSynchronize(s));
   return 1;
 }

@@ -9,7 +9,12 @@
 int pmmg_snap_adjacency(hipStream_t s, int np, int ne, const int *tetv, int *adja, int *tet8, char *msg,
                         size_t msglen);
 
-// boundary trias (faces with adja == 0) and their adjacency.  Tetra rows are
-// int4 rows `tstride` / `astride` int4s apart (1: separate arrays, 2: tet8).
+// boundary trias (faces with adja == 0, or towards a smaller tetra reference
+// when tref[ne] is given) and their adjacency.  Tetra rows are int4 rows
+// `tstride` / `astride` int4s apart (1: separate arrays, 2: tet8).
 int pmmg_snap_boundary(hipStream_t s, int np, int ne, const int *tetv, int tstride, const int *adja, int astride,
-                       int cap, int *nt_out, int *triv, int *adjt, char *msg, size_t msglen);
+                       const int *tref, int cap, int *nt_out, int *triv, int *adjt, char *msg, size_t msglen);
+
+// adjt[3*nt] of given trias (MMG3D_hashTria: 3*t'+j' across edge j, 0 on
+// borders and on edges of more than two trias).  Synchronous.
+int pmmg_snap_tria_adjacency(hipStream_t s, int np, int nt, const int *triv, int *adjt, char *msg, size_t msglen);

@@ -1,0 +1,604 @@
+// pmmg_vol.hpp — volume points of the transfer step (included by
+// pmmg_hip.hip only): PMMG_locatePointVol (locate_pmmg.c:786-883) and the
+// interpolation PMMG_interp4bar_{iso,ani} (interpmesh_pmmg.c:206-270).
+//
+//   k_vol_walk        fp32 filter walk from a grid seed to a candidate tetra
+//   k_vol_interp_*    in input order: the reference's exact fp64 acceptance
+//                     test at the candidate, its exact coordinates, and the
+//                     interpolation of the metric and fields
+//   k_vol_walk_exact  the few queries the filter could not settle, walked and
+//                     interpolated in the reference's fp64 arithmetic (then
+//                     the exhaustive kernels, pmmg_fallback.hpp)
+#pragma once
+
+#include "pmmg_prep.hpp"
+
+namespace pmmg {
+
+// ---------------------------------------------------------------- per-query hand-offs
+//
+// vloc[ip-1]: the walk's candidate tetra (0: none, the query is on the
+// continuation list).  The interpolation kernel re-evaluates the candidate in
+// the reference's arithmetic, which also yields the exact coordinates the
+// interpolation needs, so nothing but the tetra id passes between the two
+// kernels.
+struct VolLoc {
+  int4 v;
+  double phi[4];
+};
+
+struct ContEntry {
+  int ip; // query
+  int k;  // tetra the exact walk starts from (0: no seed)
+};
+
+__device__ __forceinline__ void load_tet_pts(const Bg &bg, const int4 &tv, double (*p)[3]) {
+  load_pt(bg.xyz, tv.x, p[0]);
+  load_pt(bg.xyz, tv.y, p[1]);
+  load_pt(bg.xyz, tv.z, p[2]);
+  load_pt(bg.xyz, tv.w, p[3]);
+}
+
+// The reference's acceptance test of tetra (tv) for x, exactly
+// (PMMG_locatePointInTetra, locate_pmmg.c:441-461 + barycoord3d_evaluate):
+// accept iff min_f bary[f] > -MMG5_EPS, bary[f] = -s[f]/vol.  IEEE division
+// is sign-symmetric and monotone, so for vol > 0
+//   min_f fl(-s[f]/vol) = -fl(max_f s[f] / vol)
+// (for vol < 0 with min_f s[f]): one division decides, bit-identically to the
+// reference's four.  Degenerate tetra (vol == 0) take the four divisions.
+// On acceptance loc receives the vertex ids and -s[f]/vol (the reference's
+// coordinates, PMMG_barycoord_get: unsorted).  key[f] (when non-null): larger
+// = more negative coordinate (the reference's walk order of faces).
+__device__ __forceinline__ bool exact_accept(const double *x, const double (*p)[3], const int4 &tv, VolLoc *loc,
+                                             double *key) {
+  double s[4];
+  const double vol = tet_dots(x, p[0], p[1], p[2], p[3], s);
+  bool inside;
+  if (vol > 0.0 || vol < 0.0) {
+    double sm;
+    if (vol > 0.0) {
+      sm = s[0];
+      sm = s[1] > sm ? s[1] : sm;
+      sm = s[2] > sm ? s[2] : sm;
+      sm = s[3] > sm ? s[3] : sm;
+    } else {
+      sm = s[0];
+      sm = s[1] < sm ? s[1] : sm;
+      sm = s[2] < sm ? s[2] : sm;
+      sm = s[3] < sm ? s[3] : sm;
+    }
+    inside = -(sm / vol) > -kEps;
+    if (key)
+#pragma unroll
+      for (int f = 0; f < 4; f++) key[f] = vol > 0.0 ? s[f] : -s[f];
+  } else {
+    double b[4];
+#pragma unroll
+    for (int f = 0; f < 4; f++) b[f] = -s[f] / vol;
+    inside = min4(b) > -kEps;
+    if (key)
+#pragma unroll
+      for (int f = 0; f < 4; f++) key[f] = s[f];
+  }
+  if (inside) {
+    loc->v = tv;
+#pragma unroll
+    for (int f = 0; f < 4; f++) loc->phi[f] = -s[f] / vol;
+  }
+  return inside;
+}
+
+// index of id in t (0 when it is t.x or absent)
+__device__ __forceinline__ int idx_in(int id, const int4 &t) {
+  return (id == t.y ? 1 : 0) + (id == t.z ? 2 : 0) + (id == t.w ? 3 : 0);
+}
+
+// the eligible face with the largest key (the reference steps through the
+// first face, in its sorted order, whose neighbour exists and is unvisited,
+// locate_pmmg.c:819-833; ties: lowest face); -1 when none
+template <typename T>
+__device__ __forceinline__ int pick_face(const int4 &ad, const int *hist, const T *key) {
+  int f = -1;
+  T best = 0;
+#pragma unroll
+  for (int ff = 0; ff < 4; ff++) {
+    const int iel = sel4(ad, ff) >> 2;
+    bool vis = false;
+#pragma unroll
+    for (int h = 0; h < kHist; h++) vis = vis || (hist[h] == iel);
+    if (iel != 0 && !vis && (f < 0 || key[ff] > best)) {
+      f = ff;
+      best = key[ff];
+    }
+  }
+  return f;
+}
+
+// the vertices of the tetra reached through face f: the new tetra tn's local
+// vertex l sits in the slot of the same vertex of the previous tetra tv (slot
+// map m), except its vertex opposite the crossed face (iopp), which takes the
+// slot of the vertex left behind (f)
+__device__ __forceinline__ int4 next_slots(const int4 &m, const int4 &tv, const int4 &tn, int f, int iopp) {
+  const int sf = sel4(m, f);
+  int4 mn; // branch-free (a ternary with a costly arm becomes a divergent branch)
+  mn.x = (int)bsel((unsigned)sel4(m, idx_in(tn.x, tv)), (unsigned)sf, iopp == 0);
+  mn.y = (int)bsel((unsigned)sel4(m, idx_in(tn.y, tv)), (unsigned)sf, iopp == 1);
+  mn.z = (int)bsel((unsigned)sel4(m, idx_in(tn.z, tv)), (unsigned)sf, iopp == 2);
+  mn.w = (int)bsel((unsigned)sel4(m, idx_in(tn.w, tv)), (unsigned)sf, iopp == 3);
+  return mn;
+}
+
+// ---------------------------------------------------------------- fp32 filter walk
+//
+// The walk itself only has to reach the accepting tetra; the reference's
+// exact arithmetic is needed for the acceptance decision and the coordinates
+// of that one tetra.  So each step runs in fp32 on the vertices relative to
+// the query (q = p - x, rounded once), where the four face numerators are
+// triple products: with x at the origin
+//   s_f = (x - a_f) . ((b_f - a_f) x (c_f - a_f)) = -det(a_f, b_f, c_f)
+// (faces idir = {1,2,3}, {0,3,2}, {0,1,3}, {0,2,1}), three cross products
+// shared by the four faces, and vol = orvol = -(s0 + s1 + s2 + s3).
+// A step stops the walk when min_f bary[f] > -(EPS + kFilterMargin) in fp32:
+// every tetra the reference's test could accept passes (the fp32 error of a
+// coordinate, ~1e-6 at most for the meshes at hand, is far below the
+// margin).  The exact test then runs once per query, in the interpolation
+// kernel; a query it rejects (within the margin of a face, ~1e-3 of the
+// queries) continues in exact arithmetic (k_vol_walk_exact).  Every located
+// tetra is therefore accepted by the reference's own test, with its exact
+// coordinates.
+//
+// The fp32 step is ~30 single-precision operations instead of ~100
+// double-precision ones plus a division, and it keeps the vertices as 12-byte
+// LDS slots instead of 24-byte ones: fewer registers, more waves in flight
+// for a walk whose steps are two dependent gathers each.
+constexpr float kFilterMargin = 1.220703125e-4f; // 2^-13
+
+struct LaneSlotsF { // this lane's view of the wave's slot image [slot*3 + dim][64]
+  float *base;
+  __device__ __forceinline__ void put(int slot, const float *q) const {
+#pragma unroll
+    for (int d = 0; d < 3; d++) base[(slot * 3 + d) * 64] = q[d];
+  }
+  __device__ __forceinline__ void get(int slot, float *q) const {
+#pragma unroll
+    for (int d = 0; d < 3; d++) q[d] = base[(slot * 3 + d) * 64];
+  }
+};
+
+__device__ __forceinline__ void rel_pt(const double *xyz, int v, const double *x, float *q) {
+  const double *p = xyz + 3 * (size_t)(v - 1);
+  q[0] = (float)(p[0] - x[0]);
+  q[1] = (float)(p[1] - x[1]);
+  q[2] = (float)(p[2] - x[2]);
+}
+
+__device__ __forceinline__ void cross3(const float *a, const float *b, float *c) {
+  c[0] = a[1] * b[2] - a[2] * b[1];
+  c[1] = a[2] * b[0] - a[0] * b[2];
+  c[2] = a[0] * b[1] - a[1] * b[0];
+}
+__device__ __forceinline__ float dot3(const float *a, const float *b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+
+// returns 1 candidate (filter passed), 0 moved (k, tv, ad, m, hist updated),
+// 2 stuck (no eligible neighbour)
+__device__ __forceinline__ int step_f32(const Bg &bg, const double *x, int &k, int4 &tv, int4 &ad, int4 &m, int *hist,
+                                        const LaneSlotsF &L) {
+  float q[4][3];
+  L.get(m.x, q[0]);
+  L.get(m.y, q[1]);
+  L.get(m.z, q[2]);
+  L.get(m.w, q[3]);
+  float c23[3], c13[3], c12[3], s[4];
+  cross3(q[2], q[3], c23);
+  cross3(q[1], q[3], c13);
+  cross3(q[1], q[2], c12);
+  s[0] = -dot3(q[1], c23);
+  s[1] = dot3(q[0], c23);
+  s[2] = -dot3(q[0], c13);
+  s[3] = dot3(q[0], c12);
+  const float vol = -((s[0] + s[1]) + (s[2] + s[3]));
+  float key[4];
+#pragma unroll
+  for (int f = 0; f < 4; f++) key[f] = vol < 0.f ? -s[f] : s[f];
+  const float kmax = fmaxf(fmaxf(key[0], key[1]), fmaxf(key[2], key[3]));
+  if (vol != 0.f && kmax < (float)(kEps + kFilterMargin) * fabsf(vol)) return 1;
+  const int f = pick_face<float>(ad, hist, key);
+  if (f < 0) return 2;
+#pragma unroll
+  for (int h = kHist - 1; h > 0; h--) hist[h] = hist[h - 1];
+  hist[0] = k;
+  const int code = sel4(ad, f);
+  k = code >> 2;
+  const int iopp = code & 3;
+  const int4 tn = tetv_row(bg, k);
+  ad = adja_row(bg, k);
+  float qn[3];
+  rel_pt(bg.xyz, sel4(tn, iopp), x, qn);
+  const int sf = sel4(m, f);
+  m = next_slots(m, tv, tn, f, iopp);
+  L.put(sf, qn);
+  tv = tn;
+  return 0;
+}
+
+// Walk kernel: one query per lane, the 64 lanes of a one-wave block on 64
+// consecutive queries of the processing order, so neighbouring walks run in
+// lockstep through the same tetra and share cache lines inside each
+// wave-instruction.  Input order (st->sorted == 0): i = ip - 1 and the lane
+// takes the point only if it is a volume point; Morton order: order[i].
+// vloc[ip-1] = the candidate tetra; stuck / over-long walks go to the
+// continuation list with the tetra they stopped at.
+__global__ __launch_bounds__(64) void k_vol_walk(Bg bg, const Frame *fr, const unsigned long long *grid, int g,
+                                                 const double *qxyz, const uint8_t *pclass, const int *order, int np,
+                                                 int *vloc, ContEntry *cont, DevStats *st, int maxstep) {
+  __shared__ BlockStats bs;
+  __shared__ float slot_img[12 * 64];
+  const LaneSlotsF L{&slot_img[__lane_id()]};
+  bstats_init(&bs);
+  __syncthreads();
+  const int i = xcd_block() * 64 + threadIdx.x;
+  bool active;
+  int ip = 0;
+  if (st->sorted) {
+    active = i < st->nvol;
+    if (active) ip = order[i];
+  } else {
+    active = i < np && pclass[i] == PMMG_PT_VOL;
+    ip = i + 1;
+  }
+  int status = 0, steps = 0, k = 0;
+  if (active) {
+    double x[3];
+    load_pt_nt(qxyz, ip, x); // streamed once: non-temporal
+    k = seed_vol(grid, g, fr, x);
+    if (k == 0) {
+      status = 2;
+    } else {
+      int4 tv = tetv_row(bg, k), ad = adja_row(bg, k), m = make_int4(0, 1, 2, 3);
+      {
+        float q[3];
+        rel_pt(bg.xyz, tv.x, x, q);
+        L.put(0, q);
+        rel_pt(bg.xyz, tv.y, x, q);
+        L.put(1, q);
+        rel_pt(bg.xyz, tv.z, x, q);
+        L.put(2, q);
+        rel_pt(bg.xyz, tv.w, x, q);
+        L.put(3, q);
+      }
+      int hist[kHist];
+#pragma unroll
+      for (int h = 0; h < kHist; h++) hist[h] = 0;
+      for (;;) {
+        if (steps >= maxstep) {
+          status = 3;
+          break;
+        }
+        ++steps;
+        const int r = step_f32(bg, x, k, tv, ad, m, hist, L);
+        if (r != 0) {
+          status = r;
+          break;
+        }
+      }
+    }
+    __builtin_nontemporal_store(status == 1 ? k : 0, vloc + ip - 1);
+  }
+  const bool more = active && status != 1;
+  const int slot = wave_append(&st->ncont, more);
+  if (more) cont[slot] = ContEntry{ip, k};
+  wave_stats(&bs, active, 0, steps);
+  wave_count(&bs, kCntVolQueries, active);
+  wave_count(&bs, kCntExact, more);
+  __syncthreads();
+  bstats_flush(&bs, st);
+}
+
+// ---------------------------------------------------------------- exact continuation
+
+// fp64 walk with the tetra's vertices kept in LDS slots (per lane 4 slots x 3
+// doubles, lane-interleaved: conflict-free): the reference's arithmetic at
+// every step.  Returns 1 found (loc), 2 stuck, 3 limit reached.
+struct LaneSlotsD {
+  double *base;
+  __device__ __forceinline__ void put(int slot, const double *p) const {
+#pragma unroll
+    for (int d = 0; d < 3; d++) base[(slot * 3 + d) * 64] = p[d];
+  }
+  __device__ __forceinline__ void get(int slot, double *p) const {
+#pragma unroll
+    for (int d = 0; d < 3; d++) p[d] = base[(slot * 3 + d) * 64];
+  }
+};
+
+__device__ __forceinline__ int walk_exact(const Bg &bg, const double *x, int &k, int &steps, int limit, VolLoc *loc,
+                                          const LaneSlotsD &L) {
+  int hist[kHist];
+#pragma unroll
+  for (int h = 0; h < kHist; h++) hist[h] = 0;
+  int4 tv = tetv_row(bg, k), ad = adja_row(bg, k);
+  {
+    double p[4][3];
+    load_tet_pts(bg, tv, p);
+#pragma unroll
+    for (int l = 0; l < 4; l++) L.put(l, p[l]);
+  }
+  int4 m = make_int4(0, 1, 2, 3);
+  for (int n = 0;; n++) {
+    if (n >= limit) return 3;
+    ++steps;
+    double p[4][3];
+    L.get(m.x, p[0]);
+    L.get(m.y, p[1]);
+    L.get(m.z, p[2]);
+    L.get(m.w, p[3]);
+    double key[4];
+    if (exact_accept(x, p, tv, loc, key)) return 1;
+    const int f = pick_face<double>(ad, hist, key);
+    if (f < 0) return 2;
+#pragma unroll
+    for (int h = kHist - 1; h > 0; h--) hist[h] = hist[h - 1];
+    hist[0] = k;
+    const int code = sel4(ad, f);
+    k = code >> 2;
+    const int iopp = code & 3;
+    const int4 tn = tetv_row(bg, k);
+    ad = adja_row(bg, k);
+    double pn[3];
+    load_pt(bg.xyz, sel4(tn, iopp), pn);
+    const int sf = sel4(m, f);
+    m = next_slots(m, tv, tn, f, iopp);
+    L.put(sf, pn);
+    tv = tn;
+  }
+}
+
+// the queries the filter walk handed over, walked in exact arithmetic from
+// where it stopped (fresh visited history) and interpolated here (per-lane
+// gathers: these are few); failures -> the exhaustive list.  Fixed grid: the
+// count is read on the device.
+__global__ __launch_bounds__(64) void k_vol_walk_exact(Bg bg, const double *qxyz, int *fb, const ContEntry *cont,
+                                                       DevStats *st, Slots S, int *elem_out, int8_t *hit_out,
+                                                       int maxstep) {
+  __shared__ BlockStats bs;
+  __shared__ double slot_img[12 * 64];
+  const LaneSlotsD L{&slot_img[__lane_id()]};
+  bstats_init(&bs);
+  __syncthreads();
+  const XcdChunk ch = xcd_chunk(st->ncont);
+  for (int it = 0; it < ch.iters; it++) {
+    const long long j = ch.start + it * ch.stride;
+    const bool active = j < ch.hi;
+    int status = 0, steps = 0, ip = 0;
+    if (active) {
+      const ContEntry e = cont[j];
+      ip = e.ip;
+      int k = e.k;
+      if (k > 0) {
+        double x[3];
+        load_pt(qxyz, ip, x);
+        VolLoc loc;
+        status = walk_exact(bg, x, k, steps, maxstep, &loc, L);
+        if (status == 1) {
+          const int v[4] = {loc.v.x, loc.v.y, loc.v.z, loc.v.w};
+          for (int sl = 0; sl < S.n; sl++) interp_dyn<4>(S.s[sl], ip, v, loc.phi);
+          if (elem_out) elem_out[ip - 1] = k;
+          if (hit_out) hit_out[ip - 1] = (int8_t)PMMG_HIT_VOL_WALK;
+        }
+      }
+    }
+    const bool fail = active && status != 1;
+    const int slot = wave_append(&st->nfb_vol, fail);
+    if (fail) fb[slot] = ip;
+    wave_stats(&bs, active, status == 1 ? PMMG_HIT_VOL_WALK : 0, steps);
+  }
+  __syncthreads();
+  bstats_flush(&bs, st);
+}
+
+// ---------------------------------------------------------------- interpolation
+
+__device__ __forceinline__ void wait_lgkm() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// Output rows of one slot for the wave's 64 consecutive queries, written as
+// whole cache lines: each lane puts its row into a wave-private LDS image,
+// then lane l of store instruction t writes piece t*64+l of the image (16-byte
+// pieces for 6-double rows, 8-byte pieces for 3-double rows: every piece
+// inside one row), skipping the rows of `mask` bit 0 (other classes, failed
+// walks, failed inversions: the reference leaves those rows untouched, and
+// the surface kernel writes its own rows concurrently).  A lane storing its
+// own 48-byte row with three 16-byte stores instead writes partial lines in
+// every instruction; that cost ~1 ms of the 2 ms interpolation at cfg4.
+template <int C>
+__device__ __forceinline__ void wave_store_rows(double *out, const double *row, unsigned long long mask,
+                                                double *img) {
+  const int lane = __lane_id();
+  if constexpr (C == 1) {
+    if ((mask >> lane) & 1ULL) nt_store(out + lane, row[0]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < C; j++) img[C * lane + j] = row[j];
+    wait_lgkm();
+    if constexpr (C == 6) {
+      const ntd2 *src = reinterpret_cast<const ntd2 *>(img);
+#pragma unroll
+      for (int t = 0; t < 3; t++) {
+        const int p = 64 * t + lane; // 16-byte piece
+        if ((mask >> (p / 3)) & 1ULL) __builtin_nontemporal_store(src[p], reinterpret_cast<ntd2 *>(out) + p);
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < C; t++) {
+        const int p = 64 * t + lane; // 8-byte piece
+        if ((mask >> (p / C)) & 1ULL) nt_store(out + p, img[p]);
+      }
+    }
+    wait_lgkm(); // the image is reused by the next slot
+  }
+}
+
+// Cooperative row gathers.  The 64 lanes of a wave gather the 256 rows (64
+// queries x 4 vertices) of one 3- or 6-double slot together: piece p = 64 t +
+// lane of the slot's row image (16-byte pieces for 6-double rows, 8-byte
+// pieces for 3-double rows, 3 pieces per row) is loaded by one lane, so a
+// row's pieces share an instruction and every instruction covers ~21 whole
+// rows.  A 6-double slot's rows are gathered in two passes of 128 rows
+// (vertices 0-1, then 2-3 of the wave's queries) through a 768-double image
+// per wave; each lane reads its rows back and evaluates the reference
+// interpolator (same arithmetic, same order).  Scalar slots keep per-lane
+// gathers.
+template <int PASS>
+__device__ __forceinline__ void coop_gather6_pair(const double *in, const int *vid, double *img, double (*m)[6]) {
+  const int lane = __lane_id();
+  double2 b[6];
+#pragma unroll
+  for (int t = 0; t < 6; t++) {
+    const int p = 64 * t + lane, r = p / 3, k = p - 3 * r; // r in [0, 128): query r/2, vertex 2*PASS + r%2
+    const int v = vid[4 * (r >> 1) + 2 * PASS + (r & 1)];
+    b[t] = *reinterpret_cast<const double2 *>(in + (size_t)6 * (v - 1) + 2 * k);
+  }
+#pragma unroll
+  for (int t = 0; t < 6; t++) reinterpret_cast<double2 *>(img)[64 * t + lane] = b[t];
+  wait_lgkm();
+  __builtin_amdgcn_wave_barrier();
+  load6(img + 12 * lane, m[2 * PASS]);
+  load6(img + 12 * lane + 6, m[2 * PASS + 1]);
+  wait_lgkm();
+  __builtin_amdgcn_wave_barrier(); // every lane has read its rows: the image is free again
+}
+
+template <int C>
+__device__ __forceinline__ void coop_slot(const Slot &sl, bool act, const int *v, const double *phi, const int *vid,
+                                          double *img, size_t i0) {
+  if constexpr (C == 6) {
+    double m[4][6];
+    coop_gather6_pair<0>(sl.in, vid, img, m);
+    coop_gather6_pair<1>(sl.in, vid, img, m);
+    double mint[6], mi[6], r[6];
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < 4; i++) { // PMMG_interp4bar_ani: M = invmat(sum_i phi_i invmat(M_i))
+      ok = invmat(m[i], mi) && ok;
+#pragma unroll
+      for (int q = 0; q < 6; q++) mint[q] = (i == 0) ? phi[0] * mi[q] : mint[q] + phi[i] * mi[q];
+    }
+    ok = invmat(mint, r) && ok && act;
+    wave_store_rows<6>(sl.out + (size_t)6 * i0, r, __ballot(ok), img);
+  } else if constexpr (C == 3) {
+    const int lane = __lane_id();
+    double b[12];
+#pragma unroll
+    for (int t = 0; t < 12; t++) {
+      const int p = 64 * t + lane, r = p / 3, k = p - 3 * r;
+      b[t] = sl.in[(size_t)3 * (vid[r] - 1) + k];
+    }
+#pragma unroll
+    for (int t = 0; t < 12; t++) img[64 * t + lane] = b[t];
+    wait_lgkm();
+    __builtin_amdgcn_wave_barrier();
+    const double *base = img + 12 * lane;
+    double row[4][3], r[3];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int j = 0; j < 3; j++) row[i][j] = base[3 * i + j];
+    wait_lgkm();
+    __builtin_amdgcn_wave_barrier(); // the image becomes the store image
+#pragma unroll
+    for (int j = 0; j < 3; j++) r[j] = 0.0; // PMMG_interp4bar_iso: sum from 0.0 in vertex order
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int j = 0; j < 3; j++) r[j] += phi[i] * row[i][j];
+    wave_store_rows<3>(sl.out + (size_t)3 * i0, r, __ballot(act), img);
+  } else if constexpr (C == 1) {
+    double r[1];
+    interp_iso_row<4, 1>(sl.in, v, phi, r);
+    wave_store_rows<1>(sl.out + i0, r, __ballot(act), img);
+  }
+}
+
+// The query's candidate tetra in the reference's arithmetic (exact_accept):
+// on acceptance loc = its vertex ids and exact coordinates; a rejected
+// candidate (the query lies within the filter's margin outside it) goes to
+// the continuation list.  Returns whether the lane interpolates.
+__device__ __forceinline__ bool accept_candidate(const Bg &bg, const double *qxyz, int i, int k, bool act,
+                                                 VolLoc &loc, ContEntry *cont, DevStats *st) {
+  bool acc = false;
+  if (act) {
+    double x[3], p[4][3];
+    load_pt_nt(qxyz, i + 1, x);
+    const int4 tv = tetv_row(bg, k);
+    load_tet_pts(bg, tv, p);
+    acc = exact_accept(x, p, tv, &loc, nullptr);
+  }
+  const bool more = act && !acc;
+  const int slot = wave_append(&st->ncont, more);
+  if (more) cont[slot] = ContEntry{i + 1, k};
+  const unsigned long long hits = __ballot(acc), exact = __ballot(more);
+  if (__lane_id() == 0) {
+    StatPart *pt = stat_part(st);
+    if (hits) atomicAdd(&pt->cnt[PMMG_HIT_VOL_WALK], (unsigned long long)__popcll(hits));
+    if (exact) atomicAdd(&pt->cnt[kCntExact], (unsigned long long)__popcll(exact));
+  }
+  if (!acc) { // idle lanes gather a valid row, never stored
+    loc.v = make_int4(1, 1, 1, 1);
+#pragma unroll
+    for (int f = 0; f < 4; f++) loc.phi[f] = 0.0;
+  }
+  return acc;
+}
+
+// interpolation of the located volume queries in input order (coalesced
+// output rows); the slot layout is a template (codes 1 / 3 / 6, 0 = none)
+template <int C0, int C1, int C2, int C3, int C4, int C5>
+__global__ __launch_bounds__(kBlock) void k_vol_interp(Bg bg, const double *qxyz, const uint8_t *pclass, int np,
+                                                       const int *vloc, ContEntry *cont, DevStats *st, Slots S,
+                                                       int *elem_out, int8_t *hit_out) {
+  __shared__ double img_all[kBlock / 64][256 * 3];
+  __shared__ int vid_all[kBlock / 64][256];
+  double *img = img_all[threadIdx.x >> 6];
+  int *vid = vid_all[threadIdx.x >> 6];
+  const int i = xcd_block() * blockDim.x + threadIdx.x;
+  bool act = i < np && __builtin_nontemporal_load(pclass + i) == PMMG_PT_VOL;
+  const int k = act ? __builtin_nontemporal_load(vloc + i) : 0;
+  act = act && k != 0;
+  if (!__any(act)) return;
+  VolLoc loc;
+  act = accept_candidate(bg, qxyz, i, k, act, loc, cont, st);
+  if (!__any(act)) return;
+  const int v[4] = {loc.v.x, loc.v.y, loc.v.z, loc.v.w};
+  reinterpret_cast<int4 *>(vid)[__lane_id()] = loc.v;
+  wait_lgkm();
+  __builtin_amdgcn_wave_barrier();
+  const size_t w0 = (size_t)(i - __lane_id());
+  coop_slot<C0>(S.s[0], act, v, loc.phi, vid, img, w0);
+  coop_slot<C1>(S.s[1], act, v, loc.phi, vid, img, w0);
+  coop_slot<C2>(S.s[2], act, v, loc.phi, vid, img, w0);
+  coop_slot<C3>(S.s[3], act, v, loc.phi, vid, img, w0);
+  coop_slot<C4>(S.s[4], act, v, loc.phi, vid, img, w0);
+  coop_slot<C5>(S.s[5], act, v, loc.phi, vid, img, w0);
+  if (!act) return;
+  if (elem_out) __builtin_nontemporal_store(k, elem_out + i);
+  if (hit_out) __builtin_nontemporal_store((int8_t)PMMG_HIT_VOL_WALK, hit_out + i);
+}
+
+// any other slot layout (up to kMaxSlot slots in any order): one lane per
+// query, per-lane gathers and stores
+__global__ __launch_bounds__(kBlock) void k_vol_interp_generic(Bg bg, const double *qxyz, const uint8_t *pclass,
+                                                               int np, const int *vloc, ContEntry *cont, DevStats *st,
+                                                               Slots S, int *elem_out, int8_t *hit_out) {
+  const int i = xcd_block() * blockDim.x + threadIdx.x;
+  bool act = i < np && pclass[i] == PMMG_PT_VOL;
+  const int k = act ? vloc[i] : 0;
+  act = act && k != 0;
+  if (!__any(act)) return;
+  VolLoc loc;
+  if (!accept_candidate(bg, qxyz, i, k, act, loc, cont, st)) return;
+  const int v[4] = {loc.v.x, loc.v.y, loc.v.z, loc.v.w};
+  for (int s = 0; s < S.n; s++) interp_dyn<4>(S.s[s], i + 1, v, loc.phi);
+  if (elem_out) elem_out[i] = k;
+  if (hit_out) hit_out[i] = (int8_t)PMMG_HIT_VOL_WALK;
+}
+
+} // namespace pmmg

@@ -17,7 +17,7 @@ import numpy as np
 from ._native import host_lib
 from .synth import Mesh
 
-DEFAULT_HALO = -1.0  # the largest tetra extent around the range's box (> hausd, >> EPS)
+DEFAULT_HALO = -1.0  # the largest tetra extent around the range's box (and never less than hausd)
 
 
 def _p(a):
@@ -58,13 +58,18 @@ def max_tet_extent(bg: Mesh) -> float:
     return float(host_lib().pmmg_max_tet_extent(bg.np, _p(bg.xyz), bg.ne, _p(bg.tetv)))
 
 
-def halo_shard(bg: Mesh, lo, hi, halo: float = DEFAULT_HALO) -> HaloShard:
+def halo_shard(bg: Mesh, lo, hi, halo: float = DEFAULT_HALO, hausd: float = 0.0) -> HaloShard:
     """Shard of `bg` around the box [lo, hi] (halo < 0: in units of the
-    largest tetra extent)."""
+    largest tetra extent).  The halo is never less than 1.01 * hausd: a tria
+    accepts a surface point within hausd of its plane (PMMG_locateChkDistTria,
+    locate_pmmg.c:347-366) and the wedge / cone tests reach hausd too, so a
+    thinner halo could drop the lowest-index accepting tria of a point and
+    change the exhaustive search's answer against the whole group."""
     lib = host_lib()
     lo = np.ascontiguousarray(lo, np.float64)
     hi = np.ascontiguousarray(hi, np.float64)
     h = -halo * max_tet_extent(bg) if halo < 0 else float(halo)
+    h = max(h, 1.01 * float(hausd))
     tet_map = np.empty(bg.ne, np.int32)
     vert_map = np.empty(bg.np, np.int32)
     counts = (ctypes.c_int64 * 2)()

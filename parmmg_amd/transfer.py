@@ -77,37 +77,15 @@ def pack_tet8(tetv: np.ndarray, adja: np.ndarray) -> np.ndarray:
     return np.ascontiguousarray(np.hstack([np.asarray(tetv, np.int32), np.asarray(adja, np.int32)]))
 
 
-def pack_solutions(met, fields):
-    """Packed per-vertex records of the metric and fields
-    (pmmg_hip_set_solutions_packed): size-6 slots first (even columns), then
-    size-3, then size-1, the record padded to an even number of doubles.
-    Returns (rec, met_size, met_off, field_sizes, field_offs)."""
-    slots = ([("m", met)] if met is not None else []) + [(j, f) for j, f in enumerate(fields)]
-    order = sorted(slots, key=lambda s: -s[1].shape[1])  # stable: 6, 3, 1
-    off, col = {}, 0
-    for key, a in order:
-        off[key] = col
-        col += a.shape[1]
-    stride = col + (col & 1)
-    npt = (met if met is not None else fields[0]).shape[0]
-    rec = np.zeros((npt, max(stride, 2)), np.float64)
-    for key, a in slots:
-        rec[:, off[key]:off[key] + a.shape[1]] = a
-    msize = 0 if met is None else met.shape[1]
-    return (rec, msize, off.get("m", 0), [f.shape[1] for f in fields], [off[j] for j in range(len(fields))])
-
-
 class TransferContext:
     """One ``pmmg_hip_ctx`` on a HIP device."""
 
-    def __init__(self, device: int = 0, sort: bool | None = None, scan: bool = False, fused: bool = False):
-        """Volume points are located by per-query adjacency walks (default)
-        or, with scan=True, by the tetra-centric scan.  sort=None picks the
-        query order automatically (Morton-bin unless the numbering is
-        coherent); True / False force binning / input order.  fused=True runs
-        the walk and the interpolation as one kernel."""
+    def __init__(self, device: int = 0, sort: bool | None = None):
+        """sort=None picks the query order on the device (Morton-bin unless
+        the numbering is spatially coherent); True / False force binning /
+        input order."""
         self.lib = hip_lib()
-        opts = (0 if sort is None else (2 if sort else 1)) | (4 if scan else 0) | (8 if fused else 0)
+        opts = 0 if sort is None else (2 if sort else 1)
         self.h = self.lib.pmmg_hip_create(int(device), opts)
         if not self.h:
             raise RuntimeError(f"pmmg_hip_create({device}) failed: no usable HIP device (the transfer step has "
@@ -158,8 +136,11 @@ class TransferContext:
 
     # ------------------------------------------------------------------ C-ABI
     def set_background(self, xyz, tetv, adja, triv, adjt, hausd: float) -> None:
+        """adja None: adjacency built on the device; triv None: boundary trias
+        and their adjacency built on the device; adjt None (triv given): tria
+        adjacency built on the device."""
         where = DEVICE if _is_dev(xyz) else HOST
-        npt, ne, nt = xyz.shape[0], tetv.shape[0], triv.shape[0]
+        npt, ne, nt = xyz.shape[0], tetv.shape[0], (-1 if triv is None else triv.shape[0])
         self._keep = [xyz, tetv, adja, triv, adjt]
         self._ck(self.lib.pmmg_hip_set_background(self.h, npt, _p(xyz), ne, _p(tetv), _p(adja), nt, _p(triv),
                                                   _p(adjt), float(hausd), where), "set_background")
@@ -184,17 +165,18 @@ class TransferContext:
         return a, t
 
     def build_boundary(self, npt: int, tet8: DeviceArray | None = None, tetv: DeviceArray | None = None,
-                       adja: DeviceArray | None = None, adjt: bool = True):
-        """Device-side MMG5_chkBdryTria + MMG3D_hashTria: (triv, adjt) DeviceArrays of nt rows."""
+                       adja: DeviceArray | None = None, adjt: bool = True, tref: DeviceArray | None = None):
+        """Device-side MMG5_chkBdryTria + MMG3D_hashTria: (triv, adjt) DeviceArrays of nt rows
+        (tref: tetra references, for interface faces of a multi-material mesh)."""
         ne = (tet8 if tet8 is not None else tetv).shape[0]
         nt = ctypes.c_int(0)
         # capacity 0: the call only counts (it fails when there are trias, with nt set)
-        self.lib.pmmg_hip_build_boundary(self.h, int(npt), ne, _p(tet8), _p(tetv), _p(adja), 0, ctypes.byref(nt),
-                                         None, None)
+        self.lib.pmmg_hip_build_boundary(self.h, int(npt), ne, _p(tet8), _p(tetv), _p(adja), _p(tref), 0,
+                                         ctypes.byref(nt), None, None)
         n = nt.value
         triv = self.empty((n, 3), np.int32)
         at = self.empty((n, 3), np.int32) if adjt else None
-        self._ck(self.lib.pmmg_hip_build_boundary(self.h, int(npt), ne, _p(tet8), _p(tetv), _p(adja), n,
+        self._ck(self.lib.pmmg_hip_build_boundary(self.h, int(npt), ne, _p(tet8), _p(tetv), _p(adja), _p(tref), n,
                                                   ctypes.byref(nt), _p(triv), _p(at)), "build_boundary")
         return triv, at
 
@@ -207,16 +189,6 @@ class TransferContext:
         self._sol_keep = [met, fields, sizes, ptrs]
         self._ck(self.lib.pmmg_hip_set_solutions(self.h, msize, _p(met), len(fields), sizes, ptrs, where),
                  "set_solutions")
-
-    def set_solutions_packed(self, rec, met_size: int, met_off: int, field_sizes, field_offs) -> None:
-        """Solutions as packed per-vertex records (pack_solutions)."""
-        where = DEVICE if _is_dev(rec) else HOST
-        nf = len(field_sizes)
-        sizes = (ctypes.c_int * max(1, nf))(*[int(x) for x in field_sizes])
-        offs = (ctypes.c_int * max(1, nf))(*[int(x) for x in field_offs])
-        self._sol_keep = [rec, sizes, offs]
-        self._ck(self.lib.pmmg_hip_set_solutions_packed(self.h, int(met_size), int(met_off), nf, sizes, offs, _p(rec),
-                                                        int(rec.shape[1]), where), "set_solutions_packed")
 
     def locate_interp(self, xyz_new, pclass, met_out, fields_out, elem_out=None, hit_out=None,
                       sync: bool = True) -> HipStats | None:
@@ -273,51 +245,100 @@ def transfer(mesh_old, met, fields, xyz_new, pclass, hausd=0.01, device=0, sort=
 
 class OldGroup(ctypes.Structure):
     _fields_ = [("np", ctypes.c_int), ("ne", ctypes.c_int), ("nt", ctypes.c_int),
-                ("xyz", ctypes.c_void_p), ("tetv", ctypes.c_void_p), ("adja", ctypes.c_void_p),
-                ("triv", ctypes.c_void_p), ("adjt", ctypes.c_void_p), ("hausd", ctypes.c_double),
-                ("met_size", ctypes.c_int), ("met", ctypes.c_void_p), ("nfield", ctypes.c_int),
-                ("field_size", ctypes.c_void_p), ("field", ctypes.c_void_p)]
+                ("xyz", ctypes.c_void_p), ("tag", ctypes.c_void_p), ("tetv", ctypes.c_void_p),
+                ("adja", ctypes.c_void_p), ("triv", ctypes.c_void_p), ("adjt", ctypes.c_void_p),
+                ("hausd", ctypes.c_double), ("met_size", ctypes.c_int), ("met", ctypes.c_void_p),
+                ("nfield", ctypes.c_int), ("field_size", ctypes.c_void_p), ("field", ctypes.c_void_p)]
 
 
 class NewGroup(ctypes.Structure):
     _fields_ = [("np", ctypes.c_int), ("ne", ctypes.c_int), ("xyz", ctypes.c_void_p), ("tag", ctypes.c_void_p),
-                ("tetv", ctypes.c_void_p), ("met", ctypes.c_void_p), ("field", ctypes.c_void_p),
-                ("elem", ctypes.c_void_p), ("hit", ctypes.c_void_p)]
+                ("tetv", ctypes.c_void_p), ("met_size", ctypes.c_int), ("met", ctypes.c_void_p),
+                ("field", ctypes.c_void_p), ("elem", ctypes.c_void_p), ("hit", ctypes.c_void_p),
+                ("hsiz", ctypes.c_double), ("hmin", ctypes.c_double), ("hmax", ctypes.c_double),
+                ("ani", ctypes.c_int)]
 
 
 TAG_REQ, TAG_BDY, TAG_NUL = 1 << 2, 1 << 4, 1 << 14
 
 
-def interp_metrics_and_fields(ctx: TransferContext, old_groups, new_groups, input_met: int = 1, hsiz: float = 0.0):
-    """PMMG_interpMetricsAndFields over groups (src/interpmesh_pmmg.c:663-741).
+class _Groups:
+    """ctypes views of old/new group dicts (keeps every array alive).
 
-    ``old_groups``: list of dicts {mesh, met, fields, hausd};
-    ``new_groups``: list of dicts {xyz, tag, tetv, met, fields[, elem, hit]} whose
-    ``met`` / ``fields`` arrays are filled in place.  Returns (ier, stats)."""
-    lib = host_lib()
-    fn = lib.pmmg_interp_metrics_and_fields
-    fn.restype = ctypes.c_int
-    fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_double,
-                   ctypes.POINTER(HipStats)]
-    ng = len(old_groups)
-    olds = (OldGroup * ng)()
-    news = (NewGroup * ng)()
-    keep = []
-    for i, (o, g) in enumerate(zip(old_groups, new_groups)):
-        m = o["mesh"]
-        fs = list(o.get("fields", []))
-        fsz = (ctypes.c_int * max(1, len(fs)))(*[f.shape[1] for f in fs])
-        fpt = (ctypes.c_void_p * max(1, len(fs)))(*[_p(f) for f in fs])
-        met = o.get("met")
-        olds[i] = OldGroup(m.np, m.ne, m.nt, _p(m.xyz), _p(m.tetv), _p(m.adja), _p(m.triv), _p(m.adjt),
-                           float(o.get("hausd", 0.01)), 0 if met is None else met.shape[1], _p(met), len(fs),
-                           ctypes.cast(fsz, ctypes.c_void_p), ctypes.cast(fpt, ctypes.c_void_p))
-        gf = list(g.get("fields", []))
-        gpt = (ctypes.c_void_p * max(1, len(gf)))(*[_p(f) for f in gf])
-        news[i] = NewGroup(g["xyz"].shape[0], g["tetv"].shape[0], _p(g["xyz"]), _p(g.get("tag")), _p(g["tetv"]),
-                           _p(g.get("met")), ctypes.cast(gpt, ctypes.c_void_p), _p(g.get("elem")), _p(g.get("hit")))
-        keep += [fsz, fpt, gpt]
+    old: {mesh, met, fields, hausd[, tag, device_adjacency, device_boundary]}
+    new: {xyz, tag, tetv, met, fields[, elem, hit, hsiz, hmin, hmax, ani]}"""
+
+    def __init__(self, old_groups, new_groups):
+        ng = len(old_groups)
+        self.olds = (OldGroup * ng)()
+        self.news = (NewGroup * ng)()
+        self.keep = []
+        for i, (o, g) in enumerate(zip(old_groups, new_groups)):
+            m = o["mesh"]
+            fs = list(o.get("fields", []))
+            fsz = (ctypes.c_int * max(1, len(fs)))(*[f.shape[1] for f in fs])
+            fpt = (ctypes.c_void_p * max(1, len(fs)))(*[_p(f) for f in fs])
+            met = o.get("met")
+            dev_bdy = o.get("device_boundary", False)
+            self.olds[i] = OldGroup(m.np, m.ne, -1 if dev_bdy else m.nt, _p(m.xyz), _p(o.get("tag")), _p(m.tetv),
+                                    None if o.get("device_adjacency", False) else _p(m.adja),
+                                    None if dev_bdy else _p(m.triv), None if dev_bdy else _p(m.adjt),
+                                    float(o.get("hausd", 0.01)), 0 if met is None else met.shape[1], _p(met),
+                                    len(fs), ctypes.cast(fsz, ctypes.c_void_p), ctypes.cast(fpt, ctypes.c_void_p))
+            gf = list(g.get("fields", []))
+            gpt = (ctypes.c_void_p * max(1, len(gf)))(*[_p(f) for f in gf])
+            gm = g.get("met")
+            self.news[i] = NewGroup(g["xyz"].shape[0], g["tetv"].shape[0], _p(g["xyz"]), _p(g.get("tag")),
+                                    _p(g["tetv"]), 0 if gm is None else gm.shape[1], _p(gm),
+                                    ctypes.cast(gpt, ctypes.c_void_p), _p(g.get("elem")), _p(g.get("hit")),
+                                    float(g.get("hsiz", 0.0)), float(g.get("hmin", 0.0)), float(g.get("hmax", 0.0)),
+                                    int(g.get("ani", 0)))
+            self.keep += [fsz, fpt, gpt]
+
+
+def interp_metrics_and_fields(ctx: TransferContext, old_groups, new_groups, input_met: int = 1):
+    """PMMG_interpMetricsAndFields over groups (src/interpmesh_pmmg.c:663-741)
+    through the C host layer (pmmg_interp_metrics_and_fields).  The new
+    groups' ``met`` / ``fields`` arrays are filled in place; per-group
+    ``hsiz`` > 0 replaces the metric by a constant (MMG3D_Set_constantSize).
+    Returns (ier, stats)."""
+    G = _Groups(old_groups, new_groups)
     st = HipStats()
-    ier = fn(ctx.h, ng, ctypes.cast(olds, ctypes.c_void_p), ctypes.cast(news, ctypes.c_void_p), int(input_met),
-             float(hsiz), ctypes.byref(st))
+    ier = host_lib().pmmg_interp_metrics_and_fields(ctx.h, len(old_groups), ctypes.cast(G.olds, ctypes.c_void_p),
+                                                    ctypes.cast(G.news, ctypes.c_void_p), int(input_met),
+                                                    ctypes.byref(st))
     return ier, st
+
+
+def copy_metrics_and_fields_point(old_group, new_group, perm_nod_glob=None, renum: int = 1, input_met: int = 1):
+    """PMMG_copyMetricsAndFields_point (src/interpmesh_pmmg.c:432-446) through
+    the C host layer: rows of the old group's valid MG_REQ points copied into
+    the new group's arrays (through perm_nod_glob, 1-based with entry 0
+    unused, when renum and a permutation are given).  Returns 1/0."""
+    G = _Groups([old_group], [new_group])
+    perm = None if perm_nod_glob is None else np.ascontiguousarray(perm_nod_glob, np.int32)
+    return host_lib().pmmg_copy_metrics_and_fields_point(ctypes.cast(G.olds, ctypes.c_void_p),
+                                                         ctypes.cast(G.news, ctypes.c_void_p), _p(perm),
+                                                         int(renum), int(input_met))
+
+
+def classify_points(new_group) -> np.ndarray:
+    """The reference's point classification (src/interpmesh_pmmg.c:535-550)
+    through the C host layer: PT_SKIP / PT_VOL / PT_BDY per new point."""
+    g = dict(new_group)
+    g.setdefault("fields", [])
+    G = _Groups([dict(mesh=_EmptyMesh(), fields=[])], [g])
+    pc = np.empty(g["xyz"].shape[0], np.uint8)
+    host_lib().pmmg_classify_points(ctypes.cast(G.news, ctypes.c_void_p), _p(pc))
+    return pc
+
+
+def set_constant_metric(new_group) -> int:
+    """MMG3D_Set_constantSize's fill through the C host layer (restated, unpinned)."""
+    G = _Groups([dict(mesh=_EmptyMesh(), fields=[])], [new_group])
+    return host_lib().pmmg_set_constant_metric(ctypes.cast(G.news, ctypes.c_void_p))
+
+
+class _EmptyMesh:
+    np = ne = nt = 0
+    xyz = tetv = adja = triv = adjt = None

@@ -25,7 +25,6 @@ EPS = O.EPS
 REL_TOL = 1e-12
 
 VOL_WALK, VOL_EXHAUST, VOL_CLOSEST = 1, 2, 3
-VOL_SCAN = 12
 BDY_FACE, BDY_EDGE, BDY_VERTEX, BDY_WEDGE, BDY_CONE, BDY_EXHAUST, BDY_STALE, BDY_CLOSEST = range(4, 12)
 
 
@@ -46,22 +45,17 @@ def make_case(kind=synth.CUBE, n_old=6, n_new=7, metric=synth.F_ANI,
     return case
 
 
-def run_gpu(case, sort=None, ctx=None, scan=False, fused=False, tet8=False, packed=False):
+def run_gpu(case, sort=None, ctx=None, tet8=False):
     bg, new = case["bg"], case["new"]
     own = ctx is None
-    ctx = ctx or TransferContext(0, sort=sort, scan=scan, fused=fused)
+    ctx = ctx or TransferContext(0, sort=sort)
     try:
         if tet8:
             from parmmg_amd.transfer import pack_tet8
             ctx.set_background_tet8(bg.xyz, pack_tet8(bg.tetv, bg.adja), bg.triv, bg.adjt, case["hausd"])
         else:
             ctx.set_background(bg.xyz, bg.tetv, bg.adja, bg.triv, bg.adjt, case["hausd"])
-        if packed:
-            from parmmg_amd.transfer import pack_solutions
-            rec, ms, mo, fs, fo = pack_solutions(case["met"], case["fields"])
-            ctx.set_solutions_packed(rec, ms, mo, fs, fo)
-        else:
-            ctx.set_solutions(case["met"], case["fields"])
+        ctx.set_solutions(case["met"], case["fields"])
         npn = new.np
         met_out = None if case["met"] is None else np.full((npn, case["met"].shape[1]), np.nan)
         f_out = [np.full((npn, f.shape[1]), np.nan) for f in case["fields"]]
@@ -115,7 +109,7 @@ def check(case, gpu, max_points=None):
         # (ii) acceptance of the chosen element
         if h == VOL_WALK:
             assert not is_bdy and O.tetra_minbary(B, k, x) > -EPS, (i, h, k)
-        elif h in (VOL_EXHAUST, VOL_SCAN):
+        elif h == VOL_EXHAUST:
             assert not is_bdy and k == O.first_accepting_tetra(B, x), (i, h, k)
         elif h == VOL_CLOSEST:
             kb = O.closest_tetra(B, x)
@@ -148,7 +142,7 @@ def check(case, gpu, max_points=None):
         # (i) identical element where the reference is unambiguous
         if ref is not None:
             rh = int(ref["hit"][i])
-            if rh in (VOL_WALK, VOL_EXHAUST, VOL_SCAN) and ref["minbary"][i] > EPS:
+            if rh in (VOL_WALK, VOL_EXHAUST) and ref["minbary"][i] > EPS:
                 rep["class_i"] += 1
                 same_elem = int(ref["elem"][i]) == k
                 rep["class_i_same"] += int(same_elem)

@@ -12,7 +12,7 @@ import pytest
 
 from parity import check, make_case, run_gpu
 from parmmg_amd import configs, synth
-from parmmg_amd.transfer import TransferContext, pack_solutions, pack_tet8
+from parmmg_amd.transfer import TransferContext, pack_tet8
 
 C = synth.CUBE
 
@@ -57,7 +57,7 @@ def test_background_without_trias_volume_only():
 ])
 def test_unusual_slot_layouts(fields):
     case = make_case(kind=C, n_old=5, n_new=6, metric=synth.F_ISO, fields=fields)
-    for kw in ({}, dict(packed=True, tet8=True)):
+    for kw in ({}, dict(tet8=True)):
         gpu = run_gpu(case, **kw)
         rep = check(case, gpu)
         assert rep["class_i"] == rep["class_i_same"]
@@ -82,17 +82,17 @@ def _full_size(w, seed=synth.SEED):
     return bg, new, met, fields, pc
 
 
-def _run_dev(ctx, bg, new, met, fields, pc, hausd, packed=False):
-    d = dict(xyz=ctx.upload(bg.xyz), tet8=ctx.upload(pack_tet8(bg.tetv, bg.adja)), triv=ctx.upload(bg.triv),
-             adjt=ctx.upload(bg.adjt), q=ctx.upload(new.xyz), pc=ctx.upload(pc))
-    ctx.set_background_tet8(d["xyz"], d["tet8"], d["triv"], d["adjt"], hausd)
-    if packed:
-        rec, *meta = pack_solutions(met, fields)
-        d["rec"] = ctx.upload(rec)
-        ctx.set_solutions_packed(d["rec"], *meta)
+def _run_dev(ctx, bg, new, met, fields, pc, hausd, separate=False):
+    d = dict(xyz=ctx.upload(bg.xyz), triv=ctx.upload(bg.triv), adjt=ctx.upload(bg.adjt), q=ctx.upload(new.xyz),
+             pc=ctx.upload(pc))
+    if separate:
+        d["tetv"], d["adja"] = ctx.upload(bg.tetv), ctx.upload(bg.adja)
+        ctx.set_background(d["xyz"], d["tetv"], d["adja"], d["triv"], d["adjt"], hausd)
     else:
-        d["met"], d["f"] = ctx.upload(met), [ctx.upload(f) for f in fields]
-        ctx.set_solutions(d["met"], d["f"])
+        d["tet8"] = ctx.upload(pack_tet8(bg.tetv, bg.adja))
+        ctx.set_background_tet8(d["xyz"], d["tet8"], d["triv"], d["adjt"], hausd)
+    d["met"], d["f"] = ctx.upload(met), [ctx.upload(f) for f in fields]
+    ctx.set_solutions(d["met"], d["f"])
     mo = ctx.empty((new.np, met.shape[1]), np.float64)
     fo = [ctx.empty((new.np, f.shape[1]), np.float64) for f in fields]
     el, hit = ctx.empty((new.np,), np.int32), ctx.empty((new.np,), np.int8)
@@ -110,7 +110,7 @@ def test_full_size_cfg3_properties():
     bg, new, met, fields, pc = _full_size(w)
     with TransferContext(0) as ctx:
         mo, fo, el, hit, st = _run_dev(ctx, bg, new, met, fields, pc, w.hausd)
-        mo2, fo2, el2, hit2, _ = _run_dev(ctx, bg, new, met, fields, pc, w.hausd, packed=True)
+        mo2, fo2, el2, hit2, _ = _run_dev(ctx, bg, new, met, fields, pc, w.hausd, separate=True)
     act = pc != 0
     assert ((hit & 15) != 0).sum() == act.sum()
     assert ((hit & 15)[~act] == 0).all()
@@ -125,7 +125,7 @@ def test_full_size_cfg3_properties():
                                rtol=1e-12)
     # metric: SPD, finite on every processed point
     assert np.isfinite(mo[act]).all()
-    # packed records give bit-identical results (same kernels, same elements)
+    # separate tetv / adja arrays give bit-identical results (same kernels, same elements)
     np.testing.assert_array_equal(el, el2)
     np.testing.assert_array_equal(mo, mo2)
     for a, b in zip(fo, fo2):

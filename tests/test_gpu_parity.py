@@ -22,10 +22,10 @@ CASES = {
 }
 
 
-MODES = {"auto": {}, "morton": dict(sort=True), "nosort": dict(sort=False), "fused": dict(fused=True),
-         "scan": dict(scan=True),
-         "tet8": dict(tet8=True), "tet8-scan": dict(tet8=True, scan=True),
-         "packed": dict(tet8=True, packed=True), "packed-fused-morton": dict(tet8=True, packed=True, fused=True, sort=True)}
+# the shipped paths: query order chosen on the device, forced Morton bins,
+# forced input order; separate tetv/adja arrays or packed tet8 records
+MODES = {"auto": {}, "morton": dict(sort=True), "nosort": dict(sort=False), "tet8": dict(tet8=True),
+         "tet8-morton": dict(tet8=True, sort=True)}
 
 
 @pytest.mark.gpu
@@ -41,7 +41,7 @@ def test_parity_small(name, mode):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["auto", "scan"])
+@pytest.mark.parametrize("mode", ["auto", "morton"])
 def test_fallback_paths_outside_domain(mode):
     """Points pushed outside the background make the walks get stuck; the
     exhaustive / closest kernels must reproduce the reference semantics."""
@@ -78,9 +78,13 @@ def test_invmat_failure_leaves_rows_untouched():
 
 
 @pytest.mark.gpu
-def test_host_layer_groups_and_hsiz():
+@pytest.mark.parametrize("device_built", [False, True])
+def test_host_layer_groups_and_hsiz(device_built):
     """C host layer (PMMG_interpMetricsAndFields mirror): two groups, REQ
-    points copied, hsiz > 0 replaces the metric by a constant."""
+    points skipped, hsiz > 0 replaces the metric by a constant.  With
+    device_built the adjacency and the boundary trias are not handed over:
+    the module builds them on the device (MMG3D_hashTetra / MMG5_chkBdryTria
+    results), with identical outputs."""
     from parmmg_amd.transfer import TAG_BDY, TAG_REQ, TransferContext, interp_metrics_and_fields
 
     olds, news, cases = [], [], []
@@ -89,14 +93,15 @@ def test_host_layer_groups_and_hsiz():
         new = case["new"]
         tag = np.where(new.isbdy == 1, TAG_BDY, 0).astype(np.uint16)
         tag[::11] |= TAG_REQ
-        olds.append(dict(mesh=case["bg"], met=case["met"], fields=case["fields"], hausd=case["hausd"]))
+        olds.append(dict(mesh=case["bg"], met=case["met"], fields=case["fields"], hausd=case["hausd"],
+                         device_adjacency=device_built, device_boundary=device_built))
         met = np.full((new.np, 6), np.nan)
         fs = [np.full((new.np, f.shape[1]), np.nan) for f in case["fields"]]
-        news.append(dict(xyz=new.xyz, tag=tag, tetv=new.tetv, met=met, fields=fs,
+        news.append(dict(xyz=new.xyz, tag=tag, tetv=new.tetv, met=met, fields=fs, ani=1,
                          elem=np.zeros(new.np, np.int32), hit=np.zeros(new.np, np.int8)))
         cases.append(case)
     with TransferContext(0) as ctx:
-        ier, st = interp_metrics_and_fields(ctx, olds, news, input_met=1, hsiz=0.0)
+        ier, st = interp_metrics_and_fields(ctx, olds, news, input_met=1)
         assert ier == 1
         for case, g in zip(cases, news):
             req = (g["tag"] & TAG_REQ) != 0
@@ -104,53 +109,38 @@ def test_host_layer_groups_and_hsiz():
             case["pclass"] = np.where(req, 0, np.where(case["new"].isbdy == 1, 2, 1)).astype(np.uint8)
             rep = check(case, dict(met=g["met"], fields=g["fields"], elem=g["elem"], hit=g["hit"]))
             assert rep["n"] == int((~req).sum())
-        # hsiz > 0: constant metric, fields still interpolated
+        # hsiz > 0: constant metric (clamped to hmax), fields still interpolated
         for g in news:
             g["met"][:] = np.nan
-        ier, st = interp_metrics_and_fields(ctx, olds, news, input_met=1, hsiz=0.05)
+            g["hsiz"], g["hmax"] = 0.05, 0.04
+        ier, st = interp_metrics_and_fields(ctx, olds, news, input_met=1)
         assert ier == 1
         for g in news:
-            np.testing.assert_array_equal(g["met"][:, 0], np.full(g["met"].shape[0], 1.0 / 0.05 ** 2))
+            np.testing.assert_array_equal(g["met"][:, 0], np.full(g["met"].shape[0], 1.0 / 0.04 ** 2))
             np.testing.assert_array_equal(g["met"][:, 1], 0.0)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["cube-ani-6-7", "shell-ani-8-12", "cube-nomet-tensor-5-9"])
-def test_interp_gather_variants_identical(name, monkeypatch):
-    """Per-lane gathers (COOP=0), cooperative gathers (1) and cooperative
-    gathers through the half-size image (2) give bit-identical outputs, which
-    meet the parity contract."""
+@pytest.mark.parametrize("name", ["cube-ani-6-7", "shell-ani-8-12", "cube-jitterbg-10-13", "cube-nomet-tensor-5-9"])
+def test_filter_walk_vs_exact_walk(name, monkeypatch):
+    """PMMG_HIP_FILTER_STEPS=0 (test-only) hands every volume query straight
+    to the exact fp64 walk (k_vol_walk_exact); both paths meet the contract,
+    locate every class (i) point in the same tetra, and give bit-identical
+    values wherever they chose the same tetra."""
     case = make_case(**CASES[name])
     outs = {}
-    for coop in ("0", "1", "2"):
-        monkeypatch.setenv("PMMG_HIP_COOP", coop)  # read by pmmg_hip_create
-        outs[coop] = run_gpu(case, tet8=True)
-    rep = check(case, outs["2"])
-    assert rep["n"] == int((case["pclass"] != 0).sum()) and rep["class_i"] == rep["class_i_same"]
-    for coop in ("0", "1"):
-        a, b = outs[coop], outs["2"]
-        assert np.array_equal(a["elem"], b["elem"]) and np.array_equal(a["hit"], b["hit"])
-        for x, y in zip(([a["met"]] if a["met"] is not None else []) + a["fields"],
-                        ([b["met"]] if b["met"] is not None else []) + b["fields"]):
-            assert np.array_equal(x, y, equal_nan=True)
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("name", ["cube-ani-6-7", "shell-iso-12-16"])
-@pytest.mark.parametrize("knob", ["PMMG_HIP_WALKB", "PMMG_HIP_BDYEARLY", "PMMG_HIP_INTERPB"])
-def test_walk_block_sizes_identical(name, knob, monkeypatch):
-    """One-wave walk blocks (PMMG_HIP_WALKB=64 vs 256) and the surface kernel
-    enqueued before the walk (PMMG_HIP_BDYEARLY=1 vs 0) locate and
-    interpolate exactly alike."""
-    case = make_case(**CASES[name])
-    outs = {}
-    sized = knob.endswith("B") and not knob.endswith("EARLY")
-    for wb, val in (("256", "256" if sized else "0"), ("64", "64" if sized else "1")):
-        monkeypatch.setenv(knob, val)  # read by pmmg_hip_create
-        outs[wb] = run_gpu(case, tet8=True)
-    rep = check(case, outs["64"])
-    assert rep["n"] == int((case["pclass"] != 0).sum()) and rep["class_i"] == rep["class_i_same"]
-    a, b = outs["256"], outs["64"]
-    assert np.array_equal(a["elem"], b["elem"]) and np.array_equal(a["hit"], b["hit"])
-    for x, y in zip([a["met"]] + a["fields"], [b["met"]] + b["fields"]):
-        assert np.array_equal(x, y, equal_nan=True)
+    for val in ("0", None):
+        if val is None:
+            monkeypatch.delenv("PMMG_HIP_FILTER_STEPS", raising=False)
+        else:
+            monkeypatch.setenv("PMMG_HIP_FILTER_STEPS", val)  # read by pmmg_hip_create
+        outs[val] = run_gpu(case, tet8=True)
+        rep = check(case, outs[val])
+        assert rep["n"] == int((case["pclass"] != 0).sum()) and rep["class_i"] == rep["class_i_same"]
+    a, b = outs["0"], outs[None]
+    assert a["stats"]["nvol_exact"] == a["stats"]["nvol"]
+    same = a["elem"] == b["elem"]
+    assert same.mean() > 0.99
+    for x, y in zip(([a["met"]] if a["met"] is not None else []) + a["fields"],
+                    ([b["met"]] if b["met"] is not None else []) + b["fields"]):
+        assert np.array_equal(x[same], y[same], equal_nan=True)
