@@ -28,6 +28,7 @@ HIP_SO = os.path.join(PKG, "libpmmg_hip.so")
 HOST_SO = os.path.join(PKG, "libpmmg_host.so")
 SYNTH_SO = os.path.join(PKG, "libpmmg_synth.so")
 ORACLE_SO = os.path.join(ORACLE, "liboracle.so")
+C_TEST = os.path.join(ROOT, "tests", "c", "test_c_abi")
 
 ARCH = "gfx950"
 
@@ -95,11 +96,26 @@ def build_oracle(force: bool = False) -> str:
     return ORACLE_SO
 
 
+def build_c_test(force: bool = False) -> str:
+    """tests/c/test_c_abi: the C-ABI driven from C, linked against both
+    product libraries (rpath relative to the binary, so it runs from any copy
+    of the tree)."""
+    src = os.path.join(ROOT, "tests", "c", "test_c_abi.c")
+    synth = os.path.join(CSRC, "pmmg_synth.c")
+    deps = [src, synth, HIP_SO, HOST_SO, os.path.join(INC, "parmmg_hip.h"), os.path.join(CSRC, "pmmg_host.h"),
+            __file__]
+    if force or _stale(C_TEST, deps):
+        _run(["gcc", "-O2", "-std=c99", "-Wall", "-Wextra", f"-I{INC}", f"-I{CSRC}", "-o", C_TEST, src, synth,
+              f"-L{PKG}", "-lpmmg_host", "-lpmmg_hip", "-lm", "-Wl,-rpath,$ORIGIN/../../parmmg_amd"])
+    return C_TEST
+
+
 def build_all(force: bool = False) -> None:
     build_hip(force)
     build_host(force)
     build_synth(force)
     build_oracle(force)
+    build_c_test(force)
 
 
 if __name__ == "__main__":

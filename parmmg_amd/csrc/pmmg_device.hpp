@@ -30,6 +30,7 @@ constexpr int kBlock = 256;
 // line, so a walk step costs one line request for the tetra instead of two.
 struct Bg {
   const double *xyz;
+  const int *xq; // fixed-point copy of xyz (3 int32 per vertex, Frame::quant), built per call
   const int4 *tetv;
   const int4 *adja;
   const int *triv;

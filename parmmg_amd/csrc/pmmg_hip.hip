@@ -46,18 +46,18 @@ namespace {
 
 // ---------------------------------------------------------------- slot layouts
 
-typedef void (*VolInterpFn)(Bg, const double *, const uint8_t *, int, const int *, ContEntry *, DevStats *, Slots,
-                            int *, int8_t *);
+typedef void (*VolFn)(Bg, const Frame *, const unsigned long long *, int, const double *, const uint8_t *,
+                      const int *, int, ContEntry *, DevStats *, Slots, int *, int8_t *, int);
 
 struct LayoutEntry {
   int c[6];
-  VolInterpFn fn;
+  VolFn fn;
 };
 
-#define PMMG_LAYOUT(a, b, c, d, e, f) {{a, b, c, d, e, f}, k_vol_interp<a, b, c, d, e, f>}
+#define PMMG_LAYOUT(a, b, c, d, e, f) {{a, b, c, d, e, f}, k_vol<a, b, c, d, e, f>}
 // common slot layouts (metric first): aniso metric + scalar/vector/tensor
 // (BASELINE cfg3/cfg4, libexamples cube-solphys.sol), iso metric + scalars
-// (cfg2, cfg5), metric only; anything else runs k_vol_interp_generic
+// (cfg2, cfg5), metric only; anything else runs the runtime-layout variant
 const LayoutEntry kLayouts[] = {
     PMMG_LAYOUT(6, 1, 3, 6, 0, 0), PMMG_LAYOUT(6, 1, 3, 6, 1, 0), PMMG_LAYOUT(1, 1, 0, 0, 0, 0),
     PMMG_LAYOUT(1, 1, 1, 1, 1, 1), PMMG_LAYOUT(1, 1, 1, 0, 0, 0), PMMG_LAYOUT(6, 0, 0, 0, 0, 0),
@@ -65,7 +65,7 @@ const LayoutEntry kLayouts[] = {
 };
 #undef PMMG_LAYOUT
 
-VolInterpFn pick_layout(const Slots &S) {
+VolFn pick_layout(const Slots &S) {
   for (const LayoutEntry &e : kLayouts) {
     int n = 0;
     while (n < 6 && e.c[n] > 0) n++;
@@ -74,7 +74,7 @@ VolInterpFn pick_layout(const Slots &S) {
     for (int j = 0; j < n; j++) ok = ok && (S.s[j].code == e.c[j]);
     if (ok) return e.fn;
   }
-  return k_vol_interp_generic;
+  return k_vol<-1, 0, 0, 0, 0, 0>;
 }
 
 // zero n ints when the device's order flag equals `want` (-1: always)
@@ -94,7 +94,7 @@ struct DevBuf {
 };
 
 enum {
-  EV_START, EV_PREP, EV_ORDER, EV_WALK, EV_VOL, EV_JOIN, EV_END, EV_BDY0, EV_BDY1, EV_COUNT
+  EV_START, EV_FRAME, EV_PREP, EV_ORDER, EV_VOL0, EV_WALK, EV_VOL, EV_JOIN, EV_END, EV_BDY0, EV_BDY1, EV_COUNT
 };
 
 struct pmmg_hip_ctx {
@@ -113,7 +113,7 @@ struct pmmg_hip_ctx {
   DevBuf o_xyz, o_tetv, o_adja, o_triv, o_adjt, o_met;
   std::vector<DevBuf> o_f;
   // work buffers
-  DevBuf frame, stats, grid, sgrid, cnt, off, binrank, order_v, order_b, vloc, cont;
+  DevBuf frame, stats, grid, sgrid, cnt, off, binrank, order_v, order_b, cont, xq;
   DevBuf scan_a, cls_cnt;                    // scan block sums, class counts
   DevBuf qmin;                               // tetra quality minimum (pmmg_hip_tetra_qual)
   DevBuf fb_vol, fb_bdy, best, ckey, cidx, bbest, bckey, bcidx;
@@ -387,7 +387,7 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   (void)hipStreamSynchronize(c->stream2);
   DevBuf *bufs[] = {&c->o_xyz, &c->o_tetv, &c->o_adja, &c->o_triv, &c->o_adjt, &c->o_met, &c->frame,
                     &c->stats, &c->grid, &c->sgrid, &c->cnt, &c->off, &c->binrank, &c->order_v,
-                    &c->order_b, &c->vloc, &c->cont, &c->scan_a, &c->cls_cnt, &c->qmin, &c->fb_vol, &c->fb_bdy,
+                    &c->order_b, &c->cont, &c->xq, &c->scan_a, &c->cls_cnt, &c->qmin, &c->fb_vol, &c->fb_bdy,
                     &c->best, &c->ckey, &c->cidx, &c->bbest, &c->bckey, &c->bcidx, &c->h_xyz,
                     &c->h_cls, &c->h_met, &c->h_elem, &c->h_hit};
   for (DevBuf *b : bufs) release(*b);
@@ -683,7 +683,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   const long long nbin2 = 2LL * nbins;
   if (!ensure(c, c->frame, sizeof(Frame)) || !ensure(c, c->stats, sizeof(DevStats) + kStatParts * sizeof(StatPart)) ||
       !ensure(c, c->grid, 8 * (size_t)ng) || !ensure(c, c->sgrid, 4 * (size_t)nsg) || !ensure(c, c->order_v, 4 * nq) ||
-      !ensure(c, c->order_b, 4 * nq) || !ensure(c, c->vloc, 4 * nq) ||
+      !ensure(c, c->order_b, 4 * nq) || 
       !ensure(c, c->cont, sizeof(ContEntry) * nq) || !ensure(c, c->cnt, 4 * (size_t)nbin2) ||
       !ensure(c, c->off, 4 * (size_t)(nbin2 + 1)) || !ensure(c, c->binrank, 8 * nq) ||
       !ensure(c, c->scan_a, 4 * (size_t)(nbin2 / kScanChunk + 1)) || !ensure(c, c->cls_cnt, 4 * (size_t)ncls) ||
@@ -691,6 +691,8 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
       !ensure(c, c->ckey, 8 * nq) || !ensure(c, c->cidx, 4 * nq) || !ensure(c, c->bbest, 4 * nq) ||
       !ensure(c, c->bckey, 8 * nq) || !ensure(c, c->bcidx, 4 * nq))
     return 0;
+  if (!ensure(c, c->xq, sizeof(int) * 3 * (size_t)bg.np)) return 0;
+  bg.xq = (const int *)c->xq.p;
   Frame *fr = (Frame *)c->frame.p;
   DevStats *st = (DevStats *)c->stats.p;
   unsigned long long *grid = (unsigned long long *)c->grid.p;
@@ -698,13 +700,47 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   int *order_v = (int *)c->order_v.p, *order_b = (int *)c->order_b.p;
   const int force = (c->options & PMMG_HIP_OPT_SORT) ? 1 : (c->options & PMMG_HIP_OPT_NOSORT) ? 0 : -1;
 
-  // ---- preparation (main stream)
+  // ---- frame (main stream)
   HIPCK(c, hipEventRecord(c->ev[EV_START], s));
   hipLaunchKernelGGL(k_reset, dim3(blocks_for(ng > nsg ? ng : nsg, 2048)), dim3(kBlock), 0, s, fr, st, grid, ng,
                      sgrid, nsg);
-  hipLaunchKernelGGL(k_coherence, dim3(1), dim3(kBlock), 0, s, xyz_new, np_new, st, force);
-  hipLaunchKernelGGL(k_bbox, dim3(blocks_for(bg.np / 16 + 1, 1024)), dim3(kBlock), 0, s, bg.xyz, bg.np, fr, 16);
+  hipLaunchKernelGGL(k_bbox, dim3(blocks_for(bg.np / 16 + 1, 256)), dim3(kBlock), 0, s, bg.xyz, bg.np, fr, 16);
   hipLaunchKernelGGL(k_frame_final, dim3(1), dim3(1), 0, s, fr, g, gs, gb);
+  HIPCK(c, hipGetLastError());
+  HIPCK(c, hipEventRecord(c->ev[EV_FRAME], s));
+
+  // ---- query order (second stream, concurrent with the seed grid): the
+  // coherence test decides on the device; Morton bins (sorted == 1) or the
+  // stable class compaction of the surface points (sorted == 0) are both
+  // enqueued, one runs
+  HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_FRAME], 0));
+  hipLaunchKernelGGL(k_coherence, dim3(1), dim3(kBlock), 0, sb, xyz_new, np_new, st, force);
+  {
+    const int gq = blocks_for(np_new, 4096);
+    hipLaunchKernelGGL(k_zero, dim3(blocks_for(nbin2, 4096)), dim3(kBlock), 0, sb, (int *)c->cnt.p, nbin2,
+                       (const DevStats *)st, 1);
+    hipLaunchKernelGGL(k_bin_count, dim3(gq), dim3(kBlock), 0, sb, xyz_new, pclass, np_new, (const Frame *)fr, gb,
+                       nbins, (int *)c->cnt.p, (int2 *)c->binrank.p, (const DevStats *)st);
+    launch_scan((const int *)c->cnt.p, nbin2, (int *)c->off.p, (int *)c->scan_a.p, st, 1, sb);
+    hipLaunchKernelGGL(k_bin_scatter, dim3(gq), dim3(kBlock), 0, sb, np_new, (const int2 *)c->binrank.p,
+                       (const int *)c->off.p, nbins, order_v, order_b, (const DevStats *)st);
+    hipLaunchKernelGGL(k_bin_total, dim3(1), dim3(1), 0, sb, (const int *)c->off.p, nbins, st);
+    if (bg.nt > 0) {
+      int *bc = (int *)c->cls_cnt.p;
+      hipLaunchKernelGGL(k_cls_count, dim3((unsigned)ncls), dim3(kBlock), 0, sb, pclass, (long long)np_new,
+                         (int)PMMG_PT_BDY, bc, (const DevStats *)st);
+      hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, sb, bc, (int)ncls, &st->nbdy,
+                         (const int *)&st->sorted, 0);
+      hipLaunchKernelGGL(k_cls_scatter, dim3((unsigned)ncls), dim3(kBlock), 0, sb, pclass, (long long)np_new,
+                         (int)PMMG_PT_BDY, (const int *)bc, order_b, (const DevStats *)st);
+    }
+  }
+  HIPCK(c, hipGetLastError());
+  HIPCK(c, hipEventRecord(c->ev[EV_ORDER], sb));
+
+  // ---- seed grid (main stream): fixed-point vertex copy, volume seeds
+  hipLaunchKernelGGL(k_quantize, dim3(blocks_for(3LL * bg.np, 8192)), dim3(kBlock), 0, s, bg.xyz, (long long)bg.np,
+                     (const Frame *)fr, (int *)c->xq.p);
   {
     const long long nsamp = ng < bg.ne ? ng : bg.ne;
     hipLaunchKernelGGL(k_seed_vol, dim3((blocks_for(nsamp, 8192) + 7) & ~7), dim3(kBlock), 0, s, bg, fr, grid, g,
@@ -713,33 +749,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[EV_PREP], s));
 
-  // ---- query order: Morton bins (sorted == 1) or the stable class
-  // compaction of the surface points (sorted == 0), both enqueued, one runs
-  {
-    hipLaunchKernelGGL(k_zero, dim3(blocks_for(nbin2, 4096)), dim3(kBlock), 0, s, (int *)c->cnt.p, nbin2,
-                       (const DevStats *)st, 1);
-    hipLaunchKernelGGL(k_bin_count, dim3(blocks_for(np_new, 1 << 30)), dim3(kBlock), 0, s, xyz_new, pclass, np_new,
-                       (const Frame *)fr, gb, nbins, (int *)c->cnt.p, (int2 *)c->binrank.p, (const DevStats *)st);
-    launch_scan((const int *)c->cnt.p, nbin2, (int *)c->off.p, (int *)c->scan_a.p, st, 1, s);
-    hipLaunchKernelGGL(k_bin_scatter, dim3(blocks_for(np_new, 1 << 30)), dim3(kBlock), 0, s, np_new,
-                       (const int2 *)c->binrank.p, (const int *)c->off.p, nbins, order_v, order_b,
-                       (const DevStats *)st);
-    hipLaunchKernelGGL(k_bin_total, dim3(1), dim3(1), 0, s, (const int *)c->off.p, nbins, st);
-    if (bg.nt > 0) {
-      int *bc = (int *)c->cls_cnt.p;
-      hipLaunchKernelGGL(k_cls_count, dim3((unsigned)ncls), dim3(kBlock), 0, s, pclass, (long long)np_new,
-                         (int)PMMG_PT_BDY, bc, (const DevStats *)st);
-      hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, s, bc, (int)ncls, &st->nbdy, (const int *)&st->sorted,
-                         0);
-      hipLaunchKernelGGL(k_cls_scatter, dim3((unsigned)ncls), dim3(kBlock), 0, s, pclass, (long long)np_new,
-                         (int)PMMG_PT_BDY, (const int *)bc, order_b, (const DevStats *)st);
-    }
-  }
-  HIPCK(c, hipGetLastError());
-  HIPCK(c, hipEventRecord(c->ev[EV_ORDER], s));
-
-  // ---- surface branch (second stream): seeds, k_bdy
-  HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_ORDER], 0));
+  // ---- surface branch (second stream, after the order): seeds, k_bdy
   HIPCK(c, hipEventRecord(c->ev[EV_BDY0], sb));
   if (bg.nt > 0) {
     hipLaunchKernelGGL(k_seed_srf, dim3(blocks_for(bg.nt, 4096)), dim3(kBlock), 0, sb, bg, (const Frame *)fr, sgrid,
@@ -751,14 +761,14 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   }
   HIPCK(c, hipEventRecord(c->ev[EV_BDY1], sb));
 
-  // ---- volume (main stream): filter walk, exact test + interpolation,
-  // exact continuation of the few queries the filter did not settle
-  hipLaunchKernelGGL(k_vol_walk, dim3((np_new + 63) / 64), dim3(64), 0, s, bg, (const Frame *)fr,
+  HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_ORDER], 0));
+  HIPCK(c, hipEventRecord(c->ev[EV_VOL0], s));
+  // ---- volume (main stream): walk + exact test + interpolation in one
+  // kernel, then the exact continuation of the few queries it did not settle
+  hipLaunchKernelGGL(pick_layout(S), dim3((np_new + 63) / 64), dim3(64), 0, s, bg, (const Frame *)fr,
                      (const unsigned long long *)grid, g, xyz_new, pclass, (const int *)order_v, np_new,
-                     (int *)c->vloc.p, (ContEntry *)c->cont.p, st, c->filter_steps);
+                     (ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->filter_steps);
   HIPCK(c, hipEventRecord(c->ev[EV_WALK], s));
-  hipLaunchKernelGGL(pick_layout(S), dim3((np_new + kBlock - 1) / kBlock), dim3(kBlock), 0, s, bg, xyz_new, pclass,
-                     np_new, (const int *)c->vloc.p, (ContEntry *)c->cont.p, st, S, elem_out, hit_out);
   hipLaunchKernelGGL(k_vol_walk_exact, dim3(8 * 64), dim3(64), 0, s, bg, xyz_new, (int *)c->fb_vol.p,
                      (const ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->maxstep);
   HIPCK(c, hipGetLastError());
@@ -808,11 +818,11 @@ static int collect_stats(pmmg_hip_ctx *c, pmmg_hip_stats *out) {
   float ms = 0.f;
   HIPCK(c, hipEventElapsedTime(&ms, c->ev[EV_START], c->ev[EV_PREP]));
   out->ms_prepare = ms;
-  HIPCK(c, hipEventElapsedTime(&ms, c->ev[EV_PREP], c->ev[EV_ORDER]));
-  out->ms_sort = ms;
-  HIPCK(c, hipEventElapsedTime(&ms, c->ev[EV_ORDER], c->ev[EV_VOL]));
+  HIPCK(c, hipEventElapsedTime(&ms, c->ev[EV_FRAME], c->ev[EV_ORDER]));
+  out->ms_sort = ms; // on the second stream, concurrent with the seed grid
+  HIPCK(c, hipEventElapsedTime(&ms, c->ev[EV_VOL0], c->ev[EV_VOL]));
   out->ms_vol = ms;
-  HIPCK(c, hipEventElapsedTime(&ms, c->ev[EV_ORDER], c->ev[EV_WALK]));
+  HIPCK(c, hipEventElapsedTime(&ms, c->ev[EV_VOL0], c->ev[EV_WALK]));
   out->ms_vol_locate = ms;
   HIPCK(c, hipEventElapsedTime(&ms, c->ev[EV_BDY0], c->ev[EV_BDY1]));
   out->ms_bdy = ms; // on the surface stream, concurrent with the volume kernels

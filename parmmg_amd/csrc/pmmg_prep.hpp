@@ -101,7 +101,28 @@ struct Frame {
   unsigned long long key_lo[3], key_hi[3];
   double lo[3], ext[3];
   double inv_vol[3], inv_srf[3], inv_bin[3];
+  double qc[3], qs; // fixed-point frame of the walk's vertex copy
 };
+
+// Fixed-point coordinates for the filter walk and the seed grid: int32
+// (x - qc) * qs with |x - qc| <= 0.625 * (largest bbox side) mapped into
+// +-2^29, so the difference of two vertices in range is exact in int32 and
+// its rounding to fp32 costs the same relative precision as the fp64
+// difference rounded to fp32.  12 bytes per vertex (one dwordx3 load)
+// instead of 24.  A vertex outside the range (the bbox is sampled) clamps;
+// that can only misdirect the filter walk, never an accepted result (the
+// exact test uses the fp64 coordinates).
+constexpr double kQuantHalf = 536870912.0; // 2^29
+__device__ __forceinline__ int quant(double x, const Frame *fr, int d) {
+  double t = (x - fr->qc[d]) * fr->qs;
+  t = t > 2.0 * kQuantHalf ? 2.0 * kQuantHalf : (t < -2.0 * kQuantHalf ? -2.0 * kQuantHalf : t);
+  return __double2int_rn(t);
+}
+
+__global__ __launch_bounds__(kBlock) void k_quantize(const double *xyz, long long np, const Frame *fr, int *xq) {
+  for (long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x; j < 3 * np; j += (long long)gridDim.x * blockDim.x)
+    xq[j] = quant(__builtin_nontemporal_load(xyz + j), fr, (int)(j % 3));
+}
 
 // one launch initialises the per-call state: frame accumulators, counters,
 // seed grids
@@ -168,6 +189,7 @@ __global__ __launch_bounds__(kBlock) void k_bbox(const double *xyz, int np, Fram
 }
 
 __global__ void k_frame_final(Frame *fr, int g, int gs, int gb) {
+  double emax = 0.0;
   for (int d = 0; d < 3; d++) {
     double lo = dunkey(fr->key_lo[d]), hi = dunkey(fr->key_hi[d]);
     double ext = hi - lo;
@@ -176,7 +198,10 @@ __global__ void k_frame_final(Frame *fr, int g, int gs, int gb) {
     fr->inv_vol[d] = ext > 0.0 ? (double)g / ext : 0.0;
     fr->inv_srf[d] = ext > 0.0 ? (double)gs / ext : 0.0;
     fr->inv_bin[d] = ext > 0.0 ? (double)gb / ext : 0.0;
+    fr->qc[d] = lo + 0.5 * ext;
+    emax = ext > emax ? ext : emax;
   }
+  fr->qs = emax > 0.0 ? kQuantHalf / (0.625 * emax) : 1.0;
 }
 
 // ---------------------------------------------------------------- volume seed grid
@@ -221,12 +246,12 @@ __global__ __launch_bounds__(kBlock) void k_seed_vol(Bg bg, const Frame *fr, uns
     unsigned long long key = ~0ULL;
     long long ci = -1;
     if (ok) {
-      double p[3], a[3], b[3], e[3];
-      load_pt(bg.xyz, tv.x, p);
-      load_pt(bg.xyz, tv.y, a);
-      load_pt(bg.xyz, tv.z, b);
-      load_pt(bg.xyz, tv.w, e);
-      for (int d = 0; d < 3; d++) p[d] = 0.25 * (p[d] + a[d] + b[d] + e[d]);
+      // centroid from the fixed-point copy (12-byte rows)
+      const int *q0 = bg.xq + 3 * (size_t)(tv.x - 1), *q1 = bg.xq + 3 * (size_t)(tv.y - 1);
+      const int *q2 = bg.xq + 3 * (size_t)(tv.z - 1), *q3 = bg.xq + 3 * (size_t)(tv.w - 1);
+      double p[3];
+      for (int d = 0; d < 3; d++)
+        p[d] = fr->qc[d] + 0.25 * ((double)q0[d] + (double)q1[d] + (double)q2[d] + (double)q3[d]) / fr->qs;
       int c[3];
       unsigned long long off = 0;
       float d2 = 0.f;
@@ -523,29 +548,29 @@ __global__ __launch_bounds__(kBlock) void k_coherence(const double *xyz, int np,
 __global__ __launch_bounds__(kBlock) void k_bin_count(const double *xyz, const uint8_t *pclass, int np, const Frame *fr,
                                                       int gb, int nbins, int *cnt, int2 *binrank, const DevStats *st) {
   if (!st->sorted) return;
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= np) return;
-  int c = pclass[i];
-  if (c != PMMG_PT_VOL && c != PMMG_PT_BDY) {
-    binrank[i] = make_int2(-1, 0);
-    return;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < np; i += gridDim.x * blockDim.x) {
+    int c = pclass[i];
+    if (c != PMMG_PT_VOL && c != PMMG_PT_BDY) {
+      binrank[i] = make_int2(-1, 0);
+      continue;
+    }
+    uint32_t q[3];
+    for (int d = 0; d < 3; d++) q[d] = (uint32_t)cell_coord(xyz[3 * (size_t)i + d], fr->lo[d], fr->inv_bin[d], gb);
+    int bin = (int)((expand10(q[0]) << 2) | (expand10(q[1]) << 1) | expand10(q[2])) + (c == PMMG_PT_BDY ? nbins : 0);
+    int r = atomicAdd(&cnt[bin], 1);
+    binrank[i] = make_int2(bin, r);
   }
-  uint32_t q[3];
-  for (int d = 0; d < 3; d++) q[d] = (uint32_t)cell_coord(xyz[3 * (size_t)i + d], fr->lo[d], fr->inv_bin[d], gb);
-  int bin = (int)((expand10(q[0]) << 2) | (expand10(q[1]) << 1) | expand10(q[2])) + (c == PMMG_PT_BDY ? nbins : 0);
-  int r = atomicAdd(&cnt[bin], 1);
-  binrank[i] = make_int2(bin, r);
 }
 
 __global__ __launch_bounds__(kBlock) void k_bin_scatter(int np, const int2 *binrank, const int *off, int nbins,
                                                         int *order_v, int *order_b, const DevStats *st) {
   if (!st->sorted) return;
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= np) return;
-  int2 br = binrank[i];
-  if (br.x < 0) return;
-  if (br.x < nbins) order_v[off[br.x] + br.y] = i + 1;
-  else order_b[off[br.x] - off[nbins] + br.y] = i + 1;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < np; i += gridDim.x * blockDim.x) {
+    int2 br = binrank[i];
+    if (br.x < 0) continue;
+    if (br.x < nbins) order_v[off[br.x] + br.y] = i + 1;
+    else order_b[off[br.x] - off[nbins] + br.y] = i + 1;
+  }
 }
 
 __global__ void k_bin_total(const int *off, int nbins, DevStats *st) {

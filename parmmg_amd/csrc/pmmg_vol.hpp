@@ -2,10 +2,10 @@
 // pmmg_hip.hip only): PMMG_locatePointVol (locate_pmmg.c:786-883) and the
 // interpolation PMMG_interp4bar_{iso,ani} (interpmesh_pmmg.c:206-270).
 //
-//   k_vol_walk        fp32 filter walk from a grid seed to a candidate tetra
-//   k_vol_interp_*    in input order: the reference's exact fp64 acceptance
-//                     test at the candidate, its exact coordinates, and the
-//                     interpolation of the metric and fields
+//   k_vol             per query: fp32 filter walk from a grid seed to a
+//                     candidate tetra, the reference's exact fp64 acceptance
+//                     test there (and its exact coordinates), interpolation
+//                     of the metric and fields
 //   k_vol_walk_exact  the few queries the filter could not settle, walked and
 //                     interpolated in the reference's fp64 arithmetic (then
 //                     the exhaustive kernels, pmmg_fallback.hpp)
@@ -15,13 +15,8 @@
 
 namespace pmmg {
 
-// ---------------------------------------------------------------- per-query hand-offs
-//
-// vloc[ip-1]: the walk's candidate tetra (0: none, the query is on the
-// continuation list).  The interpolation kernel re-evaluates the candidate in
-// the reference's arithmetic, which also yields the exact coordinates the
-// interpolation needs, so nothing but the tetra id passes between the two
-// kernels.
+// a located query: the tetra's vertex ids and the reference's (exact,
+// unsorted) barycentric coordinates
 struct VolLoc {
   int4 v;
   double phi[4];
@@ -141,9 +136,9 @@ __device__ __forceinline__ int4 next_slots(const int4 &m, const int4 &tv, const 
 // A step stops the walk when min_f bary[f] > -(EPS + kFilterMargin) in fp32:
 // every tetra the reference's test could accept passes (the fp32 error of a
 // coordinate, ~1e-6 at most for the meshes at hand, is far below the
-// margin).  The exact test then runs once per query, in the interpolation
-// kernel; a query it rejects (within the margin of a face, ~1e-3 of the
-// queries) continues in exact arithmetic (k_vol_walk_exact).  Every located
+// margin).  The exact test then runs once per query, at the candidate; a
+// query it rejects (within the margin of a face, ~1e-3 of the queries)
+// continues in exact arithmetic (k_vol_walk_exact).  Every located
 // tetra is therefore accepted by the reference's own test, with its exact
 // coordinates.
 //
@@ -165,11 +160,13 @@ struct LaneSlotsF { // this lane's view of the wave's slot image [slot*3 + dim][
   }
 };
 
-__device__ __forceinline__ void rel_pt(const double *xyz, int v, const double *x, float *q) {
-  const double *p = xyz + 3 * (size_t)(v - 1);
-  q[0] = (float)(p[0] - x[0]);
-  q[1] = (float)(p[1] - x[1]);
-  q[2] = (float)(p[2] - x[2]);
+// vertex v relative to the query, from the fixed-point copy (exact integer
+// difference, one rounding to fp32)
+__device__ __forceinline__ void rel_pt(const int *xq, int v, const int *xqq, float *q) {
+  const int *p = xq + 3 * (size_t)(v - 1);
+  q[0] = (float)(p[0] - xqq[0]);
+  q[1] = (float)(p[1] - xqq[1]);
+  q[2] = (float)(p[2] - xqq[2]);
 }
 
 __device__ __forceinline__ void cross3(const float *a, const float *b, float *c) {
@@ -181,7 +178,7 @@ __device__ __forceinline__ float dot3(const float *a, const float *b) { return a
 
 // returns 1 candidate (filter passed), 0 moved (k, tv, ad, m, hist updated),
 // 2 stuck (no eligible neighbour)
-__device__ __forceinline__ int step_f32(const Bg &bg, const double *x, int &k, int4 &tv, int4 &ad, int4 &m, int *hist,
+__device__ __forceinline__ int step_f32(const Bg &bg, const int *x, int &k, int4 &tv, int4 &ad, int4 &m, int *hist,
                                         const LaneSlotsF &L) {
   float q[4][3];
   L.get(m.x, q[0]);
@@ -213,85 +210,12 @@ __device__ __forceinline__ int step_f32(const Bg &bg, const double *x, int &k, i
   const int4 tn = tetv_row(bg, k);
   ad = adja_row(bg, k);
   float qn[3];
-  rel_pt(bg.xyz, sel4(tn, iopp), x, qn);
+  rel_pt(bg.xq, sel4(tn, iopp), x, qn);
   const int sf = sel4(m, f);
   m = next_slots(m, tv, tn, f, iopp);
   L.put(sf, qn);
   tv = tn;
   return 0;
-}
-
-// Walk kernel: one query per lane, the 64 lanes of a one-wave block on 64
-// consecutive queries of the processing order, so neighbouring walks run in
-// lockstep through the same tetra and share cache lines inside each
-// wave-instruction.  Input order (st->sorted == 0): i = ip - 1 and the lane
-// takes the point only if it is a volume point; Morton order: order[i].
-// vloc[ip-1] = the candidate tetra; stuck / over-long walks go to the
-// continuation list with the tetra they stopped at.
-__global__ __launch_bounds__(64) void k_vol_walk(Bg bg, const Frame *fr, const unsigned long long *grid, int g,
-                                                 const double *qxyz, const uint8_t *pclass, const int *order, int np,
-                                                 int *vloc, ContEntry *cont, DevStats *st, int maxstep) {
-  __shared__ BlockStats bs;
-  __shared__ float slot_img[12 * 64];
-  const LaneSlotsF L{&slot_img[__lane_id()]};
-  bstats_init(&bs);
-  __syncthreads();
-  const int i = xcd_block() * 64 + threadIdx.x;
-  bool active;
-  int ip = 0;
-  if (st->sorted) {
-    active = i < st->nvol;
-    if (active) ip = order[i];
-  } else {
-    active = i < np && pclass[i] == PMMG_PT_VOL;
-    ip = i + 1;
-  }
-  int status = 0, steps = 0, k = 0;
-  if (active) {
-    double x[3];
-    load_pt_nt(qxyz, ip, x); // streamed once: non-temporal
-    k = seed_vol(grid, g, fr, x);
-    if (k == 0) {
-      status = 2;
-    } else {
-      int4 tv = tetv_row(bg, k), ad = adja_row(bg, k), m = make_int4(0, 1, 2, 3);
-      {
-        float q[3];
-        rel_pt(bg.xyz, tv.x, x, q);
-        L.put(0, q);
-        rel_pt(bg.xyz, tv.y, x, q);
-        L.put(1, q);
-        rel_pt(bg.xyz, tv.z, x, q);
-        L.put(2, q);
-        rel_pt(bg.xyz, tv.w, x, q);
-        L.put(3, q);
-      }
-      int hist[kHist];
-#pragma unroll
-      for (int h = 0; h < kHist; h++) hist[h] = 0;
-      for (;;) {
-        if (steps >= maxstep) {
-          status = 3;
-          break;
-        }
-        ++steps;
-        const int r = step_f32(bg, x, k, tv, ad, m, hist, L);
-        if (r != 0) {
-          status = r;
-          break;
-        }
-      }
-    }
-    __builtin_nontemporal_store(status == 1 ? k : 0, vloc + ip - 1);
-  }
-  const bool more = active && status != 1;
-  const int slot = wave_append(&st->ncont, more);
-  if (more) cont[slot] = ContEntry{ip, k};
-  wave_stats(&bs, active, 0, steps);
-  wave_count(&bs, kCntVolQueries, active);
-  wave_count(&bs, kCntExact, more);
-  __syncthreads();
-  bstats_flush(&bs, st);
 }
 
 // ---------------------------------------------------------------- exact continuation
@@ -437,168 +361,217 @@ __device__ __forceinline__ void wave_store_rows(double *out, const double *row, 
   }
 }
 
-// Cooperative row gathers.  The 64 lanes of a wave gather the 256 rows (64
-// queries x 4 vertices) of one 3- or 6-double slot together: piece p = 64 t +
-// lane of the slot's row image (16-byte pieces for 6-double rows, 8-byte
-// pieces for 3-double rows, 3 pieces per row) is loaded by one lane, so a
-// row's pieces share an instruction and every instruction covers ~21 whole
-// rows.  A 6-double slot's rows are gathered in two passes of 128 rows
-// (vertices 0-1, then 2-3 of the wave's queries) through a 768-double image
-// per wave; each lane reads its rows back and evaluates the reference
-// interpolator (same arithmetic, same order).  Scalar slots keep per-lane
-// gathers.
-template <int PASS>
-__device__ __forceinline__ void coop_gather6_pair(const double *in, const int *vid, double *img, double (*m)[6]) {
+// ---------------------------------------------------------------- fused volume kernel
+//
+// One query per lane, the 64 lanes of a one-wave block on 64 consecutive
+// queries of the processing order, in three phases per wave:
+//   1. the fp32 filter walk from the grid seed to a candidate tetra
+//      (neighbouring walks run in lockstep through the same tetra and share
+//      cache lines inside each wave-instruction);
+//   2. the reference's exact test at the candidate (its 4 vertex rows are
+//      still in L1/L2 from the walk's last step), which gives the exact
+//      coordinates; rejected candidates, stuck and over-long walks go to the
+//      continuation list (k_vol_walk_exact);
+//   3. the interpolation of every slot (layout = template: codes 1 / 3 / 6,
+//      0 = none; C0 < 0 = runtime layout, per-lane).  A 3- or 6-double slot
+//      is gathered one vertex at a time: in pass i the 64 lanes load the 64
+//      rows of vertex i of the wave's queries cooperatively (3 pieces of a
+//      row in one wave-instruction, lane l of instruction t loading piece
+//      64t+l of the rows' image) into LDS, each lane reads back its own row
+//      and accumulates it in the reference's order (PMMG_interp4bar_ani:
+//      mint = sum_i phi_i invmat(M_i), then invmat(mint)), so only one row is
+//      live per lane.  In input order the rows are stored as whole cache lines
+//      through the same LDS image; Morton-binned queries store per lane.
+// The walk's vertex slots and the gather image share one 3 KiB LDS buffer
+// (the phases are sequential within the wave).
+struct VolShared {
+  BlockStats bs;
+  union {
+    float slots[12 * 64]; // walk: [slot*3 + dim][lane]
+    double img[6 * 64];   // interpolation: 64 rows of up to 6 doubles
+  } u;
+};
+
+// rows of one vertex of the wave's 64 queries (myv = this lane's vertex id)
+// into img (row r = query r), C doubles per row; returns this lane's row
+template <int C>
+__device__ __forceinline__ void coop_vertex_rows(const double *in, int myv, double *img, double *row) {
   const int lane = __lane_id();
-  double2 b[6];
+  if constexpr (C == 6) {
+    double2 b[3];
 #pragma unroll
-  for (int t = 0; t < 6; t++) {
-    const int p = 64 * t + lane, r = p / 3, k = p - 3 * r; // r in [0, 128): query r/2, vertex 2*PASS + r%2
-    const int v = vid[4 * (r >> 1) + 2 * PASS + (r & 1)];
-    b[t] = *reinterpret_cast<const double2 *>(in + (size_t)6 * (v - 1) + 2 * k);
+    for (int t = 0; t < 3; t++) {
+      const int p = 64 * t + lane, r = p / 3, k = p - 3 * r;
+      const int v = __shfl(myv, r);
+      b[t] = *reinterpret_cast<const double2 *>(in + (size_t)6 * (v - 1) + 2 * k);
+    }
+#pragma unroll
+    for (int t = 0; t < 3; t++) reinterpret_cast<double2 *>(img)[64 * t + lane] = b[t];
+  } else {
+    double b[3];
+#pragma unroll
+    for (int t = 0; t < 3; t++) {
+      const int p = 64 * t + lane, r = p / 3, k = p - 3 * r;
+      const int v = __shfl(myv, r);
+      b[t] = in[(size_t)3 * (v - 1) + k];
+    }
+#pragma unroll
+    for (int t = 0; t < 3; t++) img[64 * t + lane] = b[t];
   }
-#pragma unroll
-  for (int t = 0; t < 6; t++) reinterpret_cast<double2 *>(img)[64 * t + lane] = b[t];
   wait_lgkm();
   __builtin_amdgcn_wave_barrier();
-  load6(img + 12 * lane, m[2 * PASS]);
-  load6(img + 12 * lane + 6, m[2 * PASS + 1]);
+#pragma unroll
+  for (int j = 0; j < C; j++) row[j] = img[C * lane + j];
   wait_lgkm();
-  __builtin_amdgcn_wave_barrier(); // every lane has read its rows: the image is free again
+  __builtin_amdgcn_wave_barrier(); // every lane has read its row: the image is free again
 }
 
+// one slot of the wave's queries: rows gathered, interpolated, stored
 template <int C>
-__device__ __forceinline__ void coop_slot(const Slot &sl, bool act, const int *v, const double *phi, const int *vid,
-                                          double *img, size_t i0) {
-  if constexpr (C == 6) {
-    double m[4][6];
-    coop_gather6_pair<0>(sl.in, vid, img, m);
-    coop_gather6_pair<1>(sl.in, vid, img, m);
-    double mint[6], mi[6], r[6];
-    bool ok = true;
+__device__ __forceinline__ void vol_slot(const Slot &sl, bool act, const int4 &v, const double *phi, double *img,
+                                         bool coalesced, size_t w0, int ip) {
+  if constexpr (C > 0) {
+    double r[C];
+    bool ok = act;
+    if constexpr (C == 6) {
+      double mint[6], m[6], mi[6];
 #pragma unroll
-    for (int i = 0; i < 4; i++) { // PMMG_interp4bar_ani: M = invmat(sum_i phi_i invmat(M_i))
-      ok = invmat(m[i], mi) && ok;
+      for (int i = 0; i < 4; i++) {
+        coop_vertex_rows<6>(sl.in, sel4(v, i), img, m);
+        ok = invmat(m, mi) && ok;
 #pragma unroll
-      for (int q = 0; q < 6; q++) mint[q] = (i == 0) ? phi[0] * mi[q] : mint[q] + phi[i] * mi[q];
+        for (int q = 0; q < 6; q++) mint[q] = (i == 0) ? phi[0] * mi[q] : mint[q] + phi[i] * mi[q];
+      }
+      ok = invmat(mint, r) && ok;
+    } else if constexpr (C == 3) {
+      double m[3];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        coop_vertex_rows<3>(sl.in, sel4(v, i), img, m);
+#pragma unroll
+        for (int q = 0; q < 3; q++) r[q] = (i == 0) ? 0.0 + phi[0] * m[q] : r[q] + phi[i] * m[q];
+      }
+    } else {
+      const int vv[4] = {v.x, v.y, v.z, v.w};
+      interp_iso_row<4, 1>(sl.in, vv, phi, r);
     }
-    ok = invmat(mint, r) && ok && act;
-    wave_store_rows<6>(sl.out + (size_t)6 * i0, r, __ballot(ok), img);
-  } else if constexpr (C == 3) {
-    const int lane = __lane_id();
-    double b[12];
+    if (coalesced) {
+      wave_store_rows<C>(sl.out + (size_t)C * w0, r, __ballot(ok), img);
+    } else if (ok) {
+      double *o = sl.out + (size_t)C * (ip - 1);
+      if constexpr (C == 6) store6(o, r);
+      else
 #pragma unroll
-    for (int t = 0; t < 12; t++) {
-      const int p = 64 * t + lane, r = p / 3, k = p - 3 * r;
-      b[t] = sl.in[(size_t)3 * (vid[r] - 1) + k];
+        for (int q = 0; q < C; q++) nt_store(o + q, r[q]);
     }
-#pragma unroll
-    for (int t = 0; t < 12; t++) img[64 * t + lane] = b[t];
-    wait_lgkm();
-    __builtin_amdgcn_wave_barrier();
-    const double *base = img + 12 * lane;
-    double row[4][3], r[3];
-#pragma unroll
-    for (int i = 0; i < 4; i++)
-#pragma unroll
-      for (int j = 0; j < 3; j++) row[i][j] = base[3 * i + j];
-    wait_lgkm();
-    __builtin_amdgcn_wave_barrier(); // the image becomes the store image
-#pragma unroll
-    for (int j = 0; j < 3; j++) r[j] = 0.0; // PMMG_interp4bar_iso: sum from 0.0 in vertex order
-#pragma unroll
-    for (int i = 0; i < 4; i++)
-#pragma unroll
-      for (int j = 0; j < 3; j++) r[j] += phi[i] * row[i][j];
-    wave_store_rows<3>(sl.out + (size_t)3 * i0, r, __ballot(act), img);
-  } else if constexpr (C == 1) {
-    double r[1];
-    interp_iso_row<4, 1>(sl.in, v, phi, r);
-    wave_store_rows<1>(sl.out + i0, r, __ballot(act), img);
   }
 }
 
-// The query's candidate tetra in the reference's arithmetic (exact_accept):
-// on acceptance loc = its vertex ids and exact coordinates; a rejected
-// candidate (the query lies within the filter's margin outside it) goes to
-// the continuation list.  Returns whether the lane interpolates.
-__device__ __forceinline__ bool accept_candidate(const Bg &bg, const double *qxyz, int i, int k, bool act,
-                                                 VolLoc &loc, ContEntry *cont, DevStats *st) {
+template <int C0, int C1, int C2, int C3, int C4, int C5>
+__global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsigned long long *grid, int g,
+                                            const double *qxyz, const uint8_t *pclass, const int *order, int np,
+                                            ContEntry *cont, DevStats *st, Slots S, int *elem_out, int8_t *hit_out,
+                                            int filter_steps) {
+  __shared__ VolShared sh;
+  bstats_init(&sh.bs);
+  __syncthreads();
+  const LaneSlotsF L{&sh.u.slots[__lane_id()]};
+  const int i = xcd_block() * 64 + threadIdx.x;
+  const bool sorted = st->sorted != 0;
+  bool active;
+  int ip = 0;
+  if (sorted) {
+    active = i < st->nvol;
+    if (active) ip = order[i];
+  } else {
+    active = i < np && __builtin_nontemporal_load(pclass + i) == PMMG_PT_VOL;
+    ip = i + 1;
+  }
+  // 1. filter walk
+  int status = 0, steps = 0, k = 0;
+  double x[3];
+  int4 tv = make_int4(1, 1, 1, 1);
+  if (active) {
+    load_pt_nt(qxyz, ip, x); // streamed once: non-temporal
+    k = seed_vol(grid, g, fr, x);
+    if (k == 0) {
+      status = 2;
+    } else {
+      const int xq[3] = {quant(x[0], fr, 0), quant(x[1], fr, 1), quant(x[2], fr, 2)};
+      tv = tetv_row(bg, k);
+      int4 ad = adja_row(bg, k), m = make_int4(0, 1, 2, 3);
+      {
+        float q[3];
+        rel_pt(bg.xq, tv.x, xq, q);
+        L.put(0, q);
+        rel_pt(bg.xq, tv.y, xq, q);
+        L.put(1, q);
+        rel_pt(bg.xq, tv.z, xq, q);
+        L.put(2, q);
+        rel_pt(bg.xq, tv.w, xq, q);
+        L.put(3, q);
+      }
+      int hist[kHist];
+#pragma unroll
+      for (int h = 0; h < kHist; h++) hist[h] = 0;
+      for (;;) {
+        if (steps >= filter_steps) {
+          status = 3;
+          break;
+        }
+        ++steps;
+        const int r = step_f32(bg, xq, k, tv, ad, m, hist, L);
+        if (r != 0) {
+          status = r;
+          break;
+        }
+      }
+    }
+  }
+  // 2. the reference's exact test at the candidate
+  VolLoc loc;
   bool acc = false;
-  if (act) {
-    double x[3], p[4][3];
-    load_pt_nt(qxyz, i + 1, x);
-    const int4 tv = tetv_row(bg, k);
+  if (status == 1) {
+    double p[4][3];
     load_tet_pts(bg, tv, p);
     acc = exact_accept(x, p, tv, &loc, nullptr);
   }
-  const bool more = act && !acc;
+  const bool more = active && !acc;
   const int slot = wave_append(&st->ncont, more);
-  if (more) cont[slot] = ContEntry{i + 1, k};
-  const unsigned long long hits = __ballot(acc), exact = __ballot(more);
-  if (__lane_id() == 0) {
-    StatPart *pt = stat_part(st);
-    if (hits) atomicAdd(&pt->cnt[PMMG_HIT_VOL_WALK], (unsigned long long)__popcll(hits));
-    if (exact) atomicAdd(&pt->cnt[kCntExact], (unsigned long long)__popcll(exact));
-  }
-  if (!acc) { // idle lanes gather a valid row, never stored
-    loc.v = make_int4(1, 1, 1, 1);
+  if (more) cont[slot] = ContEntry{ip, k};
+  wave_stats(&sh.bs, active, acc ? PMMG_HIT_VOL_WALK : 0, steps);
+  wave_count(&sh.bs, kCntVolQueries, active);
+  wave_count(&sh.bs, kCntExact, more);
+  // 3. interpolation
+  if (__any(acc)) {
+    if (!acc) { // idle lanes gather a valid row, never stored
+      loc.v = make_int4(1, 1, 1, 1);
 #pragma unroll
-    for (int f = 0; f < 4; f++) loc.phi[f] = 0.0;
+      for (int f = 0; f < 4; f++) loc.phi[f] = 0.0;
+    }
+    double *img = sh.u.img;
+    __builtin_amdgcn_wave_barrier(); // the walk's slots are dead: the buffer becomes the gather image
+    const size_t w0 = (size_t)(i - __lane_id());
+    if constexpr (C0 < 0) {
+      if (acc) {
+        const int vv[4] = {loc.v.x, loc.v.y, loc.v.z, loc.v.w};
+        for (int s2 = 0; s2 < S.n; s2++) interp_dyn<4>(S.s[s2], ip, vv, loc.phi);
+      }
+    } else {
+      vol_slot<C0>(S.s[0], acc, loc.v, loc.phi, img, !sorted, w0, ip);
+      vol_slot<C1>(S.s[1], acc, loc.v, loc.phi, img, !sorted, w0, ip);
+      vol_slot<C2>(S.s[2], acc, loc.v, loc.phi, img, !sorted, w0, ip);
+      vol_slot<C3>(S.s[3], acc, loc.v, loc.phi, img, !sorted, w0, ip);
+      vol_slot<C4>(S.s[4], acc, loc.v, loc.phi, img, !sorted, w0, ip);
+      vol_slot<C5>(S.s[5], acc, loc.v, loc.phi, img, !sorted, w0, ip);
+    }
+    if (acc) {
+      if (elem_out) __builtin_nontemporal_store(k, elem_out + ip - 1);
+      if (hit_out) __builtin_nontemporal_store((int8_t)PMMG_HIT_VOL_WALK, hit_out + ip - 1);
+    }
   }
-  return acc;
-}
-
-// interpolation of the located volume queries in input order (coalesced
-// output rows); the slot layout is a template (codes 1 / 3 / 6, 0 = none)
-template <int C0, int C1, int C2, int C3, int C4, int C5>
-__global__ __launch_bounds__(kBlock) void k_vol_interp(Bg bg, const double *qxyz, const uint8_t *pclass, int np,
-                                                       const int *vloc, ContEntry *cont, DevStats *st, Slots S,
-                                                       int *elem_out, int8_t *hit_out) {
-  __shared__ double img_all[kBlock / 64][256 * 3];
-  __shared__ int vid_all[kBlock / 64][256];
-  double *img = img_all[threadIdx.x >> 6];
-  int *vid = vid_all[threadIdx.x >> 6];
-  const int i = xcd_block() * blockDim.x + threadIdx.x;
-  bool act = i < np && __builtin_nontemporal_load(pclass + i) == PMMG_PT_VOL;
-  const int k = act ? __builtin_nontemporal_load(vloc + i) : 0;
-  act = act && k != 0;
-  if (!__any(act)) return;
-  VolLoc loc;
-  act = accept_candidate(bg, qxyz, i, k, act, loc, cont, st);
-  if (!__any(act)) return;
-  const int v[4] = {loc.v.x, loc.v.y, loc.v.z, loc.v.w};
-  reinterpret_cast<int4 *>(vid)[__lane_id()] = loc.v;
-  wait_lgkm();
-  __builtin_amdgcn_wave_barrier();
-  const size_t w0 = (size_t)(i - __lane_id());
-  coop_slot<C0>(S.s[0], act, v, loc.phi, vid, img, w0);
-  coop_slot<C1>(S.s[1], act, v, loc.phi, vid, img, w0);
-  coop_slot<C2>(S.s[2], act, v, loc.phi, vid, img, w0);
-  coop_slot<C3>(S.s[3], act, v, loc.phi, vid, img, w0);
-  coop_slot<C4>(S.s[4], act, v, loc.phi, vid, img, w0);
-  coop_slot<C5>(S.s[5], act, v, loc.phi, vid, img, w0);
-  if (!act) return;
-  if (elem_out) __builtin_nontemporal_store(k, elem_out + i);
-  if (hit_out) __builtin_nontemporal_store((int8_t)PMMG_HIT_VOL_WALK, hit_out + i);
-}
-
-// any other slot layout (up to kMaxSlot slots in any order): one lane per
-// query, per-lane gathers and stores
-__global__ __launch_bounds__(kBlock) void k_vol_interp_generic(Bg bg, const double *qxyz, const uint8_t *pclass,
-                                                               int np, const int *vloc, ContEntry *cont, DevStats *st,
-                                                               Slots S, int *elem_out, int8_t *hit_out) {
-  const int i = xcd_block() * blockDim.x + threadIdx.x;
-  bool act = i < np && pclass[i] == PMMG_PT_VOL;
-  const int k = act ? vloc[i] : 0;
-  act = act && k != 0;
-  if (!__any(act)) return;
-  VolLoc loc;
-  if (!accept_candidate(bg, qxyz, i, k, act, loc, cont, st)) return;
-  const int v[4] = {loc.v.x, loc.v.y, loc.v.z, loc.v.w};
-  for (int s = 0; s < S.n; s++) interp_dyn<4>(S.s[s], i + 1, v, loc.phi);
-  if (elem_out) elem_out[i] = k;
-  if (hit_out) hit_out[i] = (int8_t)PMMG_HIT_VOL_WALK;
+  __syncthreads();
+  bstats_flush(&sh.bs, st);
 }
 
 } // namespace pmmg

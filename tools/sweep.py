@@ -1,6 +1,7 @@
 """Interleaved A/B sweep of module settings in ONE process (perf deltas from
 interleaved rounds, not from separate invocations).  Each variant is a set of
-PMMG_HIP_* environment values read by pmmg_hip_create:
+PMMG_HIP_* environment values read by pmmg_hip_create (and sort=0/1, the
+context's query-order option):
 
   python tools/sweep.py --config cfg4 --variants "TPC=8;TPC=4;TPC=16" --rounds 3
 """
@@ -36,10 +37,16 @@ def main():
         for k in list(os.environ):
             if k.startswith("PMMG_HIP_"):
                 os.environ.pop(k)
+        sort = None
         for item in filter(None, spec.split(",")):
             k, v = item.split("=")
-            os.environ["PMMG_HIP_" + k.upper()] = v
-        ctxs.append(TransferContext(0))
+            if k.lower() == "sort":  # context option: 1 Morton bins, 0 input order
+                sort = v == "1"
+            elif k.lower() == "sol":  # measurement only: none / met / all solution slots
+                pass
+            else:
+                os.environ["PMMG_HIP_" + k.upper()] = v
+        ctxs.append(TransferContext(0, sort=sort))
     for k in list(os.environ):
         if k.startswith("PMMG_HIP_"):
             os.environ.pop(k)
@@ -51,11 +58,15 @@ def main():
              el=base.empty((new.np,), np.int32), hit=base.empty((new.np,), np.int8))
     cols = ["ms_total", "ms_prepare", "ms_sort", "ms_vol_locate", "ms_vol", "ms_bdy", "ms_fallback"]
     res = {v: {c: [] for c in cols + ["steps_pp", "iters", "exact"]} for v in variants}
+    def sols(spec):
+        which = dict(item.split("=") for item in spec.split(",") if item).get("sol", "all")
+        return {"none": (None, []), "met": (d["met"], []), "all": (d["met"], d["f"])}[which]
+
     for r in range(args.rounds):
         for spec, ctx in zip(variants, ctxs):
             for s in range(args.steps + 1):
                 ctx.set_background_tet8(d["xyz"], d["tet8"], d["triv"], d["adjt"], w.hausd)
-                ctx.set_solutions(d["met"], d["f"])
+                ctx.set_solutions(*sols(spec))
                 ctx.locate_interp(d["q"], d["pc"], d["mo"], d["fo"], d["el"], d["hit"], sync=False)
                 st = ctx.sync()
                 if s == 0:
