@@ -68,6 +68,36 @@ def run_gpu(case, sort=None, ctx=None, tet8=False):
             ctx.close()
 
 
+def run_dev(ctx, bg, new_xyz, met, fields, pc, hausd, separate=False):
+    """One transfer with every array resident on the device (the bench's
+    device mode): returns (met, fields, elem, hit) downloaded + the stats."""
+    from parmmg_amd.transfer import pack_tet8
+
+    nq = new_xyz.shape[0]
+    d = dict(xyz=ctx.upload(bg.xyz), triv=ctx.upload(bg.triv), adjt=ctx.upload(bg.adjt), q=ctx.upload(new_xyz),
+             pc=ctx.upload(pc))
+    if separate:
+        d["tetv"], d["adja"] = ctx.upload(bg.tetv), ctx.upload(bg.adja)
+        ctx.set_background(d["xyz"], d["tetv"], d["adja"], d["triv"], d["adjt"], hausd)
+    else:
+        d["tet8"] = ctx.upload(pack_tet8(bg.tetv, bg.adja))
+        ctx.set_background_tet8(d["xyz"], d["tet8"], d["triv"], d["adjt"], hausd)
+    d["met"] = None if met is None else ctx.upload(met)
+    d["f"] = [ctx.upload(f) for f in fields]
+    ctx.set_solutions(d["met"], d["f"])
+    mo = None if met is None else ctx.empty((nq, met.shape[1]), np.float64)
+    fo = [ctx.empty((nq, f.shape[1]), np.float64) for f in fields]
+    el, hit = ctx.empty((nq,), np.int32), ctx.empty((nq,), np.int8)
+    ctx.locate_interp(d["q"], d["pc"], mo, fo, el, hit, sync=False)
+    st = ctx.sync()
+    out = (None if mo is None else mo.download(), [f.download() for f in fo], el.download(), hit.download(), st)
+    for a in list(d.values()) + [mo, el, hit] + fo:
+        for b in (a if isinstance(a, list) else [a]):
+            if b is not None:
+                b.free()
+    return out
+
+
 def _same(a, b):
     """bit-equal or both NaN (rows left untouched by a failed tensor inversion)"""
     return np.all((a == b) | (np.isnan(a) & np.isnan(b)))

@@ -10,7 +10,7 @@ checked against the oracle, and determinism across runs.
 import numpy as np
 import pytest
 
-from parity import check, make_case, run_gpu
+from parity import check, make_case, run_dev, run_gpu
 from parmmg_amd import configs, synth
 from parmmg_amd.transfer import TransferContext, pack_tet8
 
@@ -83,22 +83,7 @@ def _full_size(w, seed=synth.SEED):
 
 
 def _run_dev(ctx, bg, new, met, fields, pc, hausd, separate=False):
-    d = dict(xyz=ctx.upload(bg.xyz), triv=ctx.upload(bg.triv), adjt=ctx.upload(bg.adjt), q=ctx.upload(new.xyz),
-             pc=ctx.upload(pc))
-    if separate:
-        d["tetv"], d["adja"] = ctx.upload(bg.tetv), ctx.upload(bg.adja)
-        ctx.set_background(d["xyz"], d["tetv"], d["adja"], d["triv"], d["adjt"], hausd)
-    else:
-        d["tet8"] = ctx.upload(pack_tet8(bg.tetv, bg.adja))
-        ctx.set_background_tet8(d["xyz"], d["tet8"], d["triv"], d["adjt"], hausd)
-    d["met"], d["f"] = ctx.upload(met), [ctx.upload(f) for f in fields]
-    ctx.set_solutions(d["met"], d["f"])
-    mo = ctx.empty((new.np, met.shape[1]), np.float64)
-    fo = [ctx.empty((new.np, f.shape[1]), np.float64) for f in fields]
-    el, hit = ctx.empty((new.np,), np.int32), ctx.empty((new.np,), np.int8)
-    ctx.locate_interp(d["q"], d["pc"], mo, fo, el, hit, sync=False)
-    st = ctx.sync()
-    return mo.download(), [f.download() for f in fo], el.download(), hit.download(), st
+    return run_dev(ctx, bg, new.xyz, met, fields, pc, hausd, separate)
 
 
 @pytest.mark.gpu
