@@ -223,6 +223,35 @@ int pmmg_hip_tetra_qual(pmmg_hip_ctx *ctx, int np, const double *xyz, int ne,
                         const int *tetv, int met_size, const double *met,
                         double *qual, double *minqual);
 
+/* Load-balancing weights from the interpolated metric (SURVEY.md §8(f)
+ * rank 2, the second consumer after PMMG_tetraQual), device arrays, 1-based
+ * vertex ids, synchronous.
+ *
+ * pmmg_hip_compute_wgt_mesh replaces PMMG_computeWgt_mesh
+ * (src/metis_pmmg.c:242-266): for every used tetra k (tetv[4k] > 0) with an
+ * xtetra (xt[k] != 0), qual[k] = sum over its faces f with (ftag[4k+f] & tag)
+ * of PMMG_computeWgt(mesh, met, pt, f) (:280-300); the other entries of qual
+ * are left untouched.  ftag = the xtetra face tags gathered per tetra
+ * (pxt->ftag[0..3]).
+ *
+ * pmmg_hip_compute_wgt_faces: PMMG_computeWgt of a list of faces
+ * face[2j] = tetra (1-based), face[2j+1] = local face index (the graph
+ * weights of src/metis_pmmg.c:812, :959) into wgt[j].
+ *
+ * PMMG_computeWgt: the three edges of the face have lengths len in the
+ * metric (MMG5_lenedg: met_size 1 MMG5_lenedgCoor_iso, 6
+ * MMG5_lenedgCoor_ani); res = sum (len - 1) for len <= 1 else (1/len - 1);
+ * weight = min(1/exp(28 res / 3), PMMG_WGTVAL_HUGEINT); met_size 0 (no
+ * metric): PMMG_WGTVAL_HUGEINT.  Mmg's special metric storage at ridge
+ * points (MG_GEO edges of an aniso metric) is not modelled.
+ * Returns 1, or 0 on invalid arguments. */
+int pmmg_hip_compute_wgt_mesh(pmmg_hip_ctx *ctx, int np, const double *xyz, int ne,
+                              const int *tetv, const int *xt, const uint16_t *ftag,
+                              int met_size, const double *met, int tag, double *qual);
+int pmmg_hip_compute_wgt_faces(pmmg_hip_ctx *ctx, int np, const double *xyz,
+                               const int *tetv, int nface, const int *face,
+                               int met_size, const double *met, double *wgt);
+
 /* Device memory helpers for callers that keep data resident (bench, shims
  * that reuse buffers across iterations). */
 void *pmmg_hip_malloc(pmmg_hip_ctx *ctx, int64_t bytes);

@@ -74,6 +74,10 @@ def lib():
         L.orc_invmat.restype = ci
         L.orc_tetra_qual.argtypes = [ci, vp, ci, vp, ci, vp, vp]
         L.orc_tetra_qual.restype = cd
+        L.orc_face_wgt.argtypes = [vp, vp, ci, ci, vp]
+        L.orc_face_wgt.restype = cd
+        L.orc_compute_wgt_mesh.argtypes = [ci, vp, vp, vp, vp, ci, vp, ci, vp]
+        L.orc_compute_wgt_mesh.restype = None
         L.orc_check_batch.argtypes = [vp, vp, vp, vp, ctypes.c_int64, vp, vp, vp, vp, vp, vp, vp, ci, cd, vp]
         L.orc_check_batch.restype = ci
         _lib = L
@@ -249,3 +253,24 @@ def tetra_qual(xyz, tetv, met=None):
     mn = lib().orc_tetra_qual(xyz.shape[0], _p(xyz), tetv.shape[0], _p(tetv), 0 if met is None else met.shape[1],
                               _p(met), _p(qual))
     return qual, mn
+
+
+def face_wgt(xyz, v, ifac, met=None):
+    """PMMG_computeWgt of face ifac of the tetra with vertices v (1-based)."""
+    xyz = np.ascontiguousarray(xyz, np.float64)
+    v = np.ascontiguousarray(v, np.int32)
+    met = None if met is None else np.ascontiguousarray(met, np.float64)
+    return lib().orc_face_wgt(_p(xyz), _p(v), int(ifac), 0 if met is None else met.shape[1], _p(met))
+
+
+def compute_wgt_mesh(xyz, tetv, xt, ftag, met, tag, qual):
+    """PMMG_computeWgt_mesh restated: qual updated in place (a copy is returned)."""
+    q = np.array(qual, np.float64, copy=True)
+    xyz = np.ascontiguousarray(xyz, np.float64)
+    tetv = np.ascontiguousarray(tetv, np.int32)
+    xt = np.ascontiguousarray(xt, np.int32)
+    ftag = np.ascontiguousarray(ftag, np.uint16)
+    met = None if met is None else np.ascontiguousarray(met, np.float64)
+    lib().orc_compute_wgt_mesh(tetv.shape[0], _p(tetv), _p(xt), _p(ftag), _p(xyz),
+                               0 if met is None else met.shape[1], _p(met), int(tag), _p(q))
+    return q

@@ -1196,3 +1196,64 @@ double orc_tetra_qual(int np, const double *xyz, int ne, const int *tetv, int me
   }
   return ORC_ALPHAD * minqual;
 }
+
+/* ------------------------------------------------------------------ metis weights
+ * PMMG_computeWgt (src/metis_pmmg.c:280-300) and PMMG_computeWgt_mesh
+ * (:242-266): per tetra face, the three face edges' lengths in the metric
+ * (MMG5_lenedg: MMG5_lenedgCoor_iso / MMG5_lenedgCoor_ani of Mmg @889d408,
+ * restated from its published source — Mmg is not in the image, parity
+ * unpinned; aniso edges use the general formula, Mmg's special ridge-point
+ * storage (MG_GEO edges) is not modelled), res = sum over the edges of
+ * (len - 1) for len <= 1 else (1/len - 1), weight = min(1/exp(28 res / 3),
+ * PMMG_WGTVAL_HUGEINT); without a metric the weight is PMMG_WGTVAL_HUGEINT. */
+static const int kIare[6][2] = {{0, 1}, {0, 2}, {0, 3}, {1, 2}, {1, 3}, {2, 3}}; /* MMG5_iare */
+static const int kIarf[4][3] = {{5, 4, 3}, {5, 1, 2}, {4, 2, 0}, {3, 0, 1}};     /* MMG5_iarf */
+#define ORC_WGTVAL_HUGEINT 1000000
+#define ORC_MMG5_EPS 1.0e-06
+
+static double lenedg_iso(const double *ca, const double *cb, double h1, double h2) {
+  double l = (cb[0] - ca[0]) * (cb[0] - ca[0]) + (cb[1] - ca[1]) * (cb[1] - ca[1]) + (cb[2] - ca[2]) * (cb[2] - ca[2]);
+  l = sqrt(l);
+  const double r = h2 / h1 - 1.0;
+  return (fabs(r) < ORC_MMG5_EPS) ? (l / h1) : (l / (h2 - h1) * log1p(r));
+}
+
+static double lenedg_ani(const double *ca, const double *cb, const double *sa, const double *sb) {
+  const double ux = cb[0] - ca[0], uy = cb[1] - ca[1], uz = cb[2] - ca[2];
+  double dd1 = sa[0] * ux * ux + sa[3] * uy * uy + sa[5] * uz * uz + 2.0 * (sa[1] * ux * uy + sa[2] * ux * uz + sa[4] * uy * uz);
+  if (dd1 <= 0.0) dd1 = 0.0;
+  double dd2 = sb[0] * ux * ux + sb[3] * uy * uy + sb[5] * uz * uz + 2.0 * (sb[1] * ux * uy + sb[2] * ux * uz + sb[4] * uy * uz);
+  if (dd2 <= 0.0) dd2 = 0.0;
+  if (fabs(dd1 - dd2) < 0.05) return sqrt(0.5 * (dd1 + dd2));
+  return (sqrt(dd1) + sqrt(dd2) + 4.0 * sqrt(0.5 * (dd1 + dd2))) / 6.0;
+}
+
+double orc_face_wgt(const double *xyz, const int *v, int ifac, int met_size, const double *met) {
+  if (met_size != 1 && met_size != 6) return (double)ORC_WGTVAL_HUGEINT;
+  double res = 0.0;
+  for (int i = 0; i < 3; i++) {
+    const int ia = kIarf[ifac][i];
+    const int ip1 = v[kIare[ia][0]], ip2 = v[kIare[ia][1]];
+    const double *ca = xyz + 3 * (int64_t)(ip1 - 1), *cb = xyz + 3 * (int64_t)(ip2 - 1);
+    const double len = met_size == 1 ? lenedg_iso(ca, cb, met[ip1 - 1], met[ip2 - 1])
+                                     : lenedg_ani(ca, cb, met + 6 * (int64_t)(ip1 - 1), met + 6 * (int64_t)(ip2 - 1));
+    if (len <= 1.0)
+      res += len - 1.0;
+    else
+      res += 1.0 / len - 1.0;
+  }
+  const double w = 1.0 / exp(28.0 * res / 3.0);
+  return w < (double)ORC_WGTVAL_HUGEINT ? w : (double)ORC_WGTVAL_HUGEINT;
+}
+
+void orc_compute_wgt_mesh(int ne, const int *tetv, const int *xt, const uint16_t *ftag, const double *xyz,
+                          int met_size, const double *met, int tag, double *qual) {
+  for (int k = 0; k < ne; k++) {
+    const int *v = tetv + 4 * (int64_t)k;
+    if (v[0] <= 0 || !xt[k]) continue; /* !MG_EOK, or no xtetra: qual untouched */
+    double q = 0.0;
+    for (int f = 0; f < 4; f++)
+      if (ftag[4 * (int64_t)k + f] & tag) q += orc_face_wgt(xyz, v, f, met_size, met);
+    qual[k] = q;
+  }
+}

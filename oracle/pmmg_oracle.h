@@ -159,6 +159,14 @@ int orc_invmat(const double *m, double *mi);
 double orc_tetra_qual(int np, const double *xyz, int ne, const int *tetv, int met_size, const double *met,
                       double *qual);
 
+/* PMMG_computeWgt (src/metis_pmmg.c:280-300) of face ifac of the tetra with
+ * vertices v[4] (1-based), and PMMG_computeWgt_mesh (:242-266): for every
+ * used tetra with xt[k] != 0, qual[k] = sum over faces with ftag[4k+f] & tag
+ * of the face weight (other tetra untouched). */
+double orc_face_wgt(const double *xyz, const int *v, int ifac, int met_size, const double *met);
+void orc_compute_wgt_mesh(int ne, const int *tetv, const int *xt, const uint16_t *ftag, const double *xyz,
+                          int met_size, const double *met, int tag, double *qual);
+
 #ifdef __cplusplus
 }
 #endif

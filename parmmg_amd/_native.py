@@ -50,6 +50,10 @@ HIP_API = {
     "pmmg_hip_build_adjacency": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "pmmg_hip_build_boundary": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                                         c_void_p, c_void_p, c_void_p]),
+    "pmmg_hip_compute_wgt_mesh": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
+                                          c_void_p, c_int, c_void_p]),
+    "pmmg_hip_compute_wgt_faces": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p,
+                                           c_void_p]),
     "pmmg_hip_tetra_qual": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p,
                                     P(c_double)]),
     "pmmg_hip_memcpy_h2d": (c_int, [c_void_p, c_void_p, c_void_p, c_int64]),
@@ -107,6 +111,10 @@ HOST_API = {
     "pmmg_shard_fill": (c_int64, [c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_void_p, c_void_p, c_void_p]),
+    "pmmg_medit_read_mesh": (c_int, [ctypes.c_char_p, c_void_p, ctypes.c_char_p, c_int]),
+    "pmmg_medit_read_sol": (c_int, [ctypes.c_char_p, c_void_p, ctypes.c_char_p, c_int]),
+    "pmmg_medit_free_mesh": (None, [c_void_p]),
+    "pmmg_medit_free_sol": (None, [c_void_p]),
 }
 
 

@@ -70,10 +70,12 @@ def build_hip(force: bool = False) -> str:
 def build_host(force: bool = False) -> str:
     src = os.path.join(CSRC, "pmmg_host.c")
     shard = os.path.join(CSRC, "pmmg_shard.c")
-    deps = [src, shard, os.path.join(CSRC, "pmmg_host.h"), os.path.join(INC, "parmmg_hip.h"), HIP_SO, __file__]
+    medit = os.path.join(CSRC, "pmmg_medit.c")
+    deps = [src, shard, medit, os.path.join(CSRC, "pmmg_host.h"), os.path.join(CSRC, "pmmg_medit.h"),
+            os.path.join(INC, "parmmg_hip.h"), HIP_SO, __file__]
     if force or _stale(HOST_SO, deps):
         _run(["gcc", "-O2", "-std=c99", "-Wall", "-Wextra", "-fPIC", "-shared", f"-I{INC}", f"-I{CSRC}",
-              "-o", HOST_SO, src, shard, f"-L{PKG}", "-lpmmg_hip", "-Wl,-rpath,$ORIGIN"])
+              "-o", HOST_SO, src, shard, medit, f"-L{PKG}", "-lpmmg_hip", "-Wl,-rpath,$ORIGIN"])
     return HOST_SO
 
 
@@ -103,7 +105,7 @@ def build_c_test(force: bool = False) -> str:
     src = os.path.join(ROOT, "tests", "c", "test_c_abi.c")
     synth = os.path.join(CSRC, "pmmg_synth.c")
     deps = [src, synth, HIP_SO, HOST_SO, os.path.join(INC, "parmmg_hip.h"), os.path.join(CSRC, "pmmg_host.h"),
-            __file__]
+            os.path.join(CSRC, "pmmg_medit.h"), __file__]
     if force or _stale(C_TEST, deps):
         _run(["gcc", "-O2", "-std=c99", "-Wall", "-Wextra", f"-I{INC}", f"-I{CSRC}", "-o", C_TEST, src, synth,
               f"-L{PKG}", "-lpmmg_host", "-lpmmg_hip", "-lm", "-Wl,-rpath,$ORIGIN/../../parmmg_amd"])

@@ -25,6 +25,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <chrono>
 #include <condition_variable>
 #include <functional>
 #include <mutex>
@@ -125,10 +126,19 @@ struct pmmg_hip_ctx {
   // host-mode transfers: two pinned staging buffers, filled / drained by a
   // small pool of host threads while the DMA engine moves the other one
   void *stage[2] = {nullptr, nullptr};
+  void *stage_dev[2] = {nullptr, nullptr}; // their device addresses (kernel downloads)
   hipEvent_t stage_ev[2] = {};
   int stage_i = 0;
   struct Pool *pool = nullptr;
   DevBuf o_tet4; // device copy of a host tetv (input of the device adjacency)
+  // host mode: the device-built background (adjacency, boundary trias) runs
+  // on `stream` in a host thread while set_solutions' uploads go through
+  // `cstream` (the DMA engine works beside the snapshot kernels); every other
+  // entry point joins it first (snap_join)
+  hipStream_t cstream = nullptr;
+  std::thread snap;
+  int snap_ok = 1;
+  int verbose = 0; // PMMG_HIP_VERBOSE: host-mode transfer timings on stderr
   int tpc = 8;        // background tetra per volume seed cell (PMMG_HIP_TPC)
   int qpb = 8;        // queries per Morton bin
   int maxstep = 4096; // longer walks go to the exact continuation / exhaustive kernels (PMMG_HIP_MAXSTEP; the
@@ -249,19 +259,36 @@ struct Pool { // fixed host threads running [begin, end) slices of one job at a 
   }
 };
 
+static int env_int(const char *name, int def);
+
 constexpr size_t kStageBytes = 32u << 20;
 constexpr size_t kStageMin = 4u << 20; // smaller copies go straight through the runtime
 constexpr unsigned long long kSentinel = 0x7FF4A5A5A5A5A5A5ULL; // a signalling NaN no arithmetic produces
+
+// device -> pinned host copies by a kernel (the GPU's PCIe writes into the
+// mapped staging buffer; used for every host-mode download)
+__global__ __launch_bounds__(kBlock) void k_copy16(const ntd2 *src, ntd2 *dst, long long n) {
+  for (long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x; j < n; j += (long long)gridDim.x * blockDim.x)
+    __builtin_nontemporal_store(__builtin_nontemporal_load(src + j), dst + j);
+}
+__global__ __launch_bounds__(kBlock) void k_copy1(const char *src, char *dst, long long n) {
+  for (long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x; j < n; j += (long long)gridDim.x * blockDim.x)
+    dst[j] = src[j];
+}
 
 static int stage_ready(pmmg_hip_ctx *c) {
   if (c->stage[0]) return 1;
   for (int b = 0; b < 2; b++) {
     HIPCK(c, hipHostMalloc(&c->stage[b], kStageBytes, hipHostMallocDefault));
+    HIPCK(c, hipHostGetDevicePointer(&c->stage_dev[b], c->stage[b], 0));
     HIPCK(c, hipEventCreateWithFlags(&c->stage_ev[b], hipEventDisableTiming));
   }
   if (!c->pool) {
-    unsigned hw = std::thread::hardware_concurrency();
-    c->pool = new Pool((int)(hw > 8 ? 7 : (hw > 1 ? hw - 1 : 0)));
+    // helper threads for the staging copies: 15 (a one-GPU lease of the pool
+    // gives 16 CPUs; hardware_concurrency shows the whole machine), fewer on
+    // a smaller host, PMMG_HIP_HOST_THREADS to override
+    const int hw = (int)std::thread::hardware_concurrency();
+    c->pool = new Pool(env_int("PMMG_HIP_HOST_THREADS", hw > 16 ? 16 : (hw > 1 ? hw : 1)) - 1);
   }
   return 1;
 }
@@ -273,10 +300,10 @@ static void par_copy(pmmg_hip_ctx *c, void *dst, const void *src, size_t n) {
 
 // host -> device, queued on the context stream; the host buffer may be
 // reused as soon as the call returns
-static int h2d(pmmg_hip_ctx *c, void *dst, const void *src, size_t bytes) {
+static int h2d(pmmg_hip_ctx *c, void *dst, const void *src, size_t bytes, hipStream_t s) {
   if (bytes == 0) return 1;
   if (bytes < kStageMin) {
-    HIPCK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
     return 1;
   }
   if (!stage_ready(c)) return 0;
@@ -286,8 +313,8 @@ static int h2d(pmmg_hip_ctx *c, void *dst, const void *src, size_t bytes) {
     const size_t n = bytes - off < kStageBytes ? bytes - off : kStageBytes;
     HIPCK(c, hipEventSynchronize(c->stage_ev[b])); // the buffer's previous DMA is done
     par_copy(c, c->stage[b], (const char *)src + off, n);
-    HIPCK(c, hipMemcpyAsync((char *)dst + off, c->stage[b], n, hipMemcpyHostToDevice, c->stream));
-    HIPCK(c, hipEventRecord(c->stage_ev[b], c->stream));
+    HIPCK(c, hipMemcpyAsync((char *)dst + off, c->stage[b], n, hipMemcpyHostToDevice, s));
+    HIPCK(c, hipEventRecord(c->stage_ev[b], s));
     off += n;
   }
   return 1;
@@ -298,24 +325,43 @@ static int h2d(pmmg_hip_ctx *c, void *dst, const void *src, size_t bytes) {
 struct AllRows {
   bool operator()(size_t, const char *) const { return true; }
 };
+static double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 template <class Keep>
 static int d2h_rows(pmmg_hip_ctx *c, void *dst, const void *src, size_t nrows, size_t row, const Keep &keep) {
   const size_t bytes = nrows * row;
   if (bytes == 0) return 1;
   if (!stage_ready(c)) return 0;
+  double t_wait = 0.0;
+  const double t_start = now_s();
   const size_t per = kStageBytes / row; // rows per chunk
   const size_t nch = (nrows + per - 1) / per;
   auto issue = [&](size_t j) -> int {
     const int b = (int)(j & 1);
     const size_t r0 = j * per, n = (nrows - r0 < per ? nrows - r0 : per) * row;
-    HIPCK(c, hipMemcpyAsync(c->stage[b], (const char *)src + r0 * row, n, hipMemcpyDeviceToHost, c->stream));
+    // the GPU writes the chunk into the mapped pinned buffer: its PCIe writes
+    // reach ~2x the rate of the DMA engine's device->host copies (r02m: 48-byte
+    // row arrays 36 -> 20-24 ms per GB; the host-side scatter now bounds it)
+    const char *from = (const char *)src + r0 * row;
+    if (((uintptr_t)from & 15) == 0 && (n & 15) == 0) {
+      hipLaunchKernelGGL(k_copy16, dim3(1024), dim3(kBlock), 0, c->stream, (const ntd2 *)from, (ntd2 *)c->stage_dev[b],
+                         (long long)(n / 16));
+    } else {
+      hipLaunchKernelGGL(k_copy1, dim3(1024), dim3(kBlock), 0, c->stream, from, (char *)c->stage_dev[b], (long long)n);
+    }
+    HIPCK(c, hipGetLastError());
     HIPCK(c, hipEventRecord(c->stage_ev[b], c->stream));
     return 1;
   };
   if (!issue(0)) return 0;
   for (size_t j = 0; j < nch; j++) {
     const int b = (int)(j & 1);
+    const double t0 = now_s();
     HIPCK(c, hipEventSynchronize(c->stage_ev[b]));
+    const double t1 = now_s();
+    t_wait += t1 - t0;
     if (j + 1 < nch && !issue(j + 1)) return 0; // the next chunk moves while this one is scattered
     const size_t r0 = j * per, nr = nrows - r0 < per ? nrows - r0 : per;
     const char *sb = (const char *)c->stage[b];
@@ -323,18 +369,38 @@ static int d2h_rows(pmmg_hip_ctx *c, void *dst, const void *src, size_t nrows, s
     if constexpr (std::is_same<Keep, AllRows>::value) {
       par_copy(c, db, sb, nr * row);
     } else {
+      // runs of consecutive kept rows go out as one memcpy each (nearly every
+      // row is kept in a transfer: one copy per slice instead of one per row)
       c->pool->run(nr, nr >= 65536 ? c->pool->th.size() + 1 : 1, [&](size_t a, size_t e) {
-        for (size_t r = a; r < e; r++)
-          if (keep(r0 + r, sb + r * row)) memcpy(db + r * row, sb + r * row, row);
+        size_t r = a;
+        while (r < e) {
+          while (r < e && !keep(r0 + r, sb + r * row)) r++;
+          const size_t s0 = r;
+          while (r < e && keep(r0 + r, sb + r * row)) r++;
+          if (r > s0) memcpy(db + s0 * row, sb + s0 * row, (r - s0) * row);
+        }
       });
     }
   }
+  if (c->verbose)
+    fprintf(stderr, "[parmmg_hip] d2h %zu rows x %zu B: %.2f ms DMA wait, %.2f ms in total\n", nrows, row,
+            1e3 * t_wait, 1e3 * (now_s() - t_start));
   return 1;
 }
 
-static int upload(pmmg_hip_ctx *c, DevBuf &b, const void *src, size_t bytes) {
+static int upload(pmmg_hip_ctx *c, DevBuf &b, const void *src, size_t bytes, hipStream_t s = nullptr) {
   if (!ensure(c, b, bytes)) return 0;
-  return h2d(c, b.p, src, bytes);
+  return h2d(c, b.p, src, bytes, s ? s : c->stream);
+}
+
+// wait for a deferred device snapshot (host-mode set_background); 0 if it failed
+static int snap_join(pmmg_hip_ctx *c) {
+  if (c->snap.joinable()) c->snap.join();
+  if (!c->snap_ok) {
+    c->snap_ok = 1; // reported once, by the call that joined it
+    return 0;
+  }
+  return 1;
 }
 
 __global__ void k_fill64(unsigned long long *a, long long n, unsigned long long v) {
@@ -366,13 +432,15 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   c->device = device;
   c->options = options;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
+      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking) != hipSuccess) {
     fprintf(stderr, "[parmmg_hip] cannot initialise device %d\n", device);
     delete c;
     return nullptr;
   }
   for (int i = 0; i < EV_COUNT; i++) (void)hipEventCreate(&c->ev[i]);
   c->tpc = env_int("PMMG_HIP_TPC", c->tpc);
+  c->verbose = env_int("PMMG_HIP_VERBOSE", 0);
   c->maxstep = env_int("PMMG_HIP_MAXSTEP", c->maxstep);
   c->filter_steps = c->maxstep;
   if (const char *e = getenv("PMMG_HIP_FILTER_STEPS"))
@@ -383,8 +451,10 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
 void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
+  (void)snap_join(c);
   (void)hipStreamSynchronize(c->stream);
   (void)hipStreamSynchronize(c->stream2);
+  if (c->cstream) (void)hipStreamSynchronize(c->cstream);
   DevBuf *bufs[] = {&c->o_xyz, &c->o_tetv, &c->o_adja, &c->o_triv, &c->o_adjt, &c->o_met, &c->frame,
                     &c->stats, &c->grid, &c->sgrid, &c->cnt, &c->off, &c->binrank, &c->order_v,
                     &c->order_b, &c->cont, &c->xq, &c->scan_a, &c->cls_cnt, &c->qmin, &c->fb_vol, &c->fb_bdy,
@@ -403,6 +473,7 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   release(c->o_tet4);
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->cstream) (void)hipStreamDestroy(c->cstream);
   delete c;
 }
 
@@ -419,6 +490,7 @@ static int set_background_impl(pmmg_hip_ctx *c, int np, const double *xyz, int n
                                const int *tet8, int nt, const int *triv, const int *adjt, double hausd, int where) {
   if (!c) return 0;
   HIPCK(c, hipSetDevice(c->device));
+  if (!snap_join(c)) return 0;
   const bool packed = tet8 != nullptr;
   const bool build_bdy = nt < 0 && !triv;
   if (np <= 0 || ne <= 0 || !xyz || (!packed && !tetv) || (nt < 0 && triv) || (nt > 0 && !triv)) {
@@ -448,6 +520,7 @@ static int set_background_impl(pmmg_hip_ctx *c, int np, const double *xyz, int n
     c->bg.xyz = (const double *)c->o_xyz.p;
   }
   // tetra
+  const int *d_tetv = nullptr; // input of the device adjacency
   if (packed) {
     if (dev) {
       c->bg.tetv = reinterpret_cast<const int4 *>(tet8);
@@ -469,56 +542,79 @@ static int set_background_impl(pmmg_hip_ctx *c, int np, const double *xyz, int n
     }
     c->bg.tstride = 1;
   } else { // device adjacency into owned tet8 records
-    const int *d_tetv = tetv;
+    d_tetv = tetv;
     if (!dev) {
       if (!upload(c, c->o_tet4, tetv, sizeof(int) * 4 * (size_t)ne)) return 0;
       d_tetv = (const int *)c->o_tet4.p;
     }
     if (!ensure(c, c->o_tetv, sizeof(int) * 8 * (size_t)ne)) return 0;
-    if (!pmmg_snap_adjacency(c->stream, np, ne, d_tetv, nullptr, (int *)c->o_tetv.p, c->err, sizeof(c->err))) {
-      fprintf(stderr, "[parmmg_hip] %s\n", c->err);
-      return 0;
-    }
     c->bg.tetv = (const int4 *)c->o_tetv.p;
     c->bg.adja = c->bg.tetv + 1;
     c->bg.tstride = 2;
   }
-  // boundary trias
-  if (build_bdy) {
-    const int *t0 = reinterpret_cast<const int *>(c->bg.tetv), *a0 = reinterpret_cast<const int *>(c->bg.adja);
-    int cnt = 0;
-    char msg[256];
-    pmmg_snap_boundary(c->stream, np, ne, t0, c->bg.tstride, a0, c->bg.tstride, nullptr, 0, &cnt, nullptr, nullptr,
-                       msg, sizeof(msg)); // counts (fails on capacity 0 when there are trias)
-    if (!ensure(c, c->o_triv, sizeof(int) * 3 * (size_t)cnt) || !ensure(c, c->o_adjt, sizeof(int) * 3 * (size_t)cnt))
-      return 0;
-    if (!pmmg_snap_boundary(c->stream, np, ne, t0, c->bg.tstride, a0, c->bg.tstride, nullptr, cnt, &nt,
-                            (int *)c->o_triv.p, (int *)c->o_adjt.p, c->err, sizeof(c->err))) {
+  // boundary trias handed over
+  if (!build_bdy) {
+    if (dev) {
+      c->bg.triv = triv;
+      c->bg.adjt = adjt;
+    } else {
+      if (!upload(c, c->o_triv, triv, sizeof(int) * 3 * (size_t)nt)) return 0;
+      c->bg.triv = (const int *)c->o_triv.p;
+      c->bg.adjt = nullptr;
+      if (adjt) {
+        if (!upload(c, c->o_adjt, adjt, sizeof(int) * 3 * (size_t)nt)) return 0;
+        c->bg.adjt = (const int *)c->o_adjt.p;
+      }
+    }
+    c->bg.nt = nt;
+  }
+  const bool tria_adj = !build_bdy && nt > 0 && !adjt;
+  // the device snapshot (PMMG_create_oldGrp's arrays): adjacency, boundary
+  // trias, tria adjacency, each on the context stream
+  auto snapshot = [c, np, ne, d_tetv, build_bdy, tria_adj]() -> int {
+    if (d_tetv && !pmmg_snap_adjacency(c->stream, np, ne, d_tetv, nullptr, (int *)c->o_tetv.p, c->err, sizeof(c->err))) {
       fprintf(stderr, "[parmmg_hip] %s\n", c->err);
       return 0;
     }
-    c->bg.triv = (const int *)c->o_triv.p;
-    c->bg.adjt = (const int *)c->o_adjt.p;
-  } else if (dev) {
-    c->bg.triv = triv;
-    c->bg.adjt = adjt;
-  } else {
-    if (!upload(c, c->o_triv, triv, sizeof(int) * 3 * (size_t)nt)) return 0;
-    c->bg.triv = (const int *)c->o_triv.p;
-    if (adjt) {
-      if (!upload(c, c->o_adjt, adjt, sizeof(int) * 3 * (size_t)nt)) return 0;
+    if (build_bdy) {
+      const int *t0 = reinterpret_cast<const int *>(c->bg.tetv), *a0 = reinterpret_cast<const int *>(c->bg.adja);
+      int cnt = 0, ntb = 0;
+      char msg[256];
+      pmmg_snap_boundary(c->stream, np, ne, t0, c->bg.tstride, a0, c->bg.tstride, nullptr, 0, &cnt, nullptr, nullptr,
+                         msg, sizeof(msg)); // counts (fails on capacity 0 when there are trias)
+      if (!ensure(c, c->o_triv, sizeof(int) * 3 * (size_t)cnt) || !ensure(c, c->o_adjt, sizeof(int) * 3 * (size_t)cnt))
+        return 0;
+      if (!pmmg_snap_boundary(c->stream, np, ne, t0, c->bg.tstride, a0, c->bg.tstride, nullptr, cnt, &ntb,
+                              (int *)c->o_triv.p, (int *)c->o_adjt.p, c->err, sizeof(c->err))) {
+        fprintf(stderr, "[parmmg_hip] %s\n", c->err);
+        return 0;
+      }
+      c->bg.triv = (const int *)c->o_triv.p;
+      c->bg.adjt = (const int *)c->o_adjt.p;
+      c->bg.nt = ntb;
+    }
+    if (tria_adj) {
+      if (!ensure(c, c->o_adjt, sizeof(int) * 3 * (size_t)c->bg.nt)) return 0;
+      if (!pmmg_snap_tria_adjacency(c->stream, np, c->bg.nt, c->bg.triv, (int *)c->o_adjt.p, c->err,
+                                    sizeof(c->err))) {
+        fprintf(stderr, "[parmmg_hip] %s\n", c->err);
+        return 0;
+      }
       c->bg.adjt = (const int *)c->o_adjt.p;
     }
+    return 1;
+  };
+  if (!dev && (d_tetv || build_bdy || tria_adj)) {
+    // host mode: the snapshot runs in a host thread (its kernels on the
+    // context stream) while the caller goes on to set_solutions, whose
+    // uploads use the copy stream; the next other call joins it
+    c->snap_ok = 1;
+    c->snap = std::thread([c, snapshot] {
+      c->snap_ok = hipSetDevice(c->device) == hipSuccess ? snapshot() : 0;
+    });
+    return 1;
   }
-  if (!build_bdy && nt > 0 && !adjt) {
-    if (!ensure(c, c->o_adjt, sizeof(int) * 3 * (size_t)nt)) return 0;
-    if (!pmmg_snap_tria_adjacency(c->stream, np, nt, c->bg.triv, (int *)c->o_adjt.p, c->err, sizeof(c->err))) {
-      fprintf(stderr, "[parmmg_hip] %s\n", c->err);
-      return 0;
-    }
-    c->bg.adjt = (const int *)c->o_adjt.p;
-  }
-  c->bg.nt = nt;
+  if (!snapshot()) return 0;
   if (!dev) HIPCK(c, hipStreamSynchronize(c->stream));
   return 1;
 }
@@ -586,16 +682,17 @@ int pmmg_hip_set_solutions(pmmg_hip_ctx *c, int met_size, const double *met, int
     for (int j = 0; j < nfield; j++) c->fin[j] = fields[j];
     return 1;
   }
+  // host mode: through the copy stream (beside a deferred snapshot)
   if (met_size) {
-    if (!upload(c, c->o_met, met, sizeof(double) * met_size * np)) return 0;
+    if (!upload(c, c->o_met, met, sizeof(double) * met_size * np, c->cstream)) return 0;
     c->met = (const double *)c->o_met.p;
   }
   c->o_f.resize(nfield);
   for (int j = 0; j < nfield; j++) {
-    if (!upload(c, c->o_f[j], fields[j], sizeof(double) * field_size[j] * np)) return 0;
+    if (!upload(c, c->o_f[j], fields[j], sizeof(double) * field_size[j] * np, c->cstream)) return 0;
     c->fin[j] = (const double *)c->o_f[j].p;
   }
-  HIPCK(c, hipStreamSynchronize(c->stream));
+  HIPCK(c, hipStreamSynchronize(c->cstream));
   return 1;
 }
 
@@ -836,6 +933,7 @@ static int collect_stats(pmmg_hip_ctx *c, pmmg_hip_stats *out) {
 int pmmg_hip_sync(pmmg_hip_ctx *c, pmmg_hip_stats *stats) {
   if (!c) return 0;
   HIPCK(c, hipSetDevice(c->device));
+  if (!snap_join(c)) return 0;
   HIPCK(c, hipStreamSynchronize(c->stream));
   if (stats && c->pending) return collect_stats(c, stats);
   return 1;
@@ -846,6 +944,7 @@ int pmmg_hip_locate_interp(pmmg_hip_ctx *c, int np_new, const double *xyz_new, c
                            pmmg_hip_stats *stats, int where) {
   if (!c) return 0;
   HIPCK(c, hipSetDevice(c->device));
+  if (!snap_join(c)) return 0;
   if (c->bg.ne <= 0) {
     set_err(c, "locate_interp: no background set");
     return 0;
@@ -872,6 +971,7 @@ int pmmg_hip_locate_interp(pmmg_hip_ctx *c, int np_new, const double *xyz_new, c
   // step wrote (sentinel gone; elem / hit where hit != 0) are copied back, so
   // the caller's other rows stay untouched without being uploaded.
   size_t n = (size_t)np_new;
+  const double t0 = now_s();
   if (!upload(c, c->h_xyz, xyz_new, sizeof(double) * 3 * n)) return 0;
   if (!upload(c, c->h_cls, pclass, n)) return 0;
   double *dmet = nullptr;
@@ -904,8 +1004,10 @@ int pmmg_hip_locate_interp(pmmg_hip_ctx *c, int np_new, const double *xyz_new, c
   if (!run_device(c, np_new, (const double *)c->h_xyz.p, (const uint8_t *)c->h_cls.p, dmet, dfields.data(),
                   (int *)c->h_elem.p, (int8_t *)c->h_hit.p))
     return 0;
+  const double t1 = now_s();
   std::vector<int8_t> hh(n);
   if (!d2h_rows(c, hh.data(), c->h_hit.p, n, 1, AllRows{})) return 0;
+  const double t2 = now_s();
   auto written = [&](size_t, const char *row) {
     unsigned long long u;
     memcpy(&u, row, 8);
@@ -917,8 +1019,13 @@ int pmmg_hip_locate_interp(pmmg_hip_ctx *c, int np_new, const double *xyz_new, c
     if (!d2h_rows(c, fields_out[j], dfields[j], n, sizeof(double) * c->fsize[j], written)) return 0;
   if (elem_out && !d2h_rows(c, elem_out, c->h_elem.p, n, sizeof(int), processed)) return 0;
   if (hit_out)
-    for (size_t r = 0; r < n; r++)
-      if (hh[r]) hit_out[r] = hh[r];
+    c->pool->run(n, n >= 65536 ? c->pool->th.size() + 1 : 1, [&](size_t a, size_t e) {
+      for (size_t r = a; r < e; r++)
+        if (hh[r]) hit_out[r] = hh[r];
+    });
+  if (c->verbose)
+    fprintf(stderr, "[parmmg_hip] host locate: uploads + enqueue %.2f ms, step + hit codes %.2f ms, rows %.2f ms\n",
+            1e3 * (t1 - t0), 1e3 * (t2 - t1), 1e3 * (now_s() - t2));
   if (stats) return collect_stats(c, stats);
   return 1;
 }
@@ -930,6 +1037,7 @@ static bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
 int pmmg_hip_build_adjacency(pmmg_hip_ctx *c, int np, int ne, const int *tetv, int *adja, int *tet8) {
   if (!c) return 0;
   HIPCK(c, hipSetDevice(c->device));
+  if (!snap_join(c)) return 0;
   if (np <= 0 || ne <= 0 || !tetv || (!adja && !tet8)) {
     set_err(c, "build_adjacency: invalid arguments (np=%d ne=%d)", np, ne);
     return 0;
@@ -949,6 +1057,7 @@ int pmmg_hip_tetra_qual(pmmg_hip_ctx *c, int np, const double *xyz, int ne, cons
                         const double *met, double *qual, double *minqual) {
   if (!c) return 0;
   HIPCK(c, hipSetDevice(c->device));
+  if (!snap_join(c)) return 0;
   if (np < 0 || ne < 0 || (ne > 0 && (!xyz || !tetv || !qual)) || !minqual ||
       (met_size == 6 && ne > 0 && !met) || (met_size != 0 && met_size != 1 && met_size != 6)) {
     set_err(c, "tetra_qual: invalid arguments (np=%d ne=%d met_size=%d)", np, ne, met_size);
@@ -976,10 +1085,54 @@ int pmmg_hip_tetra_qual(pmmg_hip_ctx *c, int np, const double *xyz, int ne, cons
   return 1;
 }
 
+int pmmg_hip_compute_wgt_mesh(pmmg_hip_ctx *c, int np, const double *xyz, int ne, const int *tetv, const int *xt,
+                              const uint16_t *ftag, int met_size, const double *met, int tag, double *qual) {
+  if (!c) return 0;
+  HIPCK(c, hipSetDevice(c->device));
+  if (!snap_join(c)) return 0;
+  if (np < 0 || ne < 0 || (ne > 0 && (!xyz || !tetv || !xt || !ftag || !qual)) ||
+      (met_size != 0 && met_size != 1 && met_size != 6) || (met_size && ne > 0 && !met)) {
+    set_err(c, "compute_wgt_mesh: invalid arguments (np=%d ne=%d met_size=%d)", np, ne, met_size);
+    return 0;
+  }
+  if (ne > 0 && (!aligned16(tetv) || ((uintptr_t)ftag & 7))) {
+    set_err(c, "compute_wgt_mesh: tetv must be 16-byte and ftag 8-byte aligned");
+    return 0;
+  }
+  if (!pmmg_wgt_mesh(c->stream, xyz, ne, tetv, xt, ftag, met_size, met, tag, qual)) {
+    set_err(c, "compute_wgt_mesh: kernel launch failed");
+    return 0;
+  }
+  return 1;
+}
+
+int pmmg_hip_compute_wgt_faces(pmmg_hip_ctx *c, int np, const double *xyz, const int *tetv, int nface,
+                               const int *face, int met_size, const double *met, double *wgt) {
+  if (!c) return 0;
+  HIPCK(c, hipSetDevice(c->device));
+  if (!snap_join(c)) return 0;
+  if (np < 0 || nface < 0 || (nface > 0 && (!xyz || !tetv || !face || !wgt)) ||
+      (met_size != 0 && met_size != 1 && met_size != 6) || (met_size && nface > 0 && !met)) {
+    set_err(c, "compute_wgt_faces: invalid arguments (np=%d nface=%d met_size=%d)", np, nface, met_size);
+    return 0;
+  }
+  if (nface > 0 && (!aligned16(tetv) || ((uintptr_t)face & 7))) {
+    set_err(c, "compute_wgt_faces: tetv must be 16-byte and face 8-byte aligned");
+    return 0;
+  }
+  if (!pmmg_wgt_faces(c->stream, xyz, tetv, nface, face, met_size, met, wgt)) {
+    set_err(c, "compute_wgt_faces: kernel launch failed");
+    return 0;
+  }
+  return 1;
+}
+
 int pmmg_hip_build_boundary(pmmg_hip_ctx *c, int np, int ne, const int *tet8, const int *tetv, const int *adja,
                             const int *tref, int cap, int *nt, int *triv, int *adjt) {
   if (!c) return 0;
   HIPCK(c, hipSetDevice(c->device));
+  if (!snap_join(c)) return 0;
+  if (!snap_join(c)) return 0;
   const bool packed = tet8 != nullptr;
   if (np <= 0 || ne <= 0 || !nt || (!packed && (!tetv || !adja)) || cap < 0 || (cap > 0 && !triv)) {
     set_err(c, "build_boundary: invalid arguments (np=%d ne=%d cap=%d)", np, ne, cap);
@@ -1008,6 +1161,7 @@ void *pmmg_hip_malloc(pmmg_hip_ctx *c, int64_t bytes) {
 int pmmg_hip_free(pmmg_hip_ctx *c, void *p) {
   if (!c) return 0;
   HIPCK(c, hipSetDevice(c->device));
+  if (!snap_join(c)) return 0;
   HIPCK(c, hipFree(p));
   return 1;
 }
@@ -1015,7 +1169,8 @@ int pmmg_hip_free(pmmg_hip_ctx *c, void *p) {
 int pmmg_hip_memcpy_h2d(pmmg_hip_ctx *c, void *dst, const void *src, int64_t bytes) {
   if (!c || bytes < 0) return 0;
   HIPCK(c, hipSetDevice(c->device));
-  if (!h2d(c, dst, src, (size_t)bytes)) return 0;
+  if (!snap_join(c)) return 0;
+  if (!h2d(c, dst, src, (size_t)bytes, c->stream)) return 0;
   HIPCK(c, hipStreamSynchronize(c->stream));
   return 1;
 }
@@ -1023,6 +1178,7 @@ int pmmg_hip_memcpy_h2d(pmmg_hip_ctx *c, void *dst, const void *src, int64_t byt
 int pmmg_hip_memcpy_d2h(pmmg_hip_ctx *c, void *dst, const void *src, int64_t bytes) {
   if (!c || bytes < 0) return 0;
   HIPCK(c, hipSetDevice(c->device));
+  if (!snap_join(c)) return 0;
   if ((size_t)bytes < kStageMin) {
     HIPCK(c, hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToHost, c->stream));
     HIPCK(c, hipStreamSynchronize(c->stream));

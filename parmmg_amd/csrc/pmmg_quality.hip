@@ -128,6 +128,85 @@ __global__ __launch_bounds__(kQBlock) void k_tetra_qual(const double *xyz, int n
   }
 }
 
+// ---------------------------------------------------------------- metis weights
+//
+// PMMG_computeWgt (src/metis_pmmg.c:280-300): weight of a tetra face from the
+// lengths of its three edges in the metric (MMG5_lenedg = MMG5_lenedgCoor_iso
+// / MMG5_lenedgCoor_ani of Mmg @889d408, restated; aniso ridge-point storage
+// not modelled), the load-balancing weight of the faces on parallel
+// interfaces.  Same operation order as oracle/pmmg_oracle.c orc_face_wgt;
+// exp / log1p are the device library's (within an ulp of the host's).
+constexpr double kHugeWgt = 1000000.0; // PMMG_WGTVAL_HUGEINT
+constexpr double kMmgEps = 1.0e-06;    // MMG5_EPS
+__constant__ int kIare[6][2] = {{0, 1}, {0, 2}, {0, 3}, {1, 2}, {1, 3}, {2, 3}}; // MMG5_iare
+__constant__ int kIarf[4][3] = {{5, 4, 3}, {5, 1, 2}, {4, 2, 0}, {3, 0, 1}};     // MMG5_iarf
+
+__device__ __forceinline__ double lenedg_iso(const double *ca, const double *cb, double h1, double h2) {
+  double l = (cb[0] - ca[0]) * (cb[0] - ca[0]) + (cb[1] - ca[1]) * (cb[1] - ca[1]) + (cb[2] - ca[2]) * (cb[2] - ca[2]);
+  l = sqrt(l);
+  const double r = h2 / h1 - 1.0;
+  return (fabs(r) < kMmgEps) ? (l / h1) : (l / (h2 - h1) * log1p(r));
+}
+
+__device__ __forceinline__ double lenedg_ani(const double *ca, const double *cb, const double *sa, const double *sb) {
+  const double ux = cb[0] - ca[0], uy = cb[1] - ca[1], uz = cb[2] - ca[2];
+  double dd1 = sa[0] * ux * ux + sa[3] * uy * uy + sa[5] * uz * uz + 2.0 * (sa[1] * ux * uy + sa[2] * ux * uz + sa[4] * uy * uz);
+  if (dd1 <= 0.0) dd1 = 0.0;
+  double dd2 = sb[0] * ux * ux + sb[3] * uy * uy + sb[5] * uz * uz + 2.0 * (sb[1] * ux * uy + sb[2] * ux * uz + sb[4] * uy * uz);
+  if (dd2 <= 0.0) dd2 = 0.0;
+  if (fabs(dd1 - dd2) < 0.05) return sqrt(0.5 * (dd1 + dd2));
+  return (sqrt(dd1) + sqrt(dd2) + 4.0 * sqrt(0.5 * (dd1 + dd2))) / 6.0;
+}
+
+__device__ double face_wgt(const double *xyz, const int *v, int ifac, int met_size, const double *met) {
+  if (met_size != 1 && met_size != 6) return kHugeWgt;
+  double res = 0.0;
+  for (int i = 0; i < 3; i++) {
+    const int ia = kIarf[ifac][i];
+    const int ip1 = v[kIare[ia][0]], ip2 = v[kIare[ia][1]];
+    const double *ca = xyz + 3 * (size_t)(ip1 - 1), *cb = xyz + 3 * (size_t)(ip2 - 1);
+    const double len = met_size == 1 ? lenedg_iso(ca, cb, met[ip1 - 1], met[ip2 - 1])
+                                     : lenedg_ani(ca, cb, met + 6 * (size_t)(ip1 - 1), met + 6 * (size_t)(ip2 - 1));
+    if (len <= 1.0)
+      res += len - 1.0;
+    else
+      res += 1.0 / len - 1.0;
+  }
+  const double w = 1.0 / exp(28.0 * res / 3.0);
+  return w < kHugeWgt ? w : kHugeWgt;
+}
+
+// PMMG_computeWgt_mesh: qual[k] = sum over the faces of k tagged `tag` of the
+// face weight, for used tetra with an xtetra; the others keep qual[k]
+__global__ __launch_bounds__(kQBlock) void k_wgt_mesh(const double *xyz, int ne, const int4 *tetv, const int *xt,
+                                                      const uint16_t *ftag, int met_size, const double *met, int tag,
+                                                      double *qual) {
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < ne; k += gridDim.x * blockDim.x) {
+    const int4 t = tetv[k];
+    if (t.x <= 0 || !xt[k]) continue;
+    const int v[4] = {t.x, t.y, t.z, t.w};
+    const ushort4 ft = reinterpret_cast<const ushort4 *>(ftag)[k];
+    const int f4[4] = {ft.x, ft.y, ft.z, ft.w};
+    double q = 0.0;
+    for (int f = 0; f < 4; f++)
+      if (f4[f] & tag) q += face_wgt(xyz, v, f, met_size, met);
+    qual[k] = q;
+  }
+}
+
+// the weights of a list of (tetra, face) pairs (the graph weights of
+// src/metis_pmmg.c:812, :959): face[2j] = tetra (1-based), face[2j+1] = ifac
+__global__ __launch_bounds__(kQBlock) void k_wgt_faces(const double *xyz, const int4 *tetv, int nface,
+                                                       const int2 *face, int met_size, const double *met,
+                                                       double *wgt) {
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nface; j += gridDim.x * blockDim.x) {
+    const int2 fj = face[j];
+    const int4 t = tetv[fj.x - 1];
+    const int v[4] = {t.x, t.y, t.z, t.w};
+    wgt[j] = face_wgt(xyz, v, fj.y, met_size, met);
+  }
+}
+
 } // namespace
 
 int pmmg_qual_tetra(hipStream_t s, int np, const double *xyz, int ne, const int *tetv, int met_size,
@@ -143,5 +222,28 @@ int pmmg_qual_tetra(hipStream_t s, int np, const double *xyz, int ne, const int 
   }
   if (hipMemcpyAsync(h_minbits, d_minbits, sizeof(unsigned long long), hipMemcpyDeviceToHost, s) != hipSuccess)
     return 0;
+  return hipStreamSynchronize(s) == hipSuccess;
+}
+
+int pmmg_wgt_mesh(hipStream_t s, const double *xyz, int ne, const int *tetv, const int *xt, const uint16_t *ftag,
+                  int met_size, const double *met, int tag, double *qual) {
+  if (ne > 0) {
+    const int need = (ne + kQBlock - 1) / kQBlock;
+    hipLaunchKernelGGL(k_wgt_mesh, dim3(need < 16384 ? need : 16384), dim3(kQBlock), 0, s, xyz, ne,
+                       reinterpret_cast<const int4 *>(tetv), xt, ftag, met_size, met, tag, qual);
+    if (hipGetLastError() != hipSuccess) return 0;
+  }
+  return hipStreamSynchronize(s) == hipSuccess;
+}
+
+int pmmg_wgt_faces(hipStream_t s, const double *xyz, const int *tetv, int nface, const int *face, int met_size,
+                   const double *met, double *wgt) {
+  if (nface > 0) {
+    const int need = (nface + kQBlock - 1) / kQBlock;
+    hipLaunchKernelGGL(k_wgt_faces, dim3(need < 16384 ? need : 16384), dim3(kQBlock), 0, s, xyz,
+                       reinterpret_cast<const int4 *>(tetv), nface, reinterpret_cast<const int2 *>(face), met_size,
+                       met, wgt);
+    if (hipGetLastError() != hipSuccess) return 0;
+  }
   return hipStreamSynchronize(s) == hipSuccess;
 }

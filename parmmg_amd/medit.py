@@ -138,3 +138,64 @@ def refine8(xyz: np.ndarray, tetv: np.ndarray):
     tet_new = np.ascontiguousarray(np.concatenate(t, 0).astype(np.int32))
     is_mid = np.r_[np.zeros(npo, bool), np.ones(mid.shape[0], bool)]
     return np.ascontiguousarray(xyz_new), tet_new, is_mid
+
+
+# ---------------------------------------------------------------- C reader
+# pmmg_medit_read_mesh / pmmg_medit_read_sol of libpmmg_host (csrc/pmmg_medit.c),
+# the reader a C shim or program uses; the numpy reader above is the fixture
+# tool the tests compare it with.
+
+import ctypes as _ct  # noqa: E402
+
+
+class _CMesh(_ct.Structure):
+    _fields_ = [("np", _ct.c_int), ("ne", _ct.c_int), ("nt", _ct.c_int), ("xyz", _ct.POINTER(_ct.c_double)),
+                ("vref", _ct.POINTER(_ct.c_int)), ("tetv", _ct.POINTER(_ct.c_int)), ("tref", _ct.POINTER(_ct.c_int)),
+                ("triv", _ct.POINTER(_ct.c_int)), ("trref", _ct.POINTER(_ct.c_int))]
+
+
+_MAXSOL = 32
+
+
+class _CSol(_ct.Structure):
+    _fields_ = [("np", _ct.c_int), ("nsol", _ct.c_int), ("type", _ct.c_int * _MAXSOL), ("size", _ct.c_int * _MAXSOL),
+                ("val", _ct.POINTER(_ct.c_double) * _MAXSOL)]
+
+
+def _arr(ptr, n, dtype, cols):
+    if n == 0:
+        return np.zeros((0, cols) if cols > 1 else (0,), dtype)
+    a = np.ctypeslib.as_array(ptr, shape=(n * cols,)).astype(dtype, copy=True)
+    return a.reshape(n, cols) if cols > 1 else a
+
+
+def read_mesh_c(path: str) -> dict:
+    """The C reader (libpmmg_host): xyz, vref, tetv, tref, triv, trref."""
+    from ._native import host_lib
+
+    lib = host_lib()
+    m = _CMesh()
+    err = _ct.create_string_buffer(512)
+    if not lib.pmmg_medit_read_mesh(path.encode(), _ct.byref(m), err, 512):
+        raise ValueError(err.value.decode())
+    try:
+        return {"xyz": _arr(m.xyz, m.np, np.float64, 3), "vref": _arr(m.vref, m.np, np.int32, 1),
+                "tetv": _arr(m.tetv, m.ne, np.int32, 4), "tref": _arr(m.tref, m.ne, np.int32, 1),
+                "triv": _arr(m.triv, m.nt, np.int32, 3), "trref": _arr(m.trref, m.nt, np.int32, 1)}
+    finally:
+        lib.pmmg_medit_free_mesh(_ct.byref(m))
+
+
+def read_sol_c(path: str) -> list[np.ndarray]:
+    """The C reader: one (np, size) array per solution (MMG5 tensor order)."""
+    from ._native import host_lib
+
+    lib = host_lib()
+    s = _CSol()
+    err = _ct.create_string_buffer(512)
+    if not lib.pmmg_medit_read_sol(path.encode(), _ct.byref(s), err, 512):
+        raise ValueError(err.value.decode())
+    try:
+        return [_arr(s.val[j], s.np, np.float64, s.size[j]).reshape(s.np, s.size[j]) for j in range(s.nsol)]
+    finally:
+        lib.pmmg_medit_free_sol(_ct.byref(s))

@@ -216,6 +216,27 @@ class TransferContext:
                                               ctypes.byref(mn)), "tetra_qual")
         return qual, mn.value
 
+    def compute_wgt_mesh(self, xyz, tetv, xt, ftag, met, tag, qual):
+        """PMMG_computeWgt_mesh on the device (pmmg_hip_compute_wgt_mesh):
+        device arrays; qual is updated in place for tetra with an xtetra."""
+        if not all(_is_dev(a) for a in (xyz, tetv, xt, ftag, qual)) or (met is not None and not _is_dev(met)):
+            raise ValueError("compute_wgt_mesh takes device arrays")
+        self._ck(self.lib.pmmg_hip_compute_wgt_mesh(self.h, xyz.shape[0], _p(xyz), tetv.shape[0], _p(tetv), _p(xt),
+                                                    _p(ftag), 0 if met is None else int(met.shape[1]), _p(met),
+                                                    int(tag), _p(qual)), "compute_wgt_mesh")
+        return qual
+
+    def compute_wgt_faces(self, xyz, tetv, face, met, wgt=None):
+        """PMMG_computeWgt of a (tetra, face) list (pmmg_hip_compute_wgt_faces)."""
+        if not all(_is_dev(a) for a in (xyz, tetv, face)) or (met is not None and not _is_dev(met)):
+            raise ValueError("compute_wgt_faces takes device arrays")
+        nf = face.shape[0]
+        wgt = wgt if wgt is not None else self.empty((nf,), np.float64)
+        self._ck(self.lib.pmmg_hip_compute_wgt_faces(self.h, xyz.shape[0], _p(xyz), _p(tetv), nf, _p(face),
+                                                     0 if met is None else int(met.shape[1]), _p(met), _p(wgt)),
+                 "compute_wgt_faces")
+        return wgt
+
     def sync(self) -> HipStats:
         st = HipStats()
         self._ck(self.lib.pmmg_hip_sync(self.h, ctypes.byref(st)), "sync")

@@ -23,6 +23,7 @@
 
 #include "parmmg_hip.h"
 #include "pmmg_host.h"
+#include "pmmg_medit.h"
 #include "pmmg_synth.h"
 
 static int failures = 0;
@@ -249,7 +250,91 @@ static void device_checks(pmmg_hip_ctx *ctx) {
   }
 }
 
-int main(void) {
+/* the reference's libexamples/adaptation_example0 cube read by the C Medit
+ * reader (cube.mesh, cube-met.sol, cube-solphys.sol), transferred to its
+ * tetra centroids (volume points: P1 values = mean of the 4 vertex values)
+ * and to its own vertices as MG_BDY points (vertex hits: the vertex rows
+ * copied bit for bit) */
+static void fixture_checks(pmmg_hip_ctx *ctx, const char *dir) {
+  char path[1024], err[256];
+  pmmg_medit_mesh m;
+  pmmg_medit_sol met, phys;
+  snprintf(path, sizeof path, "%s/cube.mesh", dir);
+  CHECK(pmmg_medit_read_mesh(path, &m, err, sizeof err) == 1, "%s", err);
+  snprintf(path, sizeof path, "%s/cube-met.sol", dir);
+  CHECK(pmmg_medit_read_sol(path, &met, err, sizeof err) == 1, "%s", err);
+  snprintf(path, sizeof path, "%s/cube-solphys.sol", dir);
+  CHECK(pmmg_medit_read_sol(path, &phys, err, sizeof err) == 1, "%s", err);
+  if (failures) return;
+  CHECK(met.nsol == 1 && met.size[0] == 1 && phys.nsol == 3 && met.np == m.np, "fixture solutions");
+  const int nq = m.ne + m.np;
+  double *xq = malloc(sizeof(double) * 3 * nq);
+  uint16_t *tag = calloc(nq, sizeof(uint16_t));
+  for (int k = 0; k < m.ne; k++)
+    for (int d = 0; d < 3; d++) {
+      double c = 0.0;
+      for (int i = 0; i < 4; i++) c += m.xyz[3 * (m.tetv[4 * k + i] - 1) + d];
+      xq[3 * k + d] = 0.25 * c;
+    }
+  memcpy(xq + 3 * m.ne, m.xyz, sizeof(double) * 3 * m.np);
+  for (int i = 0; i < m.np; i++) tag[m.ne + i] = PMMG_TAG_BDY;
+  double *omet = malloc(sizeof(double) * nq), *of[3];
+  for (int j = 0; j < 3; j++) of[j] = malloc(sizeof(double) * phys.size[j] * nq);
+  int *elem = calloc(nq, sizeof(int));
+  int8_t *hit = calloc(nq, 1);
+  pmmg_old_group o = {0};
+  o.np = m.np;
+  o.ne = m.ne;
+  o.nt = -1; /* boundary trias built on the device */
+  o.xyz = m.xyz;
+  o.tetv = m.tetv;
+  o.hausd = 0.01;
+  o.met_size = 1;
+  o.met = met.val[0];
+  o.nfield = 3;
+  o.field_size = phys.size;
+  o.field = (const double *const *)phys.val;
+  pmmg_new_group g = {0};
+  g.np = nq;
+  g.xyz = xq;
+  g.tag = tag;
+  g.met_size = 1;
+  g.met = omet;
+  g.field = of;
+  g.elem = elem;
+  g.hit = hit;
+  pmmg_hip_stats st;
+  CHECK(pmmg_interp_metrics_and_fields(ctx, 1, &o, &g, 1, &st) == 1, "fixture transfer: %s", pmmg_hip_last_error(ctx));
+  int bad = 0;
+  for (int k = 0; k < m.ne; k++) { /* centroids: P1 = mean of the vertex values */
+    bad += (hit[k] & 15) != 1;
+    bad += fabs(omet[k] - met.val[0][m.tetv[4 * k] - 1]) > 1e-12 * fabs(omet[k]); /* constant size */
+    for (int j = 0; j < 2; j++)
+      for (int c = 0; c < phys.size[j]; c++) {
+        double mean = 0.0;
+        for (int i = 0; i < 4; i++) mean += 0.25 * phys.val[j][phys.size[j] * (m.tetv[4 * k + i] - 1) + c];
+        bad += fabs(of[j][phys.size[j] * k + c] - mean) > 1e-12 * (fabs(mean) + 1.0);
+      }
+    for (int c = 0; c < 6; c++) bad += !isfinite(of[2][6 * k + c]);
+  }
+  for (int i = 0; i < m.np; i++) { /* vertices: copied rows */
+    const int q = m.ne + i;
+    bad += (hit[q] & 15) != 6;
+    bad += omet[q] != met.val[0][i];
+    for (int j = 0; j < 3; j++)
+      bad += memcmp(of[j] + phys.size[j] * q, phys.val[j] + phys.size[j] * i, sizeof(double) * phys.size[j]) != 0;
+  }
+  CHECK(bad == 0, "reference cube fixture: %d wrong values", bad);
+  printf("test_c_abi: reference cube fixture (%d tetra, %d points) transferred, %d wrong values\n", m.ne, nq, bad);
+  free(xq); free(tag); free(omet); free(elem); free(hit);
+  for (int j = 0; j < 3; j++) free(of[j]);
+  pmmg_medit_free_mesh(&m);
+  pmmg_medit_free_sol(&met);
+  pmmg_medit_free_sol(&phys);
+}
+
+int main(int argc, char **argv) {
+  const char *fixtures = argc > 1 ? argv[1] : "tests/golden";
   host_only_checks();
   const int ndev = pmmg_hip_device_count();
   pmmg_hip_ctx *ctx = pmmg_hip_create(0, 0);
@@ -259,6 +344,7 @@ int main(void) {
   } else {
     CHECK(ctx != NULL, "pmmg_hip_create(0) failed");
     if (ctx) device_checks(ctx);
+    if (ctx) fixture_checks(ctx, fixtures);
     pmmg_hip_destroy(ctx);
     printf("test_c_abi: host-only and device checks %s\n", failures ? "FAILED" : "passed");
   }

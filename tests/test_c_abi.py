@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _run_c_test():
     exe = build.build_c_test()
-    return subprocess.run([exe], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
+    return subprocess.run([exe, os.path.join(ROOT, "tests", "golden")], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
 
 
 def test_c_program_host_part():
@@ -35,6 +35,7 @@ def test_c_program_on_the_gpu():
     print(p.stdout)
     assert p.returncode == 0, p.stdout
     assert "host-only and device checks passed" in p.stdout
+    assert "reference cube fixture (12 tetra, 24 points) transferred, 0 wrong values" in p.stdout
 
 
 @pytest.mark.skipif(shutil.which("cmake") is None, reason="cmake not installed")

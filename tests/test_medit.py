@@ -1,0 +1,77 @@
+"""The C Medit reader of the host library (csrc/pmmg_medit.c: the inputs of
+PMMG_loadMesh_centralized / PMMG_loadAllSols_centralized, reference
+src/inout_pmmg.c:488, :748) against the numpy reader, on the reference's own
+libexamples fixtures (tests/golden/cube*.{mesh,sol}) and on edge cases."""
+import os
+
+import numpy as np
+import pytest
+
+from parmmg_amd import medit
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def test_cube_mesh_matches_numpy_reader():
+    path = os.path.join(GOLD, "cube.mesh")
+    a, b = medit.read_mesh_c(path), medit.read_mesh(path)
+    np.testing.assert_array_equal(a["xyz"], b["xyz"])
+    np.testing.assert_array_equal(a["vref"], b["vref"])
+    np.testing.assert_array_equal(a["tetv"], b["tetv"])
+    np.testing.assert_array_equal(a["triv"], b["triv"])
+    assert a["tetv"].shape == (12, 4) and a["triv"].shape[0] == 20
+
+
+@pytest.mark.parametrize("name", ["cube-met.sol", "cube-solphys.sol"])
+def test_cube_sols_match_numpy_reader(name):
+    path = os.path.join(GOLD, name)
+    a, b = medit.read_sol_c(path), medit.read_sol(path)
+    assert len(a) == len(b)
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)
+
+
+def test_tensor_order_swap(tmp_path):
+    """Medit m11 m12 m22 m13 m23 m33 -> MMG5 m11 m12 m13 m22 m23 m33."""
+    p = tmp_path / "t.sol"
+    p.write_text("MeshVersionFormatted 2\nDimension 3\nSolAtVertices\n2\n2 1 3\n"
+                 "7 11 12 22 13 23 33\n8 1 2 3 4 5 6\nEnd\n")
+    s, v = medit.read_sol_c(str(p))
+    np.testing.assert_array_equal(s[:, 0], [7, 8])
+    np.testing.assert_array_equal(v[0], [11, 12, 13, 22, 23, 33])
+    np.testing.assert_array_equal(v[1], [1, 2, 4, 3, 5, 6])
+
+
+def test_comments_and_skipped_blocks(tmp_path):
+    p = tmp_path / "m.mesh"
+    p.write_text("# header comment\nMeshVersionFormatted 2\nDimension\n3\nVertices\n4\n"
+                 "0 0 0 1\n1 0 0 1 # trailing\n0 1 0 2\n0 0 1 3\nEdges\n1\n1 2 0\nCorners\n2\n1 2\n"
+                 "Tetrahedra\n1\n1 2 3 4 7\nEnd\n")
+    m = medit.read_mesh_c(str(p))
+    assert m["xyz"].shape == (4, 3) and m["tetv"].tolist() == [[1, 2, 3, 4]] and m["tref"].tolist() == [7]
+    np.testing.assert_array_equal(m["vref"], [1, 1, 2, 3])
+    assert m["triv"].shape == (0, 3)
+
+
+@pytest.mark.parametrize("text,msg", [
+    ("MeshVersionFormatted 2\nDimension 3\nVertices\n2\n0 0 0 0\n", "truncated"),
+    ("MeshVersionFormatted 2\nDimension 2\nVertices\n1\n0 0 0\n", "dimension"),
+    ("MeshVersionFormatted 2\nDimension 3\nVertices\n1\n0 0 0 0\nTetrahedra\n1\n1 2 3 4 0\nEnd\n", "out of range"),
+    ("MeshVersionFormatted 2\nDimension 3\nFancyBlock\n1\n1 2 3\n", "unknown block"),
+])
+def test_malformed_mesh_rejected(tmp_path, text, msg):
+    p = tmp_path / "bad.mesh"
+    p.write_text(text)
+    with pytest.raises(ValueError, match=msg):
+        medit.read_mesh_c(str(p))
+
+
+def test_missing_and_binary_files_rejected(tmp_path):
+    with pytest.raises(ValueError, match="cannot open"):
+        medit.read_mesh_c(str(tmp_path / "none.mesh"))
+    with pytest.raises(ValueError, match="binary"):
+        medit.read_mesh_c(str(tmp_path / "x.meshb"))
+    p = tmp_path / "nosol.sol"
+    p.write_text("MeshVersionFormatted 2\nDimension 3\nEnd\n")
+    with pytest.raises(ValueError, match="no SolAtVertices"):
+        medit.read_sol_c(str(p))

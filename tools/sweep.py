@@ -18,6 +18,32 @@ from parmmg_amd import configs, synth  # noqa: E402
 from parmmg_amd.transfer import TransferContext, pack_tet8  # noqa: E402
 
 
+def query_perm(xyz: np.ndarray, n: int, spec: str) -> np.ndarray:
+    """Test-only renumbering of the new points (the module keeps input order
+    when it is coherent, so this changes the order waves are dispatched in):
+    zslabZ  lattice points by (z // Z, y, z % Z, x)   (cube lattices)
+    rodsB   runs of 64 consecutive points sorted by the B-bit-per-axis Morton
+            code of each run's first point"""
+    lo, hi = xyz.min(0), xyz.max(0)
+    if spec.startswith("zslab"):
+        Z = int(spec[5:])
+        q = np.rint((xyz - lo) / (hi - lo) * n).astype(np.int64)
+        key = (((q[:, 2] // Z) * (n + 1) + q[:, 1]) * Z + q[:, 2] % Z) * (n + 1) + q[:, 0]
+        return np.argsort(key, kind="stable")
+    if spec.startswith("rods"):
+        B = int(spec[4:])
+        first = xyz[::64]
+        q = np.minimum(((first - lo) / (hi - lo) * (1 << B)).astype(np.int64), (1 << B) - 1)
+        key = np.zeros(q.shape[0], np.int64)
+        for b in range(B):
+            for d in range(3):
+                key |= ((q[:, d] >> b) & 1) << (3 * b + d)
+        rods = np.argsort(key, kind="stable")
+        idx = (rods[:, None] * 64 + np.arange(64)[None, :]).ravel()
+        return idx[idx < xyz.shape[0]]
+    raise ValueError(spec)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="cfg4")
@@ -42,7 +68,7 @@ def main():
             k, v = item.split("=")
             if k.lower() == "sort":  # context option: 1 Morton bins, 0 input order
                 sort = v == "1"
-            elif k.lower() == "sol":  # measurement only: none / met / all solution slots
+            elif k.lower() in ("sol", "perm"):  # measurement only: solution slots / query renumbering
                 pass
             else:
                 os.environ["PMMG_HIP_" + k.upper()] = v
@@ -58,6 +84,13 @@ def main():
              el=base.empty((new.np,), np.int32), hit=base.empty((new.np,), np.int8))
     cols = ["ms_total", "ms_prepare", "ms_sort", "ms_vol_locate", "ms_vol", "ms_bdy", "ms_fallback"]
     res = {v: {c: [] for c in cols + ["steps_pp", "iters", "exact"]} for v in variants}
+    qperm = {}
+    for spec in variants:
+        pspec = dict(item.split("=") for item in spec.split(",") if item).get("perm")
+        if pspec:
+            perm = query_perm(new.xyz, w.n_new, pspec)
+            qperm[spec] = (base.upload(np.ascontiguousarray(new.xyz[perm])), base.upload(np.ascontiguousarray(pc[perm])))
+
     def sols(spec):
         which = dict(item.split("=") for item in spec.split(",") if item).get("sol", "all")
         return {"none": (None, []), "met": (d["met"], []), "all": (d["met"], d["f"])}[which]
@@ -67,7 +100,8 @@ def main():
             for s in range(args.steps + 1):
                 ctx.set_background_tet8(d["xyz"], d["tet8"], d["triv"], d["adjt"], w.hausd)
                 ctx.set_solutions(*sols(spec))
-                ctx.locate_interp(d["q"], d["pc"], d["mo"], d["fo"], d["el"], d["hit"], sync=False)
+                q, qpc = qperm.get(spec, (d["q"], d["pc"]))
+                ctx.locate_interp(q, qpc, d["mo"], d["fo"], d["el"], d["hit"], sync=False)
                 st = ctx.sync()
                 if s == 0:
                     continue  # first call of a round: warm-up
