@@ -223,6 +223,19 @@ int pmmg_hip_tetra_qual(pmmg_hip_ctx *ctx, int np, const double *xyz, int ne,
                         const int *tetv, int met_size, const double *met,
                         double *qual, double *minqual);
 
+/* Solutions as packed per-vertex records: rec[RS*np], vertex v's record at
+ * rec + RS*(v-1) = [metric (met_size) | field 0 | field 1 | ...] with
+ * RS = (met_size + sum field_size) rounded up to even.  The module's
+ * preferred HBM layout (one 128-byte line per vertex for up to 16 doubles:
+ * one gather per vertex instead of one per solution); a shim builds it in the
+ * pass that packs MMG5_Point.c.  Supported: at most 16 doubles, no tensor
+ * across doubles 8/9 (the order metric, scalar, vector, tensor of BASELINE's
+ * aniso configs is), the compiled slot layouts; otherwise 0 is returned and
+ * pmmg_hip_set_solutions takes the arrays.  Device records: 16-byte aligned.
+ * Returns 1/0. */
+int pmmg_hip_set_solutions_packed(pmmg_hip_ctx *ctx, int met_size, int nfield,
+                                  const int *field_size, const double *rec, int where);
+
 /* Load-balancing weights from the interpolated metric (SURVEY.md §8(f)
  * rank 2, the second consumer after PMMG_tetraQual), device arrays, 1-based
  * vertex ids, synchronous.

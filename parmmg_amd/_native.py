@@ -50,6 +50,7 @@ HIP_API = {
     "pmmg_hip_build_adjacency": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "pmmg_hip_build_boundary": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                                         c_void_p, c_void_p, c_void_p]),
+    "pmmg_hip_set_solutions_packed": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int]),
     "pmmg_hip_compute_wgt_mesh": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
                                           c_void_p, c_int, c_void_p]),
     "pmmg_hip_compute_wgt_faces": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p,

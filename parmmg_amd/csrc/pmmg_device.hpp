@@ -47,15 +47,17 @@ __device__ __forceinline__ int4 adja_row(const Bg &bg, int k) { return bg.adja[(
 // in + code*(v-1)): code 1 = scalar, 3 = vector (both P1 iso interpolation),
 // 6 = symmetric tensor (inverse-tensor interpolation)
 struct Slot {
-  const double *in;
-  double *out;
+  const double *in; // row of vertex v at in + istride*(v-1)
+  double *out;      // row of point ip at out + code*(ip-1)
   int code;
+  int istride; // doubles between input rows: code (one array per solution) or the record stride (packed)
 };
 
 struct Slots {
   Slot s[kMaxSlot];
   int n;
-  int has_met; // slot 0 is the metric (boundary points treat it differently)
+  int has_met;        // slot 0 is the metric (boundary points treat it differently)
+  const double *rec;  // packed per-vertex records (pmmg_hip_set_solutions_packed), else null
 };
 
 // ------------------------------------------------------------ small helpers
@@ -334,12 +336,13 @@ __device__ __forceinline__ void store6(double *p, const double *m) {
 // PMMG_interp{3,4}bar_iso (interpmesh_pmmg.c:125-165, 206-246): the row
 // value acc = sum_i phi_i * row_i (accumulated from 0.0 in vertex order)
 template <int NV, int SZ>
-__device__ __forceinline__ void interp_iso_row(const double *in, const int *v, const double *phi, double *acc) {
+__device__ __forceinline__ void interp_iso_row(const double *in, int stride, const int *v, const double *phi,
+                                               double *acc) {
   double row[NV][SZ];
 #pragma unroll
   for (int i = 0; i < NV; i++)
 #pragma unroll
-    for (int j = 0; j < SZ; j++) row[i][j] = in[(size_t)SZ * (v[i] - 1) + j];
+    for (int j = 0; j < SZ; j++) row[i][j] = in[(size_t)stride * (v[i] - 1) + j];
 #pragma unroll
   for (int j = 0; j < SZ; j++) acc[j] = 0.0;
 #pragma unroll
@@ -352,10 +355,11 @@ __device__ __forceinline__ void interp_iso_row(const double *in, const int *v, c
 // M = invmat( sum_i phi_i invmat(M_i) ); false (row left untouched by the
 // reference) if any inversion fails
 template <int NV>
-__device__ __forceinline__ bool interp_ani_row(const double *in, const int *v, const double *phi, double *r) {
+__device__ __forceinline__ bool interp_ani_row(const double *in, int stride, const int *v, const double *phi,
+                                               double *r) {
   double m[NV][6];
 #pragma unroll
-  for (int i = 0; i < NV; i++) load6(in + (size_t)6 * (v[i] - 1), m[i]);
+  for (int i = 0; i < NV; i++) load6(in + (size_t)stride * (v[i] - 1), m[i]);
   double mint[6], mi[6];
   bool ok = true;
 #pragma unroll
@@ -370,9 +374,9 @@ __device__ __forceinline__ bool interp_ani_row(const double *in, const int *v, c
 // the row of one slot: returns false when the reference leaves it untouched
 template <int NV, int CODE>
 __device__ __forceinline__ bool interp_row(const Slot &sl, const int *v, const double *phi, double *r) {
-  if constexpr (CODE == 6) return interp_ani_row<NV>(sl.in, v, phi, r);
+  if constexpr (CODE == 6) return interp_ani_row<NV>(sl.in, sl.istride, v, phi, r);
   else {
-    interp_iso_row<NV, CODE>(sl.in, v, phi, r);
+    interp_iso_row<NV, CODE>(sl.in, sl.istride, v, phi, r);
     return true;
   }
 }
@@ -404,9 +408,9 @@ __device__ __forceinline__ void interp_edge(const Slot &sl, int ip, const int *v
   const double f0 = sel3d(phi[0], phi[1], phi[2], i0), f1 = sel3d(phi[0], phi[1], phi[2], i1);
   if (sl.code == 6) {
     double m[6], mi0[6], mi1[6], mint[6], r[6];
-    load6(sl.in + (size_t)6 * (v0 - 1), m);
+    load6(sl.in + (size_t)sl.istride * (v0 - 1), m);
     bool ok = invmat(m, mi0);
-    load6(sl.in + (size_t)6 * (v1 - 1), m);
+    load6(sl.in + (size_t)sl.istride * (v1 - 1), m);
     ok = invmat(m, mi1) && ok;
 #pragma unroll
     for (int s = 0; s < 6; s++) mint[s] = f0 * mi0[s] + f1 * mi1[s];
@@ -416,13 +420,13 @@ __device__ __forceinline__ void interp_edge(const Slot &sl, int ip, const int *v
     // fields always go through interp3bar)
     for (int j = 0; j < sl.code; j++)
       sl.out[(size_t)sl.code * (ip - 1) + j] =
-          f0 * sl.in[(size_t)sl.code * (v0 - 1) + j] + f1 * sl.in[(size_t)sl.code * (v1 - 1) + j];
+          f0 * sl.in[(size_t)sl.istride * (v0 - 1) + j] + f1 * sl.in[(size_t)sl.istride * (v1 - 1) + j];
   }
 }
 
 __device__ __forceinline__ void copy_row(const Slot &sl, int ip, int vsrc) {
   double *out = sl.out + (size_t)sl.code * (ip - 1);
-  const double *in = sl.in + (size_t)sl.code * (vsrc - 1);
+  const double *in = sl.in + (size_t)sl.istride * (vsrc - 1);
   if (sl.code == 6) {
     double m[6];
     load6(in, m);

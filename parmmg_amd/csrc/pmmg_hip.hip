@@ -52,10 +52,17 @@ typedef void (*VolFn)(Bg, const Frame *, const unsigned long long *, int, const 
 
 struct LayoutEntry {
   int c[6];
-  VolFn fn;
+  VolFn fn;        // one array per solution (the reference's layout)
+  VolFn fn_packed; // packed per-vertex records (null: layout not packable)
 };
 
-#define PMMG_LAYOUT(a, b, c, d, e, f) {{a, b, c, d, e, f}, k_vol<a, b, c, d, e, f>}
+template <int A, int B, int C, int D, int E, int F>
+constexpr VolFn packed_fn() {
+  if constexpr (PackedLayout<A, B, C, D, E, F>::valid()) return k_vol<true, A, B, C, D, E, F>;
+  else return nullptr;
+}
+
+#define PMMG_LAYOUT(a, b, c, d, e, f) {{a, b, c, d, e, f}, k_vol<false, a, b, c, d, e, f>, packed_fn<a, b, c, d, e, f>()}
 // common slot layouts (metric first): aniso metric + scalar/vector/tensor
 // (BASELINE cfg3/cfg4, libexamples cube-solphys.sol), iso metric + scalars
 // (cfg2, cfg5), metric only; anything else runs the runtime-layout variant
@@ -73,9 +80,18 @@ VolFn pick_layout(const Slots &S) {
     if (n != S.n) continue;
     bool ok = true;
     for (int j = 0; j < n; j++) ok = ok && (S.s[j].code == e.c[j]);
-    if (ok) return e.fn;
+    if (ok) return S.rec ? e.fn_packed : e.fn;
   }
-  return k_vol<-1, 0, 0, 0, 0, 0>;
+  return S.rec ? nullptr : k_vol<false, -1, 0, 0, 0, 0, 0>;
+}
+
+// the slot layouts the packed-record interpolation is compiled for
+bool packed_supported(int met_size, int nfield, const int *fsize) {
+  Slots S{};
+  S.rec = reinterpret_cast<const double *>(16);
+  if (met_size) S.s[S.n++].code = met_size;
+  for (int j = 0; j < nfield && S.n < kMaxSlot; j++) S.s[S.n++].code = fsize[j];
+  return pick_layout(S) != nullptr;
 }
 
 // zero n ints when the device's order flag equals `want` (-1: always)
@@ -110,8 +126,10 @@ struct pmmg_hip_ctx {
   std::vector<int> fsize;
   std::vector<const double *> fin;
   const double *met = nullptr;
+  const double *rec = nullptr; // packed per-vertex solution records (set_solutions_packed), else null
+  int rstride = 0;             // their stride in doubles
   // owned copies for PMMG_HIP_HOST inputs
-  DevBuf o_xyz, o_tetv, o_adja, o_triv, o_adjt, o_met;
+  DevBuf o_xyz, o_tetv, o_adja, o_triv, o_adjt, o_met, o_rec;
   std::vector<DevBuf> o_f;
   // work buffers
   DevBuf frame, stats, grid, sgrid, cnt, off, binrank, order_v, order_b, cont, xq;
@@ -677,6 +695,8 @@ int pmmg_hip_set_solutions(pmmg_hip_ctx *c, int met_size, const double *met, int
   c->nfield = nfield;
   c->fsize.assign(field_size, field_size + nfield);
   c->fin.resize(nfield);
+  c->rec = nullptr;
+  c->rstride = 0;
   if (where == PMMG_HIP_DEVICE) {
     c->met = met;
     for (int j = 0; j < nfield; j++) c->fin[j] = fields[j];
@@ -692,6 +712,53 @@ int pmmg_hip_set_solutions(pmmg_hip_ctx *c, int met_size, const double *met, int
     if (!upload(c, c->o_f[j], fields[j], sizeof(double) * field_size[j] * np, c->cstream)) return 0;
     c->fin[j] = (const double *)c->o_f[j].p;
   }
+  HIPCK(c, hipStreamSynchronize(c->cstream));
+  return 1;
+}
+
+int pmmg_hip_set_solutions_packed(pmmg_hip_ctx *c, int met_size, int nfield, const int *field_size,
+                                  const double *rec, int where) {
+  if (!c) return 0;
+  HIPCK(c, hipSetDevice(c->device));
+  if ((met_size != 0 && met_size != 1 && met_size != 6) || nfield < 0 || nfield + (met_size ? 1 : 0) > kMaxSlot ||
+      (nfield > 0 && !field_size) || !rec) {
+    set_err(c, "set_solutions_packed: invalid arguments (met_size=%d nfield=%d)", met_size, nfield);
+    return 0;
+  }
+  int K = met_size;
+  for (int j = 0; j < nfield; j++) {
+    if (!(field_size[j] == 1 || field_size[j] == 3 || field_size[j] == 6)) {
+      set_err(c, "set_solutions_packed: field %d has size %d (expected 1, 3 or 6)", j, field_size[j]);
+      return 0;
+    }
+    K += field_size[j];
+  }
+  if (K == 0 || !packed_supported(met_size, nfield, field_size)) {
+    set_err(c, "set_solutions_packed: slot layout not supported by the packed records (at most 16 doubles, a "
+               "tensor not across doubles 8 / 9, a compiled layout); use pmmg_hip_set_solutions");
+    return 0;
+  }
+  if (where == PMMG_HIP_DEVICE && ((uintptr_t)rec & 15)) {
+    set_err(c, "set_solutions_packed: device records must be 16-byte aligned");
+    return 0;
+  }
+  const size_t np = (size_t)c->bg.np;
+  if (np == 0) {
+    set_err(c, "set_solutions_packed: call pmmg_hip_set_background first");
+    return 0;
+  }
+  c->met_size = met_size;
+  c->nfield = nfield;
+  c->fsize.assign(field_size, field_size + nfield);
+  c->fin.assign(nfield, nullptr);
+  c->met = nullptr;
+  c->rstride = (K + 1) & ~1;
+  if (where == PMMG_HIP_DEVICE) {
+    c->rec = rec;
+    return 1;
+  }
+  if (!upload(c, c->o_rec, rec, sizeof(double) * c->rstride * np, c->cstream)) return 0;
+  c->rec = (const double *)c->o_rec.p;
   HIPCK(c, hipStreamSynchronize(c->cstream));
   return 1;
 }
@@ -760,14 +827,28 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
       set_err(c, "locate_interp: met_out is NULL");
       return 0;
     }
-    S.s[S.n++] = Slot{c->met, met_out, c->met_size};
+    S.s[S.n++] = Slot{c->met, met_out, c->met_size, c->met_size};
   }
   for (int j = 0; j < c->nfield; j++) {
     if (!fields_out || !fields_out[j]) {
       set_err(c, "locate_interp: fields_out[%d] is NULL", j);
       return 0;
     }
-    S.s[S.n++] = Slot{c->fin[j], fields_out[j], c->fsize[j]};
+    S.s[S.n++] = Slot{c->fin[j], fields_out[j], c->fsize[j], c->fsize[j]};
+  }
+  if (c->rec) { // packed records: every slot reads its columns of the record
+    S.rec = c->rec;
+    int off = 0;
+    for (int j = 0; j < S.n; j++) {
+      S.s[j].in = c->rec + off;
+      S.s[j].istride = c->rstride;
+      off += S.s[j].code;
+    }
+  }
+  const VolFn vol_fn = pick_layout(S);
+  if (!vol_fn) {
+    set_err(c, "locate_interp: no packed-record kernel for this slot layout");
+    return 0;
   }
   const int g = grid_dim(bg.ne, c->tpc, 1024);
   const int gs = bg.nt > 0 ? grid_dim(bg.nt, 2, 512) : 1;
@@ -862,7 +943,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   HIPCK(c, hipEventRecord(c->ev[EV_VOL0], s));
   // ---- volume (main stream): walk + exact test + interpolation in one
   // kernel, then the exact continuation of the few queries it did not settle
-  hipLaunchKernelGGL(pick_layout(S), dim3((np_new + 63) / 64), dim3(64), 0, s, bg, (const Frame *)fr,
+  hipLaunchKernelGGL(vol_fn, dim3((np_new + 63) / 64), dim3(64), 0, s, bg, (const Frame *)fr,
                      (const unsigned long long *)grid, g, xyz_new, pclass, (const int *)order_v, np_new,
                      (ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->filter_steps);
   HIPCK(c, hipEventRecord(c->ev[EV_WALK], s));

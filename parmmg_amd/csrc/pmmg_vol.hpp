@@ -388,14 +388,14 @@ struct VolShared {
   BlockStats bs;
   union {
     float slots[12 * 64]; // walk: [slot*3 + dim][lane]
-    double img[6 * 64];   // interpolation: 64 rows of up to 6 doubles
+    double img[8 * 64];   // interpolation: 64 rows of up to 6 doubles, or 64 x 8 doubles of packed records
   } u;
 };
 
 // rows of one vertex of the wave's 64 queries (myv = this lane's vertex id)
 // into img (row r = query r), C doubles per row; returns this lane's row
 template <int C>
-__device__ __forceinline__ void coop_vertex_rows(const double *in, int myv, double *img, double *row) {
+__device__ __forceinline__ void coop_vertex_rows(const double *in, int stride, int myv, double *img, double *row) {
   const int lane = __lane_id();
   if constexpr (C == 6) {
     double2 b[3];
@@ -403,7 +403,7 @@ __device__ __forceinline__ void coop_vertex_rows(const double *in, int myv, doub
     for (int t = 0; t < 3; t++) {
       const int p = 64 * t + lane, r = p / 3, k = p - 3 * r;
       const int v = __shfl(myv, r);
-      b[t] = *reinterpret_cast<const double2 *>(in + (size_t)6 * (v - 1) + 2 * k);
+      b[t] = *reinterpret_cast<const double2 *>(in + (size_t)stride * (v - 1) + 2 * k);
     }
 #pragma unroll
     for (int t = 0; t < 3; t++) reinterpret_cast<double2 *>(img)[64 * t + lane] = b[t];
@@ -413,7 +413,7 @@ __device__ __forceinline__ void coop_vertex_rows(const double *in, int myv, doub
     for (int t = 0; t < 3; t++) {
       const int p = 64 * t + lane, r = p / 3, k = p - 3 * r;
       const int v = __shfl(myv, r);
-      b[t] = in[(size_t)3 * (v - 1) + k];
+      b[t] = in[(size_t)stride * (v - 1) + k];
     }
 #pragma unroll
     for (int t = 0; t < 3; t++) img[64 * t + lane] = b[t];
@@ -437,7 +437,7 @@ __device__ __forceinline__ void vol_slot(const Slot &sl, bool act, const int4 &v
       double mint[6], m[6], mi[6];
 #pragma unroll
       for (int i = 0; i < 4; i++) {
-        coop_vertex_rows<6>(sl.in, sel4(v, i), img, m);
+        coop_vertex_rows<6>(sl.in, sl.istride, sel4(v, i), img, m);
         ok = invmat(m, mi) && ok;
 #pragma unroll
         for (int q = 0; q < 6; q++) mint[q] = (i == 0) ? phi[0] * mi[q] : mint[q] + phi[i] * mi[q];
@@ -447,13 +447,13 @@ __device__ __forceinline__ void vol_slot(const Slot &sl, bool act, const int4 &v
       double m[3];
 #pragma unroll
       for (int i = 0; i < 4; i++) {
-        coop_vertex_rows<3>(sl.in, sel4(v, i), img, m);
+        coop_vertex_rows<3>(sl.in, sl.istride, sel4(v, i), img, m);
 #pragma unroll
         for (int q = 0; q < 3; q++) r[q] = (i == 0) ? 0.0 + phi[0] * m[q] : r[q] + phi[i] * m[q];
       }
     } else {
       const int vv[4] = {v.x, v.y, v.z, v.w};
-      interp_iso_row<4, 1>(sl.in, vv, phi, r);
+      interp_iso_row<4, 1>(sl.in, sl.istride, vv, phi, r);
     }
     if (coalesced) {
       wave_store_rows<C>(sl.out + (size_t)C * w0, r, __ballot(ok), img);
@@ -467,7 +467,148 @@ __device__ __forceinline__ void vol_slot(const Slot &sl, bool act, const int4 &v
   }
 }
 
+// ---------------------------------------------------------------- packed records
+//
+// With packed per-vertex records (pmmg_hip_set_solutions_packed: the slots'
+// rows back to back, [slot 0 | slot 1 | ...], RS doubles per vertex) a
+// vertex's whole solution is one 128-byte line for K <= 16 doubles: the
+// interpolation gathers, per vertex of the wave's 64 queries, 64 records in
+// one or two passes of 8 doubles (64 B) per record — the 64 lanes of a load
+// instruction cover 16 records — into a 4 KiB LDS image; each lane then takes
+// its doubles of that pass and accumulates every slot component living in it
+// (an iso slot component by component, a tensor slot whole: it must not
+// straddle the 8-double pass boundary).  One slot-independent gather per
+// vertex instead of one per slot.
 template <int C0, int C1, int C2, int C3, int C4, int C5>
+struct PackedLayout {
+  static constexpr int c[6] = {C0 > 0 ? C0 : 0, C1, C2, C3, C4, C5};
+  static constexpr int K = c[0] + c[1] + c[2] + c[3] + c[4] + c[5];
+  static constexpr int RS = (K + 1) & ~1;              // record stride (doubles)
+  static constexpr int NPASS = RS <= 8 ? 1 : 2;        // passes of at most 8 doubles per record
+  static constexpr int off(int s) { return s == 0 ? 0 : off(s - 1) + c[s - 1]; }
+  static constexpr bool valid() {                      // tensors inside one pass, K <= 16
+    if (C0 < 0 || RS > 16) return false;
+    for (int s = 0; s < 6; s++)
+      if (c[s] == 6 && NPASS == 2 && off(s) < 8 && off(s) + 6 > 8) return false;
+    return true;
+  }
+};
+
+template <int C>
+struct SlotAcc {
+  double v[C > 0 ? C : 1];
+  bool ok = true;
+  // component q of vertex i's row = x (iso) — PMMG_interp4bar_iso order
+  __device__ __forceinline__ void iso(int i, double ph, int q, double x) {
+    v[q] = (i == 0) ? 0.0 + ph * x : v[q] + ph * x;
+  }
+  // vertex i's tensor row m — PMMG_interp4bar_ani: mint = sum_i phi_i invmat(M_i)
+  __device__ __forceinline__ void ani(int i, double ph, const double *m) {
+    double mi[6];
+    ok = invmat(m, mi) && ok;
+#pragma unroll
+    for (int q = 0; q < 6; q++) v[q] = (i == 0) ? ph * mi[q] : v[q] + ph * mi[q];
+  }
+};
+
+// slot s's components that live in pass `pass` (record doubles [8 pass, 8 pass + 8))
+template <class L, int S, int C>
+__device__ __forceinline__ void packed_take(SlotAcc<C> &a, int pass, int i, double ph, const double *mine) {
+  if constexpr (C > 0) {
+    constexpr int o = L::off(S);
+    const int lo = 8 * pass;
+    if constexpr (C == 6) {
+      if (o / 8 == pass || L::NPASS == 1) {
+        double m[6];
+#pragma unroll
+        for (int q = 0; q < 6; q++) m[q] = mine[o - lo + q];
+        a.ani(i, ph, m);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < C; q++)
+        if ((o + q) / 8 == pass || L::NPASS == 1) a.iso(i, ph, q, mine[o + q - lo]);
+    }
+  }
+}
+
+template <int C>
+__device__ __forceinline__ void packed_store(const Slot &sl, SlotAcc<C> &a, double *img, bool coalesced, size_t w0,
+                                             int ip) {
+  if constexpr (C > 0) {
+    double r[C];
+    bool ok = a.ok;
+    if constexpr (C == 6) ok = invmat(a.v, r) && ok;
+    else
+#pragma unroll
+      for (int q = 0; q < C; q++) r[q] = a.v[q];
+    if (coalesced) {
+      wave_store_rows<C>(sl.out + (size_t)C * w0, r, __ballot(ok), img);
+    } else if (ok) {
+      double *o = sl.out + (size_t)C * (ip - 1);
+      if constexpr (C == 6) store6(o, r);
+      else
+#pragma unroll
+        for (int q = 0; q < C; q++) nt_store(o + q, r[q]);
+    }
+  }
+}
+
+template <int C0, int C1, int C2, int C3, int C4, int C5>
+__device__ __forceinline__ void vol_interp_packed(const Slots &S, bool acc, const VolLoc &loc, double *img,
+                                                  bool coalesced, size_t w0, int ip) {
+  using L = PackedLayout<C0, C1, C2, C3, C4, C5>;
+  constexpr int PW = L::NPASS == 1 ? L::RS : 8; // doubles per record and pass
+  constexpr int PR = PW / 2;                     // 16-byte pieces per record and pass
+  const int lane = __lane_id();
+  SlotAcc<C0> a0;
+  SlotAcc<C1> a1;
+  SlotAcc<C2> a2;
+  SlotAcc<C3> a3;
+  SlotAcc<C4> a4;
+  SlotAcc<C5> a5;
+  if (!acc) { // idle lanes accumulate a valid row, never stored
+    a0.ok = a1.ok = a2.ok = a3.ok = a4.ok = a5.ok = false;
+  }
+  const double2 *rec = reinterpret_cast<const double2 *>(S.rec);
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int myv = sel4(loc.v, i);
+    const double ph = loc.phi[i];
+#pragma unroll
+    for (int pass = 0; pass < L::NPASS; pass++) {
+      // piece p = 64t + lane of the image: record p / PR, piece p % PR
+      double2 b[PR];
+#pragma unroll
+      for (int t = 0; t < PR; t++) {
+        const int p = 64 * t + lane, r = p / PR, k = p - PR * r;
+        const int v = __shfl(myv, r);
+        b[t] = rec[(size_t)(L::RS / 2) * (v - 1) + 4 * pass + k];
+      }
+#pragma unroll
+      for (int t = 0; t < PR; t++) reinterpret_cast<double2 *>(img)[64 * t + lane] = b[t];
+      wait_lgkm();
+      __builtin_amdgcn_wave_barrier();
+      const double *mine = img + PW * lane;
+      packed_take<L, 0>(a0, pass, i, ph, mine);
+      packed_take<L, 1>(a1, pass, i, ph, mine);
+      packed_take<L, 2>(a2, pass, i, ph, mine);
+      packed_take<L, 3>(a3, pass, i, ph, mine);
+      packed_take<L, 4>(a4, pass, i, ph, mine);
+      packed_take<L, 5>(a5, pass, i, ph, mine);
+      wait_lgkm();
+      __builtin_amdgcn_wave_barrier(); // every lane has read its record: the image is free again
+    }
+  }
+  packed_store<C0>(S.s[0], a0, img, coalesced, w0, ip);
+  packed_store<C1>(S.s[1], a1, img, coalesced, w0, ip);
+  packed_store<C2>(S.s[2], a2, img, coalesced, w0, ip);
+  packed_store<C3>(S.s[3], a3, img, coalesced, w0, ip);
+  packed_store<C4>(S.s[4], a4, img, coalesced, w0, ip);
+  packed_store<C5>(S.s[5], a5, img, coalesced, w0, ip);
+}
+
+template <bool PK, int C0, int C1, int C2, int C3, int C4, int C5>
 __global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsigned long long *grid, int g,
                                             const double *qxyz, const uint8_t *pclass, const int *order, int np,
                                             ContEntry *cont, DevStats *st, Slots S, int *elem_out, int8_t *hit_out,
@@ -552,7 +693,9 @@ __global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsign
     double *img = sh.u.img;
     __builtin_amdgcn_wave_barrier(); // the walk's slots are dead: the buffer becomes the gather image
     const size_t w0 = (size_t)(i - __lane_id());
-    if constexpr (C0 < 0) {
+    if constexpr (PK) {
+      vol_interp_packed<C0, C1, C2, C3, C4, C5>(S, acc, loc, img, !sorted, w0, ip);
+    } else if constexpr (C0 < 0) {
       if (acc) {
         const int vv[4] = {loc.v.x, loc.v.y, loc.v.z, loc.v.w};
         for (int s2 = 0; s2 < S.n; s2++) interp_dyn<4>(S.s[s2], ip, vv, loc.phi);

@@ -77,6 +77,21 @@ def pack_tet8(tetv: np.ndarray, adja: np.ndarray) -> np.ndarray:
     return np.ascontiguousarray(np.hstack([np.asarray(tetv, np.int32), np.asarray(adja, np.int32)]))
 
 
+def pack_solutions(met, fields) -> np.ndarray:
+    """Packed per-vertex solution records [metric | field 0 | ...], stride
+    rounded up to an even number of doubles (include/parmmg_hip.h,
+    pmmg_hip_set_solutions_packed)."""
+    cols = ([] if met is None else [np.asarray(met, np.float64)]) + [np.asarray(f, np.float64) for f in fields]
+    k = sum(c.shape[1] for c in cols)
+    rs = (k + 1) & ~1
+    rec = np.zeros((cols[0].shape[0], rs), np.float64)
+    o = 0
+    for c in cols:
+        rec[:, o:o + c.shape[1]] = c
+        o += c.shape[1]
+    return rec
+
+
 class TransferContext:
     """One ``pmmg_hip_ctx`` on a HIP device."""
 
@@ -189,6 +204,15 @@ class TransferContext:
         self._sol_keep = [met, fields, sizes, ptrs]
         self._ck(self.lib.pmmg_hip_set_solutions(self.h, msize, _p(met), len(fields), sizes, ptrs, where),
                  "set_solutions")
+
+    def set_solutions_packed(self, rec, met_size: int, field_sizes) -> None:
+        """Packed per-vertex records (pack_solutions) in host or device memory
+        (pmmg_hip_set_solutions_packed)."""
+        where = DEVICE if _is_dev(rec) else HOST
+        sizes = (ctypes.c_int * max(1, len(field_sizes)))(*[int(x) for x in field_sizes])
+        self._sol_keep = [rec, sizes]
+        self._ck(self.lib.pmmg_hip_set_solutions_packed(self.h, int(met_size), len(field_sizes), sizes, _p(rec),
+                                                        where), "set_solutions_packed")
 
     def locate_interp(self, xyz_new, pclass, met_out, fields_out, elem_out=None, hit_out=None,
                       sync: bool = True) -> HipStats | None:

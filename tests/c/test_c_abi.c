@@ -278,6 +278,16 @@ static void fixture_checks(pmmg_hip_ctx *ctx, const char *dir) {
     }
   memcpy(xq + 3 * m.ne, m.xyz, sizeof(double) * 3 * m.np);
   for (int i = 0; i < m.np; i++) tag[m.ne + i] = PMMG_TAG_BDY;
+  /* new tetra (the reference visits the new points through them): centroid
+   * k with faces of background tetra k, so every point appears */
+  int *ntet = malloc(sizeof(int) * 8 * m.ne);
+  for (int k = 0; k < m.ne; k++) {
+    ntet[8 * k] = ntet[8 * k + 4] = k + 1;
+    for (int i = 0; i < 3; i++) {
+      ntet[8 * k + 1 + i] = m.ne + m.tetv[4 * k + i];
+      ntet[8 * k + 5 + i] = m.ne + m.tetv[4 * k + 1 + i];
+    }
+  }
   double *omet = malloc(sizeof(double) * nq), *of[3];
   for (int j = 0; j < 3; j++) of[j] = malloc(sizeof(double) * phys.size[j] * nq);
   int *elem = calloc(nq, sizeof(int));
@@ -296,6 +306,8 @@ static void fixture_checks(pmmg_hip_ctx *ctx, const char *dir) {
   o.field = (const double *const *)phys.val;
   pmmg_new_group g = {0};
   g.np = nq;
+  g.ne = 2 * m.ne;
+  g.tetv = ntet;
   g.xyz = xq;
   g.tag = tag;
   g.met_size = 1;
@@ -326,7 +338,7 @@ static void fixture_checks(pmmg_hip_ctx *ctx, const char *dir) {
   }
   CHECK(bad == 0, "reference cube fixture: %d wrong values", bad);
   printf("test_c_abi: reference cube fixture (%d tetra, %d points) transferred, %d wrong values\n", m.ne, nq, bad);
-  free(xq); free(tag); free(omet); free(elem); free(hit);
+  free(xq); free(tag); free(omet); free(elem); free(hit); free(ntet);
   for (int j = 0; j < 3; j++) free(of[j]);
   pmmg_medit_free_mesh(&m);
   pmmg_medit_free_sol(&met);

@@ -45,7 +45,7 @@ def make_case(kind=synth.CUBE, n_old=6, n_new=7, metric=synth.F_ANI,
     return case
 
 
-def run_gpu(case, sort=None, ctx=None, tet8=False):
+def run_gpu(case, sort=None, ctx=None, tet8=False, packed=False):
     bg, new = case["bg"], case["new"]
     own = ctx is None
     ctx = ctx or TransferContext(0, sort=sort)
@@ -55,7 +55,13 @@ def run_gpu(case, sort=None, ctx=None, tet8=False):
             ctx.set_background_tet8(bg.xyz, pack_tet8(bg.tetv, bg.adja), bg.triv, bg.adjt, case["hausd"])
         else:
             ctx.set_background(bg.xyz, bg.tetv, bg.adja, bg.triv, bg.adjt, case["hausd"])
-        ctx.set_solutions(case["met"], case["fields"])
+        if packed:
+            from parmmg_amd.transfer import pack_solutions
+            ctx.set_solutions_packed(pack_solutions(case["met"], case["fields"]),
+                                     0 if case["met"] is None else case["met"].shape[1],
+                                     [f.shape[1] for f in case["fields"]])
+        else:
+            ctx.set_solutions(case["met"], case["fields"])
         npn = new.np
         met_out = None if case["met"] is None else np.full((npn, case["met"].shape[1]), np.nan)
         f_out = [np.full((npn, f.shape[1]), np.nan) for f in case["fields"]]
@@ -68,7 +74,7 @@ def run_gpu(case, sort=None, ctx=None, tet8=False):
             ctx.close()
 
 
-def run_dev(ctx, bg, new_xyz, met, fields, pc, hausd, separate=False):
+def run_dev(ctx, bg, new_xyz, met, fields, pc, hausd, separate=False, packed=False):
     """One transfer with every array resident on the device (the bench's
     device mode): returns (met, fields, elem, hit) downloaded + the stats."""
     from parmmg_amd.transfer import pack_tet8
@@ -82,16 +88,21 @@ def run_dev(ctx, bg, new_xyz, met, fields, pc, hausd, separate=False):
     else:
         d["tet8"] = ctx.upload(pack_tet8(bg.tetv, bg.adja))
         ctx.set_background_tet8(d["xyz"], d["tet8"], d["triv"], d["adjt"], hausd)
-    d["met"] = None if met is None else ctx.upload(met)
-    d["f"] = [ctx.upload(f) for f in fields]
-    ctx.set_solutions(d["met"], d["f"])
+    if packed:
+        from parmmg_amd.transfer import pack_solutions
+        d["rec"] = ctx.upload(pack_solutions(met, fields))
+        ctx.set_solutions_packed(d["rec"], 0 if met is None else met.shape[1], [f.shape[1] for f in fields])
+    else:
+        d["met"] = None if met is None else ctx.upload(met)
+        d["f"] = [ctx.upload(f) for f in fields]
+        ctx.set_solutions(d["met"], d["f"])
     mo = None if met is None else ctx.empty((nq, met.shape[1]), np.float64)
     fo = [ctx.empty((nq, f.shape[1]), np.float64) for f in fields]
     el, hit = ctx.empty((nq,), np.int32), ctx.empty((nq,), np.int8)
     ctx.locate_interp(d["q"], d["pc"], mo, fo, el, hit, sync=False)
     st = ctx.sync()
     out = (None if mo is None else mo.download(), [f.download() for f in fo], el.download(), hit.download(), st)
-    for a in list(d.values()) + [mo, el, hit] + fo:
+    for a in [x for x in d.values() if x is not None] + [mo, el, hit] + fo:
         for b in (a if isinstance(a, list) else [a]):
             if b is not None:
                 b.free()

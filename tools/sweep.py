@@ -68,7 +68,7 @@ def main():
             k, v = item.split("=")
             if k.lower() == "sort":  # context option: 1 Morton bins, 0 input order
                 sort = v == "1"
-            elif k.lower() in ("sol", "perm"):  # measurement only: solution slots / query renumbering
+            elif k.lower() in ("sol", "perm", "packed"):  # measurement only: slots / renumbering / packed records
                 pass
             else:
                 os.environ["PMMG_HIP_" + k.upper()] = v
@@ -84,6 +84,8 @@ def main():
              el=base.empty((new.np,), np.int32), hit=base.empty((new.np,), np.int8))
     cols = ["ms_total", "ms_prepare", "ms_sort", "ms_vol_locate", "ms_vol", "ms_bdy", "ms_fallback"]
     res = {v: {c: [] for c in cols + ["steps_pp", "iters", "exact"]} for v in variants}
+    from parmmg_amd.transfer import pack_solutions
+    d["rec"] = base.upload(pack_solutions(met, fields))
     qperm = {}
     for spec in variants:
         pspec = dict(item.split("=") for item in spec.split(",") if item).get("perm")
@@ -99,7 +101,10 @@ def main():
         for spec, ctx in zip(variants, ctxs):
             for s in range(args.steps + 1):
                 ctx.set_background_tet8(d["xyz"], d["tet8"], d["triv"], d["adjt"], w.hausd)
-                ctx.set_solutions(*sols(spec))
+                if dict(item.split("=") for item in spec.split(",") if item).get("packed") == "1":
+                    ctx.set_solutions_packed(d["rec"], w.met_size, [f.shape[1] for f in fields])
+                else:
+                    ctx.set_solutions(*sols(spec))
                 q, qpc = qperm.get(spec, (d["q"], d["pc"]))
                 ctx.locate_interp(q, qpc, d["mo"], d["fo"], d["el"], d["hit"], sync=False)
                 st = ctx.sync()
