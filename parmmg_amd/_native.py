@@ -94,7 +94,8 @@ def _load(path: str, api: dict, what: str) -> ctypes.CDLL:
 
 def hip_lib() -> ctypes.CDLL:
     """The product HIP module (include/parmmg_hip.h)."""
-    return _load(_build.HIP_SO, HIP_API, "libpmmg_hip.so")
+    # PMMG_HIP_SO: an alternative build of the same module (A/B measurements)
+    return _load(os.environ.get("PMMG_HIP_SO", _build.HIP_SO), HIP_API, "libpmmg_hip.so")
 
 
 def synth_lib() -> ctypes.CDLL:

@@ -22,6 +22,10 @@ constexpr double kEpsD2 = 1.0e-200; // MMG5_EPSD2
 constexpr int kMaxSlot = 8;         // metric + up to 7 fields
 constexpr int kHist = 4;            // visited-element history of a walk
 constexpr int kBlock = 256;
+#ifndef PMMG_XQ_STRIDE
+#define PMMG_XQ_STRIDE 3
+#endif
+constexpr int kXqStride = PMMG_XQ_STRIDE; // ints per row of the fixed-point vertex copy (4: one aligned 16-byte load)
 
 // Background mesh.  Tetra rows are read through tetv_row / adja_row: either
 // two separate arrays (the reference's MMG5_Tetra.v and adja layouts,
@@ -30,7 +34,7 @@ constexpr int kBlock = 256;
 // line, so a walk step costs one line request for the tetra instead of two.
 struct Bg {
   const double *xyz;
-  const int *xq; // fixed-point copy of xyz (3 int32 per vertex, Frame::quant), built per call
+  const int *xq; // fixed-point copy of xyz (kXqStride int32 per vertex, Frame::quant), built per call
   const int4 *tetv;
   const int4 *adja;
   const int *triv;

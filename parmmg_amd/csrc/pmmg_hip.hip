@@ -70,6 +70,7 @@ const LayoutEntry kLayouts[] = {
     PMMG_LAYOUT(6, 1, 3, 6, 0, 0), PMMG_LAYOUT(6, 1, 3, 6, 1, 0), PMMG_LAYOUT(1, 1, 0, 0, 0, 0),
     PMMG_LAYOUT(1, 1, 1, 1, 1, 1), PMMG_LAYOUT(1, 1, 1, 0, 0, 0), PMMG_LAYOUT(6, 0, 0, 0, 0, 0),
     PMMG_LAYOUT(1, 0, 0, 0, 0, 0), PMMG_LAYOUT(6, 1, 0, 0, 0, 0), PMMG_LAYOUT(1, 1, 3, 6, 0, 0),
+    PMMG_LAYOUT(0, 0, 0, 0, 0, 0), // locate only (no metric, no field)
 };
 #undef PMMG_LAYOUT
 
@@ -84,6 +85,7 @@ VolFn pick_layout(const Slots &S) {
   }
   return S.rec ? nullptr : k_vol<false, -1, 0, 0, 0, 0, 0>;
 }
+
 
 // the slot layouts the packed-record interpolation is compiled for
 bool packed_supported(int met_size, int nfield, const int *fsize) {
@@ -869,7 +871,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
       !ensure(c, c->ckey, 8 * nq) || !ensure(c, c->cidx, 4 * nq) || !ensure(c, c->bbest, 4 * nq) ||
       !ensure(c, c->bckey, 8 * nq) || !ensure(c, c->bcidx, 4 * nq))
     return 0;
-  if (!ensure(c, c->xq, sizeof(int) * 3 * (size_t)bg.np)) return 0;
+  if (!ensure(c, c->xq, sizeof(int) * kXqStride * (size_t)bg.np)) return 0;
   bg.xq = (const int *)c->xq.p;
   Frame *fr = (Frame *)c->frame.p;
   DevStats *st = (DevStats *)c->stats.p;
@@ -927,7 +929,10 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[EV_PREP], s));
 
-  // ---- surface branch (second stream, after the order): seeds, k_bdy
+  // ---- surface branch (second stream, after the order and the volume
+  // seeds: it then shares the GPU with the volume kernel instead of slowing
+  // the preparation down): seeds, k_bdy
+  HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_PREP], 0));
   HIPCK(c, hipEventRecord(c->ev[EV_BDY0], sb));
   if (bg.nt > 0) {
     hipLaunchKernelGGL(k_seed_srf, dim3(blocks_for(bg.nt, 4096)), dim3(kBlock), 0, sb, bg, (const Frame *)fr, sgrid,

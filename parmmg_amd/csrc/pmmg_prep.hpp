@@ -121,7 +121,7 @@ __device__ __forceinline__ int quant(double x, const Frame *fr, int d) {
 
 __global__ __launch_bounds__(kBlock) void k_quantize(const double *xyz, long long np, const Frame *fr, int *xq) {
   for (long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x; j < 3 * np; j += (long long)gridDim.x * blockDim.x)
-    xq[j] = quant(__builtin_nontemporal_load(xyz + j), fr, (int)(j % 3));
+    xq[kXqStride * (j / 3) + j % 3] = quant(__builtin_nontemporal_load(xyz + j), fr, (int)(j % 3));
 }
 
 // one launch initialises the per-call state: frame accumulators, counters,
@@ -247,8 +247,8 @@ __global__ __launch_bounds__(kBlock) void k_seed_vol(Bg bg, const Frame *fr, uns
     long long ci = -1;
     if (ok) {
       // centroid from the fixed-point copy (12-byte rows)
-      const int *q0 = bg.xq + 3 * (size_t)(tv.x - 1), *q1 = bg.xq + 3 * (size_t)(tv.y - 1);
-      const int *q2 = bg.xq + 3 * (size_t)(tv.z - 1), *q3 = bg.xq + 3 * (size_t)(tv.w - 1);
+      const int *q0 = bg.xq + kXqStride * (size_t)(tv.x - 1), *q1 = bg.xq + kXqStride * (size_t)(tv.y - 1);
+      const int *q2 = bg.xq + kXqStride * (size_t)(tv.z - 1), *q3 = bg.xq + kXqStride * (size_t)(tv.w - 1);
       double p[3];
       for (int d = 0; d < 3; d++)
         p[d] = fr->qc[d] + 0.25 * ((double)q0[d] + (double)q1[d] + (double)q2[d] + (double)q3[d]) / fr->qs;

@@ -163,10 +163,17 @@ struct LaneSlotsF { // this lane's view of the wave's slot image [slot*3 + dim][
 // vertex v relative to the query, from the fixed-point copy (exact integer
 // difference, one rounding to fp32)
 __device__ __forceinline__ void rel_pt(const int *xq, int v, const int *xqq, float *q) {
-  const int *p = xq + 3 * (size_t)(v - 1);
-  q[0] = (float)(p[0] - xqq[0]);
-  q[1] = (float)(p[1] - xqq[1]);
-  q[2] = (float)(p[2] - xqq[2]);
+  if constexpr (kXqStride == 4) {
+    const int4 p = reinterpret_cast<const int4 *>(xq)[v - 1];
+    q[0] = (float)(p.x - xqq[0]);
+    q[1] = (float)(p.y - xqq[1]);
+    q[2] = (float)(p.z - xqq[2]);
+  } else {
+    const int *p = xq + kXqStride * (size_t)(v - 1);
+    q[0] = (float)(p[0] - xqq[0]);
+    q[1] = (float)(p[1] - xqq[1]);
+    q[2] = (float)(p[2] - xqq[2]);
+  }
 }
 
 __device__ __forceinline__ void cross3(const float *a, const float *b, float *c) {
@@ -487,7 +494,7 @@ struct PackedLayout {
   static constexpr int NPASS = RS <= 8 ? 1 : 2;        // passes of at most 8 doubles per record
   static constexpr int off(int s) { return s == 0 ? 0 : off(s - 1) + c[s - 1]; }
   static constexpr bool valid() {                      // tensors inside one pass, K <= 16
-    if (C0 < 0 || RS > 16) return false;
+    if (C0 < 0 || K == 0 || RS > 16) return false;
     for (int s = 0; s < 6; s++)
       if (c[s] == 6 && NPASS == 2 && off(s) < 8 && off(s) + 6 > 8) return false;
     return true;
@@ -554,6 +561,28 @@ __device__ __forceinline__ void packed_store(const Slot &sl, SlotAcc<C> &a, doub
   }
 }
 
+// slot S's components in pass `pass` are accumulated there; the slot is
+// finished (stored) after the pass holding its last component
+template <class L, int S, int C>
+__device__ __forceinline__ constexpr int last_pass() {
+  return L::NPASS == 1 ? 0 : (L::off(S) + C - 1) / 8;
+}
+template <class L, int S, int C>
+__device__ __forceinline__ constexpr int first_pass() {
+  return L::NPASS == 1 ? 0 : L::off(S) / 8;
+}
+
+template <class L, int S, int C>
+__device__ __forceinline__ void packed_pass_slot(const Slots &Sl, SlotAcc<C> &a, int pass, int i, double ph,
+                                                 const double *mine, double *img, bool coalesced, size_t w0, int ip,
+                                                 bool store) {
+  if constexpr (C > 0) {
+    if (pass < first_pass<L, S, C>() || pass > last_pass<L, S, C>()) return;
+    if (!store) packed_take<L, S>(a, pass, i, ph, mine);
+    else if (pass == last_pass<L, S, C>()) packed_store<C>(Sl.s[S], a, img, coalesced, w0, ip);
+  }
+}
+
 template <int C0, int C1, int C2, int C3, int C4, int C5>
 __device__ __forceinline__ void vol_interp_packed(const Slots &S, bool acc, const VolLoc &loc, double *img,
                                                   bool coalesced, size_t w0, int ip) {
@@ -561,6 +590,8 @@ __device__ __forceinline__ void vol_interp_packed(const Slots &S, bool acc, cons
   constexpr int PW = L::NPASS == 1 ? L::RS : 8; // doubles per record and pass
   constexpr int PR = PW / 2;                     // 16-byte pieces per record and pass
   const int lane = __lane_id();
+  // pass-major: only the slots living in the current pass hold accumulators
+  // (fewer live registers than vertex-major over the whole record)
   SlotAcc<C0> a0;
   SlotAcc<C1> a1;
   SlotAcc<C2> a2;
@@ -572,11 +603,11 @@ __device__ __forceinline__ void vol_interp_packed(const Slots &S, bool acc, cons
   }
   const double2 *rec = reinterpret_cast<const double2 *>(S.rec);
 #pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const int myv = sel4(loc.v, i);
-    const double ph = loc.phi[i];
+  for (int pass = 0; pass < L::NPASS; pass++) {
 #pragma unroll
-    for (int pass = 0; pass < L::NPASS; pass++) {
+    for (int i = 0; i < 4; i++) {
+      const int myv = sel4(loc.v, i);
+      const double ph = loc.phi[i];
       // piece p = 64t + lane of the image: record p / PR, piece p % PR
       double2 b[PR];
 #pragma unroll
@@ -590,22 +621,23 @@ __device__ __forceinline__ void vol_interp_packed(const Slots &S, bool acc, cons
       wait_lgkm();
       __builtin_amdgcn_wave_barrier();
       const double *mine = img + PW * lane;
-      packed_take<L, 0>(a0, pass, i, ph, mine);
-      packed_take<L, 1>(a1, pass, i, ph, mine);
-      packed_take<L, 2>(a2, pass, i, ph, mine);
-      packed_take<L, 3>(a3, pass, i, ph, mine);
-      packed_take<L, 4>(a4, pass, i, ph, mine);
-      packed_take<L, 5>(a5, pass, i, ph, mine);
+      packed_pass_slot<L, 0>(S, a0, pass, i, ph, mine, img, coalesced, w0, ip, false);
+      packed_pass_slot<L, 1>(S, a1, pass, i, ph, mine, img, coalesced, w0, ip, false);
+      packed_pass_slot<L, 2>(S, a2, pass, i, ph, mine, img, coalesced, w0, ip, false);
+      packed_pass_slot<L, 3>(S, a3, pass, i, ph, mine, img, coalesced, w0, ip, false);
+      packed_pass_slot<L, 4>(S, a4, pass, i, ph, mine, img, coalesced, w0, ip, false);
+      packed_pass_slot<L, 5>(S, a5, pass, i, ph, mine, img, coalesced, w0, ip, false);
       wait_lgkm();
       __builtin_amdgcn_wave_barrier(); // every lane has read its record: the image is free again
     }
+    // slots whose last component lives in this pass: finished and stored
+    packed_pass_slot<L, 0>(S, a0, pass, 0, 0.0, nullptr, img, coalesced, w0, ip, true);
+    packed_pass_slot<L, 1>(S, a1, pass, 0, 0.0, nullptr, img, coalesced, w0, ip, true);
+    packed_pass_slot<L, 2>(S, a2, pass, 0, 0.0, nullptr, img, coalesced, w0, ip, true);
+    packed_pass_slot<L, 3>(S, a3, pass, 0, 0.0, nullptr, img, coalesced, w0, ip, true);
+    packed_pass_slot<L, 4>(S, a4, pass, 0, 0.0, nullptr, img, coalesced, w0, ip, true);
+    packed_pass_slot<L, 5>(S, a5, pass, 0, 0.0, nullptr, img, coalesced, w0, ip, true);
   }
-  packed_store<C0>(S.s[0], a0, img, coalesced, w0, ip);
-  packed_store<C1>(S.s[1], a1, img, coalesced, w0, ip);
-  packed_store<C2>(S.s[2], a2, img, coalesced, w0, ip);
-  packed_store<C3>(S.s[3], a3, img, coalesced, w0, ip);
-  packed_store<C4>(S.s[4], a4, img, coalesced, w0, ip);
-  packed_store<C5>(S.s[5], a5, img, coalesced, w0, ip);
 }
 
 template <bool PK, int C0, int C1, int C2, int C3, int C4, int C5>

@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-pmcv}
 mkdir -p $OUT
 IFS=';' read -ra VS <<< "${VARIANTS:-sol=none;sol=all}"
-SETS=("FETCH_SIZE" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum" "TCC_HIT_sum TCC_MISS_sum" "TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU")
+if [ -n "$SETS_OVERRIDE" ]; then IFS=';' read -ra SETS <<< "$SETS_OVERRIDE"; else SETS=("FETCH_SIZE" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum" "TCC_HIT_sum TCC_MISS_sum" "TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU"); fi
 vi=0
 for v in "${VS[@]}"; do
   vi=$((vi+1))

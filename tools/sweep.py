@@ -1,5 +1,7 @@
-"""Interleaved A/B sweep of module settings in ONE process (perf deltas from
-interleaved rounds, not from separate invocations).  Each variant is a set of
+"""Interleaved A/B sweep of module settings: rounds x variants, each variant
+run in its own process (one live context, so every variant gets the same
+hardware queues: a second live context's streams can share one queue, which
+serialises its surface branch with its volume kernel and biases the A/B).  Each variant is a set of
 PMMG_HIP_* environment values read by pmmg_hip_create (and sort=0/1, the
 context's query-order option):
 
@@ -50,18 +52,24 @@ def main():
     ap.add_argument("--variants", default="TPC=8", help='";"-separated variants of ","-separated NAME=value')
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--child", default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.child is None:
+        return parent(args)
     w = configs.SHORT[args.config]
     bg = synth.lattice(w.kind, w.n_old)
     new = synth.lattice(w.kind, w.n_new, jitter=w.jitter_new, with_trias=False, with_tetra=False)
     met = synth.solution(w.metric, bg.xyz)
     fields = [synth.solution(f, bg.xyz) for f in w.fields]
     pc = synth.classes(new)
-    variants = [v for v in args.variants.split(";") if v]
-    ctxs = []
-    for spec in variants:
+    variants = [args.child]
+
+    def make_ctx(spec):
+        """one context alive at a time: every variant gets the same hardware
+        queues (a second live context's streams can share one queue, which
+        serialises its surface branch with its volume kernel)"""
         for k in list(os.environ):
-            if k.startswith("PMMG_HIP_"):
+            if k.startswith("PMMG_HIP_") and k != "PMMG_HIP_SO":
                 os.environ.pop(k)
         sort = None
         for item in filter(None, spec.split(",")):
@@ -72,11 +80,13 @@ def main():
                 pass
             else:
                 os.environ["PMMG_HIP_" + k.upper()] = v
-        ctxs.append(TransferContext(0, sort=sort))
-    for k in list(os.environ):
-        if k.startswith("PMMG_HIP_"):
-            os.environ.pop(k)
-    base = ctxs[0]
+        ctx = TransferContext(0, sort=sort)
+        for k in list(os.environ):
+            if k.startswith("PMMG_HIP_") and k != "PMMG_HIP_SO":
+                os.environ.pop(k)
+        return ctx
+
+    base = make_ctx(args.child)  # the only live context: it owns the inputs and runs the variant
     d = dict(xyz=base.upload(bg.xyz), tet8=base.upload(pack_tet8(bg.tetv, bg.adja)), triv=base.upload(bg.triv),
              adjt=base.upload(bg.adjt), met=base.upload(met), f=[base.upload(f) for f in fields],
              q=base.upload(new.xyz), pc=base.upload(pc), mo=base.empty((new.np, w.met_size), np.float64),
@@ -97,8 +107,9 @@ def main():
         which = dict(item.split("=") for item in spec.split(",") if item).get("sol", "all")
         return {"none": (None, []), "met": (d["met"], []), "all": (d["met"], d["f"])}[which]
 
-    for r in range(args.rounds):
-        for spec, ctx in zip(variants, ctxs):
+    for r in range(1):
+        for spec in variants:
+            ctx = base
             for s in range(args.steps + 1):
                 ctx.set_background_tet8(d["xyz"], d["tet8"], d["triv"], d["adjt"], w.hausd)
                 if dict(item.split("=") for item in spec.split(",") if item).get("packed") == "1":
@@ -115,6 +126,28 @@ def main():
                 res[spec]["steps_pp"].append(st.steps_total / max(1, st.nvol + st.nbdy))
                 res[spec]["iters"].append(st.wave_iters)
                 res[spec]["exact"].append(st.nvol_exact)
+    import json
+
+    print("RESULT " + json.dumps(res[args.child]), flush=True)
+
+
+def parent(args):
+    import json
+    import subprocess
+
+    variants = [v for v in args.variants.split(";") if v]
+    cols = ["ms_total", "ms_prepare", "ms_sort", "ms_vol_locate", "ms_vol", "ms_bdy", "ms_fallback"]
+    res = {v: {} for v in variants}
+    for r in range(args.rounds):
+        for spec in variants:
+            p = subprocess.run([sys.executable, "-u", os.path.abspath(__file__), "--config", args.config, "--steps",
+                                str(args.steps), "--child", spec], stdout=subprocess.PIPE, text=True)
+            line = [x for x in p.stdout.splitlines() if x.startswith("RESULT ")]
+            if p.returncode != 0 or not line:
+                print(p.stdout[-2000:])
+                raise SystemExit(f"variant {spec} failed")
+            for k, v in json.loads(line[-1][7:]).items():
+                res[spec].setdefault(k, []).extend(v)
         print(f"round {r} done", flush=True)
     hdr = f"{'variant':28s}" + "".join(f"{c[3:]:>11s}" for c in cols) + f"{'steps/pt':>10s}{'wave_it':>10s}{'exact':>8s}"
     print(hdr)
