@@ -929,10 +929,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[EV_PREP], s));
 
-  // ---- surface branch (second stream, after the order and the volume
-  // seeds: it then shares the GPU with the volume kernel instead of slowing
-  // the preparation down): seeds, k_bdy
-  HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_PREP], 0));
+  // ---- surface branch (second stream, after the order): seeds, k_bdy
   HIPCK(c, hipEventRecord(c->ev[EV_BDY0], sb));
   if (bg.nt > 0) {
     hipLaunchKernelGGL(k_seed_srf, dim3(blocks_for(bg.nt, 4096)), dim3(kBlock), 0, sb, bg, (const Frame *)fr, sgrid,
