@@ -1,0 +1,107 @@
+"""Every hit kind of the reference's locate functions produced on the GPU
+and checked against the oracle (runs on the MI355X).
+
+  2 VOL_EXHAUST   walk stopped (test-only PMMG_HIP_MAXSTEP=1), accepting
+                  brute force: the lowest-index accepting tetra
+                  (PMMG_locatePoint_exhaustTetra, locate_pmmg.c:737-770)
+  3 VOL_CLOSEST   volume point outside the background: closest tetra
+  7 BDY_WEDGE     surface point beyond a cube edge, within hausd of it
+                  (PMMG_locatePointInWedge, locate_pmmg.c:286-334)
+  8 BDY_CONE      surface point beyond a cube corner, within hausd of it
+                  (PMMG_locatePointInCone, locate_pmmg.c:209-270)
+  9 BDY_EXHAUST   surface walk stopped (PMMG_HIP_MAXSTEP=1): the
+                  lowest-index accepting tria (locate_pmmg.c:477-515)
+ 11 BDY_CLOSEST   surface point beyond hausd of every tria
+ 10 BDY_STALE     the reference re-evaluates the last scanned tria with the
+                  closest tria's normal after a failed exhaustive search
+                  (locate_pmmg.c:505-512); restated in k_bdy_finish and the
+                  oracle, but no input found to reach it (400k random points
+                  around a flat tetra, 100k around the lattices' last trias:
+                  the closest tria's normal never accepts where the last
+                  tria's own test failed) — not asserted.
+Each test compares with tests/parity.py::check (acceptance for the hit kind,
+values of the reference interpolator, class (i) identity against the
+oracle's run)."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from parity import check, make_case, run_gpu
+from parmmg_amd import synth
+
+
+def _codes(gpu):
+    return np.bincount(gpu["hit"].astype(np.int32) & 15, minlength=12)
+
+
+def _with_points(case, xyz):
+    import dataclasses
+    case = dict(case)
+    case["new"] = dataclasses.replace(case["new"], xyz=np.ascontiguousarray(xyz))
+    vis = synth.visit_order(case["new"])
+    case["ref"] = O.run(case["B"], case["new"].xyz, case["pclass"], vis, O.MODE_FRESH)
+    return case
+
+
+@pytest.mark.gpu
+def test_forced_exhaustive_hits(monkeypatch):
+    """PMMG_HIP_MAXSTEP=1 (test-only): walks stop after one step, so the
+    exhaustive kernels run for most points: codes 2 and 9, each the
+    lowest-index accepting element."""
+    monkeypatch.setenv("PMMG_HIP_MAXSTEP", "1")  # read by pmmg_hip_create
+    case = make_case(kind=synth.CUBE, n_old=5, n_new=6)
+    gpu = run_gpu(case, tet8=True)
+    rep = check(case, gpu)
+    c = _codes(gpu)
+    print(rep, c)
+    assert c[2] > 0 and c[9] > 0
+    assert rep["class_i"] == rep["class_i_same"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("packed", [False, True])
+def test_cone_and_wedge_hits(packed):
+    """Surface points pushed beyond the cube's corners (cone, code 8) and
+    edges (wedge, code 7) by less than hausd; values from the corner vertex
+    (copyMetrics) / the edge (interp2bar)."""
+    case = make_case(kind=synth.CUBE, n_old=6, n_new=7, fields=(synth.F_SCALAR, synth.F_VECTOR, synth.F_TENSOR),
+                     with_ref=False)
+    x = case["new"].xyz.copy()
+    corner = np.all(np.isclose(x, 0) | np.isclose(x, 1), axis=1)
+    on_edge = (np.sum(np.isclose(x, 0) | np.isclose(x, 1), axis=1) == 2)
+    for i in np.nonzero(corner)[0]:
+        x[i] += 0.003 * np.where(x[i] > 0.5, 1.0, -1.0)
+    for i in np.nonzero(on_edge)[0]:
+        d = np.where(np.isclose(x[i], 1), 1.0, np.where(np.isclose(x[i], 0), -1.0, 0.0))
+        x[i] += 0.004 * d
+    case = _with_points(case, x)
+    gpu = run_gpu(case, tet8=True, packed=packed)
+    rep = check(case, gpu)
+    c = _codes(gpu)
+    print(rep, c, "oracle:", np.bincount(case["ref"]["hit"], minlength=12))
+    assert c[8] == int(corner.sum()) and c[7] > 0
+    assert ((gpu["hit"][corner] & 15) == 8).all()
+
+
+@pytest.mark.gpu
+def test_closest_hits():
+    """Volume points outside the background (code 3: closest tetra) and
+    surface points beyond hausd of every tria (code 11: closest tria)."""
+    case = make_case(kind=synth.CUBE, n_old=5, n_new=6, with_ref=False)
+    x = case["new"].xyz.copy()
+    rng = np.random.default_rng(5)
+    vol = np.nonzero(case["pclass"] == 1)[0]
+    bdy = np.nonzero(case["pclass"] == 2)[0]
+    pv = rng.choice(vol, 12, replace=False)
+    pb = rng.choice(bdy, 12, replace=False)
+    x[pv, 0] = 1.0 + rng.uniform(0.01, 0.3, 12)
+    for i in pb:  # outward along the nearest face normal, beyond hausd
+        a = int(np.argmin(np.minimum(x[i], 1 - x[i])))
+        x[i, a] += -0.05 if x[i, a] < 0.5 else 0.05
+    case = _with_points(case, x)
+    gpu = run_gpu(case, tet8=True)
+    rep = check(case, gpu)
+    c = _codes(gpu)
+    print(rep, c)
+    assert c[3] > 0 and c[11] > 0
+    assert ((gpu["hit"][pb] & 15) == (case["ref"]["hit"][pb] & 15)).all()
