@@ -463,14 +463,16 @@ def main():
         "lockstep_efficiency": round(st.steps_total / max(1, 64 * st.wave_iters), 3),
         "roofline": {
             "bound": "hbm",
-            "kernel": "volume stage: k_vol_walk + k_vol_walk_exact + k_vol_interp",
+            "kernel": "volume stage: k_vol (fused fp32 filter walk, exact fp64 acceptance, interpolation) + "
+                      "k_vol_walk_exact",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "traffic_unit": "bytes per volume stage (all walk + interpolation launches of one call; FETCH_SIZE "
-                            "calibrated per tools/calib, WRITE_SIZE)",
+            "traffic_unit": "HBM/Infinity-Cache bytes per volume stage (its launches in one call): 2 x FETCH_SIZE "
+                            "(= 128 B per TCC_EA0_RDREQ, calibrated by tools/calib/fetch_calib, profiles/r02a/calib) "
+                            "+ WRITE_SIZE",
             "traffic_source": traffic_src,
             "algorithmic_bytes_per_stage": round(kvol_bytes),
             "stage": "HIP events on the main stream from the end of the query order to the end of the "

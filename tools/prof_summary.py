@@ -34,7 +34,7 @@ def per_dispatch(path):
 
 
 def short(k):
-    k = k.replace("(anonymous namespace)::", "").replace("void ", "")
+    k = k.replace("(anonymous namespace)::", "").replace("void ", "").replace("pmmg::", "")
     return k.split("(")[0]
 
 
@@ -66,7 +66,7 @@ def main(src, dst):
                 spans.append(cur[1] - cur[0])
             cur = None
             continue
-        if k.startswith("k_vol_walk") or k.startswith("k_vol_interp") or k.startswith("k_vol_fused"):
+        if k.startswith("k_vol<") or k.startswith("k_vol_walk") or k.startswith("k_vol_interp") or k.startswith("k_vol_fused"):
             a, b = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
             cur = [a, b] if cur is None else [min(cur[0], a), max(cur[1], b)]
     if cur:
@@ -78,8 +78,10 @@ def main(src, dst):
     json.dump(kern_summary, open(os.path.join(dst, "kernels.json"), "w"), indent=1)
     fetch = per_dispatch(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"))
     write = per_dispatch(os.path.join(src, "pmc_write", "run_counter_collection.csv"))
-    pmc = {"note": "bytes per launch; FETCH_SIZE/WRITE_SIZE are KiB; FETCH doubled (gfx950 wide-read correction, "
-                   "MI355X_MICROARCH.md HBM section); counters include Infinity-Cache hits",
+    pmc = {"note": "bytes per launch; FETCH_SIZE/WRITE_SIZE are KiB; FETCH doubled: on gfx950 FETCH_SIZE = 64 B x "
+                   "TCC_EA0_RDREQ and every read request moves a 128 B line (calibrated in profiles/r02a/calib: "
+                   "streamed and gathered whole lines, 4-16 B per lane, report exactly half); counters include "
+                   "Infinity-Cache hits",
            "workload": bench["config"]["workload"], "kernels": {}}
     ncall = max(1, len(fetch.get(next((k for k in fetch if short(k) == "k_seed_vol"), ""), [])))
     for k in set(fetch) | set(write):
