@@ -3,6 +3,7 @@ its own group (weak scaling, no data-path collective), the only reductions are
 the barrier, max of the step time and sum of the points."""
 import os
 import socket
+import sys
 
 import numpy as np
 import torch.multiprocessing as mp
@@ -88,22 +89,36 @@ def test_morton_shards_partition_and_locality():
 
 
 def _gather_worker(rank, world, port, q):
+    """One rank of the Morton split with a replicated background: the oracle
+    transfers this rank's contiguous Morton range (as the module does on its
+    GPU), and {elem, hit, K doubles} rows are all-gathered."""
     import torch
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from parity import make_case
+    from oracle import oracle as O
+
     ri = ranks.init("gloo")
-    new = synth.lattice(synth.SHELL, 8, jitter=0.2, with_trias=False)  # same problem on every rank
-    pclass = synth.classes(new)
-    sh = ranks.morton_shards(new.xyz, pclass, world)
+    case = make_case(kind=synth.SHELL, n_old=8, n_new=12, with_ref=False)  # the same problem on every rank
+    sh = ranks.morton_shards(case["new"].xyz, case["pclass"], world)
     mine = sh[rank]
-    # stand-in for this rank's interpolated rows: a function of the point
-    rows = torch.from_numpy(np.concatenate([new.xyz[mine], mine[:, None].astype(np.float64)], axis=1))
-    got = ranks.allgather_rows(ri, rows, [len(s) for s in sh]).numpy()
+    r = O.run(case["B"], np.ascontiguousarray(case["new"].xyz[mine]), case["pclass"][mine],
+              np.arange(1, len(mine) + 1, dtype=np.int32), O.MODE_FRESH)
+    hit = r["hit"].astype(np.int32) | (np.maximum(r["loc"], 0).astype(np.int32) << 4)
+    rows = np.concatenate([r["elem"][:, None], hit[:, None], r["met"]] + r["fields"], axis=1).astype(np.float64)
+    got = ranks.allgather_rows(ri, torch.from_numpy(rows), [len(s) for s in sh]).numpy()
     q.put((rank, got))
     ranks.finalize(ri)
 
 
 def test_gloo_two_ranks_morton_allgather():
+    """world 2 (gloo), Morton ranges against a replicated background: every
+    rank transfers its range, the all-gathered rows are identical on both
+    ranks and meet the group's parity contract (tests/parity.py)."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from parity import check, make_case
+
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -115,10 +130,20 @@ def test_gloo_two_ranks_morton_allgather():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    new = synth.lattice(synth.SHELL, 8, jitter=0.2, with_trias=False)
-    pclass = synth.classes(new)
-    order = np.concatenate(ranks.morton_shards(new.xyz, pclass, world))
-    for r in range(world):
-        got = out[r]
-        np.testing.assert_array_equal(got[:, 3].astype(np.int64), order)  # rank-order blocks
-        np.testing.assert_array_equal(got[:, :3], new.xyz[order])
+    assert np.array_equal(out[0], out[1])
+    case = make_case(kind=synth.SHELL, n_old=8, n_new=12)
+    order = np.concatenate(ranks.morton_shards(case["new"].xyz, case["pclass"], world))
+    got = out[0]
+    n = case["new"].np
+    full = dict(elem=np.zeros(n, np.int32), hit=np.zeros(n, np.int8),
+                met=np.full((n, case["met"].shape[1]), np.nan), fields=[np.full((n, f.shape[1]), np.nan)
+                                                                         for f in case["fields"]])
+    full["elem"][order] = got[:, 0].astype(np.int32)
+    full["hit"][order] = got[:, 1].astype(np.int8)
+    c = 2 + case["met"].shape[1]
+    full["met"][order] = got[:, 2:c]
+    for f in full["fields"]:
+        f[order] = got[:, c:c + f.shape[1]]
+        c += f.shape[1]
+    rep = check(case, full)
+    assert rep["n"] == len(order) and rep["class_i"] == rep["class_i_same"] > 0
