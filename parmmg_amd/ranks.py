@@ -120,14 +120,16 @@ def morton_codes(xyz):
 def morton_shards(xyz, pclass, world: int):
     """0-based point indices of each rank: the processed points (pclass != 0)
     in Morton order (stable), cut into `world` contiguous ranges whose sizes
-    differ by at most one.  Skipped points (MG_REQ, copied by the host) are
-    in no shard."""
+    differ by at most one; inside its range a rank keeps the input order of
+    the points (a mesh numbering is spatially coherent, a Morton order is
+    not at the scale of a wave: neighbouring lanes would walk from unrelated
+    seeds).  Skipped points (MG_REQ, copied by the host) are in no shard."""
     import numpy as np
 
     idx = np.nonzero(pclass != 0)[0]
     order = idx[np.argsort(morton_codes(xyz[idx]), kind="stable")]
     cuts = [len(order) * r // world for r in range(world + 1)]
-    return [order[cuts[r]:cuts[r + 1]] for r in range(world)]
+    return [np.sort(order[cuts[r]:cuts[r + 1]]) for r in range(world)]
 
 
 def allgather_rows(ri: RankInfo, rows, counts):
