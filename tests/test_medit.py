@@ -75,3 +75,31 @@ def test_missing_and_binary_files_rejected(tmp_path):
     p.write_text("MeshVersionFormatted 2\nDimension 3\nEnd\n")
     with pytest.raises(ValueError, match="no SolAtVertices"):
         medit.read_sol_c(str(p))
+
+
+def test_reader_survives_corrupted_fixtures_under_asan(tmp_path):
+    """tests/c/fuzz_medit.c built with ASan + UBSan against pmmg_medit.c:
+    every truncation and ~8 single-byte corruptions per 3 bytes of the
+    reference's cube fixtures must return 0/1 without a memory error or a
+    leak."""
+    import shutil
+    import subprocess
+
+    gcc = shutil.which("gcc")
+    if gcc is None:
+        pytest.skip("gcc not found")
+    repo = os.path.dirname(os.path.dirname(GOLD))
+    exe = tmp_path / "fuzz_medit"
+    cmd = [gcc, "-O1", "-g", "-std=c99", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
+           "-fno-sanitize-recover=all", f"-I{os.path.join(repo, 'parmmg_amd', 'csrc')}", "-o", str(exe),
+           os.path.join(repo, "tests", "c", "fuzz_medit.c"), os.path.join(repo, "parmmg_amd", "csrc", "pmmg_medit.c")]
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if p.returncode != 0 and "sanitize" in p.stdout:
+        pytest.skip("sanitizer runtime not available: " + p.stdout[-200:])
+    assert p.returncode == 0, p.stdout
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:halt_on_error=1")
+    r = subprocess.run([str(exe), os.path.join(GOLD, "cube.mesh"), os.path.join(GOLD, "cube-solphys.sol"),
+                        str(tmp_path / "scratch.mesh")], stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                       text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stdout[-3000:]
+    assert "fuzz_medit:" in r.stdout
