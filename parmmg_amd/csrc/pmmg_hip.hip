@@ -160,7 +160,7 @@ struct pmmg_hip_ctx {
   int snap_ok = 1;
   int verbose = 0; // PMMG_HIP_VERBOSE: host-mode transfer timings on stderr
   int tpc = 8;        // background tetra per volume seed cell (PMMG_HIP_TPC)
-  int qpb = 8;        // queries per Morton bin
+  int qpb = 64;       // queries per Morton bin (PMMG_HIP_QPB; r02: 64 beats 8 on shuffled and on coherent inputs)
   int maxstep = 4096; // longer walks go to the exact continuation / exhaustive kernels (PMMG_HIP_MAXSTEP; the
                       // reference caps at ne)
   int filter_steps = 4096; // step cap of the fp32 filter walk; test-only PMMG_HIP_FILTER_STEPS=0 sends every
@@ -460,6 +460,7 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   }
   for (int i = 0; i < EV_COUNT; i++) (void)hipEventCreate(&c->ev[i]);
   c->tpc = env_int("PMMG_HIP_TPC", c->tpc);
+  c->qpb = env_int("PMMG_HIP_QPB", c->qpb);
   c->verbose = env_int("PMMG_HIP_VERBOSE", 0);
   c->maxstep = env_int("PMMG_HIP_MAXSTEP", c->maxstep);
   c->filter_steps = c->maxstep;

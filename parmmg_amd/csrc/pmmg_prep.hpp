@@ -548,17 +548,32 @@ __global__ __launch_bounds__(kBlock) void k_coherence(const double *xyz, int np,
 __global__ __launch_bounds__(kBlock) void k_bin_count(const double *xyz, const uint8_t *pclass, int np, const Frame *fr,
                                                       int gb, int nbins, int *cnt, int2 *binrank, const DevStats *st) {
   if (!st->sorted) return;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < np; i += gridDim.x * blockDim.x) {
-    int c = pclass[i];
-    if (c != PMMG_PT_VOL && c != PMMG_PT_BDY) {
-      binrank[i] = make_int2(-1, 0);
-      continue;
+  const int lane = __lane_id();
+  // uniform trip count per wave (the loop bound is the block's base), so the
+  // lanes of a wave can aggregate: consecutive lanes in the same bin (the
+  // usual case: neighbouring points) take their ranks from one atomicAdd
+  for (long long b0 = (long long)blockIdx.x * blockDim.x; b0 < np; b0 += (long long)gridDim.x * blockDim.x) {
+    const int i = (int)(b0 + threadIdx.x);
+    int bin = -1;
+    if (i < np) {
+      const int c = pclass[i];
+      if (c == PMMG_PT_VOL || c == PMMG_PT_BDY) {
+        uint32_t q[3];
+        for (int d = 0; d < 3; d++) q[d] = (uint32_t)cell_coord(xyz[3 * (size_t)i + d], fr->lo[d], fr->inv_bin[d], gb);
+        bin = (int)((expand10(q[0]) << 2) | (expand10(q[1]) << 1) | expand10(q[2])) + (c == PMMG_PT_BDY ? nbins : 0);
+      }
     }
-    uint32_t q[3];
-    for (int d = 0; d < 3; d++) q[d] = (uint32_t)cell_coord(xyz[3 * (size_t)i + d], fr->lo[d], fr->inv_bin[d], gb);
-    int bin = (int)((expand10(q[0]) << 2) | (expand10(q[1]) << 1) | expand10(q[2])) + (c == PMMG_PT_BDY ? nbins : 0);
-    int r = atomicAdd(&cnt[bin], 1);
-    binrank[i] = make_int2(bin, r);
+    const int prev = __shfl_up(bin, 1);
+    const bool start = lane == 0 || bin != prev;
+    const unsigned long long starts = __ballot(start);
+    const unsigned long long upto = lane == 63 ? ~0ULL : ((2ULL << lane) - 1); // bits 0..lane
+    const int rs = 63 - __clzll(starts & upto);                                 // this lane's run start
+    const unsigned long long after = starts & ~upto;
+    const int next = after ? __ffsll((long long)after) - 1 : 64;                // the next run's start
+    int base = 0;
+    if (start && bin >= 0) base = atomicAdd(&cnt[bin], next - lane);
+    base = __shfl(base, rs);
+    if (i < np) binrank[i] = bin >= 0 ? make_int2(bin, base + (lane - rs)) : make_int2(-1, 0);
   }
 }
 

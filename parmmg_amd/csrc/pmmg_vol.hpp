@@ -466,10 +466,11 @@ __device__ __forceinline__ void vol_slot(const Slot &sl, bool act, const int4 &v
       wave_store_rows<C>(sl.out + (size_t)C * w0, r, __ballot(ok), img);
     } else if (ok) {
       double *o = sl.out + (size_t)C * (ip - 1);
-      if constexpr (C == 6) store6(o, r);
-      else
+      // Morton-binned order: plain (cached) stores, so that L2 merges the
+      // partial lines neighbouring queries of other waves write before the
+      // lines leave (non-temporal partial-line writes go to memory alone)
 #pragma unroll
-        for (int q = 0; q < C; q++) nt_store(o + q, r[q]);
+      for (int q = 0; q < C; q++) o[q] = r[q];
     }
   }
 }
@@ -553,10 +554,11 @@ __device__ __forceinline__ void packed_store(const Slot &sl, SlotAcc<C> &a, doub
       wave_store_rows<C>(sl.out + (size_t)C * w0, r, __ballot(ok), img);
     } else if (ok) {
       double *o = sl.out + (size_t)C * (ip - 1);
-      if constexpr (C == 6) store6(o, r);
-      else
+      // Morton-binned order: plain (cached) stores, so that L2 merges the
+      // partial lines neighbouring queries of other waves write before the
+      // lines leave (non-temporal partial-line writes go to memory alone)
 #pragma unroll
-        for (int q = 0; q < C; q++) nt_store(o + q, r[q]);
+      for (int q = 0; q < C; q++) o[q] = r[q];
     }
   }
 }
@@ -741,8 +743,13 @@ __global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsign
       vol_slot<C5>(S.s[5], acc, loc.v, loc.phi, img, !sorted, w0, ip);
     }
     if (acc) {
-      if (elem_out) __builtin_nontemporal_store(k, elem_out + ip - 1);
-      if (hit_out) __builtin_nontemporal_store((int8_t)PMMG_HIT_VOL_WALK, hit_out + ip - 1);
+      if (sorted) { // scattered: cached stores (see vol_slot)
+        if (elem_out) elem_out[ip - 1] = k;
+        if (hit_out) hit_out[ip - 1] = (int8_t)PMMG_HIT_VOL_WALK;
+      } else {
+        if (elem_out) __builtin_nontemporal_store(k, elem_out + ip - 1);
+        if (hit_out) __builtin_nontemporal_store((int8_t)PMMG_HIT_VOL_WALK, hit_out + ip - 1);
+      }
     }
   }
   __syncthreads();
