@@ -288,6 +288,60 @@ def host_mode_timing(ctx, w, bg, met, fields, q_xyz, q_pc, rank: int, reps: int 
             "bytes_up": int(up), "bytes_down": int(down), "pcie_gbps_effective": round((up + down) / t / 1e9, 1)}
 
 
+def shuffled_timing(ctx, args, w, step_bg, q_xyz, q_pc, d_mo, d_fo, d_elem, d_hit, rank: int):
+    """The same step on a random renumbering of the new points (no spatial
+    coherence in the input order: the module detects it and Morton-bins the
+    queries, the path for numberings that are not spatially coherent).
+    Reported beside the bench value, which is measured on the generator's
+    lattice numbering.  Checked against the input-order step: a point
+    located in the same element gets bit-identical rows."""
+    nq = q_xyz.shape[0]
+    perm = np.random.default_rng(2024).permutation(nq)
+    s_xyz, s_pc = ctx.upload(np.ascontiguousarray(q_xyz[perm])), ctx.upload(np.ascontiguousarray(q_pc[perm]))
+    s_mo = ctx.empty((nq, w.met_size), np.float64)
+    s_fo = [ctx.empty(f.shape, np.float64) for f in d_fo]
+    s_elem, s_hit = ctx.empty((nq,), np.int32), ctx.empty((nq,), np.int8)
+
+    def step():
+        step_bg()
+        ctx.locate_interp(s_xyz, s_pc, s_mo, s_fo, s_elem, s_hit, sync=False)
+
+    for _ in range(args.warmup):
+        step()
+        ctx.sync()
+    ms, vol = [], []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        st = ctx.sync()
+        ms.append(st.ms_total)
+        vol.append(st.ms_vol)
+    wall = (time.perf_counter() - t0) / args.steps
+    # the input-order step's outputs (d_*) against the shuffled step's, point by point
+    inv = np.argsort(perm)
+    e0, e1 = d_elem.download(), s_elem.download()[inv]
+    h0, h1 = d_hit.download(), s_hit.download()[inv]
+    located = (h0 != 0) & (h1 != 0)
+    same = located & (e0 == e1) & (h0 == h1)
+    ident = same.copy()
+    for a, b in [(d_mo, s_mo)] + list(zip(d_fo, s_fo)):
+        x0, x1 = a.download(), b.download()[inv]
+        ident &= np.all(x0.view(np.uint64) == x1.view(np.uint64), axis=1)
+    npts = int(st.nvol + st.nbdy)
+    res = {"what": "the step on a random renumbering of the new points (Morton-binned by the module); not the bench "
+                   "value",
+           "morton_binned": bool(st.sorted), "ms_per_step": round(1e3 * wall, 4),
+           "mpts_per_s": round(npts / wall / 1e6, 1), "device_ms_total": round(float(np.mean(ms)), 4),
+           "volume_stage_ms": round(float(np.mean(vol)), 4),
+           "located_points": int(located.sum()), "same_element_as_input_order": int(same.sum()),
+           "same_element_rows_bit_identical": int((same & ident).sum()),
+           "ok": bool(np.all(ident[same])) and int(located.sum()) == npts}
+    log(f"[bench r{rank}] shuffled numbering: {res}")
+    for b in [s_xyz, s_pc, s_mo, s_elem, s_hit] + s_fo:
+        b.free()
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -312,6 +366,8 @@ def main():
                     help="skip the (separately reported) host-buffer, PCIe-inclusive call")
     ap.add_argument("--no-quality", action="store_true",
                     help="skip the (separately reported) tetra-quality timing of the new mesh")
+    ap.add_argument("--no-shuffled", action="store_true",
+                    help="skip the (separately reported) step on a shuffled numbering of the new points")
     ap.add_argument("--no-snapshot", action="store_true",
                     help="skip the (separately reported) device background snapshot timing")
     args = ap.parse_args()
@@ -381,12 +437,15 @@ def main():
         d_elem = ctx.empty((nq,), np.int32)
     d_hit = ctx.empty((nq,), np.int8)
 
-    def step():
+    def step_bg():
         if args.layout == "tet8":
             ctx.set_background_tet8(d_xyz, d_tet8, d_triv, d_adjt, w.hausd)
         else:
             ctx.set_background(d_xyz, d_tetv, d_adja, d_triv, d_adjt, w.hausd)
         ctx.set_solutions(d_met, d_f)
+
+    def step():
+        step_bg()
         ctx.locate_interp(d_qxyz, d_pc, d_mo, d_fo, d_elem, d_hit, sync=False)
 
     log(f"[bench r{rank}] inputs resident in HBM; warmup {args.warmup} steps")
@@ -489,6 +548,11 @@ def main():
             out["host_mode"] = host_mode_timing(ctx, w, bg, met, fields, q_xyz, q_pc, rank)
         except Exception as e:  # reported, never fatal to the bench line
             out["host_mode"] = {"error": str(e)}
+    if not args.no_shuffled and world == 1 and not split:
+        try:
+            out["shuffled_order"] = shuffled_timing(ctx, args, w, step_bg, q_xyz, q_pc, d_mo, d_fo, d_elem, d_hit, rank)
+        except Exception as e:  # reported, never fatal to the bench line
+            out["shuffled_order"] = {"error": str(e)}
     gpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not split:
         # outputs of the last timed step (the host-mode call used its own buffers)
