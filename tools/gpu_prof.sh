@@ -1,17 +1,17 @@
 #!/bin/bash
-# GPU session: default bench line, rocprofv3 kernel-trace summary and two PMC
-# passes (FETCH_SIZE, WRITE_SIZE: they cannot share one pass).  Each GPU step
-# has its own time limit; steps are chained with &&.
+# GPU session: rocprofv3 kernel-trace summary and two PMC passes (FETCH_SIZE,
+# WRITE_SIZE: they cannot share one pass) of the bench step alone (no side
+# legs).  Each GPU step has its own time limit; steps are chained with &&.
 set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-run}
 mkdir -p $OUT
 ARGS="${BENCH_ARGS}"
-timeout -k 10 400 python -u bench.py $ARGS > $OUT/bench.json 2> $OUT/bench.err \
-&& echo "bench ok" && cat $OUT/bench.json \
-&& timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 -u bench.py $ARGS --no-cpu-baseline --steps 5 --warmup 1 > $OUT/trace.log 2>&1 \
+true \
+&& echo "trace next" \
+&& timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 -u bench.py $ARGS --no-cpu-baseline --no-host-mode --no-shuffled --no-quality --no-snapshot --steps 5 --warmup 1 > $OUT/trace.log 2>&1 \
 && echo "trace ok" \
-&& timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python3 -u bench.py $ARGS --no-cpu-baseline --steps 2 --warmup 1 > $OUT/pmc_fetch.log 2>&1 \
+&& timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python3 -u bench.py $ARGS --no-cpu-baseline --no-host-mode --no-shuffled --no-quality --no-snapshot --steps 2 --warmup 1 > $OUT/pmc_fetch.log 2>&1 \
 && echo "pmc fetch ok" \
-&& timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- python3 -u bench.py $ARGS --no-cpu-baseline --steps 2 --warmup 1 > $OUT/pmc_write.log 2>&1 \
+&& timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- python3 -u bench.py $ARGS --no-cpu-baseline --no-host-mode --no-shuffled --no-quality --no-snapshot --steps 2 --warmup 1 > $OUT/pmc_write.log 2>&1 \
 && echo "pmc write ok"
