@@ -399,10 +399,11 @@ def main():
         if shard_mode == "halo":
             from parmmg_amd import shard
             t_sh = time.time()
-            lo, hi = shard.range_box(q_xyz)
-            sh = shard.halo_shard(bg, lo, hi, args.halo, hausd=w.hausd)
+            sh = shard.halo_shard_cells(bg, q_xyz, args.halo, hausd=w.hausd)
             bg, met, fields = sh.mesh, sh.rows(met), [sh.rows(f) for f in fields]
-            halo_info = {"what": "halo shard of the background around this rank's Morton range (rank 0)",
+            halo_info = {"what": "halo shard of the background around this rank's Morton range (rank 0): the tetra "
+                                 "meeting, grown by the halo, the range's box and a halo-sized grid cell holding "
+                                 "one of its points",
                          "tets": bg.ne, "verts": bg.np, "trias": bg.nt, "halo": sh.halo,
                          "tet_fraction_of_group": round(bg.ne / ne_group, 4),
                          "build_s": round(time.time() - t_sh, 2)}

@@ -110,6 +110,8 @@ HOST_API = {
     "pmmg_max_tet_extent": (c_double, [c_int, c_void_p, c_int, c_void_p]),
     "pmmg_shard_mark": (c_int, [c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_double, c_void_p,
                                 c_void_p, P(c_int64)]),
+    "pmmg_shard_mark_cells": (c_int, [c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_double,
+                                      c_void_p, c_void_p, c_double, c_void_p, c_void_p, P(c_int64)]),
     "pmmg_shard_fill": (c_int64, [c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_void_p, c_void_p, c_void_p]),

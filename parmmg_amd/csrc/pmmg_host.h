@@ -106,6 +106,15 @@ double pmmg_max_tet_extent(int np, const double *xyz, int ne, const int *tetv);
 int pmmg_shard_mark(int np, const double *xyz, int ne, const int *tetv, const double box_lo[3],
                     const double box_hi[3], double halo, int *tet_map, int *vert_map, int64_t counts[2]);
 
+/* The same, tighter: the tetra whose bounding box grown by the halo meets
+ * both the range's box (box_lo/box_hi, may be NULL) and one of the grid
+ * cells occ[g_n[0]*g_n[1]*g_n[2]] != 0 (cell (i,j,k) = g_lo + cell *
+ * [i,i+1) x [j,j+1) x [k,k+1), x fastest) that hold the range's points.  A
+ * Morton range's cells hug it; its box can hold half a shell. */
+int pmmg_shard_mark_cells(int np, const double *xyz, int ne, const int *tetv, const double box_lo[3],
+                          const double box_hi[3], const double g_lo[3], double cell, const int g_n[3],
+                          const uint8_t *occ, double halo, int *tet_map, int *vert_map, int64_t counts[2]);
+
 /* Writes the shard: s_xyz[3*nv], s_tetv/s_adja[4*nk] (neighbours outside the
  * shard -> 0), the boundary trias with all vertices in the shard
  * s_triv/s_adjt (room for nt rows) and the 1-based global ids of the local

@@ -5,7 +5,10 @@
  * new points against its own part (src/interpmesh_pmmg.c:690).  For a group
  * too large to replicate on every GPU, a rank that owns a contiguous Morton
  * range of the new points needs only the background tetra around that
- * range: the tetra whose bounding box meets the range's box grown by a halo.
+ * range: the tetra whose bounding box meets the range's box grown by a halo
+ * (pmmg_shard_mark), or, tighter, the union of the grid cells that hold the
+ * range's points (pmmg_shard_mark_cells: a Morton range of a shell has a box
+ * far larger than the range).
  * Every tetra that accepts a point of the range (min barycentric > -EPS)
  * meets that box once the halo exceeds EPS times its extent, so the shard
  * holds every candidate of the range's points.
@@ -73,6 +76,68 @@ int pmmg_shard_mark(int np, const double *xyz, int ne, const int *tetv, const do
     int meets = 1;
     for (int d = 0; d < 3; d++)
       if (th[d] < lo[d] || tl[d] > hi[d]) meets = 0;
+    if (meets) {
+      tet_map[k] = ++nk;
+      for (int i = 0; i < 4; i++) vert_map[v[i] - 1] = 1;
+    } else {
+      tet_map[k] = 0;
+    }
+  }
+  int nv = 0;
+  for (int64_t i = 0; i < np; i++)
+    if (vert_map[i]) vert_map[i] = ++nv;
+  counts[0] = nk;
+  counts[1] = nv;
+  return 1;
+}
+
+int pmmg_shard_mark_cells(int np, const double *xyz, int ne, const int *tetv, const double box_lo[3],
+                          const double box_hi[3], const double g_lo[3], double cell, const int g_n[3],
+                          const uint8_t *occ, double halo, int *tet_map, int *vert_map, int64_t counts[2]) {
+  if (np < 0 || ne < 0 || !counts || !(cell > 0.0) || !g_n || !occ || (ne > 0 && (!xyz || !tetv || !tet_map)) ||
+      (np > 0 && !vert_map))
+    return 0;
+  for (int d = 0; d < 3; d++)
+    if (g_n[d] < 1) return 0;
+  if (halo < 0.0) halo = -halo * pmmg_max_tet_extent(np, xyz, ne, tetv);
+  /* bounding box of the occupied cells: a cheap first test */
+  int clo[3] = {g_n[0], g_n[1], g_n[2]}, chi[3] = {-1, -1, -1};
+  for (int k = 0; k < g_n[2]; k++)
+    for (int j = 0; j < g_n[1]; j++)
+      for (int i = 0; i < g_n[0]; i++)
+        if (occ[i + (int64_t)g_n[0] * (j + (int64_t)g_n[1] * k)]) {
+          const int c[3] = {i, j, k};
+          for (int d = 0; d < 3; d++) {
+            if (c[d] < clo[d]) clo[d] = c[d];
+            if (c[d] > chi[d]) chi[d] = c[d];
+          }
+        }
+  memset(vert_map, 0, sizeof(int) * (size_t)np);
+  int nk = 0;
+  for (int64_t k = 0; k < ne; k++) {
+    const int *v = tetv + 4 * k;
+    for (int i = 0; i < 4; i++)
+      if (v[i] < 1 || v[i] > np) return 0;
+    double tl[3], th[3];
+    tet_box(xyz, v, tl, th);
+    int a[3], b[3], meets = 1;
+    if (box_lo && box_hi) /* and the range's box grown by the halo (pmmg_shard_mark's test) */
+      for (int d = 0; d < 3; d++)
+        if (th[d] < box_lo[d] - halo || tl[d] > box_hi[d] + halo) meets = 0;
+    for (int d = 0; d < 3 && meets; d++) { /* cells met by the tetra's box grown by the halo */
+      a[d] = (int)floor((tl[d] - halo - g_lo[d]) / cell);
+      b[d] = (int)floor((th[d] + halo - g_lo[d]) / cell);
+      if (a[d] < clo[d]) a[d] = clo[d];
+      if (b[d] > chi[d]) b[d] = chi[d];
+      if (a[d] > b[d]) meets = 0;
+    }
+    if (meets) {
+      meets = 0;
+      for (int z = a[2]; z <= b[2] && !meets; z++)
+        for (int y = a[1]; y <= b[1] && !meets; y++)
+          for (int x = a[0]; x <= b[0] && !meets; x++)
+            if (occ[x + (int64_t)g_n[0] * (y + (int64_t)g_n[1] * z)]) meets = 1;
+    }
     if (meets) {
       tet_map[k] = ++nk;
       for (int i = 0; i < 4; i++) vert_map[v[i] - 1] = 1;

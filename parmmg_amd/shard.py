@@ -76,6 +76,41 @@ def halo_shard(bg: Mesh, lo, hi, halo: float = DEFAULT_HALO, hausd: float = 0.0)
     if not lib.pmmg_shard_mark(bg.np, _p(bg.xyz), bg.ne, _p(bg.tetv), _p(lo), _p(hi), h, _p(tet_map),
                                _p(vert_map), counts):
         raise ValueError("pmmg_shard_mark: invalid background")
+    return _fill(bg, tet_map, vert_map, counts, h)
+
+
+def halo_shard_cells(bg: Mesh, q_xyz: np.ndarray, halo: float = DEFAULT_HALO, hausd: float = 0.0,
+                     cell_factor: float = 1.0) -> HaloShard:
+    """Shard of `bg` around the points q_xyz: the tetra whose bounding box,
+    grown by the halo, meets the points' box and a cell (side cell_factor x
+    halo) of a grid over the group that holds one of the points.  Same guarantees as halo_shard
+    (every tetra or tria that can accept a point is kept, the halo is never
+    less than 1.01 * hausd), far fewer tetra for a Morton range whose box is
+    large (a range of a shell)."""
+    lib = host_lib()
+    h = -halo * max_tet_extent(bg) if halo < 0 else float(halo)
+    h = max(h, 1.01 * float(hausd))
+    cell = cell_factor * h
+    g_lo = bg.xyz.min(axis=0) - cell
+    g_n = np.maximum(1, np.ceil((bg.xyz.max(axis=0) + cell - g_lo) / cell).astype(np.int64))
+    occ = np.zeros(int(np.prod(g_n)), np.uint8)
+    if q_xyz.shape[0]:
+        c = np.clip(np.floor((q_xyz - g_lo) / cell).astype(np.int64), 0, g_n - 1)
+        occ[c[:, 0] + g_n[0] * (c[:, 1] + g_n[1] * c[:, 2])] = 1
+    g_lo = np.ascontiguousarray(g_lo, np.float64)
+    g_n32 = np.ascontiguousarray(g_n, np.int32)
+    tet_map = np.empty(bg.ne, np.int32)
+    vert_map = np.empty(bg.np, np.int32)
+    counts = (ctypes.c_int64 * 2)()
+    lo, hi = (np.ascontiguousarray(x, np.float64) for x in range_box(q_xyz))
+    if not lib.pmmg_shard_mark_cells(bg.np, _p(bg.xyz), bg.ne, _p(bg.tetv), _p(lo), _p(hi), _p(g_lo), cell,
+                                     _p(g_n32), _p(occ), h, _p(tet_map), _p(vert_map), counts):
+        raise ValueError("pmmg_shard_mark_cells: invalid background")
+    return _fill(bg, tet_map, vert_map, counts, h)
+
+
+def _fill(bg: Mesh, tet_map, vert_map, counts, h: float) -> HaloShard:
+    lib = host_lib()
     nk, nv = int(counts[0]), int(counts[1])
     xyz = np.empty((nv, 3), np.float64)
     tetv = np.empty((nk, 4), np.int32)

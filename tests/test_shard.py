@@ -17,11 +17,14 @@ from parmmg_amd import ranks, shard, synth
 BDY_CODES = set(range(4, 12))
 
 
-def _shards(case, world, halo=shard.DEFAULT_HALO):
+def _shards(case, world, halo=shard.DEFAULT_HALO, mode="box"):
     new, pc = case["new"], case["pclass"]
     for mine in ranks.morton_shards(new.xyz, pc, world):
-        lo, hi = shard.range_box(new.xyz[mine])
-        yield mine, shard.halo_shard(case["bg"], lo, hi, halo)
+        if mode == "cells":
+            yield mine, shard.halo_shard_cells(case["bg"], new.xyz[mine], halo, hausd=case["hausd"])
+        else:
+            lo, hi = shard.range_box(new.xyz[mine])
+            yield mine, shard.halo_shard(case["bg"], lo, hi, halo)
 
 
 def _empty_result(case):
@@ -78,14 +81,46 @@ def test_shard_structure(kind, n):
     assert np.array_equal(np.nonzero(meets)[0] + 1, sh.tet_gid)
 
 
+def test_cell_shard_structure():
+    """pmmg_shard_mark_cells keeps exactly the tetra whose box grown by the
+    halo meets the range's box and an occupied cell (numpy restatement), a
+    subset of the box shard, with the same renumbered connectivity."""
+    bg = synth.lattice(synth.SHELL, 12)
+    new = synth.lattice(synth.SHELL, 16, jitter=0.2, with_trias=False, with_tetra=False)
+    pc = synth.classes(new)
+    for mine in ranks.morton_shards(new.xyz, pc, 4):
+        q = new.xyz[mine]
+        sh = shard.halo_shard_cells(bg, q, hausd=0.01)
+        h = sh.halo
+        cell = 1.0 * h
+        g_lo = bg.xyz.min(axis=0) - cell
+        g_n = np.maximum(1, np.ceil((bg.xyz.max(axis=0) + cell - g_lo) / cell).astype(np.int64))
+        occ = np.zeros(tuple(g_n[::-1]), bool)
+        c = np.clip(np.floor((q - g_lo) / cell).astype(np.int64), 0, g_n - 1)
+        occ[c[:, 2], c[:, 1], c[:, 0]] = True
+        tl, th = bg.xyz[bg.tetv - 1].min(axis=1), bg.xyz[bg.tetv - 1].max(axis=1)
+        lo, hi = shard.range_box(q)
+        a = np.maximum(np.floor((tl - h - g_lo) / cell).astype(np.int64), 0)
+        b = np.minimum(np.floor((th + h - g_lo) / cell).astype(np.int64), g_n - 1)
+        inbox = np.all((th >= lo - h) & (tl <= hi + h), axis=1)
+        keep = np.zeros(bg.ne, bool)
+        for k in np.nonzero(inbox)[0]:
+            keep[k] = occ[a[k, 2]:b[k, 2] + 1, a[k, 1]:b[k, 1] + 1, a[k, 0]:b[k, 0] + 1].any()
+        assert np.array_equal(np.nonzero(keep)[0] + 1, sh.tet_gid)
+        assert np.array_equal(sh.vert_gid[sh.mesh.tetv - 1], bg.tetv[sh.tet_gid - 1])
+        box = shard.halo_shard(bg, lo, hi, hausd=0.01)
+        assert set(sh.tet_gid.tolist()) <= set(box.tet_gid.tolist())
+
+
+@pytest.mark.parametrize("mode", ["box", "cells"])
 @pytest.mark.parametrize("kind,n_old,n_new,world", [(synth.CUBE, 6, 7, 2), (synth.CUBE, 5, 9, 3),
                                                     (synth.SHELL, 8, 12, 2), (synth.SHELL, 8, 12, 4)])
-def test_halo_shards_oracle_parity(kind, n_old, n_new, world):
+def test_halo_shards_oracle_parity(kind, n_old, n_new, world, mode):
     """Oracle on each rank's halo shard == contract of a transfer on the group."""
     case = make_case(kind=kind, n_old=n_old, n_new=n_new)
     full = _empty_result(case)
     nshard = 0
-    for mine, sh in _shards(case, world):
+    for mine, sh in _shards(case, world, mode=mode):
         B = O.Background(sh.mesh, None if case["met"] is None else sh.rows(case["met"]),
                          [sh.rows(f) for f in case["fields"]], case["hausd"])
         q = np.ascontiguousarray(case["new"].xyz[mine])
@@ -99,14 +134,15 @@ def test_halo_shards_oracle_parity(kind, n_old, n_new, world):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["box", "cells"])
 @pytest.mark.parametrize("kind,n_old,n_new,world", [(synth.CUBE, 6, 7, 3), (synth.SHELL, 12, 16, 4)])
-def test_halo_shards_gpu_parity(kind, n_old, n_new, world):
+def test_halo_shards_gpu_parity(kind, n_old, n_new, world, mode):
     from parmmg_amd.transfer import TransferContext
 
     case = make_case(kind=kind, n_old=n_old, n_new=n_new)
     full = _empty_result(case)
     with TransferContext(0) as ctx:
-        for mine, sh in _shards(case, world):
+        for mine, sh in _shards(case, world, mode=mode):
             m = sh.mesh
             ctx.set_background(m.xyz, m.tetv, m.adja, m.triv, m.adjt, case["hausd"])
             ctx.set_solutions(None if case["met"] is None else sh.rows(case["met"]),
@@ -132,8 +168,7 @@ def _halo_worker(rank, world, port, q):
     case = make_case(kind=synth.SHELL, n_old=8, n_new=12, with_ref=False)  # the same problem on every rank
     shards = ranks.morton_shards(case["new"].xyz, case["pclass"], world)
     mine = shards[rank]
-    lo, hi = shard.range_box(case["new"].xyz[mine])
-    sh = shard.halo_shard(case["bg"], lo, hi)
+    sh = shard.halo_shard_cells(case["bg"], case["new"].xyz[mine], hausd=case["hausd"])  # as bench.py --shard halo
     B = O.Background(sh.mesh, sh.rows(case["met"]), [sh.rows(f) for f in case["fields"]], case["hausd"])
     r = O.run(B, np.ascontiguousarray(case["new"].xyz[mine]), case["pclass"][mine],
               np.arange(1, len(mine) + 1, dtype=np.int32), O.MODE_FRESH)
@@ -182,8 +217,9 @@ def test_gloo_two_ranks_halo_shards():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["box", "cells"])
 @pytest.mark.parametrize("kind,n_old,n_new,world", [(synth.CUBE, 64, 70, 4), (synth.SHELL, 64, 72, 3)])
-def test_halo_shards_gpu_match_group_run_large(kind, n_old, n_new, world):
+def test_halo_shards_gpu_match_group_run_large(kind, n_old, n_new, world, mode):
     """Million-tetra sizes: every rank's halo-shard transfer, mapped to group
     ids, agrees with the transfer on the whole group — same element and
     bit-identical values wherever both walks accepted the same tetra (the
@@ -200,7 +236,7 @@ def test_halo_shards_gpu_match_group_run_large(kind, n_old, n_new, world):
         whole = _empty_result(case)
         ctx.locate_interp(new.xyz, pc, whole["met"], whole["fields"], whole["elem"], whole["hit"])
         parts = _empty_result(case)
-        for mine, sh in _shards(case, world):
+        for mine, sh in _shards(case, world, mode=mode):
             m = sh.mesh
             ctx.set_background(m.xyz, m.tetv, m.adja, m.triv, m.adjt, case["hausd"])
             ctx.set_solutions(sh.rows(case["met"]), [sh.rows(f) for f in case["fields"]])
@@ -213,11 +249,12 @@ def test_halo_shards_gpu_match_group_run_large(kind, n_old, n_new, world):
     done = pc != 0
     assert (parts["elem"][done] > 0).all() and ((parts["hit"][done].astype(np.int32) & 15) != 0).all()
     same = done & (parts["elem"] == whole["elem"]) & (parts["hit"] == whole["hit"])
-    assert same.sum() >= 0.999 * done.sum(), (int(same.sum()), int(done.sum()))
+    # near the cut the walks may take other paths (more cut faces for cell shards: 0.1 % of the points)
+    assert same.sum() >= 0.995 * done.sum(), (int(same.sum()), int(done.sum()))
     for a, b in zip([parts["met"]] + parts["fields"], [whole["met"]] + whole["fields"]):
         assert np.array_equal(a[same], b[same], equal_nan=True)
     # the rest: accepted elements and reference values (oracle, per point)
-    rest = np.nonzero(done & ~same)[0][:200]
+    rest = np.nonzero(done & ~same)[0][:5000]
     for i in rest:
         code = int(parts["hit"][i]) & 15
         if code == 1:  # volume walk: the group accepts the element
