@@ -94,8 +94,8 @@ typedef struct {
   float ms_prepare;      /* bbox, seed grids, input-order coherence test */
   float ms_sort;         /* query order: Morton binning, or stable class compaction */
   float ms_vol;          /* volume locate + interpolate kernels */
-  float ms_bdy;          /* surface locate + interpolate kernel */
-  float ms_fallback;     /* exhaustive / closest kernels */
+  float ms_bdy;          /* surface branch: locate + interpolate, its exhaustive / closest kernels */
+  float ms_fallback;     /* exhaustive / closest kernels of the volume queries */
   float ms_total;        /* whole call, first to last event */
   float ms_vol_locate;   /* the volume walk kernel alone (part of ms_vol) */
 } pmmg_hip_stats;

@@ -20,7 +20,7 @@ constexpr int kQB = 128; // fallback queries staged in LDS per pass
 
 __global__ void k_fallback_init(int *best, int *cidx, unsigned long long *ckey, const int *count, int *bbest,
                                 int *bcidx, unsigned long long *bckey, const int *bcount) {
-  const int n = *count, nb = *bcount;
+  const int n = count ? *count : 0, nb = bcount ? *bcount : 0;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     best[i] = INT_MAX;
     cidx[i] = INT_MAX;

@@ -793,13 +793,17 @@ static void launch_scan(const int *in, long long n, int *out, int *bsum, const D
 }
 
 // exhaustive fallbacks; every kernel reads its list's count on the device
-static void launch_fallbacks(pmmg_hip_ctx *c, const Slots &S, const double *xyz_new, int *elem_out, int8_t *hit_out) {
+// exhaustive fallbacks of the volume queries (main stream, after the exact
+// continuation) and of the surface queries (surface stream, after k_bdy): the
+// lists and their counts live on the device, every kernel reads its count
+static void launch_vol_fallbacks(pmmg_hip_ctx *c, const Slots &S, const double *xyz_new, int *elem_out,
+                                 int8_t *hit_out) {
   const Bg &bg = c->bg;
   hipStream_t s = c->stream;
   DevStats *st = (DevStats *)c->stats.p;
   hipLaunchKernelGGL(k_fallback_init, dim3(64), dim3(kBlock), 0, s, (int *)c->best.p, (int *)c->cidx.p,
-                     (unsigned long long *)c->ckey.p, (const int *)&st->nfb_vol, (int *)c->bbest.p, (int *)c->bcidx.p,
-                     (unsigned long long *)c->bckey.p, (const int *)&st->nfb_bdy);
+                     (unsigned long long *)c->ckey.p, (const int *)&st->nfb_vol, nullptr, nullptr, nullptr,
+                     (const int *)nullptr);
   const int fgrid = 1024;
   hipLaunchKernelGGL(k_vol_exhaust_accept, dim3(fgrid), dim3(kBlock), 0, s, bg, xyz_new, (const int *)c->fb_vol.p, st,
                      (int *)c->best.p);
@@ -808,13 +812,20 @@ static void launch_fallbacks(pmmg_hip_ctx *c, const Slots &S, const double *xyz_
                        st, (const int *)c->best.p, (unsigned long long *)c->ckey.p, pass, (int *)c->cidx.p);
   hipLaunchKernelGGL(k_vol_finish, dim3(64), dim3(kBlock), 0, s, bg, xyz_new, (const int *)c->fb_vol.p, st,
                      (const int *)c->best.p, (const int *)c->cidx.p, S, elem_out, hit_out);
-  if (bg.nt > 0) {
-    for (int pass = 0; pass < 3; pass++)
-      hipLaunchKernelGGL(k_bdy_exhaust, dim3(256), dim3(kBlock), 0, s, bg, xyz_new, (const int *)c->fb_bdy.p, st,
-                         (int *)c->bbest.p, (unsigned long long *)c->bckey.p, pass, (int *)c->bcidx.p);
-    hipLaunchKernelGGL(k_bdy_finish, dim3(64), dim3(kBlock), 0, s, bg, xyz_new, (const int *)c->fb_bdy.p, st,
-                       (const int *)c->bbest.p, (const int *)c->bcidx.p, S, elem_out, hit_out);
-  }
+}
+
+static void launch_bdy_fallbacks(pmmg_hip_ctx *c, hipStream_t s, const Slots &S, const double *xyz_new,
+                                 int *elem_out, int8_t *hit_out) {
+  const Bg &bg = c->bg;
+  DevStats *st = (DevStats *)c->stats.p;
+  hipLaunchKernelGGL(k_fallback_init, dim3(64), dim3(kBlock), 0, s, nullptr, nullptr, nullptr, (const int *)nullptr,
+                     (int *)c->bbest.p, (int *)c->bcidx.p, (unsigned long long *)c->bckey.p,
+                     (const int *)&st->nfb_bdy);
+  for (int pass = 0; pass < 3; pass++)
+    hipLaunchKernelGGL(k_bdy_exhaust, dim3(256), dim3(kBlock), 0, s, bg, xyz_new, (const int *)c->fb_bdy.p, st,
+                       (int *)c->bbest.p, (unsigned long long *)c->bckey.p, pass, (int *)c->bcidx.p);
+  hipLaunchKernelGGL(k_bdy_finish, dim3(64), dim3(kBlock), 0, s, bg, xyz_new, (const int *)c->fb_bdy.p, st,
+                     (const int *)c->bbest.p, (const int *)c->bcidx.p, S, elem_out, hit_out);
 }
 
 // the pipeline on device pointers; enqueues only (no host synchronisation)
@@ -938,6 +949,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     hipLaunchKernelGGL(k_bdy, dim3(8 * blocks_for((np_new + 7) / 8, 256)), dim3(kBlock), 0, sb, bg,
                        (const Frame *)fr, (const int *)sgrid, gs, xyz_new, (const int *)order_b, S, elem_out, hit_out,
                        (int *)c->fb_bdy.p, st, c->maxstep);
+    launch_bdy_fallbacks(c, sb, S, xyz_new, elem_out, hit_out);
     HIPCK(c, hipGetLastError());
   }
   HIPCK(c, hipEventRecord(c->ev[EV_BDY1], sb));
@@ -954,12 +966,12 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
                      (const ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->maxstep);
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[EV_VOL], s));
-  HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_BDY1], 0));
-  HIPCK(c, hipEventRecord(c->ev[EV_JOIN], s));
-
-  // ---- exhaustive fallbacks (lists and counts on the device)
-  launch_fallbacks(c, S, xyz_new, elem_out, hit_out);
+  // ---- exhaustive fallbacks of the volume queries (lists and counts on the
+  // device; the surface ones ran on the surface stream after k_bdy)
+  launch_vol_fallbacks(c, S, xyz_new, elem_out, hit_out);
   HIPCK(c, hipGetLastError());
+  HIPCK(c, hipEventRecord(c->ev[EV_JOIN], s));
+  HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_BDY1], 0));
   HIPCK(c, hipEventRecord(c->ev[EV_END], s));
   c->pending = true;
   return 1;
@@ -1007,8 +1019,8 @@ static int collect_stats(pmmg_hip_ctx *c, pmmg_hip_stats *out) {
   out->ms_vol_locate = ms;
   HIPCK(c, hipEventElapsedTime(&ms, c->ev[EV_BDY0], c->ev[EV_BDY1]));
   out->ms_bdy = ms; // on the surface stream, concurrent with the volume kernels
-  HIPCK(c, hipEventElapsedTime(&ms, c->ev[EV_JOIN], c->ev[EV_END]));
-  out->ms_fallback = ms;
+  HIPCK(c, hipEventElapsedTime(&ms, c->ev[EV_VOL], c->ev[EV_JOIN]));
+  out->ms_fallback = ms; // the volume queries' exhaustive search (the surface one is in ms_bdy)
   HIPCK(c, hipEventElapsedTime(&ms, c->ev[EV_START], c->ev[EV_END]));
   out->ms_total = ms;
   return 1;

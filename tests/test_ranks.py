@@ -80,7 +80,10 @@ def test_morton_shards_partition_and_locality():
         sh = ranks.morton_shards(new.xyz, pclass, world)
         allidx = np.concatenate(sh)
         assert sorted(allidx.tolist()) == np.nonzero(pclass != 0)[0].tolist()  # every processed point once
-        sizes = [len(s) for s in sh]
+        # equal cost: a surface point weighs BDY_WEIGHT volume points
+        cost = [int(np.where(pclass[s] == 2, ranks.BDY_WEIGHT, 1).sum()) for s in sh]
+        assert max(cost) - min(cost) <= ranks.BDY_WEIGHT
+        sizes = [len(s) for s in ranks.morton_shards(new.xyz, pclass, world, bdy_weight=1)]
         assert max(sizes) - min(sizes) <= 1
         codes = ranks.morton_codes(new.xyz[np.nonzero(pclass != 0)[0]])
         cmin = [int(ranks.morton_codes(new.xyz)[s].min()) for s in sh]

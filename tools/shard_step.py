@@ -27,11 +27,12 @@ def main():
     ap.add_argument("--ranks", default="0")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--bdy-weight", type=int, default=ranks.BDY_WEIGHT, help="cost of a surface point in the split")
     ap.add_argument("--mode", default="cells", choices=["cells", "box"], help="halo shard: cell union or range box")
     a = ap.parse_args()
     w = configs.SHORT[a.config]
     bg0, new, met0, fields0, pclass = bench.build_workload(w, 0)
-    shards = ranks.morton_shards(new.xyz, pclass, a.world)
+    shards = ranks.morton_shards(new.xyz, pclass, a.world, a.bdy_weight)
     for r in [int(x) for x in a.ranks.split(",")]:
         mine = shards[r]
         q_xyz, q_pc = np.ascontiguousarray(new.xyz[mine]), np.ascontiguousarray(pclass[mine])
@@ -68,7 +69,8 @@ def main():
             wall = (time.perf_counter() - t0) / a.steps
             res = {"rank": r, "world": a.world, "mode": a.mode, "nvol_exhaust": int(st.nvol_exhaust),
                    "nvol_closest": int(st.nvol_closest), "nbdy_exhaust": int(st.nbdy_exhaust),
-                   "points": int(st.nvol + st.nbdy), "shard_tets": bg.ne,
+                   "points": int(st.nvol + st.nbdy), "nbdy": int(st.nbdy), "sorted": int(st.sorted),
+                   "steps_pp": round(st.steps_total / max(1, st.nvol + st.nbdy), 3), "shard_tets": bg.ne,
                    "shard_tet_fraction": round(bg.ne / bg0.ne, 4), "ms_per_step_wall": round(1e3 * wall, 4)}
             res.update({k: round(float(np.median(v)), 4) for k, v in ms.items()})
             print(res, flush=True)
