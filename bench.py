@@ -485,7 +485,7 @@ def main():
     kvol_ms = float(np.mean(ms_vol))
     kvol_bytes = per_pt * st.nvol
     achieved = kvol_bytes / (kvol_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(w.name)
+    traffic, traffic_src = pmc_traffic(w.name) if not split else (None, "not profiled per rank")
     steps_pp = st.steps_total / max(1, st.nvol + st.nbdy)
     out = {
         "metric": METRIC,
