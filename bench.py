@@ -360,6 +360,9 @@ def main():
                     help="multi-GPU split (auto: halo for N > 1): Morton ranges of the new points against halo "
                          "shards of the background (halo) or a replicated background (morton), results "
                          "all-gathered over RCCL after the timed steps; or one group per rank (group, weak)")
+    ap.add_argument("--split", default="rcb", choices=["rcb", "morton"],
+                    help="split modes: the new points cut by recursive coordinate bisection (compact boxes of equal "
+                         "cost) or into contiguous Morton ranges")
     ap.add_argument("--halo", type=float, default=-1.0,
                     help="halo mode: growth of the range box (< 0: in largest-tetra extents, at least hausd)")
     ap.add_argument("--no-host-mode", action="store_true",
@@ -391,11 +394,11 @@ def main():
     halo_info = None
     sh = None
     if split:
-        shards = ranks.morton_shards(new.xyz, pclass, world)
+        shards = (ranks.rcb_shards if args.split == "rcb" else ranks.morton_shards)(new.xyz, pclass, world)
         mine = shards[rank]
         counts = [len(x) for x in shards]
         q_xyz, q_pc = np.ascontiguousarray(new.xyz[mine]), np.ascontiguousarray(pclass[mine])
-        log(f"[bench r{rank}] Morton range {len(mine)} of {int((pclass != 0).sum())} points")
+        log(f"[bench r{rank}] {args.split} part: {len(mine)} of {int((pclass != 0).sum())} points")
         if shard_mode == "halo":
             from parmmg_amd import shard
             t_sh = time.time()
@@ -458,18 +461,25 @@ def main():
     # timed region: barrier + device sync on both sides
     ranks.barrier(ri)
     ctx.sync()
-    ms_vol, ms_tot, ms_walk = [], [], []
+    # the K steps are enqueued back to back (each call only enqueues; the
+    # host's enqueue of step i+1 overlaps the device's step i), synchronised
+    # once at the end
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-        st = ctx.sync()  # per-step event times of this step (sync adds no device work)
+    ranks.barrier(ri)
+    st = ctx.sync()
+    elapsed = time.perf_counter() - t0
+    log(f"[bench r{rank}] timed {args.steps} steps: {1e3 * elapsed / args.steps:.3f} ms/step")
+    # per-stage device times (HIP events of each step, for the roofline): the
+    # same K steps again, each followed by a read of its event times
+    ms_vol, ms_tot, ms_walk = [], [], []
+    for _ in range(args.steps):
+        step()
+        st = ctx.sync()
         ms_vol.append(st.ms_vol)
         ms_tot.append(st.ms_total)
         ms_walk.append(st.ms_vol_locate)
-    ranks.barrier(ri)
-    ctx.sync()
-    elapsed = time.perf_counter() - t0
-    log(f"[bench r{rank}] timed {args.steps} steps: {1e3 * elapsed / args.steps:.3f} ms/step")
 
     npts = int(st.nvol + st.nbdy)
     agg = ranks.aggregate(ri, npts, elapsed, args.steps)
@@ -505,9 +515,9 @@ def main():
             "description": w.description,
             "background_tets": ne_o, "background_verts": np_o, "new_points": np_n,
             "located_points_per_step": npts, "K_doubles_per_vertex": w.K,
-            "parallelism": (f"Morton-range shards x{world}, replicated background, RCCL all-gather after the step"
+            "parallelism": (f"{args.split} parts x{world}, replicated background, RCCL all-gather after the step"
                             if shard_mode == "morton" else
-                            f"Morton-range shards x{world}, halo-sharded background, RCCL all-gather after the step"
+                            f"{args.split} parts x{world}, halo-sharded background, RCCL all-gather after the step"
                             if shard_mode == "halo" else f"one group per GPU x{world} (weak, no data-path collective)"),
             "query_order": args.sort,
             "tetra_layout": args.layout,

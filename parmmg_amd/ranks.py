@@ -146,6 +146,40 @@ def morton_shards(xyz, pclass, world: int, bdy_weight: int = BDY_WEIGHT):
     return [np.sort(order[cuts[r]:cuts[r + 1]]) for r in range(world)]
 
 
+def rcb_shards(xyz, pclass, world: int, bdy_weight: int = BDY_WEIGHT):
+    """0-based point indices of each rank by recursive coordinate bisection:
+    the processed points (pclass != 0) are cut at the cost-weighted quantile
+    (world_left / world of the cost, a surface point counting bdy_weight
+    volume points) across the longest side of their box, recursively, so
+    that every rank gets a compact box of equal cost.  A contiguous Morton
+    range of a shell can cover two pieces far apart (its box up to 4x the
+    volume its points fill); the halo shard around it and the seed grid over
+    that box are then sparse.  Inside its part a rank keeps the input order
+    of the points.  Skipped points are in no shard."""
+    import numpy as np
+
+    idx = np.nonzero(pclass != 0)[0]
+    w = np.where(pclass[idx] == 2, bdy_weight, 1).astype(np.int64)
+    out = [None] * world
+
+    def cut(sel, wsel, r0, n):
+        if n == 1 or len(sel) == 0:
+            for r in range(r0, r0 + n):
+                out[r] = np.sort(sel) if r == r0 else np.zeros(0, sel.dtype)
+            return
+        p = xyz[sel]
+        d = int(np.argmax(p.max(axis=0) - p.min(axis=0)))
+        o = np.argsort(p[:, d])  # introsort: deterministic, the same split on every rank
+        cw = np.cumsum(wsel[o])
+        nl = n // 2
+        k = int(np.searchsorted(cw, cw[-1] * nl // n, side="right"))
+        cut(sel[o[:k]], wsel[o[:k]], r0, nl)
+        cut(sel[o[k:]], wsel[o[k:]], r0 + nl, n - nl)
+
+    cut(idx, w, 0, world)
+    return out
+
+
 def allgather_rows(ri: RankInfo, rows, counts):
     """All-gather of per-rank row blocks (torch tensors [n_r, C], same dtype
     and C on every rank; counts[r] = n_r): padded to the largest block, one

@@ -91,6 +91,26 @@ def test_morton_shards_partition_and_locality():
         assert codes.dtype == np.uint32
 
 
+def test_rcb_shards_partition_and_boxes():
+    """Recursive coordinate bisection: every processed point once, equal cost
+    per rank, and on a shell compact boxes (a Morton range's box can hold
+    two pieces far apart)."""
+    new = synth.lattice(synth.SHELL, 16, jitter=0.2, with_trias=False)
+    pclass = synth.classes(new, req_every=7)
+    for world in (1, 2, 3, 8):
+        sh = ranks.rcb_shards(new.xyz, pclass, world)
+        allidx = np.concatenate(sh)
+        assert sorted(allidx.tolist()) == np.nonzero(pclass != 0)[0].tolist()
+        cost = [int(np.where(pclass[s] == 2, ranks.BDY_WEIGHT, 1).sum()) for s in sh]
+        assert max(cost) - min(cost) <= 2 * ranks.BDY_WEIGHT
+        assert all(np.all(np.diff(s) > 0) for s in sh)  # input order kept inside a part
+    # 8 parts of a shell: the octants, boxes of half the shell's extent
+    sh = ranks.rcb_shards(new.xyz, pclass, 8)
+    ext = np.ptp(new.xyz, axis=0)
+    for s in sh:
+        assert np.all(np.ptp(new.xyz[s], axis=0) <= 0.51 * ext)
+
+
 def _gather_worker(rank, world, port, q):
     """One rank of the Morton split with a replicated background: the oracle
     transfers this rank's contiguous Morton range (as the module does on its
