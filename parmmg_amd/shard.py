@@ -18,6 +18,7 @@ from ._native import host_lib
 from .synth import Mesh
 
 DEFAULT_HALO = -1.0  # the largest tetra extent around the range's box (and never less than hausd)
+MAX_CELLS = 1 << 27  # occupancy grid of halo_shard_cells (coarser cells past that: a looser, still safe shard)
 
 
 def _p(a):
@@ -91,6 +92,8 @@ def halo_shard_cells(bg: Mesh, q_xyz: np.ndarray, halo: float = DEFAULT_HALO, ha
     h = -halo * max_tet_extent(bg) if halo < 0 else float(halo)
     h = max(h, 1.01 * float(hausd))
     cell = cell_factor * h
+    ext = bg.xyz.max(axis=0) - bg.xyz.min(axis=0)
+    cell = max(cell, float(np.cbrt(np.prod(ext + 2 * cell) / MAX_CELLS)))  # a mask of at most ~MAX_CELLS bytes
     g_lo = bg.xyz.min(axis=0) - cell
     g_n = np.maximum(1, np.ceil((bg.xyz.max(axis=0) + cell - g_lo) / cell).astype(np.int64))
     occ = np.zeros(int(np.prod(g_n)), np.uint8)
