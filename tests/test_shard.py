@@ -18,9 +18,17 @@ BDY_CODES = set(range(4, 12))
 
 
 def _shards(case, world, halo=shard.DEFAULT_HALO, mode="box"):
+    """mode box: Morton ranges, each against its range's box; cells: Morton
+    ranges against the cells of their points; rcb: bench.py's default split
+    (recursive coordinate bisection) against the cells of its points"""
     new, pc = case["new"], case["pclass"]
-    for mine in ranks.morton_shards(new.xyz, pc, world):
-        if mode == "cells":
+    split = ranks.rcb_shards if mode == "rcb" else ranks.morton_shards
+    for mine in split(new.xyz, pc, world):
+        if mode == "rcb":
+            mode_ = "cells"
+        else:
+            mode_ = mode
+        if mode_ == "cells":
             yield mine, shard.halo_shard_cells(case["bg"], new.xyz[mine], halo, hausd=case["hausd"])
         else:
             lo, hi = shard.range_box(new.xyz[mine])
@@ -112,7 +120,7 @@ def test_cell_shard_structure():
         assert set(sh.tet_gid.tolist()) <= set(box.tet_gid.tolist())
 
 
-@pytest.mark.parametrize("mode", ["box", "cells"])
+@pytest.mark.parametrize("mode", ["box", "cells", "rcb"])
 @pytest.mark.parametrize("kind,n_old,n_new,world", [(synth.CUBE, 6, 7, 2), (synth.CUBE, 5, 9, 3),
                                                     (synth.SHELL, 8, 12, 2), (synth.SHELL, 8, 12, 4)])
 def test_halo_shards_oracle_parity(kind, n_old, n_new, world, mode):
@@ -166,7 +174,7 @@ def _halo_worker(rank, world, port, q):
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     ri = ranks.init("gloo")
     case = make_case(kind=synth.SHELL, n_old=8, n_new=12, with_ref=False)  # the same problem on every rank
-    shards = ranks.morton_shards(case["new"].xyz, case["pclass"], world)
+    shards = ranks.rcb_shards(case["new"].xyz, case["pclass"], world)  # bench.py's default split
     mine = shards[rank]
     sh = shard.halo_shard_cells(case["bg"], case["new"].xyz[mine], hausd=case["hausd"])  # as bench.py --shard halo
     B = O.Background(sh.mesh, sh.rows(case["met"]), [sh.rows(f) for f in case["fields"]], case["hausd"])
@@ -201,7 +209,7 @@ def test_gloo_two_ranks_halo_shards():
     case = make_case(kind=synth.SHELL, n_old=8, n_new=12)
     assert np.array_equal(out[0][0], out[1][0])
     assert all(ne < case["bg"].ne for _, ne in out.values())
-    order = np.concatenate(ranks.morton_shards(case["new"].xyz, case["pclass"], world))
+    order = np.concatenate(ranks.rcb_shards(case["new"].xyz, case["pclass"], world))
     got = out[0][0]
     full = _empty_result(case)
     full["elem"][order] = got[:, 0].astype(np.int32)
@@ -217,7 +225,7 @@ def test_gloo_two_ranks_halo_shards():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["box", "cells"])
+@pytest.mark.parametrize("mode", ["box", "cells", "rcb"])
 @pytest.mark.parametrize("kind,n_old,n_new,world", [(synth.CUBE, 64, 70, 4), (synth.SHELL, 64, 72, 3)])
 def test_halo_shards_gpu_match_group_run_large(kind, n_old, n_new, world, mode):
     """Million-tetra sizes: every rank's halo-shard transfer, mapped to group
