@@ -41,8 +41,11 @@ def short(k):
 def main(src, dst):
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
-    bench = json.loads(open(os.path.join(src, "bench.json")).read().strip().splitlines()[-1])
-    json.dump(bench, open(os.path.join(dst, "bench.json"), "w"), indent=1)
+    bpath = os.path.join(src, "bench.json")  # optional: the bench line of the same session
+    bench = {}
+    if os.path.exists(bpath):
+        bench = json.loads(open(bpath).read().strip().splitlines()[-1])
+        json.dump(bench, open(os.path.join(dst, "bench.json"), "w"), indent=1)
     kern = {}
     rows = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv"))))
     for r in rows:
@@ -82,7 +85,8 @@ def main(src, dst):
                    "TCC_EA0_RDREQ and every read request moves a 128 B line (calibrated in profiles/r02a/calib: "
                    "streamed and gathered whole lines, 4-16 B per lane, report exactly half); counters include "
                    "Infinity-Cache hits",
-           "workload": bench["config"]["workload"], "kernels": {}}
+           "workload": bench.get("config", {}).get("workload", os.environ.get("PMMG_PROF_WORKLOAD", "cfg4-shell100M-aniso")),
+           "kernels": {}}
     ncall = max(1, len(fetch.get(next((k for k in fetch if short(k) == "k_seed_vol"), ""), [])))
     for k in set(fetch) | set(write):
         f = fetch.get(k, [0.0])
