@@ -249,7 +249,7 @@ def quality_timing(ctx, w, d_qxyz, d_mo, rank: int, reps: int = 3):
             "algorithmic_gbps": round(nb / t / 1e9, 1)}
 
 
-def host_mode_timing(ctx, w, bg, met, fields, q_xyz, q_pc, rank: int, reps: int = 2):
+def host_mode_timing(ctx, w, bg, met, fields, q_xyz, q_pc, rank: int, reps: int = 3):
     """End-to-end rate with host buffers (PMMG_HIP_HOST), as the C host layer
     runs a group inside ParMmg: the vertices and tetra vertex ids go up
     through the context's pinned staging buffers, the adjacency and the
