@@ -256,7 +256,8 @@ def host_mode_timing(ctx, w, bg, met, fields, q_xyz, q_pc, rank: int, reps: int 
     boundary trias are built on the device (PMMG_create_oldGrp's arrays, not
     uploaded), then the solutions and queries go up, the step runs and the
     rows it wrote come back.  Reported beside the HBM-resident step, never as
-    the bench value."""
+    the bench value: the median of `reps` calls (the first also pays the first
+    touch of the output pages and of the staging buffers)."""
     nq = q_xyz.shape[0]
     mo = np.empty((nq, w.met_size), np.float64)
     fo = [np.empty((nq, f.shape[1]), np.float64) for f in fields]
