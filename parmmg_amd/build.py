@@ -62,7 +62,10 @@ def build_hip(force: bool = False) -> str:
         os.path.join(CSRC, h) for h in ("pmmg_device.hpp", "pmmg_prep.hpp", "pmmg_vol.hpp", "pmmg_bdy.hpp",
                                         "pmmg_fallback.hpp", "pmmg_snapshot.hpp", "pmmg_quality.hpp")]
     if force or _stale(HIP_SO, deps):
-        _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
+        # max-memory-clause scheduling: the gathers of a step issued as clauses
+        # (volume kernel -4.6 % at cfg4, same registers; profiles/r02e/sweep_sched_strategy.txt)
+        _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-mllvm", "-amdgpu-sched-strategy=max-memory-clause",
+              "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
               f"-I{INC}", "-o", HIP_SO, src, snap, qual])
     return HIP_SO
 
