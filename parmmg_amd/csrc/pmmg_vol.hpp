@@ -387,7 +387,8 @@ __device__ __forceinline__ void wave_store_rows(double *out, const double *row, 
 //      64t+l of the rows' image) into LDS, each lane reads back its own row
 //      and accumulates it in the reference's order (PMMG_interp4bar_ani:
 //      mint = sum_i phi_i invmat(M_i), then invmat(mint)), so only one row is
-//      live per lane.  In input order the rows are stored as whole cache lines
+//      live per lane; vertex i+1's loads are issued before vertex i's rows
+//      go through LDS (coop_issue* / coop_land*).  In input order the rows are stored as whole cache lines
 //      through the same LDS image; Morton-binned queries store per lane.
 // The walk's vertex slots and the gather image share one 3 KiB LDS buffer
 // (the phases are sequential within the wave).
@@ -399,38 +400,56 @@ struct VolShared {
   } u;
 };
 
-// rows of one vertex of the wave's 64 queries (myv = this lane's vertex id)
-// into img (row r = query r), C doubles per row; returns this lane's row
-template <int C>
-__device__ __forceinline__ void coop_vertex_rows(const double *in, int stride, int myv, double *img, double *row) {
+// Rows of one vertex of the wave's 64 queries, gathered cooperatively: piece
+// p = 64t + lane of the rows' image (row r = query r, 3 pieces per row: 16
+// bytes of a 6-double row, 8 of a 3-double row) is loaded by lane p % 64 of
+// instruction t.  In two halves, so that the next vertex's gathers are in
+// flight while this vertex's rows go through LDS: coop_issue* loads this
+// lane's three pieces into registers, coop_land* puts them into the image
+// and returns this lane's row.  (The pieces live in named registers: an
+// array of them indexed per vertex went to scratch memory and cost 40 %.)
+__device__ __forceinline__ void coop_issue6(const double *in, int stride, int myv, double2 &p0, double2 &p1,
+                                            double2 &p2) {
   const int lane = __lane_id();
-  if constexpr (C == 6) {
-    double2 b[3];
-#pragma unroll
-    for (int t = 0; t < 3; t++) {
-      const int p = 64 * t + lane, r = p / 3, k = p - 3 * r;
-      const int v = __shfl(myv, r);
-      b[t] = *reinterpret_cast<const double2 *>(in + (size_t)stride * (v - 1) + 2 * k);
-    }
-#pragma unroll
-    for (int t = 0; t < 3; t++) reinterpret_cast<double2 *>(img)[64 * t + lane] = b[t];
-  } else {
-    double b[3];
-#pragma unroll
-    for (int t = 0; t < 3; t++) {
-      const int p = 64 * t + lane, r = p / 3, k = p - 3 * r;
-      const int v = __shfl(myv, r);
-      b[t] = in[(size_t)stride * (v - 1) + k];
-    }
-#pragma unroll
-    for (int t = 0; t < 3; t++) img[64 * t + lane] = b[t];
-  }
+  const int q0 = lane, q1 = 64 + lane, q2 = 128 + lane;
+  const int v0 = __shfl(myv, q0 / 3), v1 = __shfl(myv, q1 / 3), v2 = __shfl(myv, q2 / 3);
+  p0 = *reinterpret_cast<const double2 *>(in + (size_t)stride * (v0 - 1) + 2 * (q0 % 3));
+  p1 = *reinterpret_cast<const double2 *>(in + (size_t)stride * (v1 - 1) + 2 * (q1 % 3));
+  p2 = *reinterpret_cast<const double2 *>(in + (size_t)stride * (v2 - 1) + 2 * (q2 % 3));
+}
+__device__ __forceinline__ void coop_land6(const double2 &p0, const double2 &p1, const double2 &p2, double *img,
+                                           double *row) {
+  const int lane = __lane_id();
+  reinterpret_cast<double2 *>(img)[lane] = p0;
+  reinterpret_cast<double2 *>(img)[64 + lane] = p1;
+  reinterpret_cast<double2 *>(img)[128 + lane] = p2;
   wait_lgkm();
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
-  for (int j = 0; j < C; j++) row[j] = img[C * lane + j];
+  for (int j = 0; j < 6; j++) row[j] = img[6 * lane + j];
   wait_lgkm();
   __builtin_amdgcn_wave_barrier(); // every lane has read its row: the image is free again
+}
+__device__ __forceinline__ void coop_issue3(const double *in, int stride, int myv, double &p0, double &p1,
+                                            double &p2) {
+  const int lane = __lane_id();
+  const int q0 = lane, q1 = 64 + lane, q2 = 128 + lane;
+  const int v0 = __shfl(myv, q0 / 3), v1 = __shfl(myv, q1 / 3), v2 = __shfl(myv, q2 / 3);
+  p0 = in[(size_t)stride * (v0 - 1) + q0 % 3];
+  p1 = in[(size_t)stride * (v1 - 1) + q1 % 3];
+  p2 = in[(size_t)stride * (v2 - 1) + q2 % 3];
+}
+__device__ __forceinline__ void coop_land3(double p0, double p1, double p2, double *img, double *row) {
+  const int lane = __lane_id();
+  img[lane] = p0;
+  img[64 + lane] = p1;
+  img[128 + lane] = p2;
+  wait_lgkm();
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int j = 0; j < 3; j++) row[j] = img[3 * lane + j];
+  wait_lgkm();
+  __builtin_amdgcn_wave_barrier();
 }
 
 // one slot of the wave's queries: rows gathered, interpolated, stored
@@ -440,24 +459,47 @@ __device__ __forceinline__ void vol_slot(const Slot &sl, bool act, const int4 &v
   if constexpr (C > 0) {
     double r[C];
     bool ok = act;
-    if constexpr (C == 6) {
+    if constexpr (C == 6) { // vertex i + 1's gathers in flight while vertex i goes through LDS
       double mint[6], m[6], mi[6];
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        coop_vertex_rows<6>(sl.in, sl.istride, sel4(v, i), img, m);
-        ok = invmat(m, mi) && ok;
-#pragma unroll
-        for (int q = 0; q < 6; q++) mint[q] = (i == 0) ? phi[0] * mi[q] : mint[q] + phi[i] * mi[q];
-      }
+      double2 a0, a1, a2, b0, b1, b2;
+#define PMMG_ACC6(i)                                                                               \
+  do {                                                                                             \
+    ok = invmat(m, mi) && ok;                                                                      \
+    _Pragma("unroll") for (int q = 0; q < 6; q++) mint[q] = (i == 0) ? phi[0] * mi[q] : mint[q] + phi[i] * mi[q]; \
+  } while (0)
+      coop_issue6(sl.in, sl.istride, v.x, a0, a1, a2);
+      coop_issue6(sl.in, sl.istride, v.y, b0, b1, b2);
+      coop_land6(a0, a1, a2, img, m);
+      PMMG_ACC6(0);
+      coop_issue6(sl.in, sl.istride, v.z, a0, a1, a2);
+      coop_land6(b0, b1, b2, img, m);
+      PMMG_ACC6(1);
+      coop_issue6(sl.in, sl.istride, v.w, b0, b1, b2);
+      coop_land6(a0, a1, a2, img, m);
+      PMMG_ACC6(2);
+      coop_land6(b0, b1, b2, img, m);
+      PMMG_ACC6(3);
       ok = invmat(mint, r) && ok;
+#undef PMMG_ACC6
     } else if constexpr (C == 3) {
-      double m[3];
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        coop_vertex_rows<3>(sl.in, sl.istride, sel4(v, i), img, m);
-#pragma unroll
-        for (int q = 0; q < 3; q++) r[q] = (i == 0) ? 0.0 + phi[0] * m[q] : r[q] + phi[i] * m[q];
-      }
+      double m[3], a0, a1, a2, b0, b1, b2;
+#define PMMG_ACC3(i)                                                                               \
+  do {                                                                                             \
+    _Pragma("unroll") for (int q = 0; q < 3; q++) r[q] = (i == 0) ? 0.0 + phi[0] * m[q] : r[q] + phi[i] * m[q]; \
+  } while (0)
+      coop_issue3(sl.in, sl.istride, v.x, a0, a1, a2);
+      coop_issue3(sl.in, sl.istride, v.y, b0, b1, b2);
+      coop_land3(a0, a1, a2, img, m);
+      PMMG_ACC3(0);
+      coop_issue3(sl.in, sl.istride, v.z, a0, a1, a2);
+      coop_land3(b0, b1, b2, img, m);
+      PMMG_ACC3(1);
+      coop_issue3(sl.in, sl.istride, v.w, b0, b1, b2);
+      coop_land3(a0, a1, a2, img, m);
+      PMMG_ACC3(2);
+      coop_land3(b0, b1, b2, img, m);
+      PMMG_ACC3(3);
+#undef PMMG_ACC3
     } else {
       const int vv[4] = {v.x, v.y, v.z, v.w};
       interp_iso_row<4, 1>(sl.in, sl.istride, vv, phi, r);
