@@ -5,14 +5,17 @@ grids + query order + volume/surface locate + metric/field interpolation +
 fallbacks, with every input already resident in HBM (device-mode C-ABI).
 
 N = 1: the whole cfg4 group on one GPU.  N > 1 (torchrun, one process per
-GPU), default ``--shard halo``: every rank owns a contiguous Morton range of
-the new points against the halo shard of the background around that range
-(SURVEY.md §8(e)); the located elements and interpolated rows are collected
-with an RCCL all-gather after the timed steps (reported separately, outside
-the step: ParMmg consumes results per rank).  Strong scaling: `value` =
-points of the whole problem / max-over-ranks step time.  ``--shard morton``
-replicates the background instead; ``--shard group`` gives every rank its own
-group (weak scaling, ParMmg's per-group sharding).
+GPU), default ``--shard halo``: every rank owns a compact part of the new
+points (recursive coordinate bisection into boxes of equal cost, ``--split
+rcb``; ``--split morton`` keeps the north_star's contiguous Morton ranges)
+against the halo shard of the background around that part (SURVEY.md
+§8(e)); the located elements and interpolated rows are collected with an
+RCCL all-gather after the timed steps (reported separately, outside the
+step: ParMmg consumes results per rank) and checked on rank 0 against an
+oracle run over a sample of the whole group (``parity``).  Strong scaling:
+`value` = points of the whole problem / max-over-ranks step time.
+``--shard morton`` replicates the background instead; ``--shard group``
+gives every rank its own group (weak scaling, ParMmg's per-group sharding).
 
 After the timed steps (rank 0, N = 1): the CPU baseline runs the oracle — a C
 restatement of the reference path — over ALL new points in the reference's
@@ -167,30 +170,81 @@ def parity_report(B, new, pclass, gpu, ref) -> dict:
     return out
 
 
-def allgather_timing(ri, d_mo, d_fo, d_elem, counts, rank: int, reps: int = 3):
-    """Split modes: collect every rank's located elements and interpolated
-    rows on every rank (ranks.allgather_rows: RCCL all_gather_into_tensor over
-    xGMI), timed on its own after the timed steps (reported
-    separately; ParMmg itself consumes the results per rank)."""
+def allgather_timing(ri, d_mo, d_fo, d_elem, d_hit, sh, counts, rank: int, reps: int = 3):
+    """Split modes: collect every rank's located elements (mapped to group
+    ids: a halo shard's local ids through its tet_gid / tria_gid), hit codes
+    and interpolated rows on every rank (ranks.allgather_rows: RCCL
+    all_gather_into_tensor over xGMI), timed on its own after the timed steps
+    (reported separately; ParMmg itself consumes the results
+    per rank).  Returns the report and the gathered (rows, elem, hit) as host
+    arrays in rank order."""
     import torch
 
     rows = torch.cat([d_mo] + list(d_fo), dim=1)
-    elem = d_elem.view(-1, 1)
+    hit = d_hit.download()
+    elem = d_elem.cpu().numpy()
+    if sh is not None:
+        elem = sh.to_group_elem(elem, (hit & 15) >= 4)
+    eh = torch.from_numpy(np.stack([elem.astype(np.int32), hit.astype(np.int32)], axis=1)).to(rows.device)
     times = []
     for _ in range(reps):
         ranks.barrier(ri)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         g_rows = ranks.allgather_rows(ri, rows, counts)
-        g_elem = ranks.allgather_rows(ri, elem, counts)
+        g_eh = ranks.allgather_rows(ri, eh, counts)
         torch.cuda.synchronize()
         times.append(ranks.max_over_ranks(ri, time.perf_counter() - t0))
-    ok = bool((g_elem > 0).all().item()) and g_rows.shape[0] == sum(counts)
-    nbytes = sum(counts) * (rows.shape[1] * 8 + 4)
+    nbytes = sum(counts) * (rows.shape[1] * 8 + 8)
     t = float(np.median(times))
-    log(f"[bench r{rank}] all-gather of {nbytes / 1e9:.2f} GB: {1e3 * t:.2f} ms, complete={ok}")
-    return {"what": "RCCL all-gather of {elem, K doubles} per point, not part of the step",
-            "ms": round(1e3 * t, 3), "bytes": int(nbytes), "gbps": round(nbytes / t / 1e9, 1), "complete": ok}
+    log(f"[bench r{rank}] all-gather of {nbytes / 1e9:.2f} GB: {1e3 * t:.2f} ms")
+    rep = {"what": "RCCL all-gather of {group elem id, hit code, K doubles} per point, not part of the step",
+           "ms": round(1e3 * t, 3), "bytes": int(nbytes), "gbps": round(nbytes / t / 1e9, 1),
+           "rows": int(g_rows.shape[0])}
+    g_eh = g_eh.cpu().numpy()
+    return rep, (g_rows.cpu().numpy(), g_eh[:, 0].copy(), g_eh[:, 1].astype(np.int8))
+
+
+def split_parity(w, bg, met, fields, new, pclass, shards, gathered, budget_s: float) -> dict:
+    """Split modes, rank 0: the all-gathered results of every rank, placed at
+    their group points, against an oracle run over the whole group (the
+    reference's visitation order cut into one range per thread, as the CPU
+    baseline, stopped after `budget_s`): every point the oracle processed is
+    checked (tests/parity.py contract: class (i) identity, acceptance, values
+    of the reference interpolator in the chosen element), and every point of
+    the group must have been located by some rank."""
+    from oracle import oracle as O
+
+    g_rows, g_elem, g_hit = gathered
+    idx_all = np.concatenate(shards)
+    n = new.xyz.shape[0]
+    elem = np.zeros(n, np.int32)
+    hit = np.zeros(n, np.int8)
+    elem[idx_all], hit[idx_all] = g_elem, g_hit
+    widths = [met.shape[1]] + [f.shape[1] for f in fields]
+    outs, c0 = [], 0
+    for wd in widths:
+        a = np.full((n, wd), np.nan)
+        a[idx_all] = g_rows[:, c0:c0 + wd]
+        outs.append(a)
+        c0 += wd
+    threads, _ = host_cores()
+    t0 = time.time()
+    new_t = synth.lattice(w.kind, w.n_new, jitter=w.jitter_new, seed=synth.SEED, with_trias=False)
+    order = synth.visit_order(new_t)
+    del new_t
+    B = O.Background(bg, met, fields, w.hausd)
+    ref = O.run(B, new.xyz, pclass, order, budget_s=budget_s, threads=threads)
+    t_run = time.time() - t0
+    pr = parity_report(B, new, pclass, {"elem": elem, "hit": hit, "met": outs[0], "fields": outs[1:]}, ref)
+    missing = int(((pclass != 0) & (hit == 0)).sum())
+    pr["what"] = ("all-gathered results of every rank (group ids) vs an oracle run over the whole group, every "
+                  "point it processed")
+    pr["points_group"] = int((pclass != 0).sum())
+    pr["points_not_located_by_any_rank"] = missing
+    pr["oracle_s"] = round(t_run, 1)
+    pr["ok"] = bool(pr["ok"] and missing == 0)
+    return pr
 
 
 def snapshot_timing(ctx, bg, rank: int, reps: int = 3):
@@ -357,6 +411,8 @@ def main():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=90.0,
                     help="cap of the CPU baseline's locate phase (it normally finishes every point first)")
     ap.add_argument("--no-cpu-baseline", action="store_true", help="skip the CPU baseline (and the parity check)")
+    ap.add_argument("--split-parity-seconds", type=float, default=30.0,
+                    help="split modes: cap of the oracle run (whole group, all threads) that checks the gathered results")
     ap.add_argument("--shard", default="auto", choices=["auto", "group", "morton", "halo"],
                     help="multi-GPU split (auto: halo for N > 1): Morton ranges of the new points against halo "
                          "shards of the background (halo) or a replicated background (morton), results "
@@ -391,6 +447,7 @@ def main():
     # split modes: every rank builds the same problem and keeps its range
     bg, new, met, fields, pclass = build_workload(w, 0 if split else rank)
     ne_group = bg.ne
+    bg_group, met_group, fields_group = bg, met, fields
     counts = None
     halo_info = None
     sh = None
@@ -485,9 +542,9 @@ def main():
 
     npts = int(st.nvol + st.nbdy)
     agg = ranks.aggregate(ri, npts, elapsed, args.steps)
-    gather = None
+    gather = gathered = None
     if split:
-        gather = allgather_timing(ri, d_mo, d_fo, d_elem, counts, rank)
+        gather, gathered = allgather_timing(ri, d_mo, d_fo, d_elem, d_hit, sh, counts, rank)
         npts = agg["points_per_step"]  # the whole problem: bytes per point below are per problem point
     ms_per_step = agg["ms_per_step"]
     value = agg["mpts_per_s"]
@@ -586,8 +643,17 @@ def main():
         log(f"[bench r{rank}] parity of the GPU outputs against the oracle run")
         out["parity"] = parity_report(B_o, new, pclass, gpu, ref)
         log(f"[bench r{rank}] parity: {out['parity']}")
+    if split and rank == 0 and not args.no_cpu_baseline:
+        log(f"[bench r{rank}] parity of the all-gathered results against an oracle run over the group")
+        try:
+            out["parity"] = split_parity(w, bg_group, met_group, fields_group, new, pclass, shards, gathered,
+                                         args.split_parity_seconds)
+        except Exception as e:  # reported, never fatal to the bench line
+            out["parity"] = {"error": str(e), "ok": False}
+        log(f"[bench r{rank}] parity: {out['parity']}")
     if rank == 0:
         print(json.dumps(out), flush=True)
+    ranks.barrier(ri)  # the other ranks wait for rank 0's check
     ranks.finalize(ri)
 
 

@@ -42,6 +42,7 @@ struct Bg {
   int np, ne, nt;
   int tstride;
   double hausd;
+  int fanmax; // cone test: fans longer than this take the full tria scan (kFanMax; test-only PMMG_HIP_FANMAX)
 };
 
 __device__ __forceinline__ int4 tetv_row(const Bg &bg, int k) { return bg.tetv[(size_t)(k - 1) * bg.tstride]; }
@@ -570,11 +571,34 @@ __device__ __forceinline__ int cone_tria(const Bg &bg, int tt, int ip, const dou
   return 1;
 }
 
-__device__ __noinline__ bool tri_cone_scan(const Bg &bg, int ip, const double *p0, const double *p, double dist) {
-  for (int tt = 1; tt <= bg.nt; tt++) {
-    const int *tv = bg.triv + 3 * (size_t)(tt - 1);
+// the O(nt) scan of the rare open / non-manifold / long fan.  Out of line,
+// and every argument passed by value: a pointer to the caller's local arrays
+// (or a reference to its Bg) across a call boundary puts them in scratch
+// memory for the whole kernel (k_bdy: 144 B per lane in r02).
+__device__ __noinline__ bool tri_cone_scan(const int *triv, const double *xyz, int nt, double hausd, int ip,
+                                           double p0x, double p0y, double p0z, double px, double py, double pz,
+                                           double dist) {
+  if (dist > hausd) { // cone_tria's test before the first edge of the first tria of ip
+    for (int tt = 1; tt <= nt; tt++) {
+      const int *tv = triv + 3 * (size_t)(tt - 1);
+      if (tv[0] > 0 && (tv[0] == ip || tv[1] == ip || tv[2] == ip)) return false;
+    }
+    return true;
+  }
+  for (int tt = 1; tt <= nt; tt++) {
+    const int *tv = triv + 3 * (size_t)(tt - 1);
     if (tv[0] <= 0 || (tv[0] != ip && tv[1] != ip && tv[2] != ip)) continue;
-    if (!cone_tria(bg, tt, ip, p0, p, dist)) return false;
+    for (int l = 0; l < 3; l++) { // cone_tria (the distance test passed above)
+      const int jp = tv[l];
+      if (jp == ip) continue;
+      const double *q = xyz + 3 * (size_t)(jp - 1);
+      const double e0 = q[0] - p0x, e1 = q[1] - p0y, e2 = q[2] - p0z;
+      double alpha = 0.0;
+      alpha += e0 * px;
+      alpha += e1 * py;
+      alpha += e2 * pz;
+      if (alpha > 0.0) return false;
+    }
   }
   return true;
 }
@@ -591,10 +615,12 @@ __device__ __forceinline__ bool tri_cone(const Bg &bg, int k, int iloc, const Tr
     int tcur = k;
     int e = dir == 0 ? (iloc + 1) % 3 : (iloc + 2) % 3; // an edge of tcur incident to ip
     for (int it = 0;; it++) {
-      if (it == kFanMax) return tri_cone_scan(bg, ip, p0, p, dist);
+      if (it == bg.fanmax)
+        return tri_cone_scan(bg.triv, bg.xyz, bg.nt, bg.hausd, ip, p0[0], p0[1], p0[2], p[0], p[1], p[2], dist);
       const int code = bg.adjt[3 * (size_t)(tcur - 1) + e];
       const int tn = code / 3, en = code % 3;
-      if (tn == 0) return tri_cone_scan(bg, ip, p0, p, dist); // open or non-manifold fan
+      if (tn == 0) // open or non-manifold fan
+        return tri_cone_scan(bg.triv, bg.xyz, bg.nt, bg.hausd, ip, p0[0], p0[1], p0[2], p[0], p[1], p[2], dist);
       if (tn == k) return true;                                // the fan closed: every tria tested
       if (!cone_tria(bg, tn, ip, p0, p, dist)) return false;
       const int *tvn = bg.triv + 3 * (size_t)(tn - 1);

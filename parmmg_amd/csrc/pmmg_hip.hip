@@ -3,8 +3,9 @@
 //
 // Replaces, behind the C-ABI of include/parmmg_hip.h, the per-group body of
 // PMMG_interpMetricsAndFields (reference src/interpmesh_pmmg.c:477-741):
-//   PMMG_locatePointVol      src/locate_pmmg.c:786-883     -> k_vol_walk, k_vol_walk_exact (pmmg_vol.hpp)
-//   PMMG_interp4bar_*        src/interpmesh_pmmg.c:206-270 -> k_vol_interp<slot layout>      (pmmg_vol.hpp)
+//   PMMG_locatePointVol      src/locate_pmmg.c:786-883     -> k_vol<layout> (fp32 filter walk + exact
+//                                                             acceptance + interpolation), k_vol_walk_exact
+//   PMMG_interp4bar_*        src/interpmesh_pmmg.c:206-270 -> vol_slot / vol_interp_packed in k_vol (pmmg_vol.hpp)
 //   PMMG_locatePointBdy      src/locate_pmmg.c:587-723     -> k_bdy (locate + interpolate)  (pmmg_bdy.hpp)
 //   exhaustive / closest     src/locate_pmmg.c:477-515, 737-770 -> k_*_exhaust*, k_*_finish (pmmg_fallback.hpp)
 // Device arithmetic: pmmg_device.hpp; preparation and query order:
@@ -163,6 +164,7 @@ struct pmmg_hip_ctx {
   int qpb = 64;       // queries per Morton bin (PMMG_HIP_QPB; r02: 64 beats 8 on shuffled and on coherent inputs)
   int maxstep = 4096; // longer walks go to the exact continuation / exhaustive kernels (PMMG_HIP_MAXSTEP; the
                       // reference caps at ne)
+  int fanmax = kFanMax;    // cone fans longer than this take the O(nt) scan (test-only PMMG_HIP_FANMAX)
   int filter_steps = 4096; // step cap of the fp32 filter walk; test-only PMMG_HIP_FILTER_STEPS=0 sends every
                            // volume query to the exact walk
 };
@@ -413,11 +415,22 @@ static int upload(pmmg_hip_ctx *c, DevBuf &b, const void *src, size_t bytes, hip
   return h2d(c, b.p, src, bytes, s ? s : c->stream);
 }
 
+// a background whose snapshot failed is dropped: its tet8 adjacency or
+// boundary trias may be partly written, so no later call may walk it (the
+// 'no background set' guard then fails them until set_background succeeds)
+static void invalidate_bg(pmmg_hip_ctx *c) {
+  c->bg.ne = c->bg.nt = c->bg.np = 0;
+  c->bg.tetv = c->bg.adja = nullptr;
+  c->bg.triv = c->bg.adjt = nullptr;
+  c->bg.xyz = nullptr;
+}
+
 // wait for a deferred device snapshot (host-mode set_background); 0 if it failed
 static int snap_join(pmmg_hip_ctx *c) {
   if (c->snap.joinable()) c->snap.join();
   if (!c->snap_ok) {
     c->snap_ok = 1; // reported once, by the call that joined it
+    invalidate_bg(c);
     return 0;
   }
   return 1;
@@ -463,6 +476,8 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   c->qpb = env_int("PMMG_HIP_QPB", c->qpb);
   c->verbose = env_int("PMMG_HIP_VERBOSE", 0);
   c->maxstep = env_int("PMMG_HIP_MAXSTEP", c->maxstep);
+  c->fanmax = env_int("PMMG_HIP_FANMAX", c->fanmax);
+  c->bg.fanmax = c->fanmax; // every kernel's Bg copy carries it
   c->filter_steps = c->maxstep;
   if (const char *e = getenv("PMMG_HIP_FILTER_STEPS"))
     if (*e && atoi(e) >= 0) c->filter_steps = atoi(e);
@@ -476,7 +491,7 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   (void)hipStreamSynchronize(c->stream);
   (void)hipStreamSynchronize(c->stream2);
   if (c->cstream) (void)hipStreamSynchronize(c->cstream);
-  DevBuf *bufs[] = {&c->o_xyz, &c->o_tetv, &c->o_adja, &c->o_triv, &c->o_adjt, &c->o_met, &c->frame,
+  DevBuf *bufs[] = {&c->o_xyz, &c->o_tetv, &c->o_adja, &c->o_triv, &c->o_adjt, &c->o_met, &c->o_rec, &c->frame,
                     &c->stats, &c->grid, &c->sgrid, &c->cnt, &c->off, &c->binrank, &c->order_v,
                     &c->order_b, &c->cont, &c->xq, &c->scan_a, &c->cls_cnt, &c->qmin, &c->fb_vol, &c->fb_bdy,
                     &c->best, &c->ckey, &c->cidx, &c->bbest, &c->bckey, &c->bcidx, &c->h_xyz,
@@ -635,7 +650,10 @@ static int set_background_impl(pmmg_hip_ctx *c, int np, const double *xyz, int n
     });
     return 1;
   }
-  if (!snapshot()) return 0;
+  if (!snapshot()) {
+    invalidate_bg(c);
+    return 0;
+  }
   if (!dev) HIPCK(c, hipStreamSynchronize(c->stream));
   return 1;
 }
@@ -1227,7 +1245,6 @@ int pmmg_hip_build_boundary(pmmg_hip_ctx *c, int np, int ne, const int *tet8, co
                             const int *tref, int cap, int *nt, int *triv, int *adjt) {
   if (!c) return 0;
   HIPCK(c, hipSetDevice(c->device));
-  if (!snap_join(c)) return 0;
   if (!snap_join(c)) return 0;
   const bool packed = tet8 != nullptr;
   if (np <= 0 || ne <= 0 || !nt || (!packed && (!tetv || !adja)) || cap < 0 || (cap > 0 && !triv)) {

@@ -124,13 +124,19 @@ int pmmg_copy_metrics_and_fields_point(const pmmg_old_group *old, pmmg_new_group
 }
 
 int pmmg_set_constant_metric(pmmg_new_group *g) {
-  /* MMG3D_Set_constantSize: met->size from info.ani; MMG5_Compute_constantSize:
-   * hsiz clamped to the user bounds; MMG5_Set_constantSize: valid points only */
+  /* MMG3D_Set_constantSize: met->size from info.ani; MMG5_Compute_constantSize
+   * (Mmg @889d408, not in the reference tree: parity unpinned) rejects a
+   * uniform size outside the user bounds ("Mismatched options: hmin ... is
+   * greater than hsiz" / "hmax ... is lower than hsiz"), and
+   * PMMG_interpMetricsAndFields_mesh then fails (src/interpmesh_pmmg.c:504);
+   * MMG5_Set_constantSize: valid points only */
   const int size = g->ani ? 6 : 1;
   if (!g->met || g->met_size != size || !(g->hsiz > 0.0)) return 0;
-  double h = g->hsiz;
-  if (g->hmax > 0.0 && h > g->hmax) h = g->hmax;
-  else if (g->hmin > 0.0 && h < g->hmin) h = g->hmin;
+  const double h = g->hsiz;
+  if ((g->hmin > 0.0 && g->hmin > h) || (g->hmax > 0.0 && g->hmax < h)) {
+    fprintf(stderr, "[parmmg_host] mismatched options: hmin (%e), hmax (%e), hsiz (%e)\n", g->hmin, g->hmax, h);
+    return 0;
+  }
   const double isq = 1.0 / (h * h);
   for (int i = 0; i < g->np; i++) {
     if (g->tag && g->tag[i] >= PMMG_TAG_NUL) continue; /* !MG_VOK */

@@ -80,10 +80,11 @@ int pmmg_copy_metrics_and_fields_point(const pmmg_old_group *old, pmmg_new_group
 
 /* MMG3D_Set_constantSize's fill (hsiz > 0 branch of the ismet logic,
  * src/interpmesh_pmmg.c:501-505), restated from Mmg @889d408 (unpinned):
- * MMG5_Compute_constantSize clamps hsiz to [hmin, hmax] (bounds <= 0 are
- * unset), then every valid point gets hsiz (iso, info.ani == 0) or
- * diag(1/hsiz^2) (aniso).  g->met_size must be 6 when g->ani, else 1.
- * Returns 1, or 0 on a size mismatch. */
+ * MMG5_Compute_constantSize rejects hsiz outside [hmin, hmax] (bounds <= 0
+ * are unset; "Mismatched options", the metric is left untouched), else every
+ * valid point gets hsiz (iso, info.ani == 0) or diag(1/hsiz^2) (aniso).
+ * g->met_size must be 6 when g->ani, else 1.  Returns 1, or 0 on a size
+ * mismatch or mismatched options. */
 int pmmg_set_constant_metric(pmmg_new_group *g);
 
 /* PMMG_interpMetricsAndFields over ngrp groups.

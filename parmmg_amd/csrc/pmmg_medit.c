@@ -139,6 +139,14 @@ int pmmg_medit_read_mesh(const char *path, pmmg_medit_mesh *m, char *err, int er
       ok = 0;
       break;
     }
+    /* a repeated entity block is a format error (it would replace the arrays
+       and the count the range checks below use) */
+    if ((!strcmp(kw, "Vertices") && m->xyz) || (!strcmp(kw, "Tetrahedra") && m->tetv) ||
+        (!strcmp(kw, "Triangles") && m->triv)) {
+      seterr(err, errlen, "%s: repeated block %s", path, kw);
+      ok = 0;
+      break;
+    }
     if (!strcmp(kw, "Vertices")) {
       m->np = (int)n;
       m->xyz = (double *)malloc(sizeof(double) * 3 * (size_t)(n ? n : 1));
@@ -156,8 +164,10 @@ int pmmg_medit_read_mesh(const char *path, pmmg_medit_mesh *m, char *err, int er
       if (!vv || !rr) ok = 0;
       for (long long i = 0; ok && i < n; i++) {
         for (int k = 0; ok && k < nv; k++) {
-          ok = read_long(&L, &v) && v >= 1;
-          vv[nv * i + k] = (int)v;
+          /* ids beyond INT_MAX would wrap in the int arrays and pass the
+             range check below: rejected here, before the cast */
+          ok = read_long(&L, &v) && v >= 1 && v <= 2147483647LL;
+          vv[nv * i + k] = ok ? (int)v : 0;
         }
         ok = ok && read_long(&L, &v);
         rr[i] = (int)v;
@@ -188,12 +198,12 @@ int pmmg_medit_read_mesh(const char *path, pmmg_medit_mesh *m, char *err, int er
     ok = 0;
   }
   for (int i = 0; ok && i < 4 * m->ne; i++)
-    if (m->tetv[i] > m->np) {
+    if (m->tetv[i] < 1 || m->tetv[i] > m->np) {
       seterr(err, errlen, "%s: tetrahedron vertex %d out of range", path, m->tetv[i]);
       ok = 0;
     }
   for (int i = 0; ok && i < 3 * m->nt; i++)
-    if (m->triv[i] > m->np) {
+    if (m->triv[i] < 1 || m->triv[i] > m->np) {
       seterr(err, errlen, "%s: triangle vertex %d out of range", path, m->triv[i]);
       ok = 0;
     }

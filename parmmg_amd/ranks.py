@@ -1,10 +1,15 @@
-"""One process per GPU: rank setup and the two reductions the bench needs.
+"""One process per GPU: rank setup, the bench's reductions and the result
+all-gather of the split modes.
 
 ParMmg runs the transfer step per group on every MPI rank with no exchange
 (src/interpmesh_pmmg.c:690-730; interface points are MG_REQ and copied), so
-the data path has no collective.  The only cross-rank traffic is the bench's
-own barrier and the max-over-ranks of the step time, done here through
-torch.distributed ("nccl" = RCCL on the GPU box, "gloo" in the CPU tests).
+the step itself has no collective.  Across ranks there is the bench's
+barrier, the max-over-ranks of the step time and, when one group is split
+over the GPUs (RCB parts or Morton ranges of its new points, bench.py
+--shard halo / morton), one all-gather per output array after the step
+(``allgather_rows``: every rank receives every part's located elements and
+interpolated rows), all through torch.distributed ("nccl" = RCCL over xGMI
+on the GPU box, "gloo" in the CPU tests).
 """
 from __future__ import annotations
 

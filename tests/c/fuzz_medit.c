@@ -20,6 +20,7 @@ static char *slurp(const char *path, long *n) {
   fseek(f, 0, SEEK_SET);
   char *b = malloc((size_t)*n + 1);
   if (fread(b, 1, (size_t)*n, f) != (size_t)*n) *n = 0;
+  b[*n] = 0; /* strstr below */
   fclose(f);
   return b;
 }
@@ -77,6 +78,39 @@ int main(int argc, char **argv) {
       dump(scratch, t, n);
       oks += run(scratch, which == 0);
       calls++;
+    }
+    if (which == 0) {
+      /* a vertex id past INT_MAX in the Tetrahedra block (would wrap to a
+         negative int): must be rejected */
+      char *tb = strstr(b, "Tetrahedra");
+      if (tb) {
+        char *nl = strchr(tb, '\n');
+        if (nl) nl = strchr(nl + 1, '\n'); /* end of the count line */
+        if (nl) {
+          FILE *f = fopen(scratch, "wb");
+          fwrite(b, 1, (size_t)(nl + 1 - b), f);
+          fputs("4294967297 1 2 3 0\n", f);
+          fwrite(nl + 1, 1, (size_t)(n - (nl + 1 - b)), f);
+          fclose(f);
+          const int ok = run(scratch, 1);
+          printf("fuzz_medit: huge vertex id accepted=%d\n", ok);
+          oks += ok;
+          calls++;
+        }
+      }
+      /* the Vertices block twice: must be rejected (no leak of the first) */
+      char *vb = strstr(b, "Vertices"), *end = strstr(b, "End");
+      if (vb && end && end > vb) {
+        FILE *f = fopen(scratch, "wb");
+        fwrite(b, 1, (size_t)(end - b), f);
+        fwrite(vb, 1, (size_t)(end - vb), f);
+        fputs("End\n", f);
+        fclose(f);
+        const int ok = run(scratch, 1);
+        printf("fuzz_medit: repeated block accepted=%d\n", ok);
+        oks += ok;
+        calls++;
+      }
     }
     free(t);
     free(b);

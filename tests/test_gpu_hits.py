@@ -84,6 +84,31 @@ def test_cone_and_wedge_hits(packed):
 
 
 @pytest.mark.gpu
+def test_cone_fan_scan_equals_rotation(monkeypatch):
+    """The cone test walks the vertex's tria fan through adjt and falls back
+    to scanning every tria (the node->tria list) when the fan is open,
+    non-manifold or longer than kFanMax.  Test-only PMMG_HIP_FANMAX=1 sends
+    every cone test through the scan: same hits, same elements, bit-identical
+    rows as the rotation."""
+    case = make_case(kind=synth.CUBE, n_old=6, n_new=7, fields=(synth.F_SCALAR, synth.F_VECTOR), with_ref=False)
+    x = case["new"].xyz.copy()
+    corner = np.all(np.isclose(x, 0) | np.isclose(x, 1), axis=1)
+    for i in np.nonzero(corner)[0]:
+        x[i] += 0.003 * np.where(x[i] > 0.5, 1.0, -1.0)
+    case = _with_points(case, x)
+    base = run_gpu(case, tet8=True)
+    monkeypatch.setenv("PMMG_HIP_FANMAX", "1")  # read by pmmg_hip_create
+    scan = run_gpu(case, tet8=True)
+    assert _codes(base)[8] == int(corner.sum())
+    np.testing.assert_array_equal(scan["hit"], base["hit"])
+    np.testing.assert_array_equal(scan["elem"], base["elem"])
+    np.testing.assert_array_equal(scan["met"], base["met"])
+    for a, b in zip(scan["fields"], base["fields"]):
+        np.testing.assert_array_equal(a, b)
+    assert check(case, scan)["class_i"] >= 0
+
+
+@pytest.mark.gpu
 def test_closest_hits():
     """Volume points outside the background (code 3: closest tetra) and
     surface points beyond hausd of every tria (code 11: closest tria)."""

@@ -119,15 +119,20 @@ def test_host_layer_groups_and_hsiz(device_built):
             case["pclass"] = np.where(req, 0, np.where(case["new"].isbdy == 1, 2, 1)).astype(np.uint8)
             rep = check(case, dict(met=g["met"], fields=g["fields"], elem=g["elem"], hit=g["hit"]))
             assert rep["n"] == int((~req).sum())
-        # hsiz > 0: constant metric (clamped to hmax), fields still interpolated
+        # hsiz > 0: constant metric, fields still interpolated
         for g in news:
             g["met"][:] = np.nan
-            g["hsiz"], g["hmax"] = 0.05, 0.04
+            g["hsiz"], g["hmax"] = 0.04, 0.05
         ier, st = interp_metrics_and_fields(ctx, olds, news, input_met=1)
         assert ier == 1
         for g in news:
             np.testing.assert_array_equal(g["met"][:, 0], np.full(g["met"].shape[0], 1.0 / 0.04 ** 2))
             np.testing.assert_array_equal(g["met"][:, 1], 0.0)
+        # hsiz above hmax: MMG5_Compute_constantSize's mismatched options -> the call fails
+        for g in news:
+            g["hsiz"], g["hmax"] = 0.05, 0.04
+        ier, st = interp_metrics_and_fields(ctx, olds, news, input_met=1)
+        assert ier == 0
 
 
 @pytest.mark.gpu

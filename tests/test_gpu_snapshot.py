@@ -80,6 +80,42 @@ def test_snapshot_rejects_invalid_connectivity():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("host_mode", [True, False])
+def test_failed_snapshot_drops_the_background(host_mode):
+    """A background whose device snapshot fails (non-manifold: a third tetra
+    on an interior face) must not stay usable: its adjacency is partly
+    written.  Host mode defers the snapshot to a host thread (the failure is
+    reported by the next call); every later locate_interp fails cleanly until
+    a valid set_background."""
+    case = make_case(kind=synth.CUBE, n_old=3, n_new=4, with_ref=False)
+    bg = case["bg"]
+    k = int(np.nonzero((bg.adja > 0).all(axis=1))[0][0])
+    extra = np.ascontiguousarray(np.concatenate([bg.tetv, bg.tetv[k:k + 1, [1, 0, 2, 3]]]).astype(np.int32))
+    q, pc = case["new"].xyz, case["pclass"]
+    n = q.shape[0]
+    with TransferContext(0) as ctx:
+        def locate():
+            mo = np.full((n, case["met"].shape[1]), np.nan)
+            fo = [np.full((n, f.shape[1]), np.nan) for f in case["fields"]]
+            ctx.locate_interp(q, pc, mo, fo, np.zeros(n, np.int32), np.zeros(n, np.int8))
+
+        if host_mode:
+            ctx.set_background(bg.xyz, extra, None, None, None, case["hausd"])  # snapshot deferred
+            with pytest.raises(RuntimeError):
+                ctx.set_solutions(case["met"], case["fields"])  # joins the failed snapshot
+        else:
+            with pytest.raises(RuntimeError, match="more than two"):
+                ctx.set_background(ctx.upload(bg.xyz), ctx.upload(extra), None, None, None, case["hausd"])
+        for _ in range(2):
+            with pytest.raises(RuntimeError):
+                locate()
+        # a valid background makes the context usable again
+        ctx.set_background(bg.xyz, bg.tetv, None, None, None, case["hausd"])
+        ctx.set_solutions(case["met"], case["fields"])
+        locate()
+
+
+@pytest.mark.gpu
 def test_transfer_on_device_snapshot_is_identical():
     """Locate + interpolate against the device-built background gives the
     same outputs bit for bit as against the host-built arrays."""

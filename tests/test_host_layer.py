@@ -135,13 +135,17 @@ def test_constant_metric(ani):
     else:
         np.testing.assert_array_equal(met[ok, 0], 0.2)
     assert np.isnan(met[3]).all()  # !MG_VOK points untouched
-    # hsiz clamped to the user bounds (MMG5_Compute_constantSize)
+    # hsiz outside the user bounds: MMG5_Compute_constantSize's "Mismatched
+    # options" error (the metric is left untouched), inside them: accepted
+    before = met.copy()
     g.update(hmin=0.3, hmax=0.0)
-    assert set_constant_metric(g) == 1
-    np.testing.assert_array_equal(met[ok, 0], 1.0 / (0.3 * 0.3) if ani else 0.3)
+    assert set_constant_metric(g) == 0
     g.update(hmin=0.0, hmax=0.1)
+    assert set_constant_metric(g) == 0
+    np.testing.assert_array_equal(met[ok], before[ok])
+    g.update(hmin=0.1, hmax=0.3)
     assert set_constant_metric(g) == 1
-    np.testing.assert_array_equal(met[ok, 0], 1.0 / (0.1 * 0.1) if ani else 0.1)
+    np.testing.assert_array_equal(met[ok, 0], 1.0 / (0.2 * 0.2) if ani else 0.2)
     # the array must have the size info.ani asks for
     g["met"] = np.zeros((n, 1 if ani else 6))
     assert set_constant_metric(g) == 0

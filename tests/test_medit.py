@@ -103,3 +103,6 @@ def test_reader_survives_corrupted_fixtures_under_asan(tmp_path):
                        text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stdout[-3000:]
     assert "fuzz_medit:" in r.stdout
+    # an id past INT_MAX and a repeated entity block are rejected
+    assert "huge vertex id accepted=0" in r.stdout, r.stdout[-500:]
+    assert "repeated block accepted=0" in r.stdout, r.stdout[-500:]
