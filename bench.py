@@ -53,9 +53,7 @@ def log(*a):
 
 def build_workload(w: configs.Workload, rank: int):
     t0 = time.time()
-    bg = synth.lattice(w.kind, w.n_old, jitter=0.0)
-    new = synth.lattice(w.kind, w.n_new, jitter=w.jitter_new, seed=synth.SEED + rank, with_trias=False,
-                        with_tetra=False)
+    bg, new = configs.build_meshes(w, seed=synth.SEED + rank)
     met = synth.solution(w.metric, bg.xyz)
     fields = [synth.solution(f, bg.xyz) for f in w.fields]
     pclass = synth.classes(new)
@@ -82,15 +80,32 @@ def pmc_traffic(workload: str):
         return None, None
 
 
+def cgroup_cpus() -> float | None:
+    """The CPU quota of this process's cgroup (cgroup v2 cpu.max: quota /
+    period), or None when unlimited / unreadable."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        return None if q == "max" else int(q) / int(p)
+    except (OSError, ValueError):
+        return None
+
+
 def host_cores() -> tuple[int, int]:
-    """(threads used, CPUs visible): the CPUs this process may run on, capped
-    at the pool's per-GPU share (a one-GPU box shows the whole machine)."""
+    """(threads used, CPUs visible): every host core this process can use —
+    the CPUs of its affinity mask, bounded by its cgroup's CPU quota (a
+    one-GPU box shows all 256 CPUs of the machine but grants the job 16 of
+    them through cpu.max; more threads than that are throttled, not
+    faster).  Without a quota: the affinity mask, capped at the pool's
+    per-GPU share."""
     try:
         vis = len(os.sched_getaffinity(0))
     except AttributeError:
         vis = os.cpu_count() or 1
     env = int(os.environ.get("PMMG_CPU_THREADS", "0"))
-    return (env or min(vis, BOX_CPU_SHARE)), vis
+    quota = cgroup_cpus()
+    usable = min(vis, max(1, int(quota))) if quota else min(vis, BOX_CPU_SHARE)
+    return (env or usable), vis
 
 
 def cpu_baseline(w, bg, met, fields, pclass, new, budget_s: float):
@@ -121,9 +136,12 @@ def cpu_baseline(w, bg, met, fields, pclass, new, budget_s: float):
         "value": round(ntot / t_full / 1e6, 4),
         "unit": "Mpts/s",
         "cores": threads,
+        "cpus_visible": visible,
+        "cgroup_cpu_quota": cgroup_cpus(),
         "kind": "port",
-        "sample": f"oracle (C restatement of the reference path) as {threads} threads ({visible} CPUs visible; "
-                  f"{BOX_CPU_SHARE} = the box's per-GPU CPU share), one contiguous range of the reference's "
+        "sample": f"oracle (C restatement of the reference path) as {threads} threads = every usable host core "
+                  f"({visible} CPUs visible, cgroup cpu.max quota {cgroup_cpus()} CPUs), one contiguous range of the "
+                  f"reference's "
                   f"visitation order each (like MPI ranks), on {w.name}: precompute over {bg.ne} tets "
                   f"({t_pre:.2f}s) + locate/interp of {nproc} of {ntot} points ({100 * frac:.1f}%, {t_loc:.2f}s)"
                   + ("" if nproc == ntot else ", rate extrapolated to all points"),
@@ -343,15 +361,31 @@ def host_mode_timing(ctx, w, bg, met, fields, q_xyz, q_pc, rank: int, reps: int 
             "bytes_up": int(up), "bytes_down": int(down), "pcie_gbps_effective": round((up + down) / t / 1e9, 1)}
 
 
-def shuffled_timing(ctx, args, w, step_bg, q_xyz, q_pc, d_mo, d_fo, d_elem, d_hit, rank: int):
-    """The same step on a random renumbering of the new points (no spatial
-    coherence in the input order: the module detects it and Morton-bins the
-    queries, the path for numberings that are not spatially coherent).
-    Reported beside the bench value, which is measured on the generator's
-    lattice numbering.  Checked against the input-order step: a point
-    located in the same element gets bit-identical rows."""
+def mmg_like_perm(nq: int) -> np.ndarray:
+    """A numbering of the new points like Mmg's output after an adaptation
+    (src/libparmmg1.c:692-741: the group is renumbered, then Mmg keeps the
+    retained vertices in their order and appends the vertices it inserts,
+    in creation order): one point in six (a splitmix64 hash of its id,
+    spread evenly over the domain) counts as inserted and moves to the end,
+    both parts keeping the generator's order.  perm[new id] = old id."""
+    ids = np.arange(nq, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = ids * np.uint64(0x9E3779B97F4A7C15) + np.uint64(0x5EED2025)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z ^= z >> np.uint64(31)
+    ins = (z % np.uint64(6)) == 0
+    return np.concatenate([np.nonzero(~ins)[0], np.nonzero(ins)[0]])
+
+
+def renumbered_timing(ctx, args, w, step_bg, q_xyz, q_pc, d_mo, d_fo, d_elem, d_hit, rank: int, perm, what: str):
+    """The same step on a renumbering of the new points (perm[new id] = old
+    id); the module decides on the device whether the numbering is
+    spatially coherent (input order) or Morton-bins the queries.  Reported
+    beside the bench value, which is measured on the generator's lattice
+    numbering.  Checked against the input-order step: a point located in
+    the same element gets bit-identical rows."""
     nq = q_xyz.shape[0]
-    perm = np.random.default_rng(2024).permutation(nq)
     s_xyz, s_pc = ctx.upload(np.ascontiguousarray(q_xyz[perm])), ctx.upload(np.ascontiguousarray(q_pc[perm]))
     s_mo = ctx.empty((nq, w.met_size), np.float64)
     s_fo = [ctx.empty(f.shape, np.float64) for f in d_fo]
@@ -383,18 +417,98 @@ def shuffled_timing(ctx, args, w, step_bg, q_xyz, q_pc, d_mo, d_fo, d_elem, d_hi
         x0, x1 = a.download(), b.download()[inv]
         ident &= np.all(x0.view(np.uint64) == x1.view(np.uint64), axis=1)
     npts = int(st.nvol + st.nbdy)
-    res = {"what": "the step on a random renumbering of the new points (Morton-binned by the module); not the bench "
-                   "value",
+    res = {"what": what,
            "morton_binned": bool(st.sorted), "ms_per_step": round(1e3 * wall, 4),
            "mpts_per_s": round(npts / wall / 1e6, 1), "device_ms_total": round(float(np.mean(ms)), 4),
            "volume_stage_ms": round(float(np.mean(vol)), 4),
            "located_points": int(located.sum()), "same_element_as_input_order": int(same.sum()),
            "same_element_rows_bit_identical": int((same & ident).sum()),
            "ok": bool(np.all(ident[same])) and int(located.sum()) == npts}
-    log(f"[bench r{rank}] shuffled numbering: {res}")
+    log(f"[bench r{rank}] renumbered ({what}): {res}")
     for b in [s_xyz, s_pc, s_mo, s_elem, s_hit] + s_fo:
         b.free()
     return res
+
+
+def surface_solo(ctx, step_bg, q_xyz, q_pc, d_mo, d_fo, d_elem, d_hit, reps: int = 5) -> dict:
+    """The surface branch (k_seed_srf + k_bdy + its fallbacks, second
+    stream) timed alone: the same call with every volume point marked
+    skipped, so nothing runs beside it (in the step it overlaps the volume
+    kernel, and its event span then includes queueing behind that kernel's
+    blocks)."""
+    pc = np.where(q_pc == 2, 2, 0).astype(np.uint8)
+    d_pc = ctx.upload(pc)
+    ms_bdy, ms_tot = [], []
+    for r in range(reps + 1):
+        step_bg()
+        ctx.locate_interp(q_xyz, d_pc, d_mo, d_fo, d_elem, d_hit, sync=False)
+        st = ctx.sync()
+        if r:
+            ms_bdy.append(st.ms_bdy)
+            ms_tot.append(st.ms_total)
+    d_pc.free()
+    return {"what": "surface branch alone (volume points skipped): HIP events of the surface stream",
+            "surface_points": int(st.nbdy), "ms_surface_branch": round(float(np.median(ms_bdy)), 4),
+            "ms_call": round(float(np.median(ms_tot)), 4)}
+
+
+def graded_leg(args, rank: int, budget_s: float = 60.0) -> dict:
+    """cfgG (configs.CFGG): cfg3's lattices graded 1000x towards three planes
+    and sheared (elements up to ~1000:1, the geometry of the reference's
+    anisotropic torus-with-a-planar-shock runs), the same step timed in its
+    own context, with the fp32 filter walk's hand-overs to the exact walk
+    (nvol_exact), the longest walk and the steps per point, and every point
+    checked against an oracle run (reported beside the bench value)."""
+    w = configs.CFGG
+    bg, new = configs.build_meshes(w, seed=synth.SEED, with_new_tetra=True)
+    visit = synth.visit_order(new)
+    pc = synth.classes(new)
+    met = synth.solution(w.metric, bg.xyz)
+    fields = [synth.solution(f, bg.xyz) for f in w.fields]
+    stats = synth.cell_stats(bg)
+    ctx = TransferContext(0)
+    d_xyz, d_tet8 = ctx.upload(bg.xyz), ctx.upload(pack_tet8(bg.tetv, bg.adja))
+    d_triv, d_adjt = ctx.upload(bg.triv), ctx.upload(bg.adjt)
+    d_met, d_f = ctx.upload(met), [ctx.upload(f) for f in fields]
+    d_q, d_pc = ctx.upload(new.xyz), ctx.upload(pc)
+    nq = new.np
+    d_mo = ctx.empty((nq, w.met_size), np.float64)
+    d_fo = [ctx.empty((nq, f.shape[1]), np.float64) for f in fields]
+    d_el, d_hit = ctx.empty((nq,), np.int32), ctx.empty((nq,), np.int8)
+
+    def step():
+        ctx.set_background_tet8(d_xyz, d_tet8, d_triv, d_adjt, w.hausd)
+        ctx.set_solutions(d_met, d_f)
+        ctx.locate_interp(d_q, d_pc, d_mo, d_fo, d_el, d_hit, sync=False)
+
+    for _ in range(max(1, args.warmup)):
+        step()
+        ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    st = ctx.sync()
+    wall = (time.perf_counter() - t0) / args.steps
+    gpu = {"elem": d_el.download(), "hit": d_hit.download(), "met": d_mo.download(),
+           "fields": [f.download() for f in d_fo]}
+    ctx.close()
+    npts = int(st.nvol + st.nbdy)
+    out = {"what": "cfgG: the step on a graded (1000x towards three planes per mesh, the new mesh's planes moved) "
+                   "and sheared cube (cfg3's lattices), own context; not the bench value",
+           "workload": w.name, "background_tets": bg.ne, "new_points": nq,
+           "size_grading": round(stats["size_grading"], 1), "max_aspect_ratio": round(stats["max_aspect"], 1),
+           "ms_per_step": round(1e3 * wall, 4), "mpts_per_s": round(npts / wall / 1e6, 1),
+           "volume_stage_ms": round(float(st.ms_vol), 4), "nvol": int(st.nvol), "nvol_exact": int(st.nvol_exact),
+           "nvol_exhaust": int(st.nvol_exhaust), "stepmax": int(st.stepmax),
+           "walk_steps_per_point": round(st.steps_total / max(1, npts), 3)}
+    if not args.no_cpu_baseline:
+        from oracle import oracle as O
+        threads, _ = host_cores()
+        B = O.Background(bg, met, fields, w.hausd)
+        ref = O.run(B, new.xyz, pc, visit, budget_s=budget_s, threads=threads)
+        out["parity"] = parity_report(B, new, pc, gpu, ref)
+    log(f"[bench r{rank}] graded leg: {out}")
+    return out
 
 
 def main():
@@ -430,6 +544,8 @@ def main():
                     help="skip the (separately reported) step on a shuffled numbering of the new points")
     ap.add_argument("--no-snapshot", action="store_true",
                     help="skip the (separately reported) device background snapshot timing")
+    ap.add_argument("--no-graded", action="store_true",
+                    help="skip the (separately reported) step on the graded and stretched cfgG meshes")
     args = ap.parse_args()
 
     # PMMG_BENCH_BACKEND=gloo: host-side collectives, ranks share the visible
@@ -619,11 +735,23 @@ def main():
             out["host_mode"] = host_mode_timing(ctx, w, bg, met, fields, q_xyz, q_pc, rank)
         except Exception as e:  # reported, never fatal to the bench line
             out["host_mode"] = {"error": str(e)}
-    if not args.no_shuffled and world == 1 and not split:
+    if world == 1 and not split:
         try:
-            out["shuffled_order"] = shuffled_timing(ctx, args, w, step_bg, q_xyz, q_pc, d_mo, d_fo, d_elem, d_hit, rank)
+            out["surface_solo"] = surface_solo(ctx, step_bg, d_qxyz, q_pc, d_mo, d_fo, d_elem, d_hit)
         except Exception as e:  # reported, never fatal to the bench line
-            out["shuffled_order"] = {"error": str(e)}
+            out["surface_solo"] = {"error": str(e)}
+    if not args.no_shuffled and world == 1 and not split:
+        legs = {"mmg_like_order": (mmg_like_perm(nq), "the step on an Mmg-like numbering of the new points (1 in 6 "
+                                   "points moved to the end as 'inserted', both parts in the generator's order); not "
+                                   "the bench value"),
+                "shuffled_order": (np.random.default_rng(2024).permutation(nq), "the step on a random renumbering of "
+                                   "the new points (Morton-binned by the module); not the bench value")}
+        for name, (perm, what) in legs.items():
+            try:
+                out[name] = renumbered_timing(ctx, args, w, step_bg, q_xyz, q_pc, d_mo, d_fo, d_elem, d_hit, rank,
+                                              perm, what)
+            except Exception as e:  # reported, never fatal to the bench line
+                out[name] = {"error": str(e)}
     gpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not split:
         # outputs of the last timed step (the host-mode call used its own buffers)
@@ -637,6 +765,11 @@ def main():
     if not args.no_snapshot and halo_info is None:  # (a shard's cut faces are no boundary trias)
         out["snapshot"] = snapshot_timing(ctx, bg, rank)
     ctx.close()
+    if not args.no_graded and world == 1 and not split and args.config == "cfg4":
+        try:
+            out["graded"] = graded_leg(args, rank)
+        except Exception as e:  # reported, never fatal to the bench line
+            out["graded"] = {"error": str(e)}
     if gpu is not None:
         log(f"[bench r{rank}] cpu baseline (oracle) over all points")
         out["cpu_baseline"], B_o, ref = cpu_baseline(w, bg, met, fields, pclass, new, args.cpu_baseline_seconds)

@@ -165,8 +165,10 @@ struct pmmg_hip_ctx {
   int maxstep = 4096; // longer walks go to the exact continuation / exhaustive kernels (PMMG_HIP_MAXSTEP; the
                       // reference caps at ne)
   int fanmax = kFanMax;    // cone fans longer than this take the O(nt) scan (test-only PMMG_HIP_FANMAX)
-  int filter_steps = 4096; // step cap of the fp32 filter walk; test-only PMMG_HIP_FILTER_STEPS=0 sends every
-                           // volume query to the exact walk
+  int filter_steps = 64; // step cap of the fp32 filter walk (then the exact fp64 walk continues from where it
+                         // stopped: a query the filter misjudges hands over early instead of cycling through a
+                         // 4-entry history for up to maxstep steps); test-only PMMG_HIP_FILTER_STEPS=0 sends every
+                         // volume query to the exact walk
 };
 
 static void set_err(pmmg_hip_ctx *c, const char *fmt, ...) {
@@ -478,7 +480,7 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   c->maxstep = env_int("PMMG_HIP_MAXSTEP", c->maxstep);
   c->fanmax = env_int("PMMG_HIP_FANMAX", c->fanmax);
   c->bg.fanmax = c->fanmax; // every kernel's Bg copy carries it
-  c->filter_steps = c->maxstep;
+  c->filter_steps = c->filter_steps < c->maxstep ? c->filter_steps : c->maxstep;
   if (const char *e = getenv("PMMG_HIP_FILTER_STEPS"))
     if (*e && atoi(e) >= 0) c->filter_steps = atoi(e);
   return c;

@@ -104,3 +104,77 @@ def classes(new: Mesh, req_every: int = 0) -> np.ndarray:
     pc = np.empty(new.np, np.uint8)
     synth_lib().synth_classes(new.np, _ptr(new.isbdy), int(req_every), _ptr(pc))
     return pc
+
+
+# ---------------------------------------------------------------- graded / stretched meshes
+#
+# The reference's anisotropic runs remesh a torus around a planar shock
+# (cmake/testing/pmmg_tests.cmake:52-63): the adapted meshes are strongly
+# graded towards the shock and their elements there are flat.  Here a cube
+# lattice is mapped per vertex: each axis d by a sinh clustering around the
+# plane x_d = c_d (cell size grows by grading[d] from that plane to the
+# farther face), then sheared so the planes are oblique (z += shear * (x -
+# 1/2)).  Cells at the centre are grading-times smaller than at the corners
+# in every direction; cells on one plane far from the others are flat
+# (aspect ratio up to the grading).  The map is monotone per axis, so every
+# Kuhn tetra keeps a positive volume; faces stay planar and map onto
+# themselves for every centre, so the boundary points of a new mesh graded
+# around other planes lie on the background's surface.
+
+
+def shock_map(t: np.ndarray, z_s: float, grading: float) -> np.ndarray:
+    """[0, 1] -> [0, 1], z(t) = z_s + A sinh(beta (t - t_s)): the cell size
+    dz/dt is smallest at the shock and `grading` times larger at the farther
+    face (beta = acosh(grading) / max(t_s, 1 - t_s))."""
+    t = np.asarray(t, np.float64)
+    if grading <= 1.0:
+        return t.copy()
+
+    def solve(beta):
+        lo, hi = 1e-12, 1.0 - 1e-12  # t_s: sinh(beta t_s) / sinh(beta (1 - t_s)) = z_s / (1 - z_s)
+        for _ in range(200):
+            mid = 0.5 * (lo + hi)
+            if np.sinh(beta * mid) * (1.0 - z_s) < np.sinh(beta * (1.0 - mid)) * z_s:
+                lo = mid
+            else:
+                hi = mid
+        return 0.5 * (lo + hi)
+
+    beta, t_s = 1.0, 0.5
+    for _ in range(50):  # fixed point: beta depends on the farther side, t_s on beta
+        t_s = solve(beta)
+        beta = float(np.arccosh(grading)) / max(t_s, 1.0 - t_s)
+    A = z_s / np.sinh(beta * t_s)
+    z = z_s + A * np.sinh(beta * (t - t_s))
+    z[t <= 0.0] = 0.0
+    z[t >= 1.0] = 1.0
+    return z
+
+
+def graded(lat: Mesh, centre=(0.5, 0.5, 0.5), grading=(1000.0, 1000.0, 1000.0), shear: float = 0.3) -> Mesh:
+    """A cube lattice (synth.CUBE, coordinates in [0, 1]^3) graded towards the
+    planes x_d = centre[d] and sheared (see above); connectivity unchanged."""
+    if lat.kind != CUBE:
+        raise ValueError("graded meshes are built from cube lattices")
+    xyz = lat.xyz.copy()
+    for d in range(3):
+        xyz[:, d] = shock_map(xyz[:, d], centre[d], grading[d])
+    xyz[:, 2] += shear * (xyz[:, 0] - 0.5)
+    m = Mesh(lat.kind, lat.n, np.ascontiguousarray(xyz), lat.tetv, lat.adja, lat.triv, lat.adjt, lat.isbdy,
+             dict(lat.extra))
+    m.extra["graded"] = dict(centre=tuple(centre), grading=tuple(grading), shear=shear)
+    return m
+
+
+def cell_stats(m: Mesh) -> dict:
+    """Element-size grading and stretching of a mesh: the ratio of the
+    largest to the smallest tetra edge-length scale (cube root of |volume|)
+    and the largest aspect ratio (longest edge / shortest edge of a tetra)."""
+    p = m.xyz[m.tetv - 1]
+    e = np.stack([p[:, 1] - p[:, 0], p[:, 2] - p[:, 0], p[:, 3] - p[:, 0],
+                  p[:, 2] - p[:, 1], p[:, 3] - p[:, 1], p[:, 3] - p[:, 2]], axis=1)
+    L = np.linalg.norm(e, axis=2)
+    vol = np.abs(np.einsum("ij,ij->i", e[:, 0], np.cross(e[:, 1], e[:, 2]))) / 6.0
+    h = np.cbrt(vol)
+    return {"size_grading": float(h.max() / h.min()), "max_aspect": float((L.max(1) / L.min(1)).max()),
+            "min_volume": float(vol.min())}

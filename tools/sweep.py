@@ -59,8 +59,7 @@ def main():
     if args.child is None:
         return parent(args)
     w = configs.SHORT[args.config]
-    bg = synth.lattice(w.kind, w.n_old)
-    new = synth.lattice(w.kind, w.n_new, jitter=w.jitter_new, with_trias=False, with_tetra=False)
+    bg, new = configs.build_meshes(w)
     met = synth.solution(w.metric, bg.xyz)
     fields = [synth.solution(f, bg.xyz) for f in w.fields]
     pc = synth.classes(new)
