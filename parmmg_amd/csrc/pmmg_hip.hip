@@ -26,6 +26,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <chrono>
 #include <condition_variable>
 #include <functional>
@@ -49,7 +50,7 @@ namespace {
 // ---------------------------------------------------------------- slot layouts
 
 typedef void (*VolFn)(Bg, const Frame *, const unsigned long long *, int, const double *, const uint8_t *,
-                      const int *, int, ContEntry *, DevStats *, Slots, int *, int8_t *, int);
+                      const int *, const double *, int, ContEntry *, DevStats *, Slots, int *, int8_t *, int);
 
 struct LayoutEntry {
   int c[6];
@@ -136,6 +137,9 @@ struct pmmg_hip_ctx {
   std::vector<DevBuf> o_f;
   // work buffers
   DevBuf frame, stats, grid, sgrid, cnt, off, binrank, order_v, order_b, cont, xq;
+  DevBuf axh;     // per-axis histograms of the seed grid map (k_axis_hist)
+  DevBuf cbase, fm, fms, scan_b; // Morton binning pass 2: chunk bases, count matrix, its scan, scan sums
+  DevBuf xs1, qs; // Morton binning: placed coordinates (pass 1), coordinates in processing order (pass 2)
   DevBuf scan_a, cls_cnt;                    // scan block sums, class counts
   DevBuf qmin;                               // tetra quality minimum (pmmg_hip_tetra_qual)
   DevBuf fb_vol, fb_bdy, best, ckey, cidx, bbest, bckey, bcidx;
@@ -161,7 +165,9 @@ struct pmmg_hip_ctx {
   int snap_ok = 1;
   int verbose = 0; // PMMG_HIP_VERBOSE: host-mode transfer timings on stderr
   int tpc = 8;        // background tetra per volume seed cell (PMMG_HIP_TPC)
-  int qpb = 64;       // queries per Morton bin (PMMG_HIP_QPB; r02: 64 beats 8 on shuffled and on coherent inputs)
+  int seed_lanes = 4;  // sampled tetra per seed run of 4 records (PMMG_HIP_SEEDLANES, 1..4)
+  int bbox_stride = 16; // the frame's bbox samples every n-th vertex (PMMG_HIP_BBOX)
+  int hist_stride = 64; // the seed grid's axis histograms sample every n-th vertex (PMMG_HIP_HIST)
   int maxstep = 4096; // longer walks go to the exact continuation / exhaustive kernels (PMMG_HIP_MAXSTEP; the
                       // reference caps at ne)
   int fanmax = kFanMax;    // cone fans longer than this take the O(nt) scan (test-only PMMG_HIP_FANMAX)
@@ -475,7 +481,9 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   }
   for (int i = 0; i < EV_COUNT; i++) (void)hipEventCreate(&c->ev[i]);
   c->tpc = env_int("PMMG_HIP_TPC", c->tpc);
-  c->qpb = env_int("PMMG_HIP_QPB", c->qpb);
+  c->seed_lanes = std::min(4, env_int("PMMG_HIP_SEEDLANES", c->seed_lanes));
+  c->bbox_stride = env_int("PMMG_HIP_BBOX", c->bbox_stride);
+  c->hist_stride = env_int("PMMG_HIP_HIST", c->hist_stride);
   c->verbose = env_int("PMMG_HIP_VERBOSE", 0);
   c->maxstep = env_int("PMMG_HIP_MAXSTEP", c->maxstep);
   c->fanmax = env_int("PMMG_HIP_FANMAX", c->fanmax);
@@ -495,7 +503,7 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   if (c->cstream) (void)hipStreamSynchronize(c->cstream);
   DevBuf *bufs[] = {&c->o_xyz, &c->o_tetv, &c->o_adja, &c->o_triv, &c->o_adjt, &c->o_met, &c->o_rec, &c->frame,
                     &c->stats, &c->grid, &c->sgrid, &c->cnt, &c->off, &c->binrank, &c->order_v,
-                    &c->order_b, &c->cont, &c->xq, &c->scan_a, &c->cls_cnt, &c->qmin, &c->fb_vol, &c->fb_bdy,
+                    &c->order_b, &c->cont, &c->xq, &c->xs1, &c->qs, &c->axh, &c->cbase, &c->fm, &c->fms, &c->scan_b, &c->scan_a, &c->cls_cnt, &c->qmin, &c->fb_vol, &c->fb_bdy,
                     &c->best, &c->ckey, &c->cidx, &c->bbest, &c->bckey, &c->bcidx, &c->h_xyz,
                     &c->h_cls, &c->h_met, &c->h_elem, &c->h_hit};
   for (DevBuf *b : bufs) release(*b);
@@ -886,24 +894,33 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   }
   const int g = grid_dim(bg.ne, c->tpc, 1024);
   const int gs = bg.nt > 0 ? grid_dim(bg.nt, 2, 512) : 1;
-  int bb = 1;
-  while (bb < 10 && (1LL << (3 * bb)) * c->qpb < (long long)np_new) bb++;
-  const int gb = 1 << bb, nbins = 1 << (3 * bb);
+  const int gb = 1 << kBinBitsAxis;
   const size_t nq = (size_t)np_new;
   const long long ng = (long long)g * g * g, nsg = bg.nt > 0 ? (long long)gs * gs * gs : 0;
   const long long ncls = (long long)(nq / kScanChunk + 1);
-  const long long nbin2 = 2LL * nbins;
+  // Morton binning: pass-1 tiles (blocks); the (digit, block) count matrix
+  const int nblk = (int)std::min<long long>(1024, std::max<long long>(1, ((long long)np_new + 4095) / 4096));
+  const long long nbin2 = (long long)kBinDigits * nblk;
+  // pass 2: chunks of at most kBinChunk queries of one digit (upper bound),
+  // and their (digit, fine, chunk) count matrix
+  const long long nchunk = ((long long)np_new + kBinChunk - 1) / kBinChunk + kBinDigits;
+  const long long nfm = nchunk * kBinFine;
   if (!ensure(c, c->frame, sizeof(Frame)) || !ensure(c, c->stats, sizeof(DevStats) + kStatParts * sizeof(StatPart)) ||
       !ensure(c, c->grid, 8 * (size_t)ng) || !ensure(c, c->sgrid, 4 * (size_t)nsg) || !ensure(c, c->order_v, 4 * nq) ||
       !ensure(c, c->order_b, 4 * nq) || 
       !ensure(c, c->cont, sizeof(ContEntry) * nq) || !ensure(c, c->cnt, 4 * (size_t)nbin2) ||
       !ensure(c, c->off, 4 * (size_t)(nbin2 + 1)) || !ensure(c, c->binrank, 8 * nq) ||
+      !ensure(c, c->xs1, 24 * nq) || !ensure(c, c->qs, 24 * nq) || !ensure(c, c->cbase, 4 * (kBinDigits + 1)) ||
+      !ensure(c, c->fm, 4 * (size_t)nfm) || !ensure(c, c->fms, 4 * (size_t)(nfm + 1)) ||
+      !ensure(c, c->scan_b, 4 * (size_t)(nfm / kScanChunk + 1)) ||
       !ensure(c, c->scan_a, 4 * (size_t)(nbin2 / kScanChunk + 1)) || !ensure(c, c->cls_cnt, 4 * (size_t)ncls) ||
       !ensure(c, c->fb_vol, 4 * nq) || !ensure(c, c->fb_bdy, 4 * nq) || !ensure(c, c->best, 4 * nq) ||
       !ensure(c, c->ckey, 8 * nq) || !ensure(c, c->cidx, 4 * nq) || !ensure(c, c->bbest, 4 * nq) ||
       !ensure(c, c->bckey, 8 * nq) || !ensure(c, c->bcidx, 4 * nq))
     return 0;
-  if (!ensure(c, c->xq, sizeof(int) * kXqStride * (size_t)bg.np)) return 0;
+  if (!ensure(c, c->xq, sizeof(int) * kXqStride * (size_t)bg.np) ||
+      !ensure(c, c->axh, sizeof(int) * 3 * kMapBins * (size_t)kHistBlocks))
+    return 0;
   bg.xq = (const int *)c->xq.p;
   Frame *fr = (Frame *)c->frame.p;
   DevStats *st = (DevStats *)c->stats.p;
@@ -916,8 +933,12 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   HIPCK(c, hipEventRecord(c->ev[EV_START], s));
   hipLaunchKernelGGL(k_reset, dim3(blocks_for(ng > nsg ? ng : nsg, 2048)), dim3(kBlock), 0, s, fr, st, grid, ng,
                      sgrid, nsg);
-  hipLaunchKernelGGL(k_bbox, dim3(blocks_for(bg.np / 16 + 1, 256)), dim3(kBlock), 0, s, bg.xyz, bg.np, fr, 16);
+  hipLaunchKernelGGL(k_bbox, dim3(blocks_for(bg.np / c->bbox_stride + 1, 256)), dim3(kBlock), 0, s, bg.xyz, bg.np, fr,
+                     c->bbox_stride);
   hipLaunchKernelGGL(k_frame_final, dim3(1), dim3(1), 0, s, fr, g, gs, gb);
+  hipLaunchKernelGGL(k_axis_hist, dim3(kHistBlocks), dim3(kBlock), 0, s, bg.xyz, bg.np, (const Frame *)fr,
+                     c->hist_stride, (int *)c->axh.p);
+  hipLaunchKernelGGL(k_axis_map, dim3(3), dim3(kBlock), 0, s, (const int *)c->axh.p, fr);
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[EV_FRAME], s));
 
@@ -928,15 +949,19 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_FRAME], 0));
   hipLaunchKernelGGL(k_coherence, dim3(1), dim3(kBlock), 0, sb, xyz_new, np_new, st, force);
   {
-    const int gq = blocks_for(np_new, 4096);
-    hipLaunchKernelGGL(k_zero, dim3(blocks_for(nbin2, 4096)), dim3(kBlock), 0, sb, (int *)c->cnt.p, nbin2,
-                       (const DevStats *)st, 1);
-    hipLaunchKernelGGL(k_bin_count, dim3(gq), dim3(kBlock), 0, sb, xyz_new, pclass, np_new, (const Frame *)fr, gb,
-                       nbins, (int *)c->cnt.p, (int2 *)c->binrank.p, (const DevStats *)st);
+    hipLaunchKernelGGL(k_bin_hist, dim3(nblk), dim3(kBlock), 0, sb, xyz_new, pclass, np_new, (const Frame *)fr,
+                       (int *)c->cnt.p, (const DevStats *)st);
     launch_scan((const int *)c->cnt.p, nbin2, (int *)c->off.p, (int *)c->scan_a.p, st, 1, sb);
-    hipLaunchKernelGGL(k_bin_scatter, dim3(gq), dim3(kBlock), 0, sb, np_new, (const int2 *)c->binrank.p,
-                       (const int *)c->off.p, nbins, order_v, order_b, (const DevStats *)st);
-    hipLaunchKernelGGL(k_bin_total, dim3(1), dim3(1), 0, sb, (const int *)c->off.p, nbins, st);
+    hipLaunchKernelGGL(k_bin_place, dim3(nblk), dim3(kBlock), 0, sb, xyz_new, pclass, np_new, (const Frame *)fr,
+                       (const int *)c->off.p, (int2 *)c->binrank.p, (double *)c->xs1.p, (const DevStats *)st);
+    hipLaunchKernelGGL(k_bin_chunks, dim3(1), dim3(kBlock), 0, sb, (const int *)c->off.p, nblk, (int *)c->cbase.p,
+                       (const DevStats *)st);
+    hipLaunchKernelGGL(k_bin_fine_hist, dim3((unsigned)nchunk), dim3(kBlock), 0, sb, (const int *)c->off.p, nblk,
+                       (const int *)c->cbase.p, (const int2 *)c->binrank.p, (int *)c->fm.p, (const DevStats *)st);
+    launch_scan((const int *)c->fm.p, nfm, (int *)c->fms.p, (int *)c->scan_b.p, st, 1, sb);
+    hipLaunchKernelGGL(k_bin_fine_place, dim3((unsigned)nchunk), dim3(kBlock), 0, sb, (const int *)c->off.p, nblk,
+                       (const int *)c->cbase.p, (const int2 *)c->binrank.p, (const double *)c->xs1.p,
+                       (const int *)c->fms.p, order_v, (double *)c->qs.p, order_b, st);
     if (bg.nt > 0) {
       int *bc = (int *)c->cls_cnt.p;
       hipLaunchKernelGGL(k_cls_count, dim3((unsigned)ncls), dim3(kBlock), 0, sb, pclass, (long long)np_new,
@@ -956,7 +981,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   {
     const long long nsamp = ng < bg.ne ? ng : bg.ne;
     hipLaunchKernelGGL(k_seed_vol, dim3((blocks_for(nsamp, 8192) + 7) & ~7), dim3(kBlock), 0, s, bg, fr, grid, g,
-                       nsamp);
+                       nsamp, c->seed_lanes);
   }
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[EV_PREP], s));
@@ -979,7 +1004,8 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   // ---- volume (main stream): walk + exact test + interpolation in one
   // kernel, then the exact continuation of the few queries it did not settle
   hipLaunchKernelGGL(vol_fn, dim3((np_new + 63) / 64), dim3(64), 0, s, bg, (const Frame *)fr,
-                     (const unsigned long long *)grid, g, xyz_new, pclass, (const int *)order_v, np_new,
+                     (const unsigned long long *)grid, g, xyz_new, pclass, (const int *)order_v,
+                     (const double *)c->qs.p, np_new,
                      (ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->filter_steps);
   HIPCK(c, hipEventRecord(c->ev[EV_WALK], s));
   hipLaunchKernelGGL(k_vol_walk_exact, dim3(8 * 64), dim3(64), 0, s, bg, xyz_new, (int *)c->fb_vol.p,
@@ -1003,9 +1029,9 @@ static int collect_stats(pmmg_hip_ctx *c, pmmg_hip_stats *out) {
   HIPCK(c, hipMemcpy(&h, c->stats.p, sizeof(DevStats), hipMemcpyDeviceToHost));
   HIPCK(c, hipMemcpy(parts.data(), (const DevStats *)c->stats.p + 1, kStatParts * sizeof(StatPart),
                      hipMemcpyDeviceToHost));
-  unsigned long long cnt[16] = {0}, steps = 0, stepmax = 0;
+  unsigned long long cnt[kNumCnt] = {0}, steps = 0, stepmax = 0;
   for (const StatPart &pt : parts) {
-    for (int j = 0; j < 16; j++) cnt[j] += pt.cnt[j];
+    for (int j = 0; j < kNumCnt; j++) cnt[j] += pt.cnt[j];
     steps += pt.steps;
     if (pt.stepmax > stepmax) stepmax = pt.stepmax;
   }
@@ -1028,6 +1054,14 @@ static int collect_stats(pmmg_hip_ctx *c, pmmg_hip_stats *out) {
   out->stepmax = (int64_t)stepmax;
   out->wave_iters = (int64_t)cnt[kCntWaveIters];
   out->sorted = h.sorted;
+  out->nvol_noseed = (int64_t)cnt[kCntNoSeed];
+  out->nvol_stuck = (int64_t)cnt[kCntStuck];
+  out->nvol_limit = (int64_t)cnt[kCntLimit];
+  {
+    int ad = 0;
+    HIPCK(c, hipMemcpy(&ad, &((const Frame *)c->frame.p)->adaptive, sizeof(int), hipMemcpyDeviceToHost));
+    out->seed_map_axes = ad;
+  }
   float ms = 0.f;
   HIPCK(c, hipEventElapsedTime(&ms, c->ev[EV_START], c->ev[EV_PREP]));
   out->ms_prepare = ms;

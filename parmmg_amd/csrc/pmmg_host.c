@@ -162,6 +162,8 @@ static void stats_add(pmmg_hip_stats *a, const pmmg_hip_stats *b) {
   if (b->stepmax > a->stepmax) a->stepmax = b->stepmax;
   a->ms_prepare += b->ms_prepare; a->ms_sort += b->ms_sort; a->ms_vol += b->ms_vol; a->ms_bdy += b->ms_bdy;
   a->ms_fallback += b->ms_fallback; a->ms_total += b->ms_total; a->ms_vol_locate += b->ms_vol_locate;
+  a->nvol_noseed += b->nvol_noseed; a->nvol_stuck += b->nvol_stuck; a->nvol_limit += b->nvol_limit;
+  a->seed_map_axes |= b->seed_map_axes;
 }
 
 int pmmg_interp_metrics_and_fields(pmmg_hip_ctx *ctx, int ngrp, const pmmg_old_group *old, pmmg_new_group *grp,

@@ -32,8 +32,12 @@ constexpr int kCntVolQueries = 12; // volume queries seen by the walk
 constexpr int kCntWaveIters = 13;  // sum over waves of the longest walk in the wave (lockstep cost)
 constexpr int kCntExact = 14;      // queries handed to the exact continuation (stuck, over-long, or rejected
                                    // by the exact test at the filter's candidate)
+constexpr int kCntNoSeed = 15;     // volume queries without a seed (empty seed neighbourhood)
+constexpr int kCntStuck = 16;      // exact walks stuck (no eligible neighbour)
+constexpr int kCntLimit = 17;      // exact walks stopped at maxstep
+constexpr int kNumCnt = 20;
 struct StatPart {
-  unsigned long long cnt[16];
+  unsigned long long cnt[kNumCnt];
   unsigned long long steps;
   unsigned long long stepmax;
 };
@@ -44,13 +48,13 @@ __device__ __forceinline__ StatPart *stat_part(DevStats *st) {
 // per-wave aggregation into the block's partial record (one LDS atomic per
 // wave and counter), flushed once per block
 struct BlockStats {
-  unsigned int cnt[16];
+  unsigned int cnt[kNumCnt];
   unsigned long long steps;
   unsigned int stepmax;
 };
 
 __device__ __forceinline__ void bstats_init(BlockStats *b) {
-  if (threadIdx.x < 16) b->cnt[threadIdx.x] = 0;
+  if (threadIdx.x < kNumCnt) b->cnt[threadIdx.x] = 0;
   if (threadIdx.x == 0) {
     b->steps = 0;
     b->stepmax = 0;
@@ -59,7 +63,7 @@ __device__ __forceinline__ void bstats_init(BlockStats *b) {
 
 __device__ __forceinline__ void bstats_flush(BlockStats *b, DevStats *st) {
   StatPart *pt = stat_part(st);
-  if (threadIdx.x < 16 && b->cnt[threadIdx.x]) atomicAdd(&pt->cnt[threadIdx.x], (unsigned long long)b->cnt[threadIdx.x]);
+  if (threadIdx.x < kNumCnt && b->cnt[threadIdx.x]) atomicAdd(&pt->cnt[threadIdx.x], (unsigned long long)b->cnt[threadIdx.x]);
   if (threadIdx.x == 0) {
     if (b->steps) atomicAdd(&pt->steps, b->steps);
     if (b->stepmax) atomicMax(&pt->stepmax, (unsigned long long)b->stepmax);
@@ -97,12 +101,45 @@ __device__ __forceinline__ void wave_count(BlockStats *bs, int slot, bool pred) 
   if (__lane_id() == 0 && m) atomicAdd(&bs->cnt[slot], (unsigned)__popcll(m));
 }
 
+// Per-axis map of the volume seed grid (r03): on a strongly graded mesh (a
+// boundary layer, a shock: elements 1000x smaller near a plane) a uniform
+// grid puts hundreds of element layers into one cell next to the plane and
+// the walks from its seed grow long (cfgG: 14.8 steps per point, stepmax
+// 382).  Cell boundaries along axis d then follow the quantiles of the
+// background vertices' coordinates (a sampled histogram of kMapBins bins,
+// linear inside a bin): each slab of cells holds the same share of the
+// vertices, which for a grading separable by axis makes every cell hold the
+// same number of tetra.  An axis whose densest bin is below kMapRatio x the
+// mean of its occupied bins keeps the uniform cells (bit 0 of `adaptive`
+// per axis clear): the shell and cube lattices are not remapped.
+constexpr int kMapBins = 2048;
+constexpr int kMapRatio = 16;
+constexpr int kHistBlocks = 128;
+
 struct Frame {
   unsigned long long key_lo[3], key_hi[3];
   double lo[3], ext[3];
   double inv_vol[3], inv_srf[3], inv_bin[3];
   double qc[3], qs; // fixed-point frame of the walk's vertex copy
+  int adaptive;     // bit d: axis d of the volume seed grid follows map[d]
+  int pad;
+  float map[3][kMapBins + 1]; // map[d][b] = share of the vertices below bin b's lower edge
 };
+
+// position along axis d in cells of the volume seed grid (g cells), in [0, g]
+__device__ __forceinline__ double seed_pos(const Frame *fr, int d, double x, int g) {
+  const double u = (x - fr->lo[d]) * fr->inv_vol[d]; // uniform cells
+  if (!((fr->adaptive >> d) & 1)) return u;
+  double b = u * ((double)kMapBins / (double)g);
+  b = b > 0.0 ? (b < (double)kMapBins ? b : (double)kMapBins - 1e-9) : 0.0;
+  const int i = (int)b;
+  const double m0 = fr->map[d][i], m1 = fr->map[d][i + 1];
+  return (m0 + (b - (double)i) * (m1 - m0)) * (double)g;
+}
+__device__ __forceinline__ int seed_cell(double t, int g) {
+  const int c = t > 0.0 ? (int)t : 0;
+  return c < g ? c : g - 1;
+}
 
 // Fixed-point coordinates for the filter walk and the seed grid: int32
 // (x - qc) * qs with |x - qc| <= 0.625 * (largest bbox side) mapped into
@@ -134,6 +171,7 @@ __global__ __launch_bounds__(kBlock) void k_reset(Frame *fr, DevStats *st, unsig
       fr->key_lo[d] = ~0ULL;
       fr->key_hi[d] = 0ULL;
     }
+    fr->adaptive = 0;
     unsigned int *w = reinterpret_cast<unsigned int *>(st);
     for (size_t j = 0; j < sizeof(DevStats) / 4; j++) w[j] = 0u;
   }
@@ -218,7 +256,7 @@ constexpr int kSeedRun = 4;
 constexpr unsigned long long kSeedIdMask = (1ULL << 29) - 1; // ids below 2^29 (the adja encoding's limit)
 
 __global__ __launch_bounds__(kBlock) void k_seed_vol(Bg bg, const Frame *fr, unsigned long long *cell, int g,
-                                                     long long nsamp) {
+                                                     long long nsamp, int lanes) {
   constexpr int R = kSeedRun;
   const long long nruns = (nsamp + R - 1) / R;
   const long long quads = bg.ne / 4;
@@ -235,7 +273,7 @@ __global__ __launch_bounds__(kBlock) void k_seed_vol(Bg bg, const Frame *fr, uns
     const int r = (int)(s % R);
     const long long base = 4 * ((run * quads) / (nruns > 0 ? nruns : 1)); // a cache line of tet8 records
     const int k = (int)(1 + base + r);
-    bool ok = s < hi && k <= bg.ne;
+    bool ok = s < hi && k <= bg.ne && r < lanes; // `lanes` of the run's 4 records are sampled
     int4 tv = make_int4(0, 0, 0, 0);
     if (ok) {
       const nti4 rr =
@@ -256,8 +294,9 @@ __global__ __launch_bounds__(kBlock) void k_seed_vol(Bg bg, const Frame *fr, uns
       unsigned long long off = 0;
       float d2 = 0.f;
       for (int d = 0; d < 3; d++) {
-        c[d] = cell_coord(p[d], fr->lo[d], fr->inv_vol[d], g);
-        float f = (float)((p[d] - fr->lo[d]) * fr->inv_vol[d] - c[d]);
+        const double t = seed_pos(fr, d, p[d], g);
+        c[d] = seed_cell(t, g);
+        float f = (float)(t - c[d]);
         f = f < 0.f ? 0.f : (f > 0.999f ? 0.999f : f);
         off |= (unsigned long long)(unsigned)(f * 512.f) << (9 * d);
         d2 += (f - 0.5f) * (f - 0.5f);
@@ -316,8 +355,8 @@ __device__ __forceinline__ int seed_vol(const unsigned long long *cell, int g, c
   int c[3], o[3];
 #pragma unroll
   for (int d = 0; d < 3; d++) {
-    t[d] = (x[d] - fr->lo[d]) * fr->inv_vol[d];
-    c[d] = cell_coord(x[d], fr->lo[d], fr->inv_vol[d], g);
+    t[d] = seed_pos(fr, d, x[d], g);
+    c[d] = seed_cell(t[d], g);
     const double f = t[d] - c[d];
     o[d] = f < 0.5 ? (c[d] > 0 ? -1 : 0) : (c[d] < g - 1 ? 1 : 0);
   }
@@ -473,6 +512,70 @@ __global__ __launch_bounds__(kBlock) void k_scan_write(const int *in, long long 
   if (i0 <= n && n < i0 + kScanItems) out[n] = pre; // the thread holding the end writes the total
 }
 
+// ---------------------------------------------------------------- seed grid axis maps
+
+// the per-axis histogram of every `stride`-th background vertex:
+// H[block][d][bin] (kHistBlocks blocks, no atomics outside LDS)
+__global__ __launch_bounds__(kBlock) void k_axis_hist(const double *xyz, int np, const Frame *fr, int stride, int *H) {
+  __shared__ int h[3][kMapBins];
+  for (int j = threadIdx.x; j < 3 * kMapBins; j += kBlock) (&h[0][0])[j] = 0;
+  __syncthreads();
+  const long long ns = ((long long)np + stride - 1) / stride;
+  for (long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x; j < ns; j += (long long)gridDim.x * blockDim.x) {
+    const long long i = j * stride;
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+      const double e = fr->ext[d];
+      double b = e > 0.0 ? (xyz[3 * i + d] - fr->lo[d]) * ((double)kMapBins / e) : 0.0;
+      const int bi = b > 0.0 ? (b < (double)kMapBins ? (int)b : kMapBins - 1) : 0;
+      atomicAdd(&h[d][bi], 1);
+    }
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < 3 * kMapBins; j += kBlock) H[(size_t)blockIdx.x * 3 * kMapBins + j] = (&h[0][0])[j];
+}
+
+// one block per axis: counts -> quantile map, adaptive bit
+__global__ __launch_bounds__(kBlock) void k_axis_map(const int *H, Frame *fr) {
+  constexpr int R = kMapBins / kBlock; // bins per thread
+  const int d = blockIdx.x;
+  int cnt[R], s = 0, mx = 0, occ = 0;
+#pragma unroll
+  for (int q = 0; q < R; q++) {
+    const int b = R * threadIdx.x + q;
+    int v = 0;
+    for (int k = 0; k < kHistBlocks; k++) v += H[(size_t)k * 3 * kMapBins + d * kMapBins + b];
+    cnt[q] = v;
+    s += v;
+    mx = v > mx ? v : mx;
+    occ += v > 0 ? 1 : 0;
+  }
+  int tot;
+  const int pre = block_excl_scan(s, &tot);
+  __shared__ int smx[kBlock], socc[kBlock];
+  smx[threadIdx.x] = mx;
+  socc[threadIdx.x] = occ;
+  __syncthreads();
+  for (int o = kBlock / 2; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      smx[threadIdx.x] = smx[threadIdx.x + o] > smx[threadIdx.x] ? smx[threadIdx.x + o] : smx[threadIdx.x];
+      socc[threadIdx.x] += socc[threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  // adaptive: the densest bin holds more than kMapRatio x the mean occupied bin
+  const bool adapt = tot > 0 && (long long)smx[0] * socc[0] > (long long)kMapRatio * tot;
+  int run = pre;
+#pragma unroll
+  for (int q = 0; q < R; q++) {
+    const int b = R * threadIdx.x + q;
+    fr->map[d][b] = adapt ? (float)((double)run / (double)tot) : (float)b / (float)kMapBins;
+    run += cnt[q];
+  }
+  if (threadIdx.x == kBlock - 1) fr->map[d][kMapBins] = 1.0f;
+  if (threadIdx.x == 0 && adapt) atomicOr(&fr->adaptive, 1 << d);
+}
+
 // ---------------------------------------------------------------- query order
 
 // Is the input numbering spatially coherent?  Distances between consecutive
@@ -542,57 +645,196 @@ __global__ __launch_bounds__(kBlock) void k_coherence(const double *xyz, int np,
   }
 }
 
-// Morton binning (st->sorted == 1 only): bin = (class, Morton code of the
-// gb^3 cell); rank inside the bin from the counter (order inside a bin is
-// irrelevant: each query's result is a pure function of the query)
-__global__ __launch_bounds__(kBlock) void k_bin_count(const double *xyz, const uint8_t *pclass, int np, const Frame *fr,
-                                                      int gb, int nbins, int *cnt, int2 *binrank, const DevStats *st) {
+// ---------------------------------------------------------------- Morton binning (st->sorted == 1 only)
+//
+// Queries of a numbering without spatial coherence are processed in Morton
+// order of a 64^3 grid over the frame, in two counting passes without global
+// atomics (r03; the r02 binning took one returning device-scope atomicAdd per
+// query on 2M bins: 1.9 ms at cfg4 on a shuffled numbering):
+//   pass 1 (k_bin_hist, scan, k_bin_place) — digit = (class, coarse cell: the
+//     top 3 bits per axis, 512 cells): per-block LDS histograms in a
+//     digit-major matrix, one device-wide scan gives every (digit, block) its
+//     range, the block places its queries there through LDS counters; a
+//     placed query carries {id, fine key} and its coordinates;
+//   pass 2 (k_bin_chunks, k_bin_fine_hist, scan, k_bin_fine_place) — the
+//     same counting sort inside every digit by the fine key (the low 4 bits
+//     per axis, 512 cells), on chunks of at most 4096 queries of one digit;
+//     the result is the order list plus a copy of the coordinates in that
+//     order (the walk then loads its queries coalesced).
+// Order inside a fine cell is not deterministic (LDS counters); every query's
+// result is a pure function of the query, so no output depends on it.
+constexpr int kBinBitsAxis = 6;                  // 64^3 grid (Frame::inv_bin)
+constexpr int kBinCoarse = 512;                  // 8^3 coarse cells per class
+constexpr int kBinDigits = 2 * kBinCoarse;       // volume digits first, then surface
+constexpr int kBinFine = 512;                    // 8^3 fine cells per coarse cell
+constexpr int kBinChunk = kBlock * 16;           // queries per pass-2 chunk
+
+// digit (-1: neither a volume nor a surface query) and fine key of query i
+__device__ __forceinline__ int bin_key(const double *xyz, const uint8_t *pclass, long long i, const Frame *fr,
+                                       int *fine, double *x) {
+  const int c = pclass[i];
+  if (c != PMMG_PT_VOL && c != PMMG_PT_BDY) return -1;
+  uint32_t q[3];
+#pragma unroll
+  for (int d = 0; d < 3; d++) {
+    x[d] = xyz[3 * i + d];
+    q[d] = (uint32_t)cell_coord(x[d], fr->lo[d], fr->inv_bin[d], 1 << kBinBitsAxis);
+  }
+  const uint32_t lo = 7u;
+  *fine = (int)((expand10(q[0] & lo) << 2) | (expand10(q[1] & lo) << 1) | expand10(q[2] & lo));
+  const int coarse = (int)((expand10(q[0] >> 3) << 2) | (expand10(q[1] >> 3) << 1) | expand10(q[2] >> 3));
+  return coarse + (c == PMMG_PT_BDY ? kBinCoarse : 0);
+}
+
+// block b's contiguous tile of the queries
+__device__ __forceinline__ void bin_tile(int np, int nblk, long long *lo, long long *hi) {
+  const long long per = ((long long)np + nblk - 1) / nblk;
+  *lo = (long long)blockIdx.x * per;
+  *hi = *lo + per < np ? *lo + per : np;
+}
+
+// pass 1: H[digit * nblk + block] = the block's count (gridDim.x == nblk)
+__global__ __launch_bounds__(kBlock) void k_bin_hist(const double *xyz, const uint8_t *pclass, int np, const Frame *fr,
+                                                     int *H, const DevStats *st) {
   if (!st->sorted) return;
-  const int lane = __lane_id();
-  // uniform trip count per wave (the loop bound is the block's base), so the
-  // lanes of a wave can aggregate: consecutive lanes in the same bin (the
-  // usual case: neighbouring points) take their ranks from one atomicAdd
-  for (long long b0 = (long long)blockIdx.x * blockDim.x; b0 < np; b0 += (long long)gridDim.x * blockDim.x) {
-    const int i = (int)(b0 + threadIdx.x);
-    int bin = -1;
-    if (i < np) {
-      const int c = pclass[i];
-      if (c == PMMG_PT_VOL || c == PMMG_PT_BDY) {
-        uint32_t q[3];
-        for (int d = 0; d < 3; d++) q[d] = (uint32_t)cell_coord(xyz[3 * (size_t)i + d], fr->lo[d], fr->inv_bin[d], gb);
-        bin = (int)((expand10(q[0]) << 2) | (expand10(q[1]) << 1) | expand10(q[2])) + (c == PMMG_PT_BDY ? nbins : 0);
-      }
+  __shared__ int h[kBinDigits];
+  for (int j = threadIdx.x; j < kBinDigits; j += kBlock) h[j] = 0;
+  __syncthreads();
+  long long lo, hi;
+  bin_tile(np, gridDim.x, &lo, &hi);
+  for (long long i = lo + threadIdx.x; i < hi; i += kBlock) {
+    int f;
+    double x[3];
+    const int d = bin_key(xyz, pclass, i, fr, &f, x);
+    if (d >= 0) atomicAdd(&h[d], 1);
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < kBinDigits; j += kBlock) H[(size_t)j * gridDim.x + blockIdx.x] = h[j];
+}
+
+// pass 1: O = exclusive scan of H; the block's queries of digit d go to
+// [O[d * nblk + b], ...): {id, fine} and the coordinates
+__global__ __launch_bounds__(kBlock) void k_bin_place(const double *xyz, const uint8_t *pclass, int np,
+                                                      const Frame *fr, const int *O, int2 *key1, double *xs1,
+                                                      const DevStats *st) {
+  if (!st->sorted) return;
+  __shared__ int cur[kBinDigits];
+  for (int j = threadIdx.x; j < kBinDigits; j += kBlock) cur[j] = O[(size_t)j * gridDim.x + blockIdx.x];
+  __syncthreads();
+  long long lo, hi;
+  bin_tile(np, gridDim.x, &lo, &hi);
+  for (long long i = lo + threadIdx.x; i < hi; i += kBlock) {
+    int f;
+    double x[3];
+    const int d = bin_key(xyz, pclass, i, fr, &f, x);
+    if (d < 0) continue;
+    const int p = atomicAdd(&cur[d], 1);
+    key1[p] = make_int2((int)(i + 1), f);
+    xs1[3 * (size_t)p] = x[0];
+    xs1[3 * (size_t)p + 1] = x[1];
+    xs1[3 * (size_t)p + 2] = x[2];
+  }
+}
+
+// pass 2 works on chunks of at most kBinChunk queries that never straddle a
+// digit: digit d's n_d queries form ceil(n_d / kBinChunk) chunks, chunk ids
+// in digit order (cbase[d] = chunks before digit d, cbase[kBinDigits] = all)
+__global__ __launch_bounds__(kBlock) void k_bin_chunks(const int *O, int nblk, int *cbase, const DevStats *st) {
+  if (!st->sorted) return;
+  constexpr int R = kBinDigits / kBlock;
+  int n[R], s = 0;
+#pragma unroll
+  for (int q = 0; q < R; q++) {
+    const int d = R * threadIdx.x + q;
+    const int cnt = O[(size_t)(d + 1) * nblk] - O[(size_t)d * nblk];
+    n[q] = (cnt + kBinChunk - 1) / kBinChunk;
+    s += n[q];
+  }
+  int tot;
+  int pre = block_excl_scan(s, &tot);
+#pragma unroll
+  for (int q = 0; q < R; q++) {
+    cbase[R * threadIdx.x + q] = pre;
+    pre += n[q];
+  }
+  if (threadIdx.x == 0) cbase[kBinDigits] = tot;
+}
+
+// chunk b of pass 2 (b < cbase[kBinDigits]): its digit d (binary search),
+// its index j inside the digit, the digit's chunk count and the queries
+// [q0, q1) of key1 / xs1
+struct BinChunk {
+  int d, j, nch, q0, q1;
+};
+__device__ __forceinline__ bool bin_chunk(const int *O, int nblk, const int *cbase, int b, BinChunk *c) {
+  if (b >= cbase[kBinDigits]) return false;
+  int lo = 0, hi = kBinDigits; // cbase[lo] <= b < cbase[hi]
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (cbase[mid] <= b) lo = mid;
+    else hi = mid;
+  }
+  c->d = lo;
+  c->j = b - cbase[lo];
+  c->nch = cbase[lo + 1] - cbase[lo];
+  const int b0 = O[(size_t)lo * nblk], b1 = O[(size_t)(lo + 1) * nblk];
+  c->q0 = b0 + c->j * kBinChunk;
+  c->q1 = c->q0 + kBinChunk < b1 ? c->q0 + kBinChunk : b1;
+  return true;
+}
+// entry (d, fine f, chunk j) of the pass-2 count matrix, ordered digit,
+// fine key, chunk: its exclusive scan is the final position of the first
+// query of chunk j with key (d, f)
+__device__ __forceinline__ size_t bin_m_index(const int *cbase, const BinChunk &c, int f) {
+  return (size_t)cbase[c.d] * kBinFine + (size_t)f * c.nch + c.j;
+}
+
+// pass 2: per chunk, the LDS histogram of its fine keys into the matrix
+// (grid: an upper bound of the chunk count; chunks past the real count exit)
+__global__ __launch_bounds__(kBlock) void k_bin_fine_hist(const int *O, int nblk, const int *cbase, const int2 *key1,
+                                                          int *M, const DevStats *st) {
+  if (!st->sorted) return;
+  BinChunk c;
+  if (!bin_chunk(O, nblk, cbase, blockIdx.x, &c)) return;
+  __shared__ int h[kBinFine];
+  for (int f = threadIdx.x; f < kBinFine; f += kBlock) h[f] = 0;
+  __syncthreads();
+  for (int q = c.q0 + threadIdx.x; q < c.q1; q += kBlock) atomicAdd(&h[key1[q].y], 1);
+  __syncthreads();
+  for (int f = threadIdx.x; f < kBinFine; f += kBlock) M[bin_m_index(cbase, c, f)] = h[f];
+}
+
+// pass 2: after the scan of M, every chunk places its queries at their final
+// positions: the order lists and, for volume queries, the coordinates in
+// processing order (the walk then loads its queries coalesced)
+__global__ __launch_bounds__(kBlock) void k_bin_fine_place(const int *O, int nblk, const int *cbase, const int2 *key1,
+                                                           const double *xs1, const int *Ms, int *order_v, double *qs,
+                                                           int *order_b, DevStats *st) {
+  if (!st->sorted) return;
+  const int nvol = O[(size_t)kBinCoarse * nblk];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    st->nvol = nvol;
+    st->nbdy = O[(size_t)kBinDigits * nblk] - nvol;
+  }
+  BinChunk c;
+  if (!bin_chunk(O, nblk, cbase, blockIdx.x, &c)) return;
+  __shared__ int cur[kBinFine];
+  for (int f = threadIdx.x; f < kBinFine; f += kBlock) cur[f] = Ms[bin_m_index(cbase, c, f)];
+  __syncthreads();
+  for (int q = c.q0 + threadIdx.x; q < c.q1; q += kBlock) {
+    const int2 kv = key1[q];
+    const int pos = atomicAdd(&cur[kv.y], 1);
+    if (c.d < kBinCoarse) {
+      order_v[pos] = kv.x;
+      qs[3 * (size_t)pos] = xs1[3 * (size_t)q];
+      qs[3 * (size_t)pos + 1] = xs1[3 * (size_t)q + 1];
+      qs[3 * (size_t)pos + 2] = xs1[3 * (size_t)q + 2];
+    } else {
+      order_b[pos - nvol] = kv.x;
     }
-    const int prev = __shfl_up(bin, 1);
-    const bool start = lane == 0 || bin != prev;
-    const unsigned long long starts = __ballot(start);
-    const unsigned long long upto = lane == 63 ? ~0ULL : ((2ULL << lane) - 1); // bits 0..lane
-    const int rs = 63 - __clzll(starts & upto);                                 // this lane's run start
-    const unsigned long long after = starts & ~upto;
-    const int next = after ? __ffsll((long long)after) - 1 : 64;                // the next run's start
-    int base = 0;
-    if (start && bin >= 0) base = atomicAdd(&cnt[bin], next - lane);
-    base = __shfl(base, rs);
-    if (i < np) binrank[i] = bin >= 0 ? make_int2(bin, base + (lane - rs)) : make_int2(-1, 0);
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_bin_scatter(int np, const int2 *binrank, const int *off, int nbins,
-                                                        int *order_v, int *order_b, const DevStats *st) {
-  if (!st->sorted) return;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < np; i += gridDim.x * blockDim.x) {
-    int2 br = binrank[i];
-    if (br.x < 0) continue;
-    if (br.x < nbins) order_v[off[br.x] + br.y] = i + 1;
-    else order_b[off[br.x] - off[nbins] + br.y] = i + 1;
-  }
-}
-
-__global__ void k_bin_total(const int *off, int nbins, DevStats *st) {
-  if (!st->sorted) return;
-  st->nvol = off[nbins];
-  st->nbdy = off[2 * nbins] - off[nbins];
-}
 
 // Stable class compaction (the surface list, input-order path only): out =
 // the ids ip (1-based) with pclass[ip-1] == cls, in input order; *count =

@@ -109,6 +109,44 @@ __device__ __forceinline__ int pick_face(const int4 &ad, const int *hist, const 
   return f;
 }
 
+// Past kDetSteps steps a walk takes the stochastic rule instead (Devillers,
+// Pion & Teillaud, "Walking in a triangulation": the remembering stochastic
+// walk terminates with probability 1 on any triangulation): the first
+// eligible face, in a cyclic order starting at a pseudo-random face, beyond
+// which the point lies (key > 0); the usual rule when there is none.  The
+// most-negative rule can cycle on sheared, strongly graded meshes (cfgG:
+// cycles longer than the 4-entry history sent ~0.1 % of the queries through
+// 4096 exact steps into the exhaustive search).  The path only decides which
+// of the accepting tetra a class (ii) point ends in; rsel is a hash of
+// (query, step), so the result stays a pure function of the query.
+constexpr int kDetSteps = 24;
+__device__ __forceinline__ unsigned walk_rsel(int ip, int steps) {
+  if (steps <= kDetSteps) return 0u;
+  unsigned h = (unsigned)ip * 0x9E3779B1u ^ (unsigned)steps * 0x85EBCA77u;
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  h ^= h >> 12;
+  return h | 0x80000000u; // nonzero
+}
+template <typename T>
+__device__ __forceinline__ int pick_face_walk(const int4 &ad, const int *hist, const T *key, unsigned rsel) {
+  if (rsel) {
+    const int f0 = (int)(rsel & 3u);
+    int f = -1;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int ff = (f0 + j) & 3;
+      const int iel = sel4(ad, ff) >> 2;
+      bool vis = false;
+#pragma unroll
+      for (int h = 0; h < kHist; h++) vis = vis || (hist[h] == iel);
+      if (f < 0 && iel != 0 && !vis && key[ff] > (T)0) f = ff;
+    }
+    if (f >= 0) return f;
+  }
+  return pick_face<T>(ad, hist, key);
+}
+
 // the vertices of the tetra reached through face f: the new tetra tn's local
 // vertex l sits in the slot of the same vertex of the previous tetra tv (slot
 // map m), except its vertex opposite the crossed face (iopp), which takes the
@@ -186,7 +224,7 @@ __device__ __forceinline__ float dot3(const float *a, const float *b) { return a
 // returns 1 candidate (filter passed), 0 moved (k, tv, ad, m, hist updated),
 // 2 stuck (no eligible neighbour)
 __device__ __forceinline__ int step_f32(const Bg &bg, const int *x, int &k, int4 &tv, int4 &ad, int4 &m, int *hist,
-                                        const LaneSlotsF &L) {
+                                        const LaneSlotsF &L, unsigned rsel) {
   float q[4][3];
   L.get(m.x, q[0]);
   L.get(m.y, q[1]);
@@ -206,7 +244,7 @@ __device__ __forceinline__ int step_f32(const Bg &bg, const int *x, int &k, int4
   for (int f = 0; f < 4; f++) key[f] = vol < 0.f ? -s[f] : s[f];
   const float kmax = fmaxf(fmaxf(key[0], key[1]), fmaxf(key[2], key[3]));
   if (vol != 0.f && kmax < (float)(kEps + kFilterMargin) * fabsf(vol)) return 1;
-  const int f = pick_face<float>(ad, hist, key);
+  const int f = pick_face_walk<float>(ad, hist, key, rsel);
   if (f < 0) return 2;
 #pragma unroll
   for (int h = kHist - 1; h > 0; h--) hist[h] = hist[h - 1];
@@ -242,8 +280,8 @@ struct LaneSlotsD {
   }
 };
 
-__device__ __forceinline__ int walk_exact(const Bg &bg, const double *x, int &k, int &steps, int limit, VolLoc *loc,
-                                          const LaneSlotsD &L) {
+__device__ __forceinline__ int walk_exact(const Bg &bg, const double *x, int ip, int &k, int &steps, int limit,
+                                          VolLoc *loc, const LaneSlotsD &L) {
   int hist[kHist];
 #pragma unroll
   for (int h = 0; h < kHist; h++) hist[h] = 0;
@@ -265,7 +303,7 @@ __device__ __forceinline__ int walk_exact(const Bg &bg, const double *x, int &k,
     L.get(m.w, p[3]);
     double key[4];
     if (exact_accept(x, p, tv, loc, key)) return 1;
-    const int f = pick_face<double>(ad, hist, key);
+    const int f = pick_face_walk<double>(ad, hist, key, walk_rsel(ip, n + 1));
     if (f < 0) return 2;
 #pragma unroll
     for (int h = kHist - 1; h > 0; h--) hist[h] = hist[h - 1];
@@ -309,7 +347,7 @@ __global__ __launch_bounds__(64) void k_vol_walk_exact(Bg bg, const double *qxyz
         double x[3];
         load_pt(qxyz, ip, x);
         VolLoc loc;
-        status = walk_exact(bg, x, k, steps, maxstep, &loc, L);
+        status = walk_exact(bg, x, ip, k, steps, maxstep, &loc, L);
         if (status == 1) {
           const int v[4] = {loc.v.x, loc.v.y, loc.v.z, loc.v.w};
           for (int sl = 0; sl < S.n; sl++) interp_dyn<4>(S.s[sl], ip, v, loc.phi);
@@ -321,6 +359,9 @@ __global__ __launch_bounds__(64) void k_vol_walk_exact(Bg bg, const double *qxyz
     const bool fail = active && status != 1;
     const int slot = wave_append(&st->nfb_vol, fail);
     if (fail) fb[slot] = ip;
+    wave_count(&bs, kCntNoSeed, fail && status == 0);
+    wave_count(&bs, kCntStuck, fail && status == 2);
+    wave_count(&bs, kCntLimit, fail && status == 3);
     wave_stats(&bs, active, status == 1 ? PMMG_HIT_VOL_WALK : 0, steps);
   }
   __syncthreads();
@@ -362,6 +403,37 @@ __device__ __forceinline__ void wave_store_rows(double *out, const double *row, 
       for (int t = 0; t < C; t++) {
         const int p = 64 * t + lane; // 8-byte piece
         if ((mask >> (p / C)) & 1ULL) nt_store(out + p, img[p]);
+      }
+    }
+    wait_lgkm(); // the image is reused by the next slot
+  }
+}
+
+// The same for the Morton-binned order, where row r goes to its own query ip
+// of lane r (scattered): the rows still go through the LDS image, so that
+// one store instruction writes the pieces of ~21 rows (one to two lines
+// each) instead of one piece of 64 rows.  Plain (cached) stores: L2 merges
+// the partial lines that queries of other waves complete.
+template <int C>
+__device__ __forceinline__ void wave_store_rows_scat(double *out, const double *row, unsigned long long mask,
+                                                     double *img, int ip) {
+  const int lane = __lane_id();
+  if constexpr (C == 1) {
+    if ((mask >> lane) & 1ULL) out[ip - 1] = row[0];
+  } else {
+#pragma unroll
+    for (int j = 0; j < C; j++) img[C * lane + j] = row[j];
+    wait_lgkm();
+    constexpr int PR = C == 6 ? 3 : C; // pieces per row: 16-byte (6-double rows) or 8-byte
+#pragma unroll
+    for (int t = 0; t < PR; t++) {
+      const int p = 64 * t + lane, r = p / PR, k = p - PR * r;
+      const int dst = __shfl(ip, r);
+      if ((mask >> r) & 1ULL) {
+        if constexpr (C == 6)
+          reinterpret_cast<double2 *>(out + (size_t)6 * (dst - 1))[k] = reinterpret_cast<const double2 *>(img)[p];
+        else
+          out[(size_t)C * (dst - 1) + k] = img[p];
       }
     }
     wait_lgkm(); // the image is reused by the next slot
@@ -504,16 +576,8 @@ __device__ __forceinline__ void vol_slot(const Slot &sl, bool act, const int4 &v
       const int vv[4] = {v.x, v.y, v.z, v.w};
       interp_iso_row<4, 1>(sl.in, sl.istride, vv, phi, r);
     }
-    if (coalesced) {
-      wave_store_rows<C>(sl.out + (size_t)C * w0, r, __ballot(ok), img);
-    } else if (ok) {
-      double *o = sl.out + (size_t)C * (ip - 1);
-      // Morton-binned order: plain (cached) stores, so that L2 merges the
-      // partial lines neighbouring queries of other waves write before the
-      // lines leave (non-temporal partial-line writes go to memory alone)
-#pragma unroll
-      for (int q = 0; q < C; q++) o[q] = r[q];
-    }
+    if (coalesced) wave_store_rows<C>(sl.out + (size_t)C * w0, r, __ballot(ok), img);
+    else wave_store_rows_scat<C>(sl.out, r, __ballot(ok), img, ip);
   }
 }
 
@@ -592,16 +656,8 @@ __device__ __forceinline__ void packed_store(const Slot &sl, SlotAcc<C> &a, doub
     else
 #pragma unroll
       for (int q = 0; q < C; q++) r[q] = a.v[q];
-    if (coalesced) {
-      wave_store_rows<C>(sl.out + (size_t)C * w0, r, __ballot(ok), img);
-    } else if (ok) {
-      double *o = sl.out + (size_t)C * (ip - 1);
-      // Morton-binned order: plain (cached) stores, so that L2 merges the
-      // partial lines neighbouring queries of other waves write before the
-      // lines leave (non-temporal partial-line writes go to memory alone)
-#pragma unroll
-      for (int q = 0; q < C; q++) o[q] = r[q];
-    }
+    if (coalesced) wave_store_rows<C>(sl.out + (size_t)C * w0, r, __ballot(ok), img);
+    else wave_store_rows_scat<C>(sl.out, r, __ballot(ok), img, ip);
   }
 }
 
@@ -686,9 +742,9 @@ __device__ __forceinline__ void vol_interp_packed(const Slots &S, bool acc, cons
 
 template <bool PK, int C0, int C1, int C2, int C3, int C4, int C5>
 __global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsigned long long *grid, int g,
-                                            const double *qxyz, const uint8_t *pclass, const int *order, int np,
-                                            ContEntry *cont, DevStats *st, Slots S, int *elem_out, int8_t *hit_out,
-                                            int filter_steps) {
+                                            const double *qxyz, const uint8_t *pclass, const int *order,
+                                            const double *qs, int np, ContEntry *cont, DevStats *st, Slots S,
+                                            int *elem_out, int8_t *hit_out, int filter_steps) {
   __shared__ VolShared sh;
   bstats_init(&sh.bs);
   __syncthreads();
@@ -709,7 +765,8 @@ __global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsign
   double x[3];
   int4 tv = make_int4(1, 1, 1, 1);
   if (active) {
-    load_pt_nt(qxyz, ip, x); // streamed once: non-temporal
+    load_pt_nt(sorted ? qs : qxyz, sorted ? i + 1 : ip, x); // streamed once: non-temporal (Morton order: the
+                                                              // binning's coordinate copy, in processing order)
     k = seed_vol(grid, g, fr, x);
     if (k == 0) {
       status = 2;
@@ -737,7 +794,7 @@ __global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsign
           break;
         }
         ++steps;
-        const int r = step_f32(bg, xq, k, tv, ad, m, hist, L);
+        const int r = step_f32(bg, xq, k, tv, ad, m, hist, L, walk_rsel(ip, steps));
         if (r != 0) {
           status = r;
           break;

@@ -143,15 +143,17 @@ def test_cfg5_full_size_visit_range():
 
 
 @pytest.mark.gpu
-def test_cfgG_graded_full_size_every_point():
+def test_cfgG_graded_full_size_visit_range():
     """cfgG: cfg3's lattices graded 1000x towards three planes (the new mesh's
     planes moved against the background's) and sheared — elements from ~1:1
     to ~1000:1, the geometry of the reference's anisotropic torus-with-shock
-    runs.  Every point against a full oracle run; the fp32 filter walk's
+    runs.  The full-size module run, checked on a 1M-point range of the
+    reference's visitation order (the oracle runs ~30k points/s per 8 threads
+    on this mesh: every point would take minutes); the fp32 filter walk's
     hand-overs to the exact walk (nvol_exact) stay a small fraction: its
     margin holds on these elements."""
-    rep, st = _config_parity(configs.CFGG)
-    assert rep["n"] > 4_000_000
+    rep, st = _config_parity(configs.CFGG, sample=1_000_000)
+    assert rep["n"] > 900_000
     print("cfgG nvol_exact", st.nvol_exact, "stepmax", st.stepmax, "steps/pt",
           st.steps_total / max(1, st.nvol + st.nbdy))
     assert st.nvol_exact < 0.01 * st.nvol
