@@ -361,23 +361,6 @@ def host_mode_timing(ctx, w, bg, met, fields, q_xyz, q_pc, rank: int, reps: int 
             "bytes_up": int(up), "bytes_down": int(down), "pcie_gbps_effective": round((up + down) / t / 1e9, 1)}
 
 
-def mmg_like_perm(nq: int) -> np.ndarray:
-    """A numbering of the new points like Mmg's output after an adaptation
-    (src/libparmmg1.c:692-741: the group is renumbered, then Mmg keeps the
-    retained vertices in their order and appends the vertices it inserts,
-    in creation order): one point in six (a splitmix64 hash of its id,
-    spread evenly over the domain) counts as inserted and moves to the end,
-    both parts keeping the generator's order.  perm[new id] = old id."""
-    ids = np.arange(nq, dtype=np.uint64)
-    with np.errstate(over="ignore"):
-        z = ids * np.uint64(0x9E3779B97F4A7C15) + np.uint64(0x5EED2025)
-        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
-        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
-        z ^= z >> np.uint64(31)
-    ins = (z % np.uint64(6)) == 0
-    return np.concatenate([np.nonzero(~ins)[0], np.nonzero(ins)[0]])
-
-
 def renumbered_timing(ctx, args, w, step_bg, q_xyz, q_pc, d_mo, d_fo, d_elem, d_hit, rank: int, perm, what: str):
     """The same step on a renumbering of the new points (perm[new id] = old
     id); the module decides on the device whether the numbering is
@@ -741,7 +724,7 @@ def main():
         except Exception as e:  # reported, never fatal to the bench line
             out["surface_solo"] = {"error": str(e)}
     if not args.no_shuffled and world == 1 and not split:
-        legs = {"mmg_like_order": (mmg_like_perm(nq), "the step on an Mmg-like numbering of the new points (1 in 6 "
+        legs = {"mmg_like_order": (synth.mmg_like_perm(nq), "the step on an Mmg-like numbering of the new points (1 in 6 "
                                    "points moved to the end as 'inserted', both parts in the generator's order); not "
                                    "the bench value"),
                 "shuffled_order": (np.random.default_rng(2024).permutation(nq), "the step on a random renumbering of "

@@ -18,6 +18,7 @@
 //                   continuation | interpolation | join | fallbacks
 //   surface stream  (after the order) surface seeds, node->tria CSR, k_bdy
 #include <hip/hip_runtime.h>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include <math.h>
 #include <stdarg.h>
@@ -50,7 +51,8 @@ namespace {
 // ---------------------------------------------------------------- slot layouts
 
 typedef void (*VolFn)(Bg, const Frame *, const unsigned long long *, int, const double *, const uint8_t *,
-                      const int *, const double *, int, ContEntry *, DevStats *, Slots, int *, int8_t *, int);
+                      const int *, const double *, int, ContEntry *, DevStats *, Slots, int *, int8_t *, int,
+                      double *, int);
 
 struct LayoutEntry {
   int c[6];
@@ -136,11 +138,13 @@ struct pmmg_hip_ctx {
   DevBuf o_xyz, o_tetv, o_adja, o_triv, o_adjt, o_met, o_rec;
   std::vector<DevBuf> o_f;
   // work buffers
-  DevBuf frame, stats, grid, sgrid, cnt, off, binrank, order_v, order_b, cont, xq;
-  DevBuf axh;     // per-axis histograms of the seed grid map (k_axis_hist)
-  DevBuf cbase, fm, fms, scan_b; // Morton binning pass 2: chunk bases, count matrix, its scan, scan sums
-  DevBuf xs1, qs; // Morton binning: placed coordinates (pass 1), coordinates in processing order (pass 2)
-  DevBuf scan_a, cls_cnt;                    // scan block sums, class counts
+  DevBuf frame, stats, grid, sgrid, order_v, order_b, cont, xq;
+  DevBuf axh;                             // per-axis histograms of the seed grid map (k_axis_hist)
+  DevBuf bkeys, bkeys2, bvals, sort_tmp;  // Morton binning: keys, sorted keys, ids, rocPRIM scratch
+  DevBuf qs;                              // volume query coordinates in processing order (Morton path)
+  DevBuf mstage, inv;                     // staged Morton path: records in processing order, inverse permutation
+  int *h_sorted = nullptr;                // pinned: the coherence test's {sorted, bin_bits}, read back in auto mode
+  DevBuf cls_cnt;                            // per-block class counts (surface list compaction)
   DevBuf qmin;                               // tetra quality minimum (pmmg_hip_tetra_qual)
   DevBuf fb_vol, fb_bdy, best, ckey, cidx, bbest, bckey, bcidx;
   // host-mode staging
@@ -168,6 +172,11 @@ struct pmmg_hip_ctx {
   int seed_lanes = 4;  // sampled tetra per seed run of 4 records (PMMG_HIP_SEEDLANES, 1..4)
   int bbox_stride = 16; // the frame's bbox samples every n-th vertex (PMMG_HIP_BBOX)
   int hist_stride = 64; // the seed grid's axis histograms sample every n-th vertex (PMMG_HIP_HIST)
+  int bin_bits = kBinBitsCoherent; // Morton bits per axis of the binning keys when the order is forced (1..7,
+                                    // PMMG_HIP_BINBITS; auto mode: the coherence test picks)
+  int stage_mode = 1;   // PMMG_HIP_STAGE (see run_device)
+  int bin_qs = 0;       // the binning copies the volume queries' coordinates in processing order (PMMG_HIP_BINQS=1;
+                        // r03: -0.5 ms in the walk on a shuffled numbering, +1 ms in the binning)
   int maxstep = 4096; // longer walks go to the exact continuation / exhaustive kernels (PMMG_HIP_MAXSTEP; the
                       // reference caps at ne)
   int fanmax = kFanMax;    // cone fans longer than this take the O(nt) scan (test-only PMMG_HIP_FANMAX)
@@ -480,10 +489,18 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
     return nullptr;
   }
   for (int i = 0; i < EV_COUNT; i++) (void)hipEventCreate(&c->ev[i]);
+  if (hipHostMalloc((void **)&c->h_sorted, 2 * sizeof(int), hipHostMallocDefault) != hipSuccess) {
+    fprintf(stderr, "[parmmg_hip] cannot allocate pinned host memory\n");
+    pmmg_hip_destroy(c);
+    return nullptr;
+  }
   c->tpc = env_int("PMMG_HIP_TPC", c->tpc);
   c->seed_lanes = std::min(4, env_int("PMMG_HIP_SEEDLANES", c->seed_lanes));
   c->bbox_stride = env_int("PMMG_HIP_BBOX", c->bbox_stride);
   c->hist_stride = env_int("PMMG_HIP_HIST", c->hist_stride);
+  c->bin_bits = std::min(7, env_int("PMMG_HIP_BINBITS", c->bin_bits));
+  c->bin_qs = env_int("PMMG_HIP_BINQS", 2) == 1;
+  c->stage_mode = env_int("PMMG_HIP_STAGE", c->stage_mode);
   c->verbose = env_int("PMMG_HIP_VERBOSE", 0);
   c->maxstep = env_int("PMMG_HIP_MAXSTEP", c->maxstep);
   c->fanmax = env_int("PMMG_HIP_FANMAX", c->fanmax);
@@ -502,8 +519,8 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   (void)hipStreamSynchronize(c->stream2);
   if (c->cstream) (void)hipStreamSynchronize(c->cstream);
   DevBuf *bufs[] = {&c->o_xyz, &c->o_tetv, &c->o_adja, &c->o_triv, &c->o_adjt, &c->o_met, &c->o_rec, &c->frame,
-                    &c->stats, &c->grid, &c->sgrid, &c->cnt, &c->off, &c->binrank, &c->order_v,
-                    &c->order_b, &c->cont, &c->xq, &c->xs1, &c->qs, &c->axh, &c->cbase, &c->fm, &c->fms, &c->scan_b, &c->scan_a, &c->cls_cnt, &c->qmin, &c->fb_vol, &c->fb_bdy,
+                    &c->stats, &c->grid, &c->sgrid, &c->order_v,
+                    &c->order_b, &c->cont, &c->xq, &c->qs, &c->axh, &c->bkeys, &c->bkeys2, &c->bvals, &c->sort_tmp, &c->mstage, &c->inv, &c->cls_cnt, &c->qmin, &c->fb_vol, &c->fb_bdy,
                     &c->best, &c->ckey, &c->cidx, &c->bbest, &c->bckey, &c->bcidx, &c->h_xyz,
                     &c->h_cls, &c->h_met, &c->h_elem, &c->h_hit};
   for (DevBuf *b : bufs) release(*b);
@@ -515,6 +532,7 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
     if (c->stage[b]) (void)hipHostFree(c->stage[b]);
     if (c->stage_ev[b]) (void)hipEventDestroy(c->stage_ev[b]);
   }
+  if (c->h_sorted) (void)hipHostFree(c->h_sorted);
   delete c->pool;
   release(c->o_tet4);
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
@@ -809,17 +827,6 @@ static int blocks_for(long long n, int cap) {
   return (int)b;
 }
 
-// device-wide exclusive scan out[0..n] of in[0..n) (pmmg_prep.hpp), gated on
-// the order flag (gate_want < 0: always); bsum: (n / kScanChunk + 1) ints
-static void launch_scan(const int *in, long long n, int *out, int *bsum, const DevStats *st, int gate_want,
-                        hipStream_t s) {
-  const int nb = (int)(n / kScanChunk + 1);
-  const int *gate = gate_want >= 0 ? &st->sorted : nullptr;
-  hipLaunchKernelGGL(k_scan_sums, dim3(nb), dim3(kBlock), 0, s, in, n, bsum, gate, gate_want);
-  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, s, bsum, nb, (int *)nullptr, gate, gate_want);
-  hipLaunchKernelGGL(k_scan_write, dim3(nb), dim3(kBlock), 0, s, in, n, (const int *)bsum, out, gate, gate_want);
-}
-
 // exhaustive fallbacks; every kernel reads its list's count on the device
 // exhaustive fallbacks of the volume queries (main stream, after the exact
 // continuation) and of the surface queries (surface stream, after k_bdy): the
@@ -898,22 +905,11 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   const size_t nq = (size_t)np_new;
   const long long ng = (long long)g * g * g, nsg = bg.nt > 0 ? (long long)gs * gs * gs : 0;
   const long long ncls = (long long)(nq / kScanChunk + 1);
-  // Morton binning: pass-1 tiles (blocks); the (digit, block) count matrix
-  const int nblk = (int)std::min<long long>(1024, std::max<long long>(1, ((long long)np_new + 4095) / 4096));
-  const long long nbin2 = (long long)kBinDigits * nblk;
-  // pass 2: chunks of at most kBinChunk queries of one digit (upper bound),
-  // and their (digit, fine, chunk) count matrix
-  const long long nchunk = ((long long)np_new + kBinChunk - 1) / kBinChunk + kBinDigits;
-  const long long nfm = nchunk * kBinFine;
   if (!ensure(c, c->frame, sizeof(Frame)) || !ensure(c, c->stats, sizeof(DevStats) + kStatParts * sizeof(StatPart)) ||
       !ensure(c, c->grid, 8 * (size_t)ng) || !ensure(c, c->sgrid, 4 * (size_t)nsg) || !ensure(c, c->order_v, 4 * nq) ||
-      !ensure(c, c->order_b, 4 * nq) || 
-      !ensure(c, c->cont, sizeof(ContEntry) * nq) || !ensure(c, c->cnt, 4 * (size_t)nbin2) ||
-      !ensure(c, c->off, 4 * (size_t)(nbin2 + 1)) || !ensure(c, c->binrank, 8 * nq) ||
-      !ensure(c, c->xs1, 24 * nq) || !ensure(c, c->qs, 24 * nq) || !ensure(c, c->cbase, 4 * (kBinDigits + 1)) ||
-      !ensure(c, c->fm, 4 * (size_t)nfm) || !ensure(c, c->fms, 4 * (size_t)(nfm + 1)) ||
-      !ensure(c, c->scan_b, 4 * (size_t)(nfm / kScanChunk + 1)) ||
-      !ensure(c, c->scan_a, 4 * (size_t)(nbin2 / kScanChunk + 1)) || !ensure(c, c->cls_cnt, 4 * (size_t)ncls) ||
+      !ensure(c, c->order_b, 4 * nq) || !ensure(c, c->cont, sizeof(ContEntry) * nq) ||
+      !ensure(c, c->bkeys, 4 * nq) || !ensure(c, c->bkeys2, 4 * nq) || !ensure(c, c->bvals, 4 * nq) ||
+      !ensure(c, c->qs, 24 * nq) || !ensure(c, c->cls_cnt, 4 * (size_t)ncls) ||
       !ensure(c, c->fb_vol, 4 * nq) || !ensure(c, c->fb_bdy, 4 * nq) || !ensure(c, c->best, 4 * nq) ||
       !ensure(c, c->ckey, 8 * nq) || !ensure(c, c->cidx, 4 * nq) || !ensure(c, c->bbest, 4 * nq) ||
       !ensure(c, c->bckey, 8 * nq) || !ensure(c, c->bcidx, 4 * nq))
@@ -938,42 +934,19 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   hipLaunchKernelGGL(k_frame_final, dim3(1), dim3(1), 0, s, fr, g, gs, gb);
   hipLaunchKernelGGL(k_axis_hist, dim3(kHistBlocks), dim3(kBlock), 0, s, bg.xyz, bg.np, (const Frame *)fr,
                      c->hist_stride, (int *)c->axh.p);
-  hipLaunchKernelGGL(k_axis_map, dim3(3), dim3(kBlock), 0, s, (const int *)c->axh.p, fr);
+  hipLaunchKernelGGL(k_axis_map, dim3(3), dim3(kBlock), 0, s, (const int *)c->axh.p, fr, g);
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[EV_FRAME], s));
 
   // ---- query order (second stream, concurrent with the seed grid): the
-  // coherence test decides on the device; Morton bins (sorted == 1) or the
-  // stable class compaction of the surface points (sorted == 0) are both
-  // enqueued, one runs
+  // coherence test runs first; in auto mode its flag is read back while the
+  // main stream builds the seed grid (the host waits ~0.1 ms, the device does
+  // not), then either the Morton binning (sorted) or the stable class
+  // compaction of the surface points (input order) is enqueued
   HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_FRAME], 0));
-  hipLaunchKernelGGL(k_coherence, dim3(1), dim3(kBlock), 0, sb, xyz_new, np_new, st, force);
-  {
-    hipLaunchKernelGGL(k_bin_hist, dim3(nblk), dim3(kBlock), 0, sb, xyz_new, pclass, np_new, (const Frame *)fr,
-                       (int *)c->cnt.p, (const DevStats *)st);
-    launch_scan((const int *)c->cnt.p, nbin2, (int *)c->off.p, (int *)c->scan_a.p, st, 1, sb);
-    hipLaunchKernelGGL(k_bin_place, dim3(nblk), dim3(kBlock), 0, sb, xyz_new, pclass, np_new, (const Frame *)fr,
-                       (const int *)c->off.p, (int2 *)c->binrank.p, (double *)c->xs1.p, (const DevStats *)st);
-    hipLaunchKernelGGL(k_bin_chunks, dim3(1), dim3(kBlock), 0, sb, (const int *)c->off.p, nblk, (int *)c->cbase.p,
-                       (const DevStats *)st);
-    hipLaunchKernelGGL(k_bin_fine_hist, dim3((unsigned)nchunk), dim3(kBlock), 0, sb, (const int *)c->off.p, nblk,
-                       (const int *)c->cbase.p, (const int2 *)c->binrank.p, (int *)c->fm.p, (const DevStats *)st);
-    launch_scan((const int *)c->fm.p, nfm, (int *)c->fms.p, (int *)c->scan_b.p, st, 1, sb);
-    hipLaunchKernelGGL(k_bin_fine_place, dim3((unsigned)nchunk), dim3(kBlock), 0, sb, (const int *)c->off.p, nblk,
-                       (const int *)c->cbase.p, (const int2 *)c->binrank.p, (const double *)c->xs1.p,
-                       (const int *)c->fms.p, order_v, (double *)c->qs.p, order_b, st);
-    if (bg.nt > 0) {
-      int *bc = (int *)c->cls_cnt.p;
-      hipLaunchKernelGGL(k_cls_count, dim3((unsigned)ncls), dim3(kBlock), 0, sb, pclass, (long long)np_new,
-                         (int)PMMG_PT_BDY, bc, (const DevStats *)st);
-      hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, sb, bc, (int)ncls, &st->nbdy,
-                         (const int *)&st->sorted, 0);
-      hipLaunchKernelGGL(k_cls_scatter, dim3((unsigned)ncls), dim3(kBlock), 0, sb, pclass, (long long)np_new,
-                         (int)PMMG_PT_BDY, (const int *)bc, order_b, (const DevStats *)st);
-    }
-  }
+  hipLaunchKernelGGL(k_coherence, dim3(1), dim3(kBlock), 0, sb, xyz_new, np_new, st, force, c->bin_bits);
+  if (force < 0) HIPCK(c, hipMemcpyAsync(c->h_sorted, &st->sorted, 2 * sizeof(int), hipMemcpyDeviceToHost, sb));
   HIPCK(c, hipGetLastError());
-  HIPCK(c, hipEventRecord(c->ev[EV_ORDER], sb));
 
   // ---- seed grid (main stream): fixed-point vertex copy, volume seeds
   hipLaunchKernelGGL(k_quantize, dim3(blocks_for(3LL * bg.np, 8192)), dim3(kBlock), 0, s, bg.xyz, (long long)bg.np,
@@ -985,6 +958,46 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   }
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[EV_PREP], s));
+
+  int sorted = force, bits = c->bin_bits;
+  if (force < 0) {
+    HIPCK(c, hipStreamSynchronize(sb));
+    sorted = c->h_sorted[0];
+    bits = c->h_sorted[1];
+  }
+  // Morton order of a numbering without coherence: rows staged in processing
+  // order and copied back by k_vol_unpermute (PMMG_HIP_STAGE: 1 auto, 2 never,
+  // 3 whenever the queries are binned)
+  int rs = 2; // record: the K doubles of the slots, the tag, a pad double when K is even (16-byte pieces)
+  for (int j = 0; j < S.n; j++) rs += S.s[j].code;
+  rs &= ~1;
+  const bool staged = sorted && np_new > 0 && pick_layout(S) != k_vol<false, -1, 0, 0, 0, 0, 0> &&
+                      rs <= kUnpermuteMaxRs && (c->stage_mode == 3 || (c->stage_mode == 1 && bits == kBinBitsAxis));
+  if (staged && (!ensure(c, c->mstage, sizeof(double) * (size_t)rs * nq) || !ensure(c, c->inv, 4 * nq))) return 0;
+  if (sorted && np_new > 0) {
+    hipLaunchKernelGGL(k_bin_keys, dim3(blocks_for(np_new, 1024)), dim3(kBlock), 0, sb, xyz_new, pclass, np_new,
+                       (const Frame *)fr, bits, (unsigned *)c->bkeys.p, (int *)c->bvals.p, st);
+    const int key_bits = 3 * bits + 2;
+    size_t tmp = 0;
+    HIPCK(c, rocprim::radix_sort_pairs(nullptr, tmp, (const unsigned *)c->bkeys.p, (unsigned *)c->bkeys2.p,
+                                       (const int *)c->bvals.p, order_v, np_new, 0, key_bits, sb));
+    if (!ensure(c, c->sort_tmp, tmp)) return 0;
+    HIPCK(c, rocprim::radix_sort_pairs(c->sort_tmp.p, tmp, (const unsigned *)c->bkeys.p, (unsigned *)c->bkeys2.p,
+                                       (const int *)c->bvals.p, order_v, np_new, 0, key_bits, sb));
+    hipLaunchKernelGGL(k_bin_split, dim3(blocks_for(np_new, 4096)), dim3(kBlock), 0, sb, (const int *)order_v, xyz_new,
+                       np_new, order_b, c->bin_qs ? (double *)c->qs.p : nullptr, staged ? (int *)c->inv.p : nullptr,
+                       (const DevStats *)st);
+  } else if (bg.nt > 0) {
+    int *bc = (int *)c->cls_cnt.p;
+    hipLaunchKernelGGL(k_cls_count, dim3((unsigned)ncls), dim3(kBlock), 0, sb, pclass, (long long)np_new,
+                       (int)PMMG_PT_BDY, bc, (const DevStats *)st);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, sb, bc, (int)ncls, &st->nbdy, (const int *)&st->sorted,
+                       0);
+    hipLaunchKernelGGL(k_cls_scatter, dim3((unsigned)ncls), dim3(kBlock), 0, sb, pclass, (long long)np_new,
+                       (int)PMMG_PT_BDY, (const int *)bc, order_b, (const DevStats *)st);
+  }
+  HIPCK(c, hipGetLastError());
+  HIPCK(c, hipEventRecord(c->ev[EV_ORDER], sb));
 
   // ---- surface branch (second stream, after the order): seeds, k_bdy
   HIPCK(c, hipEventRecord(c->ev[EV_BDY0], sb));
@@ -1005,9 +1018,14 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   // kernel, then the exact continuation of the few queries it did not settle
   hipLaunchKernelGGL(vol_fn, dim3((np_new + 63) / 64), dim3(64), 0, s, bg, (const Frame *)fr,
                      (const unsigned long long *)grid, g, xyz_new, pclass, (const int *)order_v,
-                     (const double *)c->qs.p, np_new,
-                     (ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->filter_steps);
+                     c->bin_qs ? (const double *)c->qs.p : nullptr, np_new,
+                     (ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->filter_steps,
+                     staged ? (double *)c->mstage.p : nullptr, rs);
   HIPCK(c, hipEventRecord(c->ev[EV_WALK], s));
+  if (staged)
+    hipLaunchKernelGGL(k_vol_unpermute, dim3((np_new + 63) / 64 < 65536 ? (np_new + 63) / 64 : 65536), dim3(64), 0, s,
+                       pclass, np_new,
+                       (const int *)c->inv.p, (const double *)c->mstage.p, rs, S, elem_out, hit_out);
   hipLaunchKernelGGL(k_vol_walk_exact, dim3(8 * 64), dim3(64), 0, s, bg, xyz_new, (int *)c->fb_vol.p,
                      (const ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->maxstep);
   HIPCK(c, hipGetLastError());

@@ -2,11 +2,11 @@
 // (included by pmmg_hip.hip only): state reset, background frame, volume and
 // surface seed grids, and the query order.
 //
-// Every decision is taken on the device: the input-order coherence test
-// writes DevStats::sorted, and the Morton-binning kernels and the class
-// compaction of the surface list are both enqueued and return at once when
-// the flag does not select them.  No kernel result is read back by the host
-// inside a call.
+// The input-order coherence test runs on the device (DevStats::sorted); in
+// auto mode the host reads that one flag back while the main stream builds
+// the seed grid, then enqueues either the Morton binning (a rocPRIM radix
+// sort: its kernels cannot be gated on a device flag) or the class compaction
+// of the surface list.  No other result is read back inside a call.
 #pragma once
 
 #include "pmmg_device.hpp"
@@ -23,7 +23,8 @@ struct DevStats {
   int nfb_vol, nfb_bdy; // fallback lists (exhaustive searches)
   int ncont;            // walks continued in exact arithmetic (k_vol_walk_exact)
   int sorted;           // 1: queries Morton-binned, 0: input order (coherent numbering)
-  int pad[2];
+  int bin_bits;         // Morton bits per axis of the binning keys (read back with `sorted`)
+  int pad;
 };
 
 constexpr int kStatParts = 256;
@@ -109,12 +110,12 @@ __device__ __forceinline__ void wave_count(BlockStats *bs, int slot, bool pred) 
 // background vertices' coordinates (a sampled histogram of kMapBins bins,
 // linear inside a bin): each slab of cells holds the same share of the
 // vertices, which for a grading separable by axis makes every cell hold the
-// same number of tetra.  An axis whose densest bin is below kMapRatio x the
-// mean of its occupied bins keeps the uniform cells (bit 0 of `adaptive`
-// per axis clear): the shell and cube lattices are not remapped.
+// same number of tetra.  An axis whose heaviest uniform-cell slab holds less
+// than kMapRatio x the mean slab keeps the uniform cells (its bit of
+// `adaptive` clear): the shell and cube lattices are not remapped.
 constexpr int kMapBins = 2048;
-constexpr int kMapRatio = 16;
-constexpr int kHistBlocks = 128;
+constexpr int kMapRatio = 4;
+constexpr int kHistBlocks = 32;
 
 struct Frame {
   unsigned long long key_lo[3], key_hi[3];
@@ -323,11 +324,13 @@ __global__ __launch_bounds__(kBlock) void k_seed_vol(Bg bg, const Frame *fr, uns
 }
 
 // rare path of seed_vol (the 8 cells are empty): lowest seed id in the shells
-// of radius 1 then 2 around the cell; 0 when there is none (the query then
-// goes to the exact continuation, which hands it to the exhaustive search)
+// of radius 1, 2, ... kSeedRing around the cell; 0 when there is none (the
+// query then goes to the exact continuation, which hands it to the
+// exhaustive search: O(ne) per query, so the shells go far)
+constexpr int kSeedRing = 6;
 __device__ __noinline__ int seed_vol_ring(const unsigned long long *cell, int g, int ci, int cj, int ck) {
 #pragma unroll 1
-  for (int r = 1; r <= 2; r++) {
+  for (int r = 1; r <= kSeedRing; r++) {
     unsigned long long best = ~0ULL;
 #pragma unroll 1
     for (int dk = -r; dk <= r; dk++)
@@ -429,10 +432,9 @@ __device__ int seed_srf(const int *cell, int g, const Frame *fr, const double *x
 
 // ---------------------------------------------------------------- device-wide exclusive scan
 //
-// out[0..n] = exclusive prefix sums of in[0..n) (out[n] = total), in three
-// launches (per-block sums, scan of the block sums, per-block scan).  When
-// `gate` is non-null the kernels run only if *gate == want, so a scan can be
-// enqueued for a path the device may not take.
+// block-level exclusive scans, and k_scan_top (one block: the exclusive scan
+// of a short array, e.g. per-block counts).  When `gate` is non-null the
+// kernel runs only if *gate == want.
 constexpr int kScanItems = 16, kScanChunk = kBlock * kScanItems;
 
 __device__ __forceinline__ int wave_incl_scan(int v) {
@@ -465,18 +467,6 @@ __device__ __forceinline__ int block_excl_scan(int v, int *tot) {
 
 __device__ __forceinline__ bool gate_off(const int *gate, int want) { return gate && *gate != want; }
 
-__global__ __launch_bounds__(kBlock) void k_scan_sums(const int *in, long long n, int *bsum, const int *gate,
-                                                      int want) {
-  if (gate_off(gate, want)) return;
-  const long long i0 = (long long)blockIdx.x * kScanChunk + (long long)threadIdx.x * kScanItems;
-  int s = 0;
-#pragma unroll
-  for (int j = 0; j < kScanItems; j++) s += (i0 + j < n) ? in[i0 + j] : 0;
-  int tot;
-  block_excl_scan(s, &tot);
-  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
-}
-
 // one block: bsum[0..nb) -> exclusive offsets in place; the total -> *total
 __global__ __launch_bounds__(kBlock) void k_scan_top(int *bsum, int nb, int *total, const int *gate, int want) {
   if (gate_off(gate, want)) return;
@@ -490,26 +480,6 @@ __global__ __launch_bounds__(kBlock) void k_scan_top(int *bsum, int nb, int *tot
     carry += tot;
   }
   if (threadIdx.x == 0 && total) *total = carry;
-}
-
-__global__ __launch_bounds__(kBlock) void k_scan_write(const int *in, long long n, const int *bsum, int *out,
-                                                       const int *gate, int want) {
-  if (gate_off(gate, want)) return;
-  const long long i0 = (long long)blockIdx.x * kScanChunk + (long long)threadIdx.x * kScanItems;
-  int v[kScanItems], s = 0;
-#pragma unroll
-  for (int j = 0; j < kScanItems; j++) {
-    v[j] = (i0 + j < n) ? in[i0 + j] : 0;
-    s += v[j];
-  }
-  int tot;
-  int pre = bsum[blockIdx.x] + block_excl_scan(s, &tot);
-#pragma unroll
-  for (int j = 0; j < kScanItems; j++) {
-    if (i0 + j < n) out[i0 + j] = pre;
-    pre += v[j];
-  }
-  if (i0 <= n && n < i0 + kScanItems) out[n] = pre; // the thread holding the end writes the total
 }
 
 // ---------------------------------------------------------------- seed grid axis maps
@@ -535,48 +505,69 @@ __global__ __launch_bounds__(kBlock) void k_axis_hist(const double *xyz, int np,
   for (int j = threadIdx.x; j < 3 * kMapBins; j += kBlock) H[(size_t)blockIdx.x * 3 * kMapBins + j] = (&h[0][0])[j];
 }
 
-// one block per axis: counts -> quantile map, adaptive bit
-__global__ __launch_bounds__(kBlock) void k_axis_map(const int *H, Frame *fr) {
+// one block per axis: counts -> quantile map, adaptive bit.  The test is on
+// the scale of the grid's cells: the heaviest window of kMapBins / g bins
+// (one uniform cell's slab) against the mean slab, g * max / total.  Bins
+// finer than a cell cannot decide it (a lattice's coordinates fill only the
+// bins its planes fall into).
+__global__ __launch_bounds__(kBlock) void k_axis_map(const int *H, Frame *fr, int g) {
   constexpr int R = kMapBins / kBlock; // bins per thread
   const int d = blockIdx.x;
-  int cnt[R], s = 0, mx = 0, occ = 0;
+  __shared__ int cum[kMapBins + 1]; // cum[b] = vertices in bins [0, b)
+  int cnt[R], s = 0;
 #pragma unroll
   for (int q = 0; q < R; q++) {
     const int b = R * threadIdx.x + q;
     int v = 0;
+#pragma unroll 16
     for (int k = 0; k < kHistBlocks; k++) v += H[(size_t)k * 3 * kMapBins + d * kMapBins + b];
     cnt[q] = v;
     s += v;
-    mx = v > mx ? v : mx;
-    occ += v > 0 ? 1 : 0;
   }
   int tot;
   const int pre = block_excl_scan(s, &tot);
-  __shared__ int smx[kBlock], socc[kBlock];
+  {
+    int run = pre;
+#pragma unroll
+    for (int q = 0; q < R; q++) {
+      cum[R * threadIdx.x + q] = run;
+      run += cnt[q];
+    }
+    if (threadIdx.x == kBlock - 1) cum[kMapBins] = run;
+  }
+  __syncthreads();
+  const int W = (kMapBins + g - 1) / (g > 0 ? g : 1); // bins per uniform cell
+  int mx = 0;
+#pragma unroll
+  for (int q = 0; q < R; q++) {
+    const int b = R * threadIdx.x + q, e = b + W < kMapBins ? b + W : kMapBins;
+    const int w = cum[e] - cum[b];
+    mx = w > mx ? w : mx;
+  }
+  __shared__ int smx[kBlock];
   smx[threadIdx.x] = mx;
-  socc[threadIdx.x] = occ;
   __syncthreads();
   for (int o = kBlock / 2; o > 0; o >>= 1) {
-    if (threadIdx.x < o) {
-      smx[threadIdx.x] = smx[threadIdx.x + o] > smx[threadIdx.x] ? smx[threadIdx.x + o] : smx[threadIdx.x];
-      socc[threadIdx.x] += socc[threadIdx.x + o];
-    }
+    if (threadIdx.x < o) smx[threadIdx.x] = smx[threadIdx.x + o] > smx[threadIdx.x] ? smx[threadIdx.x + o] : smx[threadIdx.x];
     __syncthreads();
   }
-  // adaptive: the densest bin holds more than kMapRatio x the mean occupied bin
-  const bool adapt = tot > 0 && (long long)smx[0] * socc[0] > (long long)kMapRatio * tot;
-  int run = pre;
+  const bool adapt = tot > 0 && (long long)smx[0] * g > (long long)kMapRatio * tot;
 #pragma unroll
   for (int q = 0; q < R; q++) {
     const int b = R * threadIdx.x + q;
-    fr->map[d][b] = adapt ? (float)((double)run / (double)tot) : (float)b / (float)kMapBins;
-    run += cnt[q];
+    fr->map[d][b] = adapt ? (float)((double)cum[b] / (double)tot) : (float)b / (float)kMapBins;
   }
   if (threadIdx.x == kBlock - 1) fr->map[d][kMapBins] = 1.0f;
   if (threadIdx.x == 0 && adapt) atomicOr(&fr->adaptive, 1 << d);
 }
 
 // ---------------------------------------------------------------- query order
+
+constexpr int kBinBitsAxis = 7;     // Morton binning: at most 128^3 cells (Frame::inv_bin); the sort keys use the top
+                                    // `bits` of every axis
+constexpr int kBinBitsCoherent = 5; // 32^3 cells for a mostly coherent numbering (r03: forced bins on the lattice
+                                    // numbering, volume stage 4.71 ms at 7 bits, 3.85 at 5; a shuffled one 7.98 at 7,
+                                    // 8.83 at 5)
 
 // Is the input numbering spatially coherent?  Distances between consecutive
 // points at 4096 pseudo-random positions against the mean spacing h of np
@@ -585,9 +576,13 @@ __global__ __launch_bounds__(kBlock) void k_axis_map(const int *H, Frame *fr) {
 // local numbering runs do not count; a shuffled numbering has almost every
 // distance at the scale of the bbox).  force: 1 always Morton-bin, 0 never,
 // -1 test.  Writes st->sorted.
-__global__ __launch_bounds__(kBlock) void k_coherence(const double *xyz, int np, DevStats *st, int force) {
+__global__ __launch_bounds__(kBlock) void k_coherence(const double *xyz, int np, DevStats *st, int force,
+                                                      int force_bits) {
   if (force >= 0) {
-    if (threadIdx.x == 0) st->sorted = force;
+    if (threadIdx.x == 0) {
+      st->sorted = force;
+      st->bin_bits = force_bits;
+    }
     return;
   }
   constexpr int nsamp = 4096, per = nsamp / kBlock;
@@ -641,200 +636,88 @@ __global__ __launch_bounds__(kBlock) void k_coherence(const double *xyz, int np,
   if (threadIdx.x == 0) {
     int tot = 0;
     for (int j = 0; j < kBlock; j++) tot += s_near[j];
-    st->sorted = (np > 1 && 2 * tot >= nsamp) ? 0 : 1;
+    // input order when 95 % of the steps are short; else Morton bins, with
+    // coarse cells (kBinBitsCoherent bits per axis: the input order inside a
+    // cell is kept and mostly coherent) when at least half are short, fine
+    // cells (kBinBitsAxis) for a numbering without coherence
+    const bool coherent = np > 1 && 20 * tot >= 19 * nsamp;
+    st->sorted = coherent ? 0 : 1;
+    st->bin_bits = 2 * tot >= nsamp ? kBinBitsCoherent : kBinBitsAxis;
   }
 }
 
-// ---------------------------------------------------------------- Morton binning (st->sorted == 1 only)
+// ---------------------------------------------------------------- Morton binning (sorted order only)
 //
 // Queries of a numbering without spatial coherence are processed in Morton
-// order of a 64^3 grid over the frame, in two counting passes without global
-// atomics (r03; the r02 binning took one returning device-scope atomicAdd per
-// query on 2M bins: 1.9 ms at cfg4 on a shuffled numbering):
-//   pass 1 (k_bin_hist, scan, k_bin_place) — digit = (class, coarse cell: the
-//     top 3 bits per axis, 512 cells): per-block LDS histograms in a
-//     digit-major matrix, one device-wide scan gives every (digit, block) its
-//     range, the block places its queries there through LDS counters; a
-//     placed query carries {id, fine key} and its coordinates;
-//   pass 2 (k_bin_chunks, k_bin_fine_hist, scan, k_bin_fine_place) — the
-//     same counting sort inside every digit by the fine key (the low 4 bits
-//     per axis, 512 cells), on chunks of at most 4096 queries of one digit;
-//     the result is the order list plus a copy of the coordinates in that
-//     order (the walk then loads its queries coalesced).
-// Order inside a fine cell is not deterministic (LDS counters); every query's
-// result is a pure function of the query, so no output depends on it.
-constexpr int kBinBitsAxis = 6;                  // 64^3 grid (Frame::inv_bin)
-constexpr int kBinCoarse = 512;                  // 8^3 coarse cells per class
-constexpr int kBinDigits = 2 * kBinCoarse;       // volume digits first, then surface
-constexpr int kBinFine = 512;                    // 8^3 fine cells per coarse cell
-constexpr int kBinChunk = kBlock * 16;           // queries per pass-2 chunk
+// order of a 128^3 grid over the frame: k_bin_keys writes one 32-bit key per
+// query {class: 0 volume, 1 surface, 2 neither | 21-bit Morton code} and its
+// id, rocPRIM's radix sort (stable, 3 passes of 8 bits) orders them (r03: the
+// earlier per-query atomicAdd on 2M bins took 1.9 ms at cfg4 on a shuffled
+// numbering; a hand-written two-level counting sort without global atomics
+// still 2.5 ms, its scattered partial-line writes across XCDs dominating),
+// and k_bin_split cuts the sorted ids into the volume list (plus a copy of
+// the volume queries' coordinates in processing order, so that the walk loads
+// them coalesced) and the surface list.  The radix sort is stable: the order
+// is a deterministic function of the input.
 
-// digit (-1: neither a volume nor a surface query) and fine key of query i
-__device__ __forceinline__ int bin_key(const double *xyz, const uint8_t *pclass, long long i, const Frame *fr,
-                                       int *fine, double *x) {
-  const int c = pclass[i];
-  if (c != PMMG_PT_VOL && c != PMMG_PT_BDY) return -1;
-  uint32_t q[3];
+__global__ __launch_bounds__(kBlock) void k_bin_keys(const double *xyz, const uint8_t *pclass, int np, const Frame *fr,
+                                                     int bits, unsigned *keys, int *vals, DevStats *st) {
+  int nv = 0, nb = 0;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < np; i += (long long)gridDim.x * blockDim.x) {
+    const int c = pclass[i];
+    unsigned cls = 2u;
+    uint32_t q[3] = {0u, 0u, 0u};
+    if (c == PMMG_PT_VOL || c == PMMG_PT_BDY) {
+      cls = c == PMMG_PT_VOL ? 0u : 1u;
+      nv += c == PMMG_PT_VOL;
+      nb += c == PMMG_PT_BDY;
 #pragma unroll
-  for (int d = 0; d < 3; d++) {
-    x[d] = xyz[3 * i + d];
-    q[d] = (uint32_t)cell_coord(x[d], fr->lo[d], fr->inv_bin[d], 1 << kBinBitsAxis);
+      for (int d = 0; d < 3; d++)
+        q[d] = (uint32_t)cell_coord(xyz[3 * i + d], fr->lo[d], fr->inv_bin[d], 1 << kBinBitsAxis) >>
+               (kBinBitsAxis - bits);
+    }
+    keys[i] = (cls << (3 * bits)) | (expand10(q[0]) << 2) | (expand10(q[1]) << 1) | expand10(q[2]);
+    vals[i] = (int)(i + 1);
   }
-  const uint32_t lo = 7u;
-  *fine = (int)((expand10(q[0] & lo) << 2) | (expand10(q[1] & lo) << 1) | expand10(q[2] & lo));
-  const int coarse = (int)((expand10(q[0] >> 3) << 2) | (expand10(q[1] >> 3) << 1) | expand10(q[2] >> 3));
-  return coarse + (c == PMMG_PT_BDY ? kBinCoarse : 0);
-}
-
-// block b's contiguous tile of the queries
-__device__ __forceinline__ void bin_tile(int np, int nblk, long long *lo, long long *hi) {
-  const long long per = ((long long)np + nblk - 1) / nblk;
-  *lo = (long long)blockIdx.x * per;
-  *hi = *lo + per < np ? *lo + per : np;
-}
-
-// pass 1: H[digit * nblk + block] = the block's count (gridDim.x == nblk)
-__global__ __launch_bounds__(kBlock) void k_bin_hist(const double *xyz, const uint8_t *pclass, int np, const Frame *fr,
-                                                     int *H, const DevStats *st) {
-  if (!st->sorted) return;
-  __shared__ int h[kBinDigits];
-  for (int j = threadIdx.x; j < kBinDigits; j += kBlock) h[j] = 0;
+  __shared__ int sv, sb;
+  if (threadIdx.x == 0) sv = sb = 0;
   __syncthreads();
-  long long lo, hi;
-  bin_tile(np, gridDim.x, &lo, &hi);
-  for (long long i = lo + threadIdx.x; i < hi; i += kBlock) {
-    int f;
-    double x[3];
-    const int d = bin_key(xyz, pclass, i, fr, &f, x);
-    if (d >= 0) atomicAdd(&h[d], 1);
+  for (int o = 32; o > 0; o >>= 1) {
+    nv += __shfl_down(nv, o);
+    nb += __shfl_down(nb, o);
+  }
+  if (__lane_id() == 0) {
+    atomicAdd(&sv, nv);
+    atomicAdd(&sb, nb);
   }
   __syncthreads();
-  for (int j = threadIdx.x; j < kBinDigits; j += kBlock) H[(size_t)j * gridDim.x + blockIdx.x] = h[j];
-}
-
-// pass 1: O = exclusive scan of H; the block's queries of digit d go to
-// [O[d * nblk + b], ...): {id, fine} and the coordinates
-__global__ __launch_bounds__(kBlock) void k_bin_place(const double *xyz, const uint8_t *pclass, int np,
-                                                      const Frame *fr, const int *O, int2 *key1, double *xs1,
-                                                      const DevStats *st) {
-  if (!st->sorted) return;
-  __shared__ int cur[kBinDigits];
-  for (int j = threadIdx.x; j < kBinDigits; j += kBlock) cur[j] = O[(size_t)j * gridDim.x + blockIdx.x];
-  __syncthreads();
-  long long lo, hi;
-  bin_tile(np, gridDim.x, &lo, &hi);
-  for (long long i = lo + threadIdx.x; i < hi; i += kBlock) {
-    int f;
-    double x[3];
-    const int d = bin_key(xyz, pclass, i, fr, &f, x);
-    if (d < 0) continue;
-    const int p = atomicAdd(&cur[d], 1);
-    key1[p] = make_int2((int)(i + 1), f);
-    xs1[3 * (size_t)p] = x[0];
-    xs1[3 * (size_t)p + 1] = x[1];
-    xs1[3 * (size_t)p + 2] = x[2];
+  if (threadIdx.x == 0) {
+    if (sv) atomicAdd(&st->nvol, sv);
+    if (sb) atomicAdd(&st->nbdy, sb);
   }
 }
 
-// pass 2 works on chunks of at most kBinChunk queries that never straddle a
-// digit: digit d's n_d queries form ceil(n_d / kBinChunk) chunks, chunk ids
-// in digit order (cbase[d] = chunks before digit d, cbase[kBinDigits] = all)
-__global__ __launch_bounds__(kBlock) void k_bin_chunks(const int *O, int nblk, int *cbase, const DevStats *st) {
-  if (!st->sorted) return;
-  constexpr int R = kBinDigits / kBlock;
-  int n[R], s = 0;
-#pragma unroll
-  for (int q = 0; q < R; q++) {
-    const int d = R * threadIdx.x + q;
-    const int cnt = O[(size_t)(d + 1) * nblk] - O[(size_t)d * nblk];
-    n[q] = (cnt + kBinChunk - 1) / kBinChunk;
-    s += n[q];
-  }
-  int tot;
-  int pre = block_excl_scan(s, &tot);
-#pragma unroll
-  for (int q = 0; q < R; q++) {
-    cbase[R * threadIdx.x + q] = pre;
-    pre += n[q];
-  }
-  if (threadIdx.x == 0) cbase[kBinDigits] = tot;
-}
-
-// chunk b of pass 2 (b < cbase[kBinDigits]): its digit d (binary search),
-// its index j inside the digit, the digit's chunk count and the queries
-// [q0, q1) of key1 / xs1
-struct BinChunk {
-  int d, j, nch, q0, q1;
-};
-__device__ __forceinline__ bool bin_chunk(const int *O, int nblk, const int *cbase, int b, BinChunk *c) {
-  if (b >= cbase[kBinDigits]) return false;
-  int lo = 0, hi = kBinDigits; // cbase[lo] <= b < cbase[hi]
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (cbase[mid] <= b) lo = mid;
-    else hi = mid;
-  }
-  c->d = lo;
-  c->j = b - cbase[lo];
-  c->nch = cbase[lo + 1] - cbase[lo];
-  const int b0 = O[(size_t)lo * nblk], b1 = O[(size_t)(lo + 1) * nblk];
-  c->q0 = b0 + c->j * kBinChunk;
-  c->q1 = c->q0 + kBinChunk < b1 ? c->q0 + kBinChunk : b1;
-  return true;
-}
-// entry (d, fine f, chunk j) of the pass-2 count matrix, ordered digit,
-// fine key, chunk: its exclusive scan is the final position of the first
-// query of chunk j with key (d, f)
-__device__ __forceinline__ size_t bin_m_index(const int *cbase, const BinChunk &c, int f) {
-  return (size_t)cbase[c.d] * kBinFine + (size_t)f * c.nch + c.j;
-}
-
-// pass 2: per chunk, the LDS histogram of its fine keys into the matrix
-// (grid: an upper bound of the chunk count; chunks past the real count exit)
-__global__ __launch_bounds__(kBlock) void k_bin_fine_hist(const int *O, int nblk, const int *cbase, const int2 *key1,
-                                                          int *M, const DevStats *st) {
-  if (!st->sorted) return;
-  BinChunk c;
-  if (!bin_chunk(O, nblk, cbase, blockIdx.x, &c)) return;
-  __shared__ int h[kBinFine];
-  for (int f = threadIdx.x; f < kBinFine; f += kBlock) h[f] = 0;
-  __syncthreads();
-  for (int q = c.q0 + threadIdx.x; q < c.q1; q += kBlock) atomicAdd(&h[key1[q].y], 1);
-  __syncthreads();
-  for (int f = threadIdx.x; f < kBinFine; f += kBlock) M[bin_m_index(cbase, c, f)] = h[f];
-}
-
-// pass 2: after the scan of M, every chunk places its queries at their final
-// positions: the order lists and, for volume queries, the coordinates in
-// processing order (the walk then loads its queries coalesced)
-__global__ __launch_bounds__(kBlock) void k_bin_fine_place(const int *O, int nblk, const int *cbase, const int2 *key1,
-                                                           const double *xs1, const int *Ms, int *order_v, double *qs,
-                                                           int *order_b, DevStats *st) {
-  if (!st->sorted) return;
-  const int nvol = O[(size_t)kBinCoarse * nblk];
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    st->nvol = nvol;
-    st->nbdy = O[(size_t)kBinDigits * nblk] - nvol;
-  }
-  BinChunk c;
-  if (!bin_chunk(O, nblk, cbase, blockIdx.x, &c)) return;
-  __shared__ int cur[kBinFine];
-  for (int f = threadIdx.x; f < kBinFine; f += kBlock) cur[f] = Ms[bin_m_index(cbase, c, f)];
-  __syncthreads();
-  for (int q = c.q0 + threadIdx.x; q < c.q1; q += kBlock) {
-    const int2 kv = key1[q];
-    const int pos = atomicAdd(&cur[kv.y], 1);
-    if (c.d < kBinCoarse) {
-      order_v[pos] = kv.x;
-      qs[3 * (size_t)pos] = xs1[3 * (size_t)q];
-      qs[3 * (size_t)pos + 1] = xs1[3 * (size_t)q + 1];
-      qs[3 * (size_t)pos + 2] = xs1[3 * (size_t)q + 2];
+// sorted ids -> volume list (order_v, in place) + the volume queries'
+// coordinates in that order (qs, when non-null) + the inverse permutation
+// (inv, when non-null), surface list (order_b)
+__global__ __launch_bounds__(kBlock) void k_bin_split(const int *sorted_ids, const double *xyz, int np, int *order_b,
+                                                      double *qs, int *inv, const DevStats *st) {
+  const int nvol = st->nvol, nbdy = st->nbdy;
+  for (long long j = (qs || inv ? 0 : nvol) + blockIdx.x * (long long)blockDim.x + threadIdx.x; j < nvol + nbdy;
+       j += (long long)gridDim.x * blockDim.x) {
+    const int ip = sorted_ids[j];
+    if (j < nvol) {
+      if (qs) {
+        qs[3 * j] = xyz[3 * (size_t)(ip - 1)];
+        qs[3 * j + 1] = xyz[3 * (size_t)(ip - 1) + 1];
+        qs[3 * j + 2] = xyz[3 * (size_t)(ip - 1) + 2];
+      }
+      if (inv) inv[ip - 1] = (int)j; // the staged path's way back (k_vol_unpermute)
     } else {
-      order_b[pos - nvol] = kv.x;
+      order_b[j - nvol] = ip;
     }
   }
 }
-
 
 // Stable class compaction (the surface list, input-order path only): out =
 // the ids ip (1-based) with pclass[ip-1] == cls, in input order; *count =

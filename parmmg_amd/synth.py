@@ -178,3 +178,20 @@ def cell_stats(m: Mesh) -> dict:
     h = np.cbrt(vol)
     return {"size_grading": float(h.max() / h.min()), "max_aspect": float((L.max(1) / L.min(1)).max()),
             "min_volume": float(vol.min())}
+
+
+def mmg_like_perm(nq: int) -> np.ndarray:
+    """A numbering of the new points like Mmg's output after an adaptation
+    (src/libparmmg1.c:692-741: the group is renumbered, then Mmg keeps the
+    retained vertices in their order and appends the vertices it inserts,
+    in creation order): one point in six (a splitmix64 hash of its id,
+    spread evenly over the domain) counts as inserted and moves to the end,
+    both parts keeping the generator's order.  perm[new id] = old id."""
+    ids = np.arange(nq, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = ids * np.uint64(0x9E3779B97F4A7C15) + np.uint64(0x5EED2025)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z ^= z >> np.uint64(31)
+    ins = (z % np.uint64(6)) == 0
+    return np.concatenate([np.nonzero(~ins)[0], np.nonzero(ins)[0]])

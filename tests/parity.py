@@ -45,10 +45,22 @@ def make_case(kind=synth.CUBE, n_old=6, n_new=7, metric=synth.F_ANI,
     return case
 
 
-def run_gpu(case, sort=None, ctx=None, tet8=False, packed=False):
+def run_gpu(case, sort=None, ctx=None, tet8=False, packed=False, env=None):
+    """env: PMMG_HIP_* settings read when the context is created (test-only
+    path selection, e.g. PMMG_HIP_STAGE=3: the staged Morton path)."""
+    import os
     bg, new = case["bg"], case["new"]
     own = ctx is None
-    ctx = ctx or TransferContext(0, sort=sort)
+    saved = {k: os.environ.get(k) for k in (env or {})}
+    os.environ.update(env or {})
+    try:
+        ctx = ctx or TransferContext(0, sort=sort)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     try:
         if tet8:
             from parmmg_amd.transfer import pack_tet8

@@ -31,9 +31,15 @@ def _packable(case):
 
 # the shipped paths: query order chosen on the device, forced Morton bins,
 # forced input order; separate tetv/adja arrays or packed tet8 records
+# (staged: the Morton path that writes records in processing order and
+# copies them back, k_vol_unpermute; auto mode takes it for numberings
+# without coherence)
+STAGED = {"PMMG_HIP_STAGE": "3"}
 MODES = {"auto": {}, "morton": dict(sort=True), "nosort": dict(sort=False), "tet8": dict(tet8=True),
          "tet8-morton": dict(tet8=True, sort=True), "packed": dict(tet8=True, packed=True),
-         "packed-morton": dict(tet8=True, packed=True, sort=True)}
+         "packed-morton": dict(tet8=True, packed=True, sort=True),
+         "morton-staged": dict(sort=True, env=STAGED), "packed-morton-staged": dict(tet8=True, packed=True, sort=True,
+                                                                                  env=STAGED)}
 
 
 @pytest.mark.gpu
@@ -74,14 +80,15 @@ def test_fallback_paths_outside_domain(mode):
 
 
 @pytest.mark.gpu
-def test_invmat_failure_leaves_rows_untouched():
+@pytest.mark.parametrize("mode", ["auto", "morton-staged"])
+def test_invmat_failure_leaves_rows_untouched(mode):
     """MMG5_invmat failure (zero tensor) -> the output row is not written
     (src/interpmesh_pmmg.c:258-267)."""
     case = make_case(kind=C, n_old=4, n_new=5, metric=synth.F_ANI, fields=(synth.F_TENSOR,), with_ref=False)
     case["met"][:40] = 0.0
     from oracle import oracle as O
     case["B"] = O.Background(case["bg"], case["met"], case["fields"], case["hausd"])
-    gpu = run_gpu(case)
+    gpu = run_gpu(case, **MODES[mode])
     rep = check(case, gpu)
     assert np.isnan(gpu["met"]).any(), "expected untouched rows"
     print(rep)

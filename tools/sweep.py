@@ -43,6 +43,8 @@ def query_perm(xyz: np.ndarray, n: int, spec: str) -> np.ndarray:
         rods = np.argsort(key, kind="stable")
         idx = (rods[:, None] * 64 + np.arange(64)[None, :]).ravel()
         return idx[idx < xyz.shape[0]]
+    if spec == "mmg":  # Mmg-like: one point in six appended at the end (bench.py's mmg_like_order leg)
+        return synth.mmg_like_perm(xyz.shape[0])
     if spec == "shuffle":  # a numbering with no spatial coherence (the module then Morton-bins)
         return np.random.default_rng(12345).permutation(xyz.shape[0])
     raise ValueError(spec)
