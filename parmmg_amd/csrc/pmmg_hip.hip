@@ -51,8 +51,7 @@ namespace {
 // ---------------------------------------------------------------- slot layouts
 
 typedef void (*VolFn)(Bg, const Frame *, const unsigned long long *, int, const double *, const uint8_t *,
-                      const int *, const double *, int, ContEntry *, DevStats *, Slots, int *, int8_t *, int,
-                      double *, int);
+                      const int *, const double *, int, ContEntry *, DevStats *, Slots, int *, int8_t *, int);
 
 struct LayoutEntry {
   int c[6];
@@ -142,7 +141,6 @@ struct pmmg_hip_ctx {
   DevBuf axh;                             // per-axis histograms of the seed grid map (k_axis_hist)
   DevBuf bkeys, bkeys2, bvals, sort_tmp;  // Morton binning: keys, sorted keys, ids, rocPRIM scratch
   DevBuf qs;                              // volume query coordinates in processing order (Morton path)
-  DevBuf mstage, inv;                     // staged Morton path: records in processing order, inverse permutation
   int *h_sorted = nullptr;                // pinned: the coherence test's {sorted, bin_bits}, read back in auto mode
   DevBuf cls_cnt;                            // per-block class counts (surface list compaction)
   DevBuf qmin;                               // tetra quality minimum (pmmg_hip_tetra_qual)
@@ -174,7 +172,6 @@ struct pmmg_hip_ctx {
   int hist_stride = 64; // the seed grid's axis histograms sample every n-th vertex (PMMG_HIP_HIST)
   int bin_bits = kBinBitsCoherent; // Morton bits per axis of the binning keys when the order is forced (1..7,
                                     // PMMG_HIP_BINBITS; auto mode: the coherence test picks)
-  int stage_mode = 1;   // PMMG_HIP_STAGE (see run_device)
   int bin_qs = 0;       // the binning copies the volume queries' coordinates in processing order (PMMG_HIP_BINQS=1;
                         // r03: -0.5 ms in the walk on a shuffled numbering, +1 ms in the binning)
   int maxstep = 4096; // longer walks go to the exact continuation / exhaustive kernels (PMMG_HIP_MAXSTEP; the
@@ -500,7 +497,6 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   c->hist_stride = env_int("PMMG_HIP_HIST", c->hist_stride);
   c->bin_bits = std::min(7, env_int("PMMG_HIP_BINBITS", c->bin_bits));
   c->bin_qs = env_int("PMMG_HIP_BINQS", 2) == 1;
-  c->stage_mode = env_int("PMMG_HIP_STAGE", c->stage_mode);
   c->verbose = env_int("PMMG_HIP_VERBOSE", 0);
   c->maxstep = env_int("PMMG_HIP_MAXSTEP", c->maxstep);
   c->fanmax = env_int("PMMG_HIP_FANMAX", c->fanmax);
@@ -520,7 +516,7 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   if (c->cstream) (void)hipStreamSynchronize(c->cstream);
   DevBuf *bufs[] = {&c->o_xyz, &c->o_tetv, &c->o_adja, &c->o_triv, &c->o_adjt, &c->o_met, &c->o_rec, &c->frame,
                     &c->stats, &c->grid, &c->sgrid, &c->order_v,
-                    &c->order_b, &c->cont, &c->xq, &c->qs, &c->axh, &c->bkeys, &c->bkeys2, &c->bvals, &c->sort_tmp, &c->mstage, &c->inv, &c->cls_cnt, &c->qmin, &c->fb_vol, &c->fb_bdy,
+                    &c->order_b, &c->cont, &c->xq, &c->qs, &c->axh, &c->bkeys, &c->bkeys2, &c->bvals, &c->sort_tmp, &c->cls_cnt, &c->qmin, &c->fb_vol, &c->fb_bdy,
                     &c->best, &c->ckey, &c->cidx, &c->bbest, &c->bckey, &c->bcidx, &c->h_xyz,
                     &c->h_cls, &c->h_met, &c->h_elem, &c->h_hit};
   for (DevBuf *b : bufs) release(*b);
@@ -965,15 +961,6 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     sorted = c->h_sorted[0];
     bits = c->h_sorted[1];
   }
-  // Morton order of a numbering without coherence: rows staged in processing
-  // order and copied back by k_vol_unpermute (PMMG_HIP_STAGE: 1 auto, 2 never,
-  // 3 whenever the queries are binned)
-  int rs = 2; // record: the K doubles of the slots, the tag, a pad double when K is even (16-byte pieces)
-  for (int j = 0; j < S.n; j++) rs += S.s[j].code;
-  rs &= ~1;
-  const bool staged = sorted && np_new > 0 && pick_layout(S) != k_vol<false, -1, 0, 0, 0, 0, 0> &&
-                      rs <= kUnpermuteMaxRs && (c->stage_mode == 3 || (c->stage_mode == 1 && bits == kBinBitsAxis));
-  if (staged && (!ensure(c, c->mstage, sizeof(double) * (size_t)rs * nq) || !ensure(c, c->inv, 4 * nq))) return 0;
   if (sorted && np_new > 0) {
     hipLaunchKernelGGL(k_bin_keys, dim3(blocks_for(np_new, 1024)), dim3(kBlock), 0, sb, xyz_new, pclass, np_new,
                        (const Frame *)fr, bits, (unsigned *)c->bkeys.p, (int *)c->bvals.p, st);
@@ -985,8 +972,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     HIPCK(c, rocprim::radix_sort_pairs(c->sort_tmp.p, tmp, (const unsigned *)c->bkeys.p, (unsigned *)c->bkeys2.p,
                                        (const int *)c->bvals.p, order_v, np_new, 0, key_bits, sb));
     hipLaunchKernelGGL(k_bin_split, dim3(blocks_for(np_new, 4096)), dim3(kBlock), 0, sb, (const int *)order_v, xyz_new,
-                       np_new, order_b, c->bin_qs ? (double *)c->qs.p : nullptr, staged ? (int *)c->inv.p : nullptr,
-                       (const DevStats *)st);
+                       np_new, order_b, c->bin_qs ? (double *)c->qs.p : nullptr, (const DevStats *)st);
   } else if (bg.nt > 0) {
     int *bc = (int *)c->cls_cnt.p;
     hipLaunchKernelGGL(k_cls_count, dim3((unsigned)ncls), dim3(kBlock), 0, sb, pclass, (long long)np_new,
@@ -1019,13 +1005,8 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   hipLaunchKernelGGL(vol_fn, dim3((np_new + 63) / 64), dim3(64), 0, s, bg, (const Frame *)fr,
                      (const unsigned long long *)grid, g, xyz_new, pclass, (const int *)order_v,
                      c->bin_qs ? (const double *)c->qs.p : nullptr, np_new,
-                     (ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->filter_steps,
-                     staged ? (double *)c->mstage.p : nullptr, rs);
+                     (ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->filter_steps);
   HIPCK(c, hipEventRecord(c->ev[EV_WALK], s));
-  if (staged)
-    hipLaunchKernelGGL(k_vol_unpermute, dim3((np_new + 63) / 64 < 65536 ? (np_new + 63) / 64 : 65536), dim3(64), 0, s,
-                       pclass, np_new,
-                       (const int *)c->inv.p, (const double *)c->mstage.p, rs, S, elem_out, hit_out);
   hipLaunchKernelGGL(k_vol_walk_exact, dim3(8 * 64), dim3(64), 0, s, bg, xyz_new, (int *)c->fb_vol.p,
                      (const ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->maxstep);
   HIPCK(c, hipGetLastError());

@@ -698,12 +698,11 @@ __global__ __launch_bounds__(kBlock) void k_bin_keys(const double *xyz, const ui
 }
 
 // sorted ids -> volume list (order_v, in place) + the volume queries'
-// coordinates in that order (qs, when non-null) + the inverse permutation
-// (inv, when non-null), surface list (order_b)
+// coordinates in that order (qs, when non-null), surface list (order_b)
 __global__ __launch_bounds__(kBlock) void k_bin_split(const int *sorted_ids, const double *xyz, int np, int *order_b,
-                                                      double *qs, int *inv, const DevStats *st) {
+                                                      double *qs, const DevStats *st) {
   const int nvol = st->nvol, nbdy = st->nbdy;
-  for (long long j = (qs || inv ? 0 : nvol) + blockIdx.x * (long long)blockDim.x + threadIdx.x; j < nvol + nbdy;
+  for (long long j = (qs ? 0 : nvol) + blockIdx.x * (long long)blockDim.x + threadIdx.x; j < nvol + nbdy;
        j += (long long)gridDim.x * blockDim.x) {
     const int ip = sorted_ids[j];
     if (j < nvol) {
@@ -712,7 +711,6 @@ __global__ __launch_bounds__(kBlock) void k_bin_split(const int *sorted_ids, con
         qs[3 * j + 1] = xyz[3 * (size_t)(ip - 1) + 1];
         qs[3 * j + 2] = xyz[3 * (size_t)(ip - 1) + 2];
       }
-      if (inv) inv[ip - 1] = (int)j; // the staged path's way back (k_vol_unpermute)
     } else {
       order_b[j - nvol] = ip;
     }

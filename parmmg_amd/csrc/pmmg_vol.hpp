@@ -440,41 +440,22 @@ __device__ __forceinline__ void wave_store_rows_scat(double *out, const double *
   }
 }
 
-// Where the rows of a wave go (one per wave, the lanes' fields per lane):
-//   kCoalesced  input order: the wave's 64 consecutive queries' rows as whole
-//               lines at w0 (wave_store_rows)
-//   kScattered  Morton order of a mostly coherent numbering: every row to its
-//               own query ip (wave_store_rows_scat)
-//   kStaged     Morton order of a numbering without coherence: one record of
-//               rs doubles per query in processing order (the slots' rows
-//               back to back, then a tag {elem, hit, slot-ok mask}), written
-//               per lane into lines the wave completes; k_vol_unpermute
-//               copies them to the outputs in input order (the random side of
-//               the permutation becomes one record read per query instead of
-//               four partial-line row writes)
-enum { kCoalesced = 0, kScattered = 1, kStaged = 2 };
+// Where the rows of a wave go: input order — the wave's 64 consecutive
+// queries' rows as whole lines at w0 (wave_store_rows); Morton order — every
+// row to its own query ip (wave_store_rows_scat).  (r03 measured a third,
+// staged, form for numberings without coherence — records in processing
+// order copied back by an un-permute kernel — and dropped it: the same
+// volume-stage time, profiles/r03m/staged_path.patch.txt.)
 struct Sink {
-  int mode;
-  size_t w0;      // the wave's first processing index
-  int ip;         // this lane's query (1-based)
-  double *stage;  // kStaged: records
-  int rs;         // kStaged: record stride (doubles)
-  unsigned okm;   // kStaged: this lane's slot-ok mask
+  bool coalesced;
+  size_t w0; // the wave's first processing index
+  int ip;    // this lane's query (1-based)
 };
 
 template <int C>
-__device__ __forceinline__ void sink_rows(const Slot &sl, int s, int off, const double *r, bool ok, double *img,
-                                          Sink &k) {
-  if (k.mode == kCoalesced) {
-    wave_store_rows<C>(sl.out + (size_t)C * k.w0, r, __ballot(ok), img);
-  } else if (k.mode == kScattered) {
-    wave_store_rows_scat<C>(sl.out, r, __ballot(ok), img, k.ip);
-  } else {
-    double *rec = k.stage + (size_t)k.rs * (k.w0 + __lane_id()) + off;
-#pragma unroll
-    for (int q = 0; q < C; q++) rec[q] = r[q];
-    k.okm |= ok ? (1u << s) : 0u;
-  }
+__device__ __forceinline__ void sink_rows(const Slot &sl, const double *r, bool ok, double *img, const Sink &k) {
+  if (k.coalesced) wave_store_rows<C>(sl.out + (size_t)C * k.w0, r, __ballot(ok), img);
+  else wave_store_rows_scat<C>(sl.out, r, __ballot(ok), img, k.ip);
 }
 
 // ---------------------------------------------------------------- fused volume kernel
@@ -563,8 +544,8 @@ __device__ __forceinline__ void coop_land3(double p0, double p1, double p2, doub
 
 // one slot of the wave's queries: rows gathered, interpolated, stored
 template <int C>
-__device__ __forceinline__ void vol_slot(const Slot &sl, int s, int off, bool act, const int4 &v, const double *phi,
-                                         double *img, Sink &k) {
+__device__ __forceinline__ void vol_slot(const Slot &sl, bool act, const int4 &v, const double *phi, double *img,
+                                         const Sink &k) {
   if constexpr (C > 0) {
     double r[C];
     bool ok = act;
@@ -613,7 +594,7 @@ __device__ __forceinline__ void vol_slot(const Slot &sl, int s, int off, bool ac
       const int vv[4] = {v.x, v.y, v.z, v.w};
       interp_iso_row<4, 1>(sl.in, sl.istride, vv, phi, r);
     }
-    sink_rows<C>(sl, s, off, r, ok, img, k);
+    sink_rows<C>(sl, r, ok, img, k);
   }
 }
 
@@ -683,7 +664,7 @@ __device__ __forceinline__ void packed_take(SlotAcc<C> &a, int pass, int i, doub
 }
 
 template <int C>
-__device__ __forceinline__ void packed_store(const Slot &sl, int s, int off, SlotAcc<C> &a, double *img, Sink &k) {
+__device__ __forceinline__ void packed_store(const Slot &sl, SlotAcc<C> &a, double *img, const Sink &k) {
   if constexpr (C > 0) {
     double r[C];
     bool ok = a.ok;
@@ -691,7 +672,7 @@ __device__ __forceinline__ void packed_store(const Slot &sl, int s, int off, Slo
     else
 #pragma unroll
       for (int q = 0; q < C; q++) r[q] = a.v[q];
-    sink_rows<C>(sl, s, off, r, ok, img, k);
+    sink_rows<C>(sl, r, ok, img, k);
   }
 }
 
@@ -708,16 +689,17 @@ __device__ __forceinline__ constexpr int first_pass() {
 
 template <class L, int S, int C>
 __device__ __forceinline__ void packed_pass_slot(const Slots &Sl, SlotAcc<C> &a, int pass, int i, double ph,
-                                                 const double *mine, double *img, Sink &k, bool store) {
+                                                 const double *mine, double *img, const Sink &k, bool store) {
   if constexpr (C > 0) {
     if (pass < first_pass<L, S, C>() || pass > last_pass<L, S, C>()) return;
     if (!store) packed_take<L, S>(a, pass, i, ph, mine);
-    else if (pass == last_pass<L, S, C>()) packed_store<C>(Sl.s[S], S, L::off(S), a, img, k);
+    else if (pass == last_pass<L, S, C>()) packed_store<C>(Sl.s[S], a, img, k);
   }
 }
 
 template <int C0, int C1, int C2, int C3, int C4, int C5>
-__device__ __forceinline__ void vol_interp_packed(const Slots &S, bool acc, const VolLoc &loc, double *img, Sink &k) {
+__device__ __forceinline__ void vol_interp_packed(const Slots &S, bool acc, const VolLoc &loc, double *img,
+                                                  const Sink &k) {
   using L = PackedLayout<C0, C1, C2, C3, C4, C5>;
   constexpr int PW = L::NPASS == 1 ? L::RS : 8; // doubles per record and pass
   constexpr int PR = PW / 2;                     // 16-byte pieces per record and pass
@@ -776,8 +758,7 @@ template <bool PK, int C0, int C1, int C2, int C3, int C4, int C5>
 __global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsigned long long *grid, int g,
                                             const double *qxyz, const uint8_t *pclass, const int *order,
                                             const double *qs, int np, ContEntry *cont, DevStats *st, Slots S,
-                                            int *elem_out, int8_t *hit_out, int filter_steps, double *stage,
-                                            int rs) {
+                                            int *elem_out, int8_t *hit_out, int filter_steps) {
   __shared__ VolShared sh;
   bstats_init(&sh.bs);
   __syncthreads();
@@ -851,8 +832,7 @@ __global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsign
   wave_count(&sh.bs, kCntVolQueries, active);
   wave_count(&sh.bs, kCntExact, more);
   // 3. interpolation
-  Sink snk{!sorted ? kCoalesced : (stage && C0 >= 0 ? kStaged : kScattered), (size_t)(i - __lane_id()), ip, stage,
-           rs, 0u};
+  const Sink snk{!sorted, (size_t)(i - __lane_id()), ip};
   if (__any(acc)) {
     if (!acc) { // idle lanes gather a valid row, never stored
       loc.v = make_int4(1, 1, 1, 1);
@@ -869,80 +849,25 @@ __global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsign
         for (int s2 = 0; s2 < S.n; s2++) interp_dyn<4>(S.s[s2], ip, vv, loc.phi);
       }
     } else {
-      constexpr int o1 = C0, o2 = o1 + C1, o3 = o2 + C2, o4 = o3 + C3, o5 = o4 + C4;
-      vol_slot<C0>(S.s[0], 0, 0, acc, loc.v, loc.phi, img, snk);
-      vol_slot<C1>(S.s[1], 1, o1, acc, loc.v, loc.phi, img, snk);
-      vol_slot<C2>(S.s[2], 2, o2, acc, loc.v, loc.phi, img, snk);
-      vol_slot<C3>(S.s[3], 3, o3, acc, loc.v, loc.phi, img, snk);
-      vol_slot<C4>(S.s[4], 4, o4, acc, loc.v, loc.phi, img, snk);
-      vol_slot<C5>(S.s[5], 5, o5, acc, loc.v, loc.phi, img, snk);
+      vol_slot<C0>(S.s[0], acc, loc.v, loc.phi, img, snk);
+      vol_slot<C1>(S.s[1], acc, loc.v, loc.phi, img, snk);
+      vol_slot<C2>(S.s[2], acc, loc.v, loc.phi, img, snk);
+      vol_slot<C3>(S.s[3], acc, loc.v, loc.phi, img, snk);
+      vol_slot<C4>(S.s[4], acc, loc.v, loc.phi, img, snk);
+      vol_slot<C5>(S.s[5], acc, loc.v, loc.phi, img, snk);
     }
-    if (acc && snk.mode == kScattered) { // cached stores (see wave_store_rows_scat)
-      if (elem_out) elem_out[ip - 1] = k;
-      if (hit_out) hit_out[ip - 1] = (int8_t)PMMG_HIT_VOL_WALK;
-    } else if (acc && snk.mode == kCoalesced) {
-      if (elem_out) __builtin_nontemporal_store(k, elem_out + ip - 1);
-      if (hit_out) __builtin_nontemporal_store((int8_t)PMMG_HIT_VOL_WALK, hit_out + ip - 1);
+    if (acc) {
+      if (sorted) { // scattered: cached stores (see wave_store_rows_scat)
+        if (elem_out) elem_out[ip - 1] = k;
+        if (hit_out) hit_out[ip - 1] = (int8_t)PMMG_HIT_VOL_WALK;
+      } else {
+        if (elem_out) __builtin_nontemporal_store(k, elem_out + ip - 1);
+        if (hit_out) __builtin_nontemporal_store((int8_t)PMMG_HIT_VOL_WALK, hit_out + ip - 1);
+      }
     }
-  }
-  if (snk.mode == kStaged && active) { // every record gets its tag (hit 0: the exact continuation writes the query)
-    const unsigned long long tag = acc ? ((unsigned long long)(unsigned)k | ((unsigned long long)PMMG_HIT_VOL_WALK << 32) |
-                                          ((unsigned long long)snk.okm << 40))
-                                       : 0ULL;
-    constexpr int K = (C0 > 0 ? C0 : 0) + C1 + C2 + C3 + C4 + C5; // record: the K doubles of the slots, the tag
-    reinterpret_cast<unsigned long long *>(stage)[(size_t)rs * i + K] = tag;
   }
   __syncthreads();
   bstats_flush(&sh.bs, st);
-}
-
-// Morton order, staged (Sink::kStaged): every volume query's record back to
-// its input position.  One wave per 64 consecutive outputs: every lane reads
-// its query's record (random: the permutation; rs even, so 16-byte pieces),
-// the 64 records go through LDS, and each slot's 64 rows leave as whole
-// lines (piece p of the slot's output block from record p / C), as in input
-// order.  Queries whose record has hit 0 were handed to the exact
-// continuation, which writes them itself; rows whose slot failed (invmat)
-// stay untouched, and so do the rows of other classes.
-constexpr int kUnpermuteMaxRs = 18; // records of at most 18 doubles (K <= 16 + the tag, rounded to even)
-__global__ __launch_bounds__(64) void k_vol_unpermute(const uint8_t *pclass, int np, const int *inv,
-                                                      const double *stage, int rs, Slots S, int *elem_out,
-                                                      int8_t *hit_out) {
-  __shared__ double img[64 * kUnpermuteMaxRs];
-  int ktag = 0; // the tag follows the slots' K doubles
-  for (int s = 0; s < S.n; s++) ktag += S.s[s].code;
-  const int lane = __lane_id();
-  for (long long i0 = (long long)blockIdx.x * 64; i0 < np; i0 += (long long)gridDim.x * 64) {
-    const long long i = i0 + lane;
-    bool vol = i < np && __builtin_nontemporal_load(pclass + i) == PMMG_PT_VOL;
-    unsigned long long tag = 0;
-    if (vol) {
-      const double2 *rec = reinterpret_cast<const double2 *>(stage + (size_t)rs * __builtin_nontemporal_load(inv + i));
-      for (int q = 0; q < rs / 2; q++) reinterpret_cast<double2 *>(img)[(rs / 2) * lane + q] = rec[q];
-      tag = reinterpret_cast<const unsigned long long *>(img)[rs * lane + ktag];
-    }
-    const int hit = (int)((tag >> 32) & 0xFFu);
-    const unsigned okm = hit ? (unsigned)(tag >> 40) : 0u;
-    if (hit) {
-      if (elem_out) elem_out[i] = (int)(unsigned)tag;
-      if (hit_out) hit_out[i] = (int8_t)hit;
-    }
-    wait_lgkm();
-    __builtin_amdgcn_wave_barrier();
-    int off = 0;
-    for (int s = 0; s < S.n; s++) {
-      const int C = S.s[s].code;
-      const unsigned long long m = __ballot((okm >> s) & 1u);
-      double *out = S.s[s].out + (size_t)C * i0;
-      for (int t = 0; t < C; t++) {
-        const int p = 64 * t + lane, r = p / C;
-        if ((m >> r) & 1ULL) out[p] = img[rs * r + off + (p - C * r)];
-      }
-      off += C;
-    }
-    wait_lgkm();
-    __builtin_amdgcn_wave_barrier();
-  }
 }
 
 } // namespace pmmg

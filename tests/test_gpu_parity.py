@@ -31,15 +31,14 @@ def _packable(case):
 
 # the shipped paths: query order chosen on the device, forced Morton bins,
 # forced input order; separate tetv/adja arrays or packed tet8 records
-# (staged: the Morton path that writes records in processing order and
-# copies them back, k_vol_unpermute; auto mode takes it for numberings
+# (morton-fine: the fine binning cells auto mode picks for a numbering
 # without coherence)
-STAGED = {"PMMG_HIP_STAGE": "3"}
+FINE = {"PMMG_HIP_BINBITS": "7"}
 MODES = {"auto": {}, "morton": dict(sort=True), "nosort": dict(sort=False), "tet8": dict(tet8=True),
          "tet8-morton": dict(tet8=True, sort=True), "packed": dict(tet8=True, packed=True),
          "packed-morton": dict(tet8=True, packed=True, sort=True),
-         "morton-staged": dict(sort=True, env=STAGED), "packed-morton-staged": dict(tet8=True, packed=True, sort=True,
-                                                                                  env=STAGED)}
+         "morton-fine": dict(sort=True, env=FINE), "packed-morton-fine": dict(tet8=True, packed=True, sort=True,
+                                                                              env=FINE)}
 
 
 @pytest.mark.gpu
@@ -80,7 +79,7 @@ def test_fallback_paths_outside_domain(mode):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["auto", "morton-staged"])
+@pytest.mark.parametrize("mode", ["auto", "morton-fine"])
 def test_invmat_failure_leaves_rows_untouched(mode):
     """MMG5_invmat failure (zero tensor) -> the output row is not written
     (src/interpmesh_pmmg.c:258-267)."""
