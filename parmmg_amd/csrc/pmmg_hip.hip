@@ -19,9 +19,6 @@
 //   surface stream  (after the order) surface seeds, node->tria CSR, k_bdy
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/device/device_select.hpp>
-#include <rocprim/iterator/counting_iterator.hpp>
-#include <rocprim/iterator/transform_iterator.hpp>
 
 #include <math.h>
 #include <stdarg.h>
@@ -102,10 +99,6 @@ bool packed_supported(int met_size, int nfield, const int *fsize) {
   return pick_layout(S) != nullptr;
 }
 
-struct IsBdy { // the surface-list predicate of the input-order path
-  __host__ __device__ bool operator()(uint8_t c) const { return c == PMMG_PT_BDY; }
-};
-
 } // namespace
 
 // ================================================================ host side
@@ -141,6 +134,7 @@ struct pmmg_hip_ctx {
   DevBuf axh;                             // per-axis histograms of the seed grid map (k_axis_hist)
   DevBuf bkeys, bkeys2, bvals, sort_tmp;  // Morton binning: keys, sorted keys, ids, rocPRIM scratch
   DevBuf qs;                              // volume query coordinates in processing order (Morton path)
+  DevBuf cls_cnt;                         // per-block class counts (surface list compaction)
   int *h_sorted = nullptr;                // pinned: the coherence test's {sorted, bin_bits}, read back in auto mode
   DevBuf qmin;                               // tetra quality minimum (pmmg_hip_tetra_qual)
   DevBuf fb_vol, fb_bdy, best, ckey, cidx, bbest, bckey, bcidx;
@@ -167,8 +161,8 @@ struct pmmg_hip_ctx {
   int verbose = 0; // PMMG_HIP_VERBOSE: host-mode transfer timings on stderr
   int tpc = 8;        // background tetra per volume seed cell (PMMG_HIP_TPC)
   int seed_lanes = 4;  // sampled tetra per seed run of 4 records (PMMG_HIP_SEEDLANES, 1..4)
-  int bbox_stride = 16; // the frame's bbox samples every n-th vertex (PMMG_HIP_BBOX)
-  int hist_stride = 64; // the seed grid's axis histograms sample every n-th vertex (PMMG_HIP_HIST)
+  int bbox_stride = 64;  // the frame's bbox samples every n-th vertex (PMMG_HIP_BBOX; r03o: 64 instead of 16 and
+  int hist_stride = 256; // 256 instead of 64 for the axis histograms: preparation -0.15 ms at cfg4, same walks)
   int bin_bits = kBinBitsCoherent; // Morton bits per axis of the binning keys when the order is forced (1..7,
                                     // PMMG_HIP_BINBITS; auto mode: the coherence test picks)
   int bin_qs = 0;       // the binning copies the volume queries' coordinates in processing order (PMMG_HIP_BINQS=1;
@@ -515,7 +509,7 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   if (c->cstream) (void)hipStreamSynchronize(c->cstream);
   DevBuf *bufs[] = {&c->o_xyz, &c->o_tetv, &c->o_adja, &c->o_triv, &c->o_adjt, &c->o_met, &c->o_rec, &c->frame,
                     &c->stats, &c->grid, &c->sgrid, &c->order_v,
-                    &c->order_b, &c->cont, &c->xq, &c->qs, &c->axh, &c->bkeys, &c->bkeys2, &c->bvals, &c->sort_tmp, &c->qmin, &c->fb_vol, &c->fb_bdy,
+                    &c->order_b, &c->cont, &c->xq, &c->qs, &c->axh, &c->bkeys, &c->bkeys2, &c->bvals, &c->sort_tmp, &c->cls_cnt, &c->qmin, &c->fb_vol, &c->fb_bdy,
                     &c->best, &c->ckey, &c->cidx, &c->bbest, &c->bckey, &c->bcidx, &c->h_xyz,
                     &c->h_cls, &c->h_met, &c->h_elem, &c->h_hit};
   for (DevBuf *b : bufs) release(*b);
@@ -899,11 +893,12 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   const int gb = 1 << kBinBitsAxis;
   const size_t nq = (size_t)np_new;
   const long long ng = (long long)g * g * g, nsg = bg.nt > 0 ? (long long)gs * gs * gs : 0;
+  const long long ncls = (long long)(nq / kScanChunk + 1);
   if (!ensure(c, c->frame, sizeof(Frame)) || !ensure(c, c->stats, sizeof(DevStats) + kStatParts * sizeof(StatPart)) ||
       !ensure(c, c->grid, 8 * (size_t)ng) || !ensure(c, c->sgrid, 4 * (size_t)nsg) || !ensure(c, c->order_v, 4 * nq) ||
       !ensure(c, c->order_b, 4 * nq) || !ensure(c, c->cont, sizeof(ContEntry) * nq) ||
       !ensure(c, c->bkeys, 4 * nq) || !ensure(c, c->bkeys2, 4 * nq) || !ensure(c, c->bvals, 4 * nq) ||
-      !ensure(c, c->qs, 24 * nq) || 
+      !ensure(c, c->qs, 24 * nq) || !ensure(c, c->cls_cnt, 4 * (size_t)ncls) || 
       !ensure(c, c->fb_vol, 4 * nq) || !ensure(c, c->fb_bdy, 4 * nq) || !ensure(c, c->best, 4 * nq) ||
       !ensure(c, c->ckey, 8 * nq) || !ensure(c, c->cidx, 4 * nq) || !ensure(c, c->bbest, 4 * nq) ||
       !ensure(c, c->bckey, 8 * nq) || !ensure(c, c->bcidx, 4 * nq))
@@ -971,16 +966,17 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
                                        (const int *)c->bvals.p, order_v, np_new, 0, key_bits, sb));
     hipLaunchKernelGGL(k_bin_split, dim3(blocks_for(np_new, 4096)), dim3(kBlock), 0, sb, (const int *)order_v, xyz_new,
                        np_new, order_b, c->bin_qs ? (double *)c->qs.p : nullptr, (const DevStats *)st);
-  } else if (bg.nt > 0 && np_new > 0) {
-    // input order: the surface points in input order (stable selection, one
-    // decoupled-look-back pass: r02's count / scan / scatter kernels took
-    // ~0.2 ms at cfg4), their count into st->nbdy
-    const auto ids = rocprim::counting_iterator<int>(1);
-    const auto flags = rocprim::make_transform_iterator(pclass, IsBdy());
-    size_t tmp = 0;
-    HIPCK(c, rocprim::select(nullptr, tmp, ids, flags, order_b, &st->nbdy, (size_t)np_new, sb));
-    if (!ensure(c, c->sort_tmp, tmp)) return 0;
-    HIPCK(c, rocprim::select(c->sort_tmp.p, tmp, ids, flags, order_b, &st->nbdy, (size_t)np_new, sb));
+  } else if (bg.nt > 0) {
+    // input order: the surface points in input order (stable compaction:
+    // per-block counts, their scan, the scatter; rocPRIM's select took 0.2 ms
+    // longer here, r03o)
+    int *bc = (int *)c->cls_cnt.p;
+    hipLaunchKernelGGL(k_cls_count, dim3((unsigned)ncls), dim3(kBlock), 0, sb, pclass, (long long)np_new,
+                       (int)PMMG_PT_BDY, bc, (const DevStats *)st);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, sb, bc, (int)ncls, &st->nbdy, (const int *)&st->sorted,
+                       0);
+    hipLaunchKernelGGL(k_cls_scatter, dim3((unsigned)ncls), dim3(kBlock), 0, sb, pclass, (long long)np_new,
+                       (int)PMMG_PT_BDY, (const int *)bc, order_b, (const DevStats *)st);
   }
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[EV_ORDER], sb));

@@ -433,7 +433,10 @@ __device__ int seed_srf(const int *cell, int g, const Frame *fr, const double *x
 
 // ---------------------------------------------------------------- block scans
 //
-// block-level exclusive scans (k_axis_map)
+// block-level exclusive scans, and k_scan_top (one block: the exclusive scan
+// of a short array, e.g. per-block counts).  When `gate` is non-null the
+// kernel runs only if *gate == want.
+constexpr int kScanItems = 16, kScanChunk = kBlock * kScanItems;
 
 __device__ __forceinline__ int wave_incl_scan(int v) {
   const int lane = __lane_id();
@@ -461,6 +464,23 @@ __device__ __forceinline__ int block_excl_scan(int v, int *tot) {
   __syncthreads();
   *tot = all;
   return pre + inc - v;
+}
+
+__device__ __forceinline__ bool gate_off(const int *gate, int want) { return gate && *gate != want; }
+
+// one block: bsum[0..nb) -> exclusive offsets in place; the total -> *total
+__global__ __launch_bounds__(kBlock) void k_scan_top(int *bsum, int nb, int *total, const int *gate, int want) {
+  if (gate_off(gate, want)) return;
+  int carry = 0;
+  for (int b0 = 0; b0 < nb; b0 += kBlock) {
+    const int b = b0 + threadIdx.x;
+    const int v = b < nb ? bsum[b] : 0;
+    int tot;
+    const int pre = block_excl_scan(v, &tot);
+    if (b < nb) bsum[b] = carry + pre;
+    carry += tot;
+  }
+  if (threadIdx.x == 0 && total) *total = carry;
 }
 
 // ---------------------------------------------------------------- seed grid axis maps
@@ -695,6 +715,53 @@ __global__ __launch_bounds__(kBlock) void k_bin_split(const int *sorted_ids, con
     } else {
       order_b[j - nvol] = ip;
     }
+  }
+}
+
+// Stable class compaction (the surface list, input-order path only): out =
+// the ids ip (1-based) with pclass[ip-1] == cls, in input order; *count =
+// their number.  Three passes over the 1-byte classes (count per block, scan
+// of the block counts, scatter).  Each block owns kScanChunk points.
+// bit j = (pclass[i0 + j] == cls); the 16 classes of a thread come in one
+// 16-byte load when the array is 16-byte aligned and the run is complete
+__device__ __forceinline__ unsigned cls_bits(const uint8_t *pclass, long long np, long long i0, int cls) {
+  unsigned m = 0;
+  if (i0 + kScanItems <= np && ((uintptr_t)pclass & 15) == 0) {
+    const uint4 w = *reinterpret_cast<const uint4 *>(pclass + i0);
+    const unsigned words[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int j = 0; j < kScanItems; j++)
+      m |= (((words[j >> 2] >> (8 * (j & 3))) & 0xFFu) == (unsigned)cls) ? (1u << j) : 0u;
+    return m;
+  }
+#pragma unroll
+  for (int j = 0; j < kScanItems; j++) {
+    const long long i = i0 + j;
+    m |= (i < np && pclass[i] == cls) ? (1u << j) : 0u;
+  }
+  return m;
+}
+
+__global__ __launch_bounds__(kBlock) void k_cls_count(const uint8_t *pclass, long long np, int cls, int *bcnt,
+                                                      const DevStats *st) {
+  if (st->sorted) return;
+  const long long i0 = (long long)blockIdx.x * kScanChunk + (long long)threadIdx.x * kScanItems;
+  int tot;
+  block_excl_scan(__popc(cls_bits(pclass, np, i0, cls)), &tot);
+  if (threadIdx.x == 0) bcnt[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(kBlock) void k_cls_scatter(const uint8_t *pclass, long long np, int cls,
+                                                        const int *boff, int *out, const DevStats *st) {
+  if (st->sorted) return;
+  const long long i0 = (long long)blockIdx.x * kScanChunk + (long long)threadIdx.x * kScanItems;
+  unsigned m = cls_bits(pclass, np, i0, cls);
+  int tot;
+  int pos = boff[blockIdx.x] + block_excl_scan(__popc(m), &tot);
+  while (m) {
+    const int j = __ffs(m) - 1;
+    m &= m - 1;
+    out[pos++] = (int)(i0 + j + 1);
   }
 }
 

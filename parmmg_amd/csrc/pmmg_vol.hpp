@@ -280,6 +280,35 @@ struct LaneSlotsD {
   }
 };
 
+// An accepted tetra whose smallest coordinate is within MMG5_EPS of a face
+// (min phi <= EPS) may have a face neighbour that holds the point strictly
+// (min phi > EPS): on a graded mesh, where the heights of two neighbours
+// across a face differ by orders of magnitude, a point inside the thin one
+// by more than EPS of its height is within EPS of the tall one's height
+// outside it, and both pass the reference's test.  The reference ends in
+// whichever its walk meets first; here the strict one is preferred, so that
+// a point with min barycentric > EPS (class (i) of tests/parity.py, the
+// north_star's bit-exact class) lands in its tetra whatever the path
+// (cfgG: 1 point in 3.9M otherwise).  The neighbour across the face of the
+// smallest coordinate is checked with the reference's own arithmetic.
+__device__ __noinline__ void prefer_strict(const Bg &bg, const double *x, const int4 &ad, int &k, VolLoc *loc) {
+  if (min4(loc->phi) > kEps) return;
+  int f = 0;
+#pragma unroll
+  for (int j = 1; j < 4; j++)
+    if (loc->phi[j] < loc->phi[f]) f = j;
+  const int nb = sel4(ad, f) >> 2;
+  if (nb == 0) return;
+  const int4 tn = tetv_row(bg, nb);
+  double q[4][3];
+  load_tet_pts(bg, tn, q);
+  VolLoc l2;
+  if (exact_accept(x, q, tn, &l2, nullptr) && min4(l2.phi) > kEps) {
+    *loc = l2;
+    k = nb;
+  }
+}
+
 __device__ __forceinline__ int walk_exact(const Bg &bg, const double *x, int ip, int &k, int &steps, int limit,
                                           VolLoc *loc, const LaneSlotsD &L) {
   int hist[kHist];
@@ -302,7 +331,10 @@ __device__ __forceinline__ int walk_exact(const Bg &bg, const double *x, int ip,
     L.get(m.z, p[2]);
     L.get(m.w, p[3]);
     double key[4];
-    if (exact_accept(x, p, tv, loc, key)) return 1;
+    if (exact_accept(x, p, tv, loc, key)) {
+      prefer_strict(bg, x, ad, k, loc);
+      return 1;
+    }
     const int f = pick_face_walk<double>(ad, hist, key, walk_rsel(ip, n + 1));
     if (f < 0) return 2;
 #pragma unroll
@@ -823,7 +855,9 @@ __global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsign
   if (status == 1) {
     double p[4][3];
     load_tet_pts(bg, tv, p);
-    acc = exact_accept(x, p, tv, &loc, nullptr);
+    // within EPS of a face: the exact continuation decides between this
+    // tetra and its neighbour (prefer_strict)
+    acc = exact_accept(x, p, tv, &loc, nullptr) && min4(loc.phi) > kEps;
   }
   const bool more = active && !acc;
   const int slot = wave_append(&st->ncont, more);

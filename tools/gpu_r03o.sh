@@ -10,3 +10,5 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_co
 && echo "pytest ok" \
 && timeout -k 10 700 python3 -u tools/sweep.py --config cfg4 --rounds 2 --steps 4 --variants "sort=0;BBOX=64,HIST=256;SEEDLANES=2;SEEDLANES=1;BBOX=64,HIST=256,SEEDLANES=1" > $OUT/sweep_prep.txt 2>&1 \
 && echo "sweep ok" && cat $OUT/sweep_prep.txt
+timeout -k 10 600 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err \
+&& echo "bench ok" && cat $OUT/bench.json
