@@ -527,6 +527,8 @@ def main():
                     help="skip the (separately reported) step on a shuffled numbering of the new points")
     ap.add_argument("--no-snapshot", action="store_true",
                     help="skip the (separately reported) device background snapshot timing")
+    ap.add_argument("--no-surface-solo", action="store_true",
+                    help="skip the (separately reported) surface branch timed alone")
     ap.add_argument("--no-graded", action="store_true",
                     help="skip the (separately reported) step on the graded and stretched cfgG meshes")
     args = ap.parse_args()
@@ -718,7 +720,7 @@ def main():
             out["host_mode"] = host_mode_timing(ctx, w, bg, met, fields, q_xyz, q_pc, rank)
         except Exception as e:  # reported, never fatal to the bench line
             out["host_mode"] = {"error": str(e)}
-    if world == 1 and not split:
+    if world == 1 and not split and not args.no_surface_solo:
         try:
             out["surface_solo"] = surface_solo(ctx, step_bg, d_qxyz, q_pc, d_mo, d_fo, d_elem, d_hit)
         except Exception as e:  # reported, never fatal to the bench line
