@@ -77,7 +77,9 @@ def build_host(force: bool = False) -> str:
     deps = [src, shard, medit, os.path.join(CSRC, "pmmg_host.h"), os.path.join(CSRC, "pmmg_medit.h"),
             os.path.join(INC, "parmmg_hip.h"), HIP_SO, __file__]
     if force or _stale(HOST_SO, deps):
-        _run(["gcc", "-O2", "-std=c99", "-Wall", "-Wextra", "-fPIC", "-shared", f"-I{INC}", f"-I{CSRC}",
+        # -fopenmp: the halo-shard builder (pmmg_shard.c) runs its passes over
+        # the group's tetra on the host threads
+        _run(["gcc", "-O2", "-std=c99", "-fopenmp", "-Wall", "-Wextra", "-fPIC", "-shared", f"-I{INC}", f"-I{CSRC}",
               "-o", HOST_SO, src, shard, medit, f"-L{PKG}", "-lpmmg_hip", "-Wl,-rpath,$ORIGIN"])
     return HOST_SO
 

@@ -163,6 +163,7 @@ struct pmmg_hip_ctx {
   int seed_lanes = 4;  // sampled tetra per seed run of 4 records (PMMG_HIP_SEEDLANES, 1..4)
   int bbox_stride = 64;  // the frame's bbox samples every n-th vertex (PMMG_HIP_BBOX; r03o: 64 instead of 16 and
   int hist_stride = 256; // 256 instead of 64 for the axis histograms: preparation -0.15 ms at cfg4, same walks)
+  int srf_g = 0;         // test-only PMMG_HIP_SRFG: the surface seed grid's cells per axis (1: one seed for all)
   int srf_mult = 8;      // the surface seed grid has srf_mult * nt / 2 cells (PMMG_HIP_SRFMULT; r03r at cfg4: 1 /
                          // 8 / 32 -> 7.4 / 3.9 / 2.7 steps per surface point, surface branch 0.446 / 0.403 /
                          // 0.399 ms: a surface grid sized like a volume grid left ~33 trias per occupied cell)
@@ -492,6 +493,7 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   c->bbox_stride = env_int("PMMG_HIP_BBOX", c->bbox_stride);
   c->hist_stride = env_int("PMMG_HIP_HIST", c->hist_stride);
   c->srf_mult = env_int("PMMG_HIP_SRFMULT", c->srf_mult);
+  c->srf_g = env_int("PMMG_HIP_SRFG", 0);
   c->bin_bits = std::min(7, env_int("PMMG_HIP_BINBITS", c->bin_bits));
   c->bin_qs = env_int("PMMG_HIP_BINQS", 2) == 1;
   c->verbose = env_int("PMMG_HIP_VERBOSE", 0);
@@ -893,7 +895,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     return 0;
   }
   const int g = grid_dim(bg.ne, c->tpc, 1024);
-  const int gs = bg.nt > 0 ? grid_dim((long long)bg.nt * c->srf_mult, 2, 1024) : 1;
+  const int gs = bg.nt <= 0 ? 1 : (c->srf_g > 0 ? c->srf_g : grid_dim((long long)bg.nt * c->srf_mult, 2, 1024));
   const int gb = 1 << kBinBitsAxis;
   const size_t nq = (size_t)np_new;
   const long long ng = (long long)g * g * g, nsg = bg.nt > 0 ? (long long)gs * gs * gs : 0;

@@ -325,9 +325,7 @@ __global__ __launch_bounds__(kBlock) void k_seed_vol(Bg bg, const Frame *fr, uns
 }
 
 // rare path of seed_vol (the 8 cells are empty): lowest seed id in the shells
-// of radius 1, 2, ... kSeedRing around the cell; 0 when there is none (the
-// query then goes to the exact continuation, which hands it to the
-// exhaustive search: O(ne) per query, so the shells go far)
+// of radius 1, 2, ... kSeedRing around the cell; 0 when there is none
 constexpr int kSeedRing = 6;
 __device__ __noinline__ int seed_vol_ring(const unsigned long long *cell, int g, int ci, int cj, int ck) {
 #pragma unroll 1
@@ -387,7 +385,11 @@ __device__ __forceinline__ int seed_vol(const unsigned long long *cell, int g, c
     }
   }
   if (bid != 0xFFFFFFFFu) return (int)bid;
-  return seed_vol_ring(cell, g, c[0], c[1], c[2]);
+  // no seed within kSeedRing cells: the walk starts at tetra 1 (a long walk,
+  // or the exhaustive search if it gets stuck, costs less than sending the
+  // query straight to the O(ne) search)
+  const int r = seed_vol_ring(cell, g, c[0], c[1], c[2]);
+  return r ? r : 1;
 }
 
 // ---------------------------------------------------------------- surface seeds and node -> tria CSR
@@ -485,21 +487,28 @@ __global__ __launch_bounds__(kBlock) void k_scan_top(int *bsum, int nb, int *tot
 
 // ---------------------------------------------------------------- seed grid axis maps
 
-// the per-axis histogram of every `stride`-th background vertex:
-// H[block][d][bin] (kHistBlocks blocks, no atomics outside LDS)
+// the per-axis histogram of np / stride background vertices at
+// pseudo-random positions (splitmix64 of the sample index: a strided sample
+// aliases with a lattice numbering's row length — cfg5's halo shard put 14 %
+// of an every-256th sample on its x = 0 plane and mapped a uniform axis);
+// vertices outside the (sampled) frame are left out, not clamped into the
+// edge bins.  H[block][d][bin] (kHistBlocks blocks, no atomics outside LDS)
 __global__ __launch_bounds__(kBlock) void k_axis_hist(const double *xyz, int np, const Frame *fr, int stride, int *H) {
   __shared__ int h[3][kMapBins];
   for (int j = threadIdx.x; j < 3 * kMapBins; j += kBlock) (&h[0][0])[j] = 0;
   __syncthreads();
   const long long ns = ((long long)np + stride - 1) / stride;
   for (long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x; j < ns; j += (long long)gridDim.x * blockDim.x) {
-    const long long i = j * stride;
+    unsigned long long z = (unsigned long long)j * 0x9E3779B97F4A7C15ULL + 0x5EED2025ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    z ^= z >> 31;
+    const long long i = (long long)(z % (unsigned long long)np);
 #pragma unroll
     for (int d = 0; d < 3; d++) {
       const double e = fr->ext[d];
-      double b = e > 0.0 ? (xyz[3 * i + d] - fr->lo[d]) * ((double)kMapBins / e) : 0.0;
-      const int bi = b > 0.0 ? (b < (double)kMapBins ? (int)b : kMapBins - 1) : 0;
-      atomicAdd(&h[d][bi], 1);
+      const double b = e > 0.0 ? (xyz[3 * i + d] - fr->lo[d]) * ((double)kMapBins / e) : 0.0;
+      if (b >= 0.0 && b < (double)kMapBins) atomicAdd(&h[d][(int)b], 1);
     }
   }
   __syncthreads();

@@ -46,6 +46,7 @@ static void tet_box(const double *xyz, const int *v, double lo[3], double hi[3])
 double pmmg_max_tet_extent(int np, const double *xyz, int ne, const int *tetv) {
   double m = 0.0;
   (void)np;
+#pragma omp parallel for reduction(max : m) schedule(static)
   for (int64_t k = 0; k < ne; k++) {
     double lo[3], hi[3];
     tet_box(xyz, tetv + 4 * k, lo, hi);
@@ -53,6 +54,31 @@ double pmmg_max_tet_extent(int np, const double *xyz, int ne, const int *tetv) {
       if (hi[d] - lo[d] > m) m = hi[d] - lo[d];
   }
   return m;
+}
+
+/* map[i] != 0 -> its rank among the nonzero entries (1-based), in index
+ * order; returns the count.  Chunked in parallel: per-chunk counts, their
+ * prefix, then the numbering (the shard keeps the group's relative order). */
+static int number_marks(int *map, int64_t n) {
+  enum { kChunks = 256 };
+  int64_t cnt[kChunks + 1];
+  const int64_t per = (n + kChunks - 1) / kChunks;
+#pragma omp parallel for schedule(static)
+  for (int c = 0; c < kChunks; c++) {
+    int64_t a = c * per, b = a + per < n ? a + per : n, k = 0;
+    for (int64_t i = a; i < b; i++) k += map[i] != 0;
+    cnt[c + 1] = k;
+  }
+  cnt[0] = 0;
+  for (int c = 0; c < kChunks; c++) cnt[c + 1] += cnt[c];
+#pragma omp parallel for schedule(static)
+  for (int c = 0; c < kChunks; c++) {
+    int64_t a = c * per, b = a + per < n ? a + per : n;
+    int next = (int)cnt[c];
+    for (int64_t i = a; i < b; i++)
+      if (map[i]) map[i] = ++next;
+  }
+  return (int)cnt[kChunks];
 }
 
 int pmmg_shard_mark(int np, const double *xyz, int ne, const int *tetv, const double box_lo[3],
@@ -66,28 +92,30 @@ int pmmg_shard_mark(int np, const double *xyz, int ne, const int *tetv, const do
     hi[d] = box_hi[d] + halo;
   }
   memset(vert_map, 0, sizeof(int) * (size_t)np);
-  int nk = 0;
+  int bad = 0;
+#pragma omp parallel for schedule(static) reduction(| : bad)
   for (int64_t k = 0; k < ne; k++) {
     const int *v = tetv + 4 * k;
     double tl[3], th[3];
+    int ok = 1;
     for (int i = 0; i < 4; i++)
-      if (v[i] < 1 || v[i] > np) return 0;
+      if (v[i] < 1 || v[i] > np) ok = 0;
+    if (!ok) {
+      bad = 1;
+      tet_map[k] = 0;
+      continue;
+    }
     tet_box(xyz, v, tl, th);
     int meets = 1;
     for (int d = 0; d < 3; d++)
       if (th[d] < lo[d] || tl[d] > hi[d]) meets = 0;
-    if (meets) {
-      tet_map[k] = ++nk;
-      for (int i = 0; i < 4; i++) vert_map[v[i] - 1] = 1;
-    } else {
-      tet_map[k] = 0;
-    }
+    tet_map[k] = meets;
+    if (meets)
+      for (int i = 0; i < 4; i++) vert_map[v[i] - 1] = 1; /* every writer stores 1 */
   }
-  int nv = 0;
-  for (int64_t i = 0; i < np; i++)
-    if (vert_map[i]) vert_map[i] = ++nv;
-  counts[0] = nk;
-  counts[1] = nv;
+  if (bad) return 0;
+  counts[0] = number_marks(tet_map, ne);
+  counts[1] = number_marks(vert_map, np);
   return 1;
 }
 
@@ -113,11 +141,18 @@ int pmmg_shard_mark_cells(int np, const double *xyz, int ne, const int *tetv, co
           }
         }
   memset(vert_map, 0, sizeof(int) * (size_t)np);
-  int nk = 0;
+  int bad = 0;
+#pragma omp parallel for schedule(static) reduction(| : bad)
   for (int64_t k = 0; k < ne; k++) {
     const int *v = tetv + 4 * k;
+    int ok = 1;
     for (int i = 0; i < 4; i++)
-      if (v[i] < 1 || v[i] > np) return 0;
+      if (v[i] < 1 || v[i] > np) ok = 0;
+    if (!ok) {
+      bad = 1;
+      tet_map[k] = 0;
+      continue;
+    }
     double tl[3], th[3];
     tet_box(xyz, v, tl, th);
     int a[3], b[3], meets = 1;
@@ -138,18 +173,13 @@ int pmmg_shard_mark_cells(int np, const double *xyz, int ne, const int *tetv, co
           for (int x = a[0]; x <= b[0] && !meets; x++)
             if (occ[x + (int64_t)g_n[0] * (y + (int64_t)g_n[1] * z)]) meets = 1;
     }
-    if (meets) {
-      tet_map[k] = ++nk;
-      for (int i = 0; i < 4; i++) vert_map[v[i] - 1] = 1;
-    } else {
-      tet_map[k] = 0;
-    }
+    tet_map[k] = meets;
+    if (meets)
+      for (int i = 0; i < 4; i++) vert_map[v[i] - 1] = 1; /* every writer stores 1 */
   }
-  int nv = 0;
-  for (int64_t i = 0; i < np; i++)
-    if (vert_map[i]) vert_map[i] = ++nv;
-  counts[0] = nk;
-  counts[1] = nv;
+  if (bad) return 0;
+  counts[0] = number_marks(tet_map, ne);
+  counts[1] = number_marks(vert_map, np);
   return 1;
 }
 
@@ -158,12 +188,15 @@ int64_t pmmg_shard_fill(int np, const double *xyz, int ne, const int *tetv, cons
                         double *s_xyz, int *s_tetv, int *s_adja, int *s_triv, int *s_adjt, int *tet_gid,
                         int *vert_gid, int *tria_gid) {
   if (np < 0 || ne < 0 || nt < 0) return -1;
+#pragma omp parallel for schedule(static)
   for (int64_t i = 0; i < np; i++) {
     int l = vert_map[i];
     if (!l) continue;
     memcpy(s_xyz + 3 * (int64_t)(l - 1), xyz + 3 * i, 3 * sizeof(double));
     if (vert_gid) vert_gid[l - 1] = (int)(i + 1);
   }
+  int bad = 0;
+#pragma omp parallel for schedule(static) reduction(| : bad)
   for (int64_t k = 0; k < ne; k++) {
     int l = tet_map[k];
     if (!l) continue;
@@ -173,13 +206,17 @@ int64_t pmmg_shard_fill(int np, const double *xyz, int ne, const int *tetv, cons
       int a = adja ? adja[4 * k + i] : 0, la = 0;
       if (a > 0) {
         int g = a / 4;
-        if (g < 1 || g > ne) return -1;
+        if (g < 1 || g > ne) {
+          bad = 1;
+          continue;
+        }
         la = tet_map[g - 1] ? 4 * tet_map[g - 1] + a % 4 : 0;
       }
       if (s_adja) s_adja[o + i] = la;
     }
     if (tet_gid) tet_gid[l - 1] = (int)(k + 1);
   }
+  if (bad) return -1;
   /* trias: kept in global order when all three vertices are in the shard */
   int *tria_map = NULL;
   if (nt > 0) {

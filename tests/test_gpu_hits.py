@@ -130,3 +130,27 @@ def test_closest_hits():
     print(rep, c)
     assert c[3] > 0 and c[11] > 0
     assert ((gpu["hit"][pb] & 15) == (case["ref"]["hit"][pb] & 15)).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,n_old,n_new", [(synth.CUBE, 8, 9), (synth.SHELL, 8, 12)])
+def test_surface_walks_from_one_far_seed(monkeypatch, kind, n_old, n_new):
+    """PMMG_HIP_SRFG=1 (test-only): one surface seed cell, so every surface
+    walk starts at the same tria and crosses the surface; on the shell the
+    inner sphere cannot be reached from the outer one (or the reverse): those
+    walks run through the 4-entry visited history until maxstep and fall to
+    the exhaustive search.  The cost of that path is known and the results
+    still meet the contract (tests/parity.py)."""
+    monkeypatch.setenv("PMMG_HIP_SRFG", "1")
+    monkeypatch.setenv("PMMG_HIP_MAXSTEP", "256")
+    case = make_case(kind=kind, n_old=n_old, n_new=n_new)
+    gpu = run_gpu(case, tet8=True)
+    rep = check(case, gpu)
+    st = gpu["stats"]
+    c = _codes(gpu)
+    print(kind, rep, c, {k: st[k] for k in ("nbdy", "nbdy_exhaust", "steps_total", "stepmax", "ms_bdy")})
+    assert rep["n"] == int((case["pclass"] != 0).sum())
+    assert rep["class_i"] == rep["class_i_same"]
+    assert st["stepmax"] > 10
+    if kind == synth.SHELL:
+        assert st["nbdy_exhaust"] > 0

@@ -7,6 +7,8 @@ transfer against the whole group: identical tetra for class (i) points,
 accepted elements otherwise, reference values in the chosen element.
 The CPU cases run the oracle on the shards; the GPU case runs the HIP module.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -272,3 +274,71 @@ def test_halo_shards_gpu_match_group_run_large(kind, n_old, n_new, world, mode):
         np.testing.assert_allclose(parts["met"][i], met_r, rtol=1e-12)
         for f, g in zip(parts["fields"], fr):
             np.testing.assert_allclose(f[i], g, rtol=1e-12)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(os.environ.get("PMMG_TEST_CFG5", "1") == "0", reason="PMMG_TEST_CFG5=0: skipped (~55 s, ~80 GB "
+                    "of host memory)")
+def test_halo_shards_gpu_cfg5_full_size():
+    """cfg5 at full size (500.7M tetra, 100.5M new points, iso metric + 5
+    fields): the group on one GPU, then its two RCB parts against their halo
+    shards one after the other on the same GPU (the split bench.py --gpus 2
+    --shard halo runs across two).  Mapped to group ids, the parts agree
+    with the group: same element and bit-identical rows wherever both walks
+    accepted the same tetra, elsewhere an element the group accepts with the
+    reference interpolator's values (oracle, 2000 points)."""
+    import time
+
+    from parmmg_amd import configs
+    from parmmg_amd.transfer import TransferContext
+
+    t0 = time.time()
+    w = configs.CFG5
+    bg, new = configs.build_meshes(w, seed=synth.SEED)
+    pc = synth.classes(new)
+    met = synth.solution(w.metric, bg.xyz)
+    fields = [synth.solution(f, bg.xyz) for f in w.fields]
+    case = dict(bg=bg, new=new, pclass=pc, met=met, fields=fields, hausd=w.hausd)
+    print(f"cfg5: {bg.ne} tetra, {new.np} points, built in {time.time() - t0:.0f} s", flush=True)
+    with TransferContext(0) as ctx:
+        ctx.set_background(bg.xyz, bg.tetv, bg.adja, bg.triv, bg.adjt, w.hausd)
+        ctx.set_solutions(met, fields)
+        whole = _empty_result(case)
+        st = ctx.locate_interp(new.xyz, pc, whole["met"], whole["fields"], whole["elem"], whole["hit"])
+        print(f"group run: {st.ms_total:.2f} ms on the device, {time.time() - t0:.0f} s, {st.as_dict()}", flush=True)
+        parts = _empty_result(case)
+        for r, mine in enumerate(ranks.rcb_shards(new.xyz, pc, 2)):
+            sh = shard.halo_shard_cells(bg, new.xyz[mine], hausd=w.hausd)
+            m = sh.mesh
+            print(f"part {r}: {len(mine)} points, shard {m.ne} tetra ({m.ne / bg.ne:.1%}), {time.time() - t0:.0f} s",
+                  flush=True)
+            ctx.set_background(m.xyz, m.tetv, m.adja, m.triv, m.adjt, w.hausd)
+            ctx.set_solutions(sh.rows(met), [sh.rows(f) for f in fields])
+            n = len(mine)
+            mo = np.full((n, met.shape[1]), np.nan)
+            fo = [np.full((n, f.shape[1]), np.nan) for f in fields]
+            elem, hit = np.zeros(n, np.int32), np.zeros(n, np.int8)
+            st = ctx.locate_interp(np.ascontiguousarray(new.xyz[mine]), np.ascontiguousarray(pc[mine]), mo, fo, elem,
+                                   hit)
+            print(f"part {r}: {st.ms_total:.2f} ms on the device, {st.as_dict()}", flush=True)
+            _scatter(parts, mine, sh, mo, fo, elem, hit)
+            del sh, m
+    done = pc != 0
+    assert (parts["elem"][done] > 0).all() and ((parts["hit"][done].astype(np.int32) & 15) != 0).all()
+    same = done & (parts["elem"] == whole["elem"]) & (parts["hit"] == whole["hit"])
+    print(f"same element as the group: {int(same.sum())} of {int(done.sum())}", flush=True)
+    assert same.sum() >= 0.995 * done.sum(), (int(same.sum()), int(done.sum()))
+    for a, b in zip([parts["met"]] + parts["fields"], [whole["met"]] + whole["fields"]):
+        assert np.array_equal(a[same], b[same], equal_nan=True)
+    B = O.Background(bg, met, fields, w.hausd)
+    rest = np.nonzero(done & ~same)[0][:2000]
+    for i in rest:
+        code = int(parts["hit"][i]) & 15
+        if code == 1:
+            assert O.tetra_minbary(B, int(parts["elem"][i]), new.xyz[i]) > -O.EPS
+        met_r, fr = O.eval_in_element(B, new.xyz[i], pc[i] == 2, int(parts["elem"][i]), code,
+                                      (int(parts["hit"][i]) >> 4) & 3)
+        np.testing.assert_allclose(parts["met"][i], met_r, rtol=1e-12)
+        for f, g in zip(parts["fields"], fr):
+            np.testing.assert_allclose(f[i], g, rtol=1e-12)
+    print(f"checked {len(rest)} of the rest against the oracle; {time.time() - t0:.0f} s", flush=True)
