@@ -161,7 +161,7 @@ struct pmmg_hip_ctx {
   int verbose = 0; // PMMG_HIP_VERBOSE: host-mode transfer timings on stderr
   int tpc = 8;        // background tetra per volume seed cell (PMMG_HIP_TPC)
   int seed_lanes = 4;  // sampled tetra per seed run of 4 records (PMMG_HIP_SEEDLANES, 1..4)
-  int bbox_stride = 64;  // the frame's bbox samples every n-th vertex (PMMG_HIP_BBOX; r03o: 64 instead of 16 and
+  int bbox_stride = 64;  // the frame's bbox samples np / n vertices (PMMG_HIP_BBOX; r03o: 64 instead of 16 and
   int hist_stride = 256; // 256 instead of 64 for the axis histograms: preparation -0.15 ms at cfg4, same walks)
   int srf_g = 0;         // test-only PMMG_HIP_SRFG: the surface seed grid's cells per axis (1: one seed for all)
   int srf_mult = 8;      // the surface seed grid has srf_mult * nt / 2 cells (PMMG_HIP_SRFMULT; r03r at cfg4: 1 /

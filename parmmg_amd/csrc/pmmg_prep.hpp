@@ -185,15 +185,21 @@ __global__ __launch_bounds__(kBlock) void k_reset(Frame *fr, DevStats *st, unsig
   for (long long j = tid; j < nsg; j += nth) sgrid[j] = INT_MAX;
 }
 
-// bbox of every `stride`-th vertex (and the last one): the frame only sizes
-// the seed / bin grids, whose cell lookups clamp, so a sampled bbox costs at
-// most slightly longer walks for the few points outside it
+// bbox of np / stride vertices at pseudo-random positions (a strided sample
+// can alias with a lattice numbering's row length and collapse an axis) and
+// of the first and last vertex: the frame only sizes the seed / bin grids,
+// whose cell lookups clamp, so a sampled bbox costs at most slightly longer
+// walks for the few points outside it
 __global__ __launch_bounds__(kBlock) void k_bbox(const double *xyz, int np, Frame *fr, int stride) {
   __shared__ unsigned long long slo[3][kBlock / 64], shi[3][kBlock / 64];
   unsigned long long lo[3] = {~0ULL, ~0ULL, ~0ULL}, hi[3] = {0ULL, 0ULL, 0ULL};
-  const long long ns = ((long long)np + stride - 1) / stride + 1;
+  const long long ns = ((long long)np + stride - 1) / stride + 2;
   for (long long j = blockIdx.x * blockDim.x + threadIdx.x; j < ns; j += gridDim.x * blockDim.x) {
-    const long long i = j * stride < np ? j * stride : np - 1;
+    unsigned long long z = (unsigned long long)j * 0x9E3779B97F4A7C15ULL + 0xB0B0B0B0ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    z ^= z >> 31;
+    const long long i = j == 0 ? 0 : (j == 1 ? np - 1 : (long long)(z % (unsigned long long)np));
 #pragma unroll
     for (int d = 0; d < 3; d++) {
       unsigned long long k = dkey(xyz[3 * i + d]);
