@@ -666,7 +666,9 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "strong" if split else "weak",
+        # N = 1 is the first point of the default N > 1 curve (the same cfg4
+        # group split over the GPUs: strong scaling); --shard group is weak
+        "scaling": "weak" if (shard_mode == "group" and world > 1) or args.shard == "group" else "strong",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (Kuhn lattices, analytic metric/fields, splitmix64 jitter)",
@@ -678,7 +680,9 @@ def main():
             "parallelism": (f"{args.split} parts x{world}, replicated background, RCCL all-gather after the step"
                             if shard_mode == "morton" else
                             f"{args.split} parts x{world}, halo-sharded background, RCCL all-gather after the step"
-                            if shard_mode == "halo" else f"one group per GPU x{world} (weak, no data-path collective)"),
+                            if shard_mode == "halo" else
+                            "the whole group on one GPU (N > 1 splits it: RCB parts x halo shards, strong scaling)"
+                            if world == 1 else f"one group per GPU x{world} (weak, no data-path collective)"),
             "query_order": args.sort,
             "tetra_layout": args.layout,
             "morton_binned": bool(st.sorted),

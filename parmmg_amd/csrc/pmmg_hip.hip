@@ -99,6 +99,13 @@ bool packed_supported(int met_size, int nfield, const int *fsize) {
   return pick_layout(S) != nullptr;
 }
 
+// the query order the host decided (after k_reset cleared the stats): read
+// by the volume kernel
+__global__ void k_set_order(DevStats *st, int sorted, int bits) {
+  st->sorted = sorted;
+  st->bin_bits = bits;
+}
+
 } // namespace
 
 // ================================================================ host side
@@ -136,6 +143,8 @@ struct pmmg_hip_ctx {
   DevBuf qs;                              // volume query coordinates in processing order (Morton path)
   DevBuf cls_cnt;                         // per-block class counts (surface list compaction)
   int *h_sorted = nullptr;                // pinned: the coherence test's {sorted, bin_bits}, read back in auto mode
+  DevBuf oflag;                           // the coherence test's {sorted, bin_bits} on the device
+  hipEvent_t ev_flag = nullptr;           // its read-back
   DevBuf qmin;                               // tetra quality minimum (pmmg_hip_tetra_qual)
   DevBuf fb_vol, fb_bdy, best, ckey, cidx, bbest, bckey, bcidx;
   // host-mode staging
@@ -483,6 +492,7 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
     return nullptr;
   }
   for (int i = 0; i < EV_COUNT; i++) (void)hipEventCreate(&c->ev[i]);
+  (void)hipEventCreateWithFlags(&c->ev_flag, hipEventDisableTiming);
   if (hipHostMalloc((void **)&c->h_sorted, 2 * sizeof(int), hipHostMallocDefault) != hipSuccess) {
     fprintf(stderr, "[parmmg_hip] cannot allocate pinned host memory\n");
     pmmg_hip_destroy(c);
@@ -515,7 +525,7 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   if (c->cstream) (void)hipStreamSynchronize(c->cstream);
   DevBuf *bufs[] = {&c->o_xyz, &c->o_tetv, &c->o_adja, &c->o_triv, &c->o_adjt, &c->o_met, &c->o_rec, &c->frame,
                     &c->stats, &c->grid, &c->sgrid, &c->order_v,
-                    &c->order_b, &c->cont, &c->xq, &c->qs, &c->axh, &c->bkeys, &c->bkeys2, &c->bvals, &c->sort_tmp, &c->cls_cnt, &c->qmin, &c->fb_vol, &c->fb_bdy,
+                    &c->order_b, &c->cont, &c->xq, &c->qs, &c->axh, &c->bkeys, &c->bkeys2, &c->bvals, &c->sort_tmp, &c->oflag, &c->cls_cnt, &c->qmin, &c->fb_vol, &c->fb_bdy,
                     &c->best, &c->ckey, &c->cidx, &c->bbest, &c->bckey, &c->bcidx, &c->h_xyz,
                     &c->h_cls, &c->h_met, &c->h_elem, &c->h_hit};
   for (DevBuf *b : bufs) release(*b);
@@ -528,6 +538,7 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
     if (c->stage_ev[b]) (void)hipEventDestroy(c->stage_ev[b]);
   }
   if (c->h_sorted) (void)hipHostFree(c->h_sorted);
+  if (c->ev_flag) (void)hipEventDestroy(c->ev_flag);
   delete c->pool;
   release(c->o_tet4);
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
@@ -909,7 +920,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
       !ensure(c, c->ckey, 8 * nq) || !ensure(c, c->cidx, 4 * nq) || !ensure(c, c->bbest, 4 * nq) ||
       !ensure(c, c->bckey, 8 * nq) || !ensure(c, c->bcidx, 4 * nq))
     return 0;
-  if (!ensure(c, c->xq, sizeof(int) * kXqStride * (size_t)bg.np) ||
+  if (!ensure(c, c->xq, sizeof(int) * kXqStride * (size_t)bg.np) || !ensure(c, c->oflag, 2 * sizeof(int)) ||
       !ensure(c, c->axh, sizeof(int) * 3 * kMapBins * (size_t)kHistBlocks))
     return 0;
   bg.xq = (const int *)c->xq.p;
@@ -922,6 +933,17 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
 
   // ---- frame (main stream)
   HIPCK(c, hipEventRecord(c->ev[EV_START], s));
+  // the coherence test first, on the second stream beside the frame kernels
+  // (it reads only the queries; its flag is read back in auto mode while the
+  // main stream builds the seed grid, so the host has enqueued the rest of the
+  // call long before the device needs it)
+  HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_START], 0));
+  hipLaunchKernelGGL(k_coherence, dim3(1), dim3(kBlock), 0, sb, xyz_new, np_new, (int *)c->oflag.p, force,
+                     c->bin_bits);
+  if (force < 0) {
+    HIPCK(c, hipMemcpyAsync(c->h_sorted, c->oflag.p, 2 * sizeof(int), hipMemcpyDeviceToHost, sb));
+    HIPCK(c, hipEventRecord(c->ev_flag, sb));
+  }
   hipLaunchKernelGGL(k_reset, dim3(blocks_for(ng > nsg ? ng : nsg, 2048)), dim3(kBlock), 0, s, fr, st, grid, ng,
                      sgrid, nsg);
   hipLaunchKernelGGL(k_bbox, dim3(blocks_for(bg.np / c->bbox_stride + 1, 256)), dim3(kBlock), 0, s, bg.xyz, bg.np, fr,
@@ -939,8 +961,6 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   // not), then either the Morton binning (sorted) or the stable class
   // compaction of the surface points (input order) is enqueued
   HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_FRAME], 0));
-  hipLaunchKernelGGL(k_coherence, dim3(1), dim3(kBlock), 0, sb, xyz_new, np_new, st, force, c->bin_bits);
-  if (force < 0) HIPCK(c, hipMemcpyAsync(c->h_sorted, &st->sorted, 2 * sizeof(int), hipMemcpyDeviceToHost, sb));
   HIPCK(c, hipGetLastError());
 
   // ---- seed grid (main stream): fixed-point vertex copy, volume seeds
@@ -956,10 +976,11 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
 
   int sorted = force, bits = c->bin_bits;
   if (force < 0) {
-    HIPCK(c, hipStreamSynchronize(sb));
+    HIPCK(c, hipEventSynchronize(c->ev_flag));
     sorted = c->h_sorted[0];
     bits = c->h_sorted[1];
   }
+  hipLaunchKernelGGL(k_set_order, dim3(1), dim3(1), 0, s, st, sorted, bits);
   if (sorted && np_new > 0) {
     hipLaunchKernelGGL(k_bin_keys, dim3(blocks_for(np_new, 1024)), dim3(kBlock), 0, sb, xyz_new, pclass, np_new,
                        (const Frame *)fr, bits, (unsigned *)c->bkeys.p, (int *)c->bvals.p, st);
@@ -978,11 +999,10 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     // longer here, r03o)
     int *bc = (int *)c->cls_cnt.p;
     hipLaunchKernelGGL(k_cls_count, dim3((unsigned)ncls), dim3(kBlock), 0, sb, pclass, (long long)np_new,
-                       (int)PMMG_PT_BDY, bc, (const DevStats *)st);
-    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, sb, bc, (int)ncls, &st->nbdy, (const int *)&st->sorted,
-                       0);
+                       (int)PMMG_PT_BDY, bc);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, sb, bc, (int)ncls, &st->nbdy, (const int *)nullptr, 0);
     hipLaunchKernelGGL(k_cls_scatter, dim3((unsigned)ncls), dim3(kBlock), 0, sb, pclass, (long long)np_new,
-                       (int)PMMG_PT_BDY, (const int *)bc, order_b, (const DevStats *)st);
+                       (int)PMMG_PT_BDY, (const int *)bc, order_b);
   }
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[EV_ORDER], sb));

@@ -591,13 +591,14 @@ constexpr int kBinBitsCoherent = 5; // 32^3 cells for a mostly coherent numberin
 // below 4h (a median test: the jumps at the ends of lattice rows or of Mmg's
 // local numbering runs do not count; a shuffled numbering has almost every
 // distance at the scale of the bbox).  force: 1 always Morton-bin, 0 never,
-// -1 test.  Writes st->sorted.
-__global__ __launch_bounds__(kBlock) void k_coherence(const double *xyz, int np, DevStats *st, int force,
+// -1 test.  Writes flag[0] (1: Morton bins) and flag[1] (their bits per
+// axis), which the host reads back; it then sets DevStats::sorted (k_set_order).
+__global__ __launch_bounds__(kBlock) void k_coherence(const double *xyz, int np, int *flag, int force,
                                                       int force_bits) {
   if (force >= 0) {
     if (threadIdx.x == 0) {
-      st->sorted = force;
-      st->bin_bits = force_bits;
+      flag[0] = force;
+      flag[1] = force_bits;
     }
     return;
   }
@@ -657,8 +658,8 @@ __global__ __launch_bounds__(kBlock) void k_coherence(const double *xyz, int np,
     // cell is kept and mostly coherent) when at least half are short, fine
     // cells (kBinBitsAxis) for a numbering without coherence
     const bool coherent = np > 1 && 20 * tot >= 19 * nsamp;
-    st->sorted = coherent ? 0 : 1;
-    st->bin_bits = 2 * tot >= nsamp ? kBinBitsCoherent : kBinBitsAxis;
+    flag[0] = coherent ? 0 : 1;
+    flag[1] = 2 * tot >= nsamp ? kBinBitsCoherent : kBinBitsAxis;
   }
 }
 
@@ -757,9 +758,7 @@ __device__ __forceinline__ unsigned cls_bits(const uint8_t *pclass, long long np
   return m;
 }
 
-__global__ __launch_bounds__(kBlock) void k_cls_count(const uint8_t *pclass, long long np, int cls, int *bcnt,
-                                                      const DevStats *st) {
-  if (st->sorted) return;
+__global__ __launch_bounds__(kBlock) void k_cls_count(const uint8_t *pclass, long long np, int cls, int *bcnt) {
   const long long i0 = (long long)blockIdx.x * kScanChunk + (long long)threadIdx.x * kScanItems;
   int tot;
   block_excl_scan(__popc(cls_bits(pclass, np, i0, cls)), &tot);
@@ -767,8 +766,7 @@ __global__ __launch_bounds__(kBlock) void k_cls_count(const uint8_t *pclass, lon
 }
 
 __global__ __launch_bounds__(kBlock) void k_cls_scatter(const uint8_t *pclass, long long np, int cls,
-                                                        const int *boff, int *out, const DevStats *st) {
-  if (st->sorted) return;
+                                                        const int *boff, int *out) {
   const long long i0 = (long long)blockIdx.x * kScanChunk + (long long)threadIdx.x * kScanItems;
   unsigned m = cls_bits(pclass, np, i0, cls);
   int tot;
