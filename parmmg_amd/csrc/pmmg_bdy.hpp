@@ -106,27 +106,33 @@ __device__ __forceinline__ int bdy_query(const Bg &bg, const Frame *fr, const in
   return hit;
 }
 
-// One lane per surface query; every wave claims the next 64 queries of its
-// XCD's eighth of the list from a counter until the eighth is done (the
-// walks differ in length: a static split over ~1.2 rounds of the grid left
-// the second round nearly empty and every block waiting on its slowest
-// wave).
+// One lane per surface query, the static XCD-chunked split of the grid
+// (default), or (dyn, PMMG_HIP_BDYDYN=1) every wave claiming the next 64
+// queries of its XCD's eighth from a counter: measured, the claiming waves
+// slowed the volume kernel beside them (profiles/r03y).
 __global__ __launch_bounds__(kBlock) void k_bdy(Bg bg, const Frame *fr, const int *sgrid, int gs, const double *qxyz,
                                                 const int *order, Slots S, int *elem_out, int8_t *hit_out, int *fb,
-                                                DevStats *st, int maxstep) {
+                                                DevStats *st, int maxstep, int dyn) {
   __shared__ BlockStats bs;
   bstats_init(&bs);
   __syncthreads();
   const long long n = st->nbdy;
   const int x = blockIdx.x & 7;
   const long long lo = n * x / 8, hi = n * (x + 1) / 8;
-  for (;;) {
-    int base = 0;
-    if (__lane_id() == 0) base = atomicAdd(&st->bdy_next[x], 64);
-    base = __shfl(base, 0);
-    if (lo + base >= hi) break;
-    const long long i = lo + base + __lane_id();
-    const bool active = i < hi;
+  const XcdChunk ch = xcd_chunk(n); // static split (dyn == 0)
+  for (int it = 0;; it++) {
+    long long i;
+    if (dyn) {
+      int base = 0;
+      if (__lane_id() == 0) base = atomicAdd(&st->bdy_next[x], 64);
+      base = __shfl(base, 0);
+      if (lo + base >= hi) break;
+      i = lo + base + __lane_id();
+    } else {
+      if (it >= ch.iters) break;
+      i = ch.start + it * ch.stride;
+    }
+    const bool active = i < (dyn ? hi : ch.hi);
     int steps = 0, hit = 0, ip = 0;
     if (active) {
       ip = order[i];

@@ -172,6 +172,8 @@ struct pmmg_hip_ctx {
   int seed_lanes = 4;  // sampled tetra per seed run of 4 records (PMMG_HIP_SEEDLANES, 1..4)
   int bbox_stride = 64;  // the frame's bbox samples np / n vertices (PMMG_HIP_BBOX; r03o: 64 instead of 16 and
   int hist_stride = 256; // 256 instead of 64 for the axis histograms: preparation -0.15 ms at cfg4, same walks)
+  int bdy_dyn = 0;       // k_bdy: waves claim work from per-XCD counters (PMMG_HIP_BDYDYN=1; r03y: the claiming
+                         // waves slowed the volume kernel beside them, 8-way rank 0.70 -> 0.64 ms static)
   int srf_g = 0;         // test-only PMMG_HIP_SRFG: the surface seed grid's cells per axis (1: one seed for all)
   int srf_mult = 8;      // the surface seed grid has srf_mult * nt / 2 cells (PMMG_HIP_SRFMULT; r03r at cfg4: 1 /
                          // 8 / 32 -> 7.4 / 3.9 / 2.7 steps per surface point, surface branch 0.446 / 0.403 /
@@ -504,6 +506,7 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   c->hist_stride = env_int("PMMG_HIP_HIST", c->hist_stride);
   c->srf_mult = env_int("PMMG_HIP_SRFMULT", c->srf_mult);
   c->srf_g = env_int("PMMG_HIP_SRFG", 0);
+  c->bdy_dyn = env_int("PMMG_HIP_BDYDYN", 2) == 1;
   c->bin_bits = std::min(7, env_int("PMMG_HIP_BINBITS", c->bin_bits));
   c->bin_qs = env_int("PMMG_HIP_BINQS", 2) == 1;
   c->verbose = env_int("PMMG_HIP_VERBOSE", 0);
@@ -1014,7 +1017,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
                        gs);
     hipLaunchKernelGGL(k_bdy, dim3(8 * blocks_for((np_new + 7) / 8, 256)), dim3(kBlock), 0, sb, bg,
                        (const Frame *)fr, (const int *)sgrid, gs, xyz_new, (const int *)order_b, S, elem_out, hit_out,
-                       (int *)c->fb_bdy.p, st, c->maxstep);
+                       (int *)c->fb_bdy.p, st, c->maxstep, c->bdy_dyn);
     launch_bdy_fallbacks(c, sb, S, xyz_new, elem_out, hit_out);
     HIPCK(c, hipGetLastError());
   }

@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--bdy-weight", type=int, default=ranks.BDY_WEIGHT, help="cost of a surface point in the split")
     ap.add_argument("--split", default="rcb", choices=["rcb", "morton"], help="partition of the new points")
     ap.add_argument("--mode", default="cells", choices=["cells", "box"], help="halo shard: cell union or range box")
+    ap.add_argument("--variants", default="", help='";"-separated PMMG_HIP_* settings NAME=v,... (sort=0/1: the '
+                                                   'context option), each timed on every rank')
     a = ap.parse_args()
     w = configs.SHORT[a.config]
     bg0, new, met0, fields0, pclass = bench.build_workload(w, 0)
@@ -43,42 +45,57 @@ def main():
         else:
             sh = shard.halo_shard(bg0, *shard.range_box(q_xyz), -1.0, hausd=w.hausd)
         bg, met, fields = sh.mesh, sh.rows(met0), [sh.rows(f) for f in fields0]
-        with TransferContext(0) as ctx:
-            d = dict(xyz=ctx.upload(bg.xyz), tet8=ctx.upload(pack_tet8(bg.tetv, bg.adja)), triv=ctx.upload(bg.triv),
-                     adjt=ctx.upload(bg.adjt), met=ctx.upload(met), f=[ctx.upload(f) for f in fields],
-                     q=ctx.upload(q_xyz), pc=ctx.upload(q_pc))
-            nq = q_xyz.shape[0]
-            mo = ctx.empty((nq, w.met_size), np.float64)
-            fo = [ctx.empty((nq, f.shape[1]), np.float64) for f in fields]
-            el, hit = ctx.empty((nq,), np.int32), ctx.empty((nq,), np.int8)
+        for var in a.variants.split(";"):
+            run_rank(a, w, r, var, bg, bg0, met, fields, q_xyz, q_pc)
 
-            def step():
-                ctx.set_background_tet8(d["xyz"], d["tet8"], d["triv"], d["adjt"], w.hausd)
-                ctx.set_solutions(d["met"], d["f"])
-                ctx.locate_interp(d["q"], d["pc"], mo, fo, el, hit, sync=False)
 
-            for _ in range(a.warmup):
-                step()
-                ctx.sync()
-            ms = {k: [] for k in ("ms_total", "ms_prepare", "ms_sort", "ms_vol", "ms_vol_locate", "ms_bdy",
-                                  "ms_fallback")}
-            t0 = time.perf_counter()
-            for _ in range(a.steps):  # back to back, as bench.py times them
-                step()
+def run_rank(a, w, r, var, bg, bg0, met, fields, q_xyz, q_pc):
+    """one rank's share timed under one variant of the module settings"""
+    sort = None
+    for k in [k for k in os.environ if k.startswith("PMMG_HIP_") and k != "PMMG_HIP_SO"]:
+        os.environ.pop(k)
+    for item in filter(None, var.split(",")):
+        k, v = item.split("=")
+        if k.lower() == "sort":
+            sort = v == "1"
+        else:
+            os.environ["PMMG_HIP_" + k.upper()] = v
+    with TransferContext(0, sort=sort) as ctx:
+        d = dict(xyz=ctx.upload(bg.xyz), tet8=ctx.upload(pack_tet8(bg.tetv, bg.adja)), triv=ctx.upload(bg.triv),
+                 adjt=ctx.upload(bg.adjt), met=ctx.upload(met), f=[ctx.upload(f) for f in fields],
+                 q=ctx.upload(q_xyz), pc=ctx.upload(q_pc))
+        nq = q_xyz.shape[0]
+        mo = ctx.empty((nq, w.met_size), np.float64)
+        fo = [ctx.empty((nq, f.shape[1]), np.float64) for f in fields]
+        el, hit = ctx.empty((nq,), np.int32), ctx.empty((nq,), np.int8)
+
+        def step():
+            ctx.set_background_tet8(d["xyz"], d["tet8"], d["triv"], d["adjt"], w.hausd)
+            ctx.set_solutions(d["met"], d["f"])
+            ctx.locate_interp(d["q"], d["pc"], mo, fo, el, hit, sync=False)
+
+        for _ in range(a.warmup):
+            step()
             ctx.sync()
-            wall = (time.perf_counter() - t0) / a.steps
-            for _ in range(a.steps):  # per-step device times
-                step()
-                st = ctx.sync()
-                for k in ms:
-                    ms[k].append(getattr(st, k))
-            res = {"rank": r, "world": a.world, "mode": a.mode, "nvol_exhaust": int(st.nvol_exhaust),
-                   "nvol_closest": int(st.nvol_closest), "nbdy_exhaust": int(st.nbdy_exhaust),
-                   "points": int(st.nvol + st.nbdy), "nbdy": int(st.nbdy), "sorted": int(st.sorted),
-                   "steps_pp": round(st.steps_total / max(1, st.nvol + st.nbdy), 3), "shard_tets": bg.ne,
-                   "shard_tet_fraction": round(bg.ne / bg0.ne, 4), "ms_per_step_wall": round(1e3 * wall, 4)}
-            res.update({k: round(float(np.median(v)), 4) for k, v in ms.items()})
-            print(res, flush=True)
+        ms = {k: [] for k in ("ms_total", "ms_prepare", "ms_sort", "ms_vol", "ms_vol_locate", "ms_bdy",
+                              "ms_fallback")}
+        t0 = time.perf_counter()
+        for _ in range(a.steps):  # back to back, as bench.py times them
+            step()
+        ctx.sync()
+        wall = (time.perf_counter() - t0) / a.steps
+        for _ in range(a.steps):  # per-step device times
+            step()
+            st = ctx.sync()
+            for k in ms:
+                ms[k].append(getattr(st, k))
+        res = {"rank": r, "variant": var, "world": a.world, "mode": a.mode, "nvol_exhaust": int(st.nvol_exhaust),
+               "nvol_closest": int(st.nvol_closest), "nbdy_exhaust": int(st.nbdy_exhaust),
+               "points": int(st.nvol + st.nbdy), "nbdy": int(st.nbdy), "sorted": int(st.sorted),
+               "steps_pp": round(st.steps_total / max(1, st.nvol + st.nbdy), 3), "shard_tets": bg.ne,
+               "shard_tet_fraction": round(bg.ne / bg0.ne, 4), "ms_per_step_wall": round(1e3 * wall, 4)}
+        res.update({k: round(float(np.median(v)), 4) for k, v in ms.items()})
+        print(res, flush=True)
 
 
 if __name__ == "__main__":
