@@ -328,10 +328,15 @@ __device__ __forceinline__ void nt_store2(double *p, double a, double b) {
   __builtin_nontemporal_store(v, reinterpret_cast<ntd2 *>(p));
 }
 
+// One lane's own row at a scattered position (the surface points, the exact
+// continuation, the fallbacks): plain stores, so that the row's pieces merge
+// in L2 into one line write (non-temporal pieces of a partial line go to
+// memory one by one; r03: the surface branch alone 0.40 -> see DESIGN §4)
 __device__ __forceinline__ void store6(double *p, const double *m) {
-  nt_store2(p, m[0], m[1]);
-  nt_store2(p + 2, m[2], m[3]);
-  nt_store2(p + 4, m[4], m[5]);
+  double2 *q = reinterpret_cast<double2 *>(p);
+  q[0] = make_double2(m[0], m[1]);
+  q[1] = make_double2(m[2], m[3]);
+  q[2] = make_double2(m[4], m[5]);
 }
 
 // ------------------------------------------------------------ interpolators
@@ -394,7 +399,7 @@ __device__ __forceinline__ void interp_code(const Slot &sl, int ip, const int *v
   if constexpr (CODE == 6) store6(out, r);
   else {
 #pragma unroll
-    for (int j = 0; j < CODE; j++) nt_store(out + j, r[j]);
+    for (int j = 0; j < CODE; j++) out[j] = r[j];
   }
 }
 

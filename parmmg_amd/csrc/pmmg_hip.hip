@@ -172,6 +172,7 @@ struct pmmg_hip_ctx {
   int seed_lanes = 4;  // sampled tetra per seed run of 4 records (PMMG_HIP_SEEDLANES, 1..4)
   int bbox_stride = 64;  // the frame's bbox samples np / n vertices (PMMG_HIP_BBOX; r03o: 64 instead of 16 and
   int hist_stride = 256; // 256 instead of 64 for the axis histograms: preparation -0.15 ms at cfg4, same walks)
+  int bdy_bpx = 512;     // k_bdy blocks per XCD at most (PMMG_HIP_BDYBPX)
   int bdy_dyn = 0;       // k_bdy: waves claim work from per-XCD counters (PMMG_HIP_BDYDYN=1; r03y: the claiming
                          // waves slowed the volume kernel beside them, 8-way rank 0.70 -> 0.64 ms static)
   int srf_g = 0;         // test-only PMMG_HIP_SRFG: the surface seed grid's cells per axis (1: one seed for all)
@@ -507,6 +508,7 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   c->srf_mult = env_int("PMMG_HIP_SRFMULT", c->srf_mult);
   c->srf_g = env_int("PMMG_HIP_SRFG", 0);
   c->bdy_dyn = env_int("PMMG_HIP_BDYDYN", 2) == 1;
+  c->bdy_bpx = env_int("PMMG_HIP_BDYBPX", c->bdy_bpx);
   c->bin_bits = std::min(7, env_int("PMMG_HIP_BINBITS", c->bin_bits));
   c->bin_qs = env_int("PMMG_HIP_BINQS", 2) == 1;
   c->verbose = env_int("PMMG_HIP_VERBOSE", 0);
@@ -1015,7 +1017,9 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   if (bg.nt > 0) {
     hipLaunchKernelGGL(k_seed_srf, dim3(blocks_for(bg.nt, 4096)), dim3(kBlock), 0, sb, bg, (const Frame *)fr, sgrid,
                        gs);
-    hipLaunchKernelGGL(k_bdy, dim3(8 * blocks_for((np_new + 7) / 8, 256)), dim3(kBlock), 0, sb, bg,
+    // one round of the grid for up to 1M surface points (static split: a
+    // second, nearly empty round doubled the surface branch alone)
+    hipLaunchKernelGGL(k_bdy, dim3(8 * blocks_for((np_new + 7) / 8, c->bdy_bpx)), dim3(kBlock), 0, sb, bg,
                        (const Frame *)fr, (const int *)sgrid, gs, xyz_new, (const int *)order_b, S, elem_out, hit_out,
                        (int *)c->fb_bdy.p, st, c->maxstep, c->bdy_dyn);
     launch_bdy_fallbacks(c, sb, S, xyz_new, elem_out, hit_out);

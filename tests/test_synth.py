@@ -79,3 +79,15 @@ def test_fields_spd_and_slab_diagonal():
     ani = synth.solution(synth.F_ANI, m.xyz)
     slab = m.xyz[:, 0] < 0.1
     assert (ani[slab][:, [1, 2, 4]] == 0).all()
+
+
+def test_mmg_like_numbering_is_a_permutation():
+    """bench.py's Mmg-like numbering: a permutation, one point in ~six
+    appended at the end, both parts in the generator's order."""
+    n = 100_000
+    perm = synth.mmg_like_perm(n)
+    assert np.array_equal(np.sort(perm), np.arange(n))
+    cut = int(np.argmax(np.diff(perm) < 0)) + 1  # the appended part starts where the order restarts
+    head, tail = perm[:cut], perm[cut:]
+    assert np.all(np.diff(head) > 0) and np.all(np.diff(tail) > 0)
+    assert 0.14 < tail.size / n < 0.19
