@@ -329,14 +329,12 @@ __device__ __forceinline__ void nt_store2(double *p, double a, double b) {
 }
 
 // One lane's own row at a scattered position (the surface points, the exact
-// continuation, the fallbacks): plain stores, so that the row's pieces merge
-// in L2 into one line write (non-temporal pieces of a partial line go to
-// memory one by one; r03: the surface branch alone 0.40 -> see DESIGN §4)
+// continuation, the fallbacks): non-temporal pieces (r03ab: plain stores
+// here made the surface branch alone 0.40 -> 0.67 ms)
 __device__ __forceinline__ void store6(double *p, const double *m) {
-  double2 *q = reinterpret_cast<double2 *>(p);
-  q[0] = make_double2(m[0], m[1]);
-  q[1] = make_double2(m[2], m[3]);
-  q[2] = make_double2(m[4], m[5]);
+  nt_store2(p, m[0], m[1]);
+  nt_store2(p + 2, m[2], m[3]);
+  nt_store2(p + 4, m[4], m[5]);
 }
 
 // ------------------------------------------------------------ interpolators
@@ -399,7 +397,7 @@ __device__ __forceinline__ void interp_code(const Slot &sl, int ip, const int *v
   if constexpr (CODE == 6) store6(out, r);
   else {
 #pragma unroll
-    for (int j = 0; j < CODE; j++) out[j] = r[j];
+    for (int j = 0; j < CODE; j++) nt_store(out + j, r[j]);
   }
 }
 

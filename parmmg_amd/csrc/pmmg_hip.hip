@@ -38,6 +38,7 @@
 
 #include "pmmg_device.hpp"
 #include "pmmg_prep.hpp"
+#include "pmmg_brick.hpp"
 #include "pmmg_vol.hpp"
 #include "pmmg_bdy.hpp"
 #include "pmmg_fallback.hpp"
@@ -140,6 +141,10 @@ struct pmmg_hip_ctx {
   DevBuf frame, stats, grid, sgrid, order_v, order_b, cont, xq;
   DevBuf axh;                             // per-axis histograms of the seed grid map (k_axis_hist)
   DevBuf bkeys, bkeys2, bvals, sort_tmp;  // Morton binning: keys, sorted keys, ids, rocPRIM scratch
+  // PMMG_HIP_BRICK (measurement only, pmmg_brick.hpp): the background renumbered by bricks
+  DevBuf brk_k, brk_k2, brk_v, brk_v2, brk_vinv, brk_tinv, brk_xq, brk_xyz, brk_sol, brk_rec, brk_tmp;
+  int brick = 0;
+  int srf_solo = 0; // test-only PMMG_HIP_SRFSOLO=1: the surface branch waits for the seed grid (its cost alone)
   DevBuf qs;                              // volume query coordinates in processing order (Morton path)
   DevBuf cls_cnt;                         // per-block class counts (surface list compaction)
   int *h_sorted = nullptr;                // pinned: the coherence test's {sorted, bin_bits}, read back in auto mode
@@ -512,6 +517,8 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   c->bin_bits = std::min(7, env_int("PMMG_HIP_BINBITS", c->bin_bits));
   c->bin_qs = env_int("PMMG_HIP_BINQS", 2) == 1;
   c->verbose = env_int("PMMG_HIP_VERBOSE", 0);
+  c->brick = env_int("PMMG_HIP_BRICK", 0);
+  c->srf_solo = env_int("PMMG_HIP_SRFSOLO", 0);
   c->maxstep = env_int("PMMG_HIP_MAXSTEP", c->maxstep);
   c->fanmax = env_int("PMMG_HIP_FANMAX", c->fanmax);
   c->bg.fanmax = c->fanmax; // every kernel's Bg copy carries it
@@ -532,7 +539,8 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
                     &c->stats, &c->grid, &c->sgrid, &c->order_v,
                     &c->order_b, &c->cont, &c->xq, &c->qs, &c->axh, &c->bkeys, &c->bkeys2, &c->bvals, &c->sort_tmp, &c->oflag, &c->cls_cnt, &c->qmin, &c->fb_vol, &c->fb_bdy,
                     &c->best, &c->ckey, &c->cidx, &c->bbest, &c->bckey, &c->bcidx, &c->h_xyz,
-                    &c->h_cls, &c->h_met, &c->h_elem, &c->h_hit};
+                    &c->h_cls, &c->h_met, &c->h_elem, &c->h_hit, &c->brk_k, &c->brk_k2, &c->brk_v, &c->brk_v2,
+                    &c->brk_vinv, &c->brk_tinv, &c->brk_xq, &c->brk_xyz, &c->brk_sol, &c->brk_rec, &c->brk_tmp};
   for (DevBuf *b : bufs) release(*b);
   for (auto &b : c->o_f) release(b);
   for (auto &b : c->h_f) release(b);
@@ -875,6 +883,54 @@ static void launch_bdy_fallbacks(pmmg_hip_ctx *c, hipStream_t s, const Slots &S,
 }
 
 // the pipeline on device pointers; enqueues only (no host synchronisation)
+// PMMG_HIP_BRICK=b: the background renumbered by bricks of b^3 seed cells
+// (measurement only: pmmg_brick.hpp); the results go nowhere
+static int brick_renumber(pmmg_hip_ctx *c, hipStream_t s, const Bg &bg, const Slots &S, const Frame *fr, int g) {
+  int lb = 0;
+  while ((2 << lb) <= c->brick) lb++;
+  const size_t nmax = (size_t)(bg.np > bg.ne ? bg.np : bg.ne);
+  size_t nsol = 0;
+  for (int j = 0; j < S.n; j++) nsol += (size_t)S.s[j].code;
+  if (!ensure(c, c->brk_k, 4 * nmax) || !ensure(c, c->brk_k2, 4 * nmax) || !ensure(c, c->brk_v, 4 * nmax) ||
+      !ensure(c, c->brk_v2, 4 * nmax) || !ensure(c, c->brk_vinv, 4 * (size_t)bg.np) ||
+      !ensure(c, c->brk_tinv, 4 * (size_t)bg.ne) || !ensure(c, c->brk_xq, 4 * kXqStride * (size_t)bg.np) ||
+      !ensure(c, c->brk_xyz, 24 * (size_t)bg.np) || !ensure(c, c->brk_sol, 8 * nsol * (size_t)bg.np + 8) ||
+      !ensure(c, c->brk_rec, 32 * (size_t)bg.ne))
+    return 0;
+  unsigned *k1 = (unsigned *)c->brk_k.p, *k2 = (unsigned *)c->brk_k2.p;
+  int *v1 = (int *)c->brk_v.p, *v2 = (int *)c->brk_v2.p;
+  int *vinv = (int *)c->brk_vinv.p, *tinv = (int *)c->brk_tinv.p;
+  const int kbits = 3 * (10 - lb);
+  size_t tmp = 0;
+  HIPCK(c, rocprim::radix_sort_pairs(nullptr, tmp, (const unsigned *)k1, k2, (const int *)v1, v2, nmax, 0, kbits, s));
+  if (!ensure(c, c->brk_tmp, tmp)) return 0;
+  // vertices: keys, sort, inverse, rows
+  hipLaunchKernelGGL(k_brick_vkeys, dim3(blocks_for(bg.np, 4096)), dim3(kBlock), 0, s, bg, fr, g, lb, k1, v1);
+  HIPCK(c, rocprim::radix_sort_pairs(c->brk_tmp.p, tmp, (const unsigned *)k1, k2, (const int *)v1, v2, (size_t)bg.np, 0,
+                                     kbits, s));
+  hipLaunchKernelGGL(k_brick_inv, dim3(blocks_for(bg.np, 4096)), dim3(kBlock), 0, s, (const int *)v2,
+                     (long long)bg.np, vinv);
+  hipLaunchKernelGGL(k_brick_vrows, dim3(blocks_for(bg.np, 4096)), dim3(kBlock), 0, s, bg, (const int *)v2,
+                     (int *)c->brk_xq.p, (double *)c->brk_xyz.p);
+  size_t off = 0;
+  for (int j = 0; j < S.n; j++) {
+    hipLaunchKernelGGL(k_brick_srows, dim3(blocks_for((long long)bg.np * S.s[j].code, 4096)), dim3(kBlock), 0, s,
+                       S.s[j].in, S.s[j].istride, S.s[j].code, (const int *)v2, (long long)bg.np,
+                       (double *)c->brk_sol.p + off * (size_t)bg.np);
+    off += (size_t)S.s[j].code;
+  }
+  // tetra: keys, sort, inverse, records (vertex ids and adjacencies renumbered)
+  hipLaunchKernelGGL(k_brick_tkeys, dim3(blocks_for(bg.ne, 4096)), dim3(kBlock), 0, s, bg, fr, g, lb, k1, v1);
+  HIPCK(c, rocprim::radix_sort_pairs(c->brk_tmp.p, tmp, (const unsigned *)k1, k2, (const int *)v1, v2, (size_t)bg.ne, 0,
+                                     kbits, s));
+  hipLaunchKernelGGL(k_brick_inv, dim3(blocks_for(bg.ne, 4096)), dim3(kBlock), 0, s, (const int *)v2, (long long)bg.ne,
+                     tinv);
+  hipLaunchKernelGGL(k_brick_trec, dim3(blocks_for(bg.ne, 4096)), dim3(kBlock), 0, s, bg, (const int *)v2,
+                     (const int *)vinv, (const int *)tinv, (int4 *)c->brk_rec.p);
+  HIPCK(c, hipGetLastError());
+  return 1;
+}
+
 static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const uint8_t *pclass, double *met_out,
                       double *const *fields_out, int *elem_out, int8_t *hit_out) {
   Bg bg = c->bg;
@@ -1013,6 +1069,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   HIPCK(c, hipEventRecord(c->ev[EV_ORDER], sb));
 
   // ---- surface branch (second stream, after the order): seeds, k_bdy
+  if (c->srf_solo) HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_PREP], 0));
   HIPCK(c, hipEventRecord(c->ev[EV_BDY0], sb));
   if (bg.nt > 0) {
     hipLaunchKernelGGL(k_seed_srf, dim3(blocks_for(bg.nt, 4096)), dim3(kBlock), 0, sb, bg, (const Frame *)fr, sgrid,
@@ -1027,6 +1084,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   }
   HIPCK(c, hipEventRecord(c->ev[EV_BDY1], sb));
 
+  if (c->brick > 0 && !brick_renumber(c, s, bg, S, fr, g)) return 0;
   HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_ORDER], 0));
   HIPCK(c, hipEventRecord(c->ev[EV_VOL0], s));
   // ---- volume (main stream): walk + exact test + interpolation in one
