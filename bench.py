@@ -413,26 +413,41 @@ def renumbered_timing(ctx, args, w, step_bg, q_xyz, q_pc, d_mo, d_fo, d_elem, d_
     return res
 
 
-def surface_solo(ctx, step_bg, q_xyz, q_pc, d_mo, d_fo, d_elem, d_hit, reps: int = 5) -> dict:
+def surface_solo(ctx, step_bg, q_xyz, q_pc, d_mo, d_fo, d_elem, d_hit, device: int, reps: int = 5) -> dict:
     """The surface branch (k_seed_srf + k_bdy + its fallbacks, second
     stream) timed alone: the same call with every volume point marked
-    skipped, so nothing runs beside it (in the step it overlaps the volume
-    kernel, and its event span then includes queueing behind that kernel's
-    blocks)."""
+    skipped.  Two figures: as in the step (the branch starts beside the seed
+    grid kernels of the main stream and shares the GPU with them), and with
+    the GPU to itself (a second context with the test-only
+    PMMG_HIP_SRFSOLO=1: the branch waits for the seed grid).  In the full
+    step it overlaps the volume kernel."""
+    from parmmg_amd.transfer import TransferContext
     pc = np.where(q_pc == 2, 2, 0).astype(np.uint8)
     d_pc = ctx.upload(pc)
-    ms_bdy, ms_tot = [], []
-    for r in range(reps + 1):
-        step_bg()
-        ctx.locate_interp(q_xyz, d_pc, d_mo, d_fo, d_elem, d_hit, sync=False)
-        st = ctx.sync()
-        if r:
-            ms_bdy.append(st.ms_bdy)
-            ms_tot.append(st.ms_total)
+
+    def run(c):
+        ms_bdy, ms_tot = [], []
+        for r in range(reps + 1):
+            step_bg(c)
+            c.locate_interp(q_xyz, d_pc, d_mo, d_fo, d_elem, d_hit, sync=False)
+            st = c.sync()
+            if r:
+                ms_bdy.append(st.ms_bdy)
+                ms_tot.append(st.ms_total)
+        return st, round(float(np.median(ms_bdy)), 4), round(float(np.median(ms_tot)), 4)
+
+    st, beside, call = run(ctx)
+    os.environ["PMMG_HIP_SRFSOLO"] = "1"
+    try:
+        with TransferContext(device) as c2:
+            _, alone, _ = run(c2)
+    finally:
+        os.environ.pop("PMMG_HIP_SRFSOLO", None)
     d_pc.free()
-    return {"what": "surface branch alone (volume points skipped): HIP events of the surface stream",
-            "surface_points": int(st.nbdy), "ms_surface_branch": round(float(np.median(ms_bdy)), 4),
-            "ms_call": round(float(np.median(ms_tot)), 4)}
+    return {"what": "surface branch alone (volume points skipped): HIP events of the surface stream; "
+                    "ms_surface_branch with the GPU to itself, ms_beside_seed_grid as it starts in the step",
+            "surface_points": int(st.nbdy), "ms_surface_branch": alone, "ms_beside_seed_grid": beside,
+            "ms_call": call}
 
 
 def graded_leg(args, rank: int, budget_s: float = 60.0) -> dict:
@@ -600,12 +615,13 @@ def main():
         d_elem = ctx.empty((nq,), np.int32)
     d_hit = ctx.empty((nq,), np.int8)
 
-    def step_bg():
+    def step_bg(c=None):
+        c = ctx if c is None else c
         if args.layout == "tet8":
-            ctx.set_background_tet8(d_xyz, d_tet8, d_triv, d_adjt, w.hausd)
+            c.set_background_tet8(d_xyz, d_tet8, d_triv, d_adjt, w.hausd)
         else:
-            ctx.set_background(d_xyz, d_tetv, d_adja, d_triv, d_adjt, w.hausd)
-        ctx.set_solutions(d_met, d_f)
+            c.set_background(d_xyz, d_tetv, d_adja, d_triv, d_adjt, w.hausd)
+        c.set_solutions(d_met, d_f)
 
     def step():
         step_bg()
@@ -726,7 +742,7 @@ def main():
             out["host_mode"] = {"error": str(e)}
     if world == 1 and not split and not args.no_surface_solo:
         try:
-            out["surface_solo"] = surface_solo(ctx, step_bg, d_qxyz, q_pc, d_mo, d_fo, d_elem, d_hit)
+            out["surface_solo"] = surface_solo(ctx, step_bg, d_qxyz, q_pc, d_mo, d_fo, d_elem, d_hit, local)
         except Exception as e:  # reported, never fatal to the bench line
             out["surface_solo"] = {"error": str(e)}
     if not args.no_shuffled and world == 1 and not split:
