@@ -52,7 +52,7 @@ namespace {
 // ---------------------------------------------------------------- slot layouts
 
 typedef void (*VolFn)(Bg, const Frame *, const unsigned long long *, int, const double *, const uint8_t *,
-                      const int *, const double *, int, ContEntry *, DevStats *, Slots, int *, int8_t *, int);
+                      const int *, const double *, int, ContEntry *, DevStats *, Slots, int *, int8_t *, int, int);
 
 struct LayoutEntry {
   int c[6];
@@ -100,8 +100,10 @@ bool packed_supported(int met_size, int nfield, const int *fsize) {
   return pick_layout(S) != nullptr;
 }
 
-// the query order the host decided (after k_reset cleared the stats): read
-// by the volume kernel
+// test-only PMMG_HIP_SETORDER=1: the query order also written to the stats
+// by a one-thread kernel on the main stream, as up to r03ad (the volume
+// kernel now takes it as an argument: one launch less between the seed grid
+// and the volume kernel)
 __global__ void k_set_order(DevStats *st, int sorted, int bits) {
   st->sorted = sorted;
   st->bin_bits = bits;
@@ -144,6 +146,8 @@ struct pmmg_hip_ctx {
   // PMMG_HIP_BRICK (measurement only, pmmg_brick.hpp): the background renumbered by bricks
   DevBuf brk_k, brk_k2, brk_v, brk_v2, brk_vinv, brk_tinv, brk_xq, brk_xyz, brk_sol, brk_rec, brk_tmp;
   int brick = 0;
+  int set_order = 0; // test-only PMMG_HIP_SETORDER=1 (see k_set_order)
+  int cur_sorted = 0; // the query order of the last call (stats)
   int srf_solo = 0; // test-only PMMG_HIP_SRFSOLO=1: the surface branch waits for the seed grid (its cost alone)
   DevBuf qs;                              // volume query coordinates in processing order (Morton path)
   DevBuf cls_cnt;                         // per-block class counts (surface list compaction)
@@ -519,6 +523,7 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   c->verbose = env_int("PMMG_HIP_VERBOSE", 0);
   c->brick = env_int("PMMG_HIP_BRICK", 0);
   c->srf_solo = env_int("PMMG_HIP_SRFSOLO", 0);
+  c->set_order = env_int("PMMG_HIP_SETORDER", 0);
   c->maxstep = env_int("PMMG_HIP_MAXSTEP", c->maxstep);
   c->fanmax = env_int("PMMG_HIP_FANMAX", c->fanmax);
   c->bg.fanmax = c->fanmax; // every kernel's Bg copy carries it
@@ -1041,7 +1046,8 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     sorted = c->h_sorted[0];
     bits = c->h_sorted[1];
   }
-  hipLaunchKernelGGL(k_set_order, dim3(1), dim3(1), 0, s, st, sorted, bits);
+  c->cur_sorted = sorted;
+  if (c->set_order) hipLaunchKernelGGL(k_set_order, dim3(1), dim3(1), 0, s, st, sorted, bits);
   if (sorted && np_new > 0) {
     hipLaunchKernelGGL(k_bin_keys, dim3(blocks_for(np_new, 1024)), dim3(kBlock), 0, sb, xyz_new, pclass, np_new,
                        (const Frame *)fr, bits, (unsigned *)c->bkeys.p, (int *)c->bvals.p, st);
@@ -1092,7 +1098,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   hipLaunchKernelGGL(vol_fn, dim3((np_new + 63) / 64), dim3(64), 0, s, bg, (const Frame *)fr,
                      (const unsigned long long *)grid, g, xyz_new, pclass, (const int *)order_v,
                      c->bin_qs ? (const double *)c->qs.p : nullptr, np_new,
-                     (ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->filter_steps);
+                     (ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->filter_steps, sorted);
   HIPCK(c, hipEventRecord(c->ev[EV_WALK], s));
   hipLaunchKernelGGL(k_vol_walk_exact, dim3(8 * 64), dim3(64), 0, s, bg, xyz_new, (int *)c->fb_vol.p,
                      (const ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->maxstep);
@@ -1122,7 +1128,7 @@ static int collect_stats(pmmg_hip_ctx *c, pmmg_hip_stats *out) {
     if (pt.stepmax > stepmax) stepmax = pt.stepmax;
   }
   memset(out, 0, sizeof(*out));
-  out->nvol = h.sorted ? (int64_t)h.nvol : (int64_t)cnt[kCntVolQueries];
+  out->nvol = c->cur_sorted ? (int64_t)h.nvol : (int64_t)cnt[kCntVolQueries];
   out->nbdy = h.nbdy;
   out->nvol_walk = (int64_t)cnt[PMMG_HIT_VOL_WALK];
   out->nvol_exhaust = (int64_t)cnt[PMMG_HIT_VOL_EXHAUST];
@@ -1139,7 +1145,7 @@ static int collect_stats(pmmg_hip_ctx *c, pmmg_hip_stats *out) {
   out->steps_total = (int64_t)steps;
   out->stepmax = (int64_t)stepmax;
   out->wave_iters = (int64_t)cnt[kCntWaveIters];
-  out->sorted = h.sorted;
+  out->sorted = c->cur_sorted;
   out->nvol_noseed = (int64_t)cnt[kCntNoSeed];
   out->nvol_stuck = (int64_t)cnt[kCntStuck];
   out->nvol_limit = (int64_t)cnt[kCntLimit];

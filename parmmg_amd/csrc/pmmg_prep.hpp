@@ -592,7 +592,7 @@ constexpr int kBinBitsCoherent = 5; // 32^3 cells for a mostly coherent numberin
 // local numbering runs do not count; a shuffled numbering has almost every
 // distance at the scale of the bbox).  force: 1 always Morton-bin, 0 never,
 // -1 test.  Writes flag[0] (1: Morton bins) and flag[1] (their bits per
-// axis), which the host reads back; it then sets DevStats::sorted (k_set_order).
+// axis), which the host reads back and passes to the volume kernel.
 __global__ __launch_bounds__(kBlock) void k_coherence(const double *xyz, int np, int *flag, int force,
                                                       int force_bits) {
   if (force >= 0) {

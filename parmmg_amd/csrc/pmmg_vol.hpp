@@ -790,13 +790,13 @@ template <bool PK, int C0, int C1, int C2, int C3, int C4, int C5>
 __global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsigned long long *grid, int g,
                                             const double *qxyz, const uint8_t *pclass, const int *order,
                                             const double *qs, int np, ContEntry *cont, DevStats *st, Slots S,
-                                            int *elem_out, int8_t *hit_out, int filter_steps) {
+                                            int *elem_out, int8_t *hit_out, int filter_steps, int sorted_order) {
   __shared__ VolShared sh;
   bstats_init(&sh.bs);
   __syncthreads();
   const LaneSlotsF L{&sh.u.slots[__lane_id()]};
   const int i = xcd_block() * 64 + threadIdx.x;
-  const bool sorted = st->sorted != 0;
+  const bool sorted = sorted_order != 0;
   bool active;
   int ip = 0;
   if (sorted) {
