@@ -69,7 +69,11 @@ def pmc_traffic(workload: str):
     or (None, None)."""
     import glob
 
-    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_{workload}.json")))
+    def order(path):  # round, then the run tag as named: r03a .. r03z, r03aa .. r03zz
+        tag = os.path.basename(os.path.dirname(path))
+        return tag[:3], len(tag), tag
+
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_{workload}.json")), key=order)
     if not paths:
         return None, None
     try:
