@@ -148,7 +148,6 @@ struct pmmg_hip_ctx {
   int brick = 0;
   int set_order = 0; // test-only PMMG_HIP_SETORDER=1 (see k_set_order)
   int cur_sorted = 0; // the query order of the last call (stats)
-  int frame_k = 0; // test-only PMMG_HIP_FRAMEK=1: the frame finalised by its own kernel (as up to r03ai)
   int srf_solo = 0; // test-only PMMG_HIP_SRFSOLO=1: the surface branch waits for the seed grid (its cost alone)
   DevBuf qs;                              // volume query coordinates in processing order (Morton path)
   DevBuf cls_cnt;                         // per-block class counts (surface list compaction)
@@ -524,7 +523,6 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   c->verbose = env_int("PMMG_HIP_VERBOSE", 0);
   c->brick = env_int("PMMG_HIP_BRICK", 0);
   c->srf_solo = env_int("PMMG_HIP_SRFSOLO", 0);
-  c->frame_k = env_int("PMMG_HIP_FRAMEK", 0);
   c->set_order = env_int("PMMG_HIP_SETORDER", 0);
   c->maxstep = env_int("PMMG_HIP_MAXSTEP", c->maxstep);
   c->fanmax = env_int("PMMG_HIP_FANMAX", c->fanmax);
@@ -1015,8 +1013,8 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   hipLaunchKernelGGL(k_reset, dim3(blocks_for(ng > nsg ? ng : nsg, 2048)), dim3(kBlock), 0, s, fr, st, grid, ng,
                      sgrid, nsg);
   hipLaunchKernelGGL(k_bbox, dim3(blocks_for(bg.np / c->bbox_stride + 1, 256)), dim3(kBlock), 0, s, bg.xyz, bg.np, fr,
-                     c->bbox_stride, c->frame_k ? -1 : g, gs, gb);
-  if (c->frame_k) hipLaunchKernelGGL(k_frame_final, dim3(1), dim3(1), 0, s, fr, g, gs, gb);
+                     c->bbox_stride);
+  hipLaunchKernelGGL(k_frame_final, dim3(1), dim3(1), 0, s, fr, g, gs, gb);
   hipLaunchKernelGGL(k_axis_hist, dim3(kHistBlocks), dim3(kBlock), 0, s, bg.xyz, bg.np, (const Frame *)fr,
                      c->hist_stride, (int *)c->axh.p);
   hipLaunchKernelGGL(k_axis_map, dim3(3), dim3(kBlock), 0, s, (const int *)c->axh.p, fr, g);

@@ -124,7 +124,7 @@ struct Frame {
   double inv_vol[3], inv_srf[3], inv_bin[3];
   double qc[3], qs; // fixed-point frame of the walk's vertex copy
   int adaptive;     // bit d: axis d of the volume seed grid follows map[d]
-  unsigned bbox_done; // k_bbox blocks finished (the last one finalises the frame)
+  int pad;
   float map[3][kMapBins + 1]; // map[d][b] = share of the vertices below bin b's lower edge
 };
 
@@ -174,7 +174,6 @@ __global__ __launch_bounds__(kBlock) void k_reset(Frame *fr, DevStats *st, unsig
       fr->key_hi[d] = 0ULL;
     }
     fr->adaptive = 0;
-    fr->bbox_done = 0u;
     unsigned int *w = reinterpret_cast<unsigned int *>(st);
     for (size_t j = 0; j < sizeof(DevStats) / 4; j++) w[j] = 0u;
   }
@@ -191,12 +190,7 @@ __global__ __launch_bounds__(kBlock) void k_reset(Frame *fr, DevStats *st, unsig
 // of the first and last vertex: the frame only sizes the seed / bin grids,
 // whose cell lookups clamp, so a sampled bbox costs at most slightly longer
 // walks for the few points outside it
-__device__ void frame_final(Frame *fr, int g, int gs, int gb);
-
-// g, gs, gb >= 0: the last block to finish also finalises the frame (one
-// launch less before the seed grid; PMMG_HIP_FRAMEK=1: k_frame_final instead)
-__global__ __launch_bounds__(kBlock) void k_bbox(const double *xyz, int np, Frame *fr, int stride, int g, int gs,
-                                                 int gb) {
+__global__ __launch_bounds__(kBlock) void k_bbox(const double *xyz, int np, Frame *fr, int stride) {
   __shared__ unsigned long long slo[3][kBlock / 64], shi[3][kBlock / 64];
   unsigned long long lo[3] = {~0ULL, ~0ULL, ~0ULL}, hi[3] = {0ULL, 0ULL, 0ULL};
   const long long ns = ((long long)np + stride - 1) / stride + 2;
@@ -238,24 +232,12 @@ __global__ __launch_bounds__(kBlock) void k_bbox(const double *xyz, int np, Fram
     atomicMin(&fr->key_lo[d], a);
     atomicMax(&fr->key_hi[d], b);
   }
-  if (g >= 0) {
-    __shared__ int last;
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0) last = atomicAdd(&fr->bbox_done, 1u) == gridDim.x - 1;
-    __syncthreads();
-    if (last && threadIdx.x == 0) {
-      __threadfence();
-      frame_final(fr, g, gs, gb);
-    }
-  }
 }
 
-__device__ void frame_final(Frame *fr, int g, int gs, int gb) {
+__global__ void k_frame_final(Frame *fr, int g, int gs, int gb) {
   double emax = 0.0;
   for (int d = 0; d < 3; d++) {
-    double lo = dunkey(__hip_atomic_load(&fr->key_lo[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    double hi = dunkey(__hip_atomic_load(&fr->key_hi[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    double lo = dunkey(fr->key_lo[d]), hi = dunkey(fr->key_hi[d]);
     double ext = hi - lo;
     fr->lo[d] = lo;
     fr->ext[d] = ext;
@@ -267,8 +249,6 @@ __device__ void frame_final(Frame *fr, int g, int gs, int gb) {
   }
   fr->qs = emax > 0.0 ? kQuantHalf / (0.625 * emax) : 1.0;
 }
-
-__global__ void k_frame_final(Frame *fr, int g, int gs, int gb) { frame_final(fr, g, gs, gb); }
 
 // ---------------------------------------------------------------- volume seed grid
 //
