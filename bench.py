@@ -420,38 +420,25 @@ def renumbered_timing(ctx, args, w, step_bg, q_xyz, q_pc, d_mo, d_fo, d_elem, d_
 def surface_solo(ctx, step_bg, q_xyz, q_pc, d_mo, d_fo, d_elem, d_hit, device: int, reps: int = 5) -> dict:
     """The surface branch (k_seed_srf + k_bdy + its fallbacks, second
     stream) timed alone: the same call with every volume point marked
-    skipped.  Two figures: as in the step (the branch starts beside the seed
-    grid kernels of the main stream and shares the GPU with them), and with
-    the GPU to itself (a second context with the test-only
-    PMMG_HIP_SRFSOLO=1: the branch waits for the seed grid).  In the full
-    step it overlaps the volume kernel."""
-    from parmmg_amd.transfer import TransferContext
+    skipped, the branch starting beside the seed grid kernels of the main
+    stream as in the step (the figure with the GPU to itself needs the
+    measurement build: tools/surface_solo.py).  In the full step it overlaps
+    the volume kernel."""
     pc = np.where(q_pc == 2, 2, 0).astype(np.uint8)
     d_pc = ctx.upload(pc)
-
-    def run(c):
-        ms_bdy, ms_tot = [], []
-        for r in range(reps + 1):
-            step_bg(c)
-            c.locate_interp(q_xyz, d_pc, d_mo, d_fo, d_elem, d_hit, sync=False)
-            st = c.sync()
-            if r:
-                ms_bdy.append(st.ms_bdy)
-                ms_tot.append(st.ms_total)
-        return st, round(float(np.median(ms_bdy)), 4), round(float(np.median(ms_tot)), 4)
-
-    st, beside, call = run(ctx)
-    os.environ["PMMG_HIP_SRFSOLO"] = "1"
-    try:
-        with TransferContext(device) as c2:
-            _, alone, _ = run(c2)
-    finally:
-        os.environ.pop("PMMG_HIP_SRFSOLO", None)
+    ms_bdy, ms_tot = [], []
+    for r in range(reps + 1):
+        step_bg(ctx)
+        ctx.locate_interp(q_xyz, d_pc, d_mo, d_fo, d_elem, d_hit, sync=False)
+        st = ctx.sync()
+        if r:
+            ms_bdy.append(st.ms_bdy)
+            ms_tot.append(st.ms_total)
     d_pc.free()
-    return {"what": "surface branch alone (volume points skipped): HIP events of the surface stream; "
-                    "ms_surface_branch with the GPU to itself, ms_beside_seed_grid as it starts in the step",
-            "surface_points": int(st.nbdy), "ms_surface_branch": alone, "ms_beside_seed_grid": beside,
-            "ms_call": call}
+    return {"what": "surface branch alone (volume points skipped): HIP events of the surface stream, "
+                    "starting beside the seed grid as in the step",
+            "surface_points": int(st.nbdy), "ms_beside_seed_grid": round(float(np.median(ms_bdy)), 4),
+            "ms_call": round(float(np.median(ms_tot)), 4)}
 
 
 def graded_leg(args, rank: int, budget_s: float = 60.0) -> dict:

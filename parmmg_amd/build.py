@@ -25,6 +25,9 @@ INC = os.path.join(ROOT, "include")
 ORACLE = os.path.join(ROOT, "oracle")
 
 HIP_SO = os.path.join(PKG, "libpmmg_hip.so")
+# the measurement build (-DPMMG_HIP_MEASURE: the A/B switches of tools/, never
+# linked by the host layer or loaded by the tests; PMMG_HIP_SO selects it)
+HIP_MEASURE_SO = os.path.join(PKG, "libpmmg_hip_measure.so")
 HOST_SO = os.path.join(PKG, "libpmmg_host.so")
 SYNTH_SO = os.path.join(PKG, "libpmmg_synth.so")
 ORACLE_SO = os.path.join(ORACLE, "liboracle.so")
@@ -54,20 +57,22 @@ def _stale(out: str, deps: list[str]) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_hip(force: bool = False) -> str:
+def build_hip(force: bool = False, measure: bool = False) -> str:
+    out = HIP_MEASURE_SO if measure else HIP_SO
     src = os.path.join(CSRC, "pmmg_hip.hip")
     snap = os.path.join(CSRC, "pmmg_snapshot.hip")
     qual = os.path.join(CSRC, "pmmg_quality.hip")
     deps = [src, snap, qual, os.path.join(INC, "parmmg_hip.h"), __file__] + [
         os.path.join(CSRC, h) for h in ("pmmg_device.hpp", "pmmg_prep.hpp", "pmmg_vol.hpp", "pmmg_bdy.hpp",
-                                        "pmmg_fallback.hpp", "pmmg_snapshot.hpp", "pmmg_quality.hpp")]
-    if force or _stale(HIP_SO, deps):
+                                        "pmmg_fallback.hpp", "pmmg_snapshot.hpp", "pmmg_quality.hpp",
+                                        "pmmg_brick.hpp")]
+    if force or _stale(out, deps):
         # max-memory-clause scheduling: the gathers of a step issued as clauses
         # (volume kernel -4.6 % at cfg4, same registers; profiles/r02e/sweep_sched_strategy.txt)
         _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-mllvm", "-amdgpu-sched-strategy=max-memory-clause",
-              "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
-              f"-I{INC}", "-o", HIP_SO, src, snap, qual])
-    return HIP_SO
+              "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared"] + (["-DPMMG_HIP_MEASURE"] if measure else []) +
+             [f"-I{INC}", "-o", out, src, snap, qual])
+    return out
 
 
 def build_host(force: bool = False) -> str:
@@ -118,7 +123,12 @@ def build_c_test(force: bool = False) -> str:
 
 
 def build_all(force: bool = False) -> None:
-    build_hip(force)
+    from concurrent.futures import ThreadPoolExecutor
+
+    with ThreadPoolExecutor(2) as ex:  # the two HIP builds side by side (hipcc is single-threaded)
+        jobs = [ex.submit(build_hip, force), ex.submit(build_hip, force, True)]
+        for j in jobs:
+            j.result()
     build_host(force)
     build_synth(force)
     build_oracle(force)

@@ -38,7 +38,9 @@
 
 #include "pmmg_device.hpp"
 #include "pmmg_prep.hpp"
-#include "pmmg_brick.hpp"
+#ifdef PMMG_HIP_MEASURE
+#include "pmmg_brick.hpp" // measurement build only
+#endif
 #include "pmmg_vol.hpp"
 #include "pmmg_bdy.hpp"
 #include "pmmg_fallback.hpp"
@@ -100,14 +102,16 @@ bool packed_supported(int met_size, int nfield, const int *fsize) {
   return pick_layout(S) != nullptr;
 }
 
-// test-only PMMG_HIP_SETORDER=1: the query order also written to the stats
-// by a one-thread kernel on the main stream, as up to r03ad (the volume
-// kernel now takes it as an argument: one launch less between the seed grid
-// and the volume kernel)
+#ifdef PMMG_HIP_MEASURE
+// measurement build, PMMG_HIP_SETORDER=1: the query order also written to
+// the stats by a one-thread kernel on the main stream, as up to r03ad (the
+// volume kernel now takes it as an argument: one launch less between the seed
+// grid and the volume kernel)
 __global__ void k_set_order(DevStats *st, int sorted, int bits) {
   st->sorted = sorted;
   st->bin_bits = bits;
 }
+#endif
 
 } // namespace
 
@@ -510,26 +514,31 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
     pmmg_hip_destroy(c);
     return nullptr;
   }
-  c->tpc = env_int("PMMG_HIP_TPC", c->tpc);
-  c->seed_lanes = std::min(4, env_int("PMMG_HIP_SEEDLANES", c->seed_lanes));
-  c->bbox_stride = env_int("PMMG_HIP_BBOX", c->bbox_stride);
-  c->hist_stride = env_int("PMMG_HIP_HIST", c->hist_stride);
-  c->srf_mult = env_int("PMMG_HIP_SRFMULT", c->srf_mult);
-  c->srf_g = env_int("PMMG_HIP_SRFG", 0);
-  c->bdy_dyn = env_int("PMMG_HIP_BDYDYN", 2) == 1;
-  c->bdy_bpx = env_int("PMMG_HIP_BDYBPX", c->bdy_bpx);
+  // documented options, each clamped to its valid range
+  c->tpc = std::min(4096, env_int("PMMG_HIP_TPC", c->tpc));
+  c->srf_mult = std::min(4096, env_int("PMMG_HIP_SRFMULT", c->srf_mult));
   c->bin_bits = std::min(7, env_int("PMMG_HIP_BINBITS", c->bin_bits));
-  c->bin_qs = env_int("PMMG_HIP_BINQS", 2) == 1;
   c->verbose = env_int("PMMG_HIP_VERBOSE", 0);
-  c->brick = env_int("PMMG_HIP_BRICK", 0);
-  c->srf_solo = env_int("PMMG_HIP_SRFSOLO", 0);
-  c->set_order = env_int("PMMG_HIP_SETORDER", 0);
   c->maxstep = env_int("PMMG_HIP_MAXSTEP", c->maxstep);
+  // test-only path selection (tests/test_gpu_hits.py, tests/test_gpu_parity.py)
   c->fanmax = env_int("PMMG_HIP_FANMAX", c->fanmax);
+  c->srf_g = std::min(1024, env_int("PMMG_HIP_SRFG", 0));
   c->bg.fanmax = c->fanmax; // every kernel's Bg copy carries it
   c->filter_steps = c->filter_steps < c->maxstep ? c->filter_steps : c->maxstep;
   if (const char *e = getenv("PMMG_HIP_FILTER_STEPS"))
     if (*e && atoi(e) >= 0) c->filter_steps = atoi(e);
+#ifdef PMMG_HIP_MEASURE
+  // A/B switches of the measurement build (libpmmg_hip_measure.so, tools/)
+  c->seed_lanes = std::min(4, env_int("PMMG_HIP_SEEDLANES", c->seed_lanes));
+  c->bbox_stride = env_int("PMMG_HIP_BBOX", c->bbox_stride);
+  c->hist_stride = env_int("PMMG_HIP_HIST", c->hist_stride);
+  c->bdy_dyn = env_int("PMMG_HIP_BDYDYN", 2) == 1;
+  c->bdy_bpx = env_int("PMMG_HIP_BDYBPX", c->bdy_bpx);
+  c->bin_qs = env_int("PMMG_HIP_BINQS", 2) == 1;
+  c->brick = env_int("PMMG_HIP_BRICK", 0);
+  c->srf_solo = env_int("PMMG_HIP_SRFSOLO", 0);
+  c->set_order = env_int("PMMG_HIP_SETORDER", 0);
+#endif
   return c;
 }
 
@@ -887,7 +896,7 @@ static void launch_bdy_fallbacks(pmmg_hip_ctx *c, hipStream_t s, const Slots &S,
                      (const int *)c->bbest.p, (const int *)c->bcidx.p, S, elem_out, hit_out);
 }
 
-// the pipeline on device pointers; enqueues only (no host synchronisation)
+#ifdef PMMG_HIP_MEASURE
 // PMMG_HIP_BRICK=b: the background renumbered by bricks of b^3 seed cells
 // (measurement only: pmmg_brick.hpp); the results go nowhere
 static int brick_renumber(pmmg_hip_ctx *c, hipStream_t s, const Bg &bg, const Slots &S, const Frame *fr, int g) {
@@ -935,7 +944,12 @@ static int brick_renumber(pmmg_hip_ctx *c, hipStream_t s, const Bg &bg, const Sl
   HIPCK(c, hipGetLastError());
   return 1;
 }
+#endif
 
+// The pipeline of one call on device pointers.  It enqueues its kernels on
+// the context's two streams; in auto order mode it reads one flag back (the
+// coherence test's, pinned, while the main stream builds the seed grid) to
+// choose between the Morton binning and the input-order compaction.
 static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const uint8_t *pclass, double *met_out,
                       double *const *fields_out, int *elem_out, int8_t *hit_out) {
   Bg bg = c->bg;
@@ -1047,7 +1061,9 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     bits = c->h_sorted[1];
   }
   c->cur_sorted = sorted;
+#ifdef PMMG_HIP_MEASURE
   if (c->set_order) hipLaunchKernelGGL(k_set_order, dim3(1), dim3(1), 0, s, st, sorted, bits);
+#endif
   if (sorted && np_new > 0) {
     hipLaunchKernelGGL(k_bin_keys, dim3(blocks_for(np_new, 1024)), dim3(kBlock), 0, sb, xyz_new, pclass, np_new,
                        (const Frame *)fr, bits, (unsigned *)c->bkeys.p, (int *)c->bvals.p, st);
@@ -1090,7 +1106,9 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   }
   HIPCK(c, hipEventRecord(c->ev[EV_BDY1], sb));
 
+#ifdef PMMG_HIP_MEASURE
   if (c->brick > 0 && !brick_renumber(c, s, bg, S, fr, g)) return 0;
+#endif
   HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_ORDER], 0));
   HIPCK(c, hipEventRecord(c->ev[EV_VOL0], s));
   // ---- volume (main stream): walk + exact test + interpolation in one

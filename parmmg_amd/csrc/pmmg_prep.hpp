@@ -124,7 +124,7 @@ struct Frame {
   double inv_vol[3], inv_srf[3], inv_bin[3];
   double qc[3], qs; // fixed-point frame of the walk's vertex copy
   int adaptive;     // bit d: axis d of the volume seed grid follows map[d]
-  int pad;
+  int seed_any;     // the lowest in-use tetra the seed grid sampled (INT_MAX: none): the last-resort seed
   float map[3][kMapBins + 1]; // map[d][b] = share of the vertices below bin b's lower edge
 };
 
@@ -174,6 +174,7 @@ __global__ __launch_bounds__(kBlock) void k_reset(Frame *fr, DevStats *st, unsig
       fr->key_hi[d] = 0ULL;
     }
     fr->adaptive = 0;
+    fr->seed_any = INT_MAX;
     unsigned int *w = reinterpret_cast<unsigned int *>(st);
     for (size_t j = 0; j < sizeof(DevStats) / 4; j++) w[j] = 0u;
   }
@@ -263,9 +264,13 @@ __global__ void k_frame_final(Frame *fr, int g, int gs, int gb) {
 constexpr int kSeedRun = 4;
 constexpr unsigned long long kSeedIdMask = (1ULL << 29) - 1; // ids below 2^29 (the adja encoding's limit)
 
-__global__ __launch_bounds__(kBlock) void k_seed_vol(Bg bg, const Frame *fr, unsigned long long *cell, int g,
+__global__ __launch_bounds__(kBlock) void k_seed_vol(Bg bg, Frame *fr, unsigned long long *cell, int g,
                                                      long long nsamp, int lanes) {
   constexpr int R = kSeedRun;
+  __shared__ int smin;
+  if (threadIdx.x == 0) smin = INT_MAX;
+  __syncthreads();
+  int kmin = INT_MAX;
   const long long nruns = (nsamp + R - 1) / R;
   const long long quads = bg.ne / 4;
   const long long nthreads = nruns * R;
@@ -327,7 +332,15 @@ __global__ __launch_bounds__(kBlock) void k_seed_vol(Bg bg, const Frame *fr, uns
       }
     }
     if (leader) atomicMin(&cell[ci], best);
+    if (ci >= 0 && k < kmin) kmin = k;
   }
+  for (int o = 32; o > 0; o >>= 1) {
+    const int u = __shfl_down(kmin, o);
+    kmin = u < kmin ? u : kmin;
+  }
+  if (__lane_id() == 0 && kmin != INT_MAX) atomicMin(&smin, kmin);
+  __syncthreads();
+  if (threadIdx.x == 0 && smin != INT_MAX) atomicMin(&fr->seed_any, smin);
 }
 
 // rare path of seed_vol (the 8 cells are empty): lowest seed id in the shells
@@ -355,7 +368,8 @@ __device__ __noinline__ int seed_vol_ring(const unsigned long long *cell, int g,
   return 0;
 }
 
-__device__ __forceinline__ int seed_vol(const unsigned long long *cell, int g, const Frame *fr, const double *x) {
+__device__ __forceinline__ int seed_vol(const unsigned long long *cell, int g, const Frame *fr, const double *x,
+                                        bool &noseed) {
   // the query's position in cell units; candidate cells: its own and the 7
   // neighbours of the octant it lies in; the seed whose (quantised) centroid
   // is nearest wins (ties: lower id)
@@ -390,12 +404,18 @@ __device__ __forceinline__ int seed_vol(const unsigned long long *cell, int g, c
       bid = id;
     }
   }
+  noseed = false;
   if (bid != 0xFFFFFFFFu) return (int)bid;
-  // no seed within kSeedRing cells: the walk starts at tetra 1 (a long walk,
-  // or the exhaustive search if it gets stuck, costs less than sending the
-  // query straight to the O(ne) search)
+  // rare: the 8 cells are empty; the lowest seed of the shells around them
   const int r = seed_vol_ring(cell, g, c[0], c[1], c[2]);
-  return r ? r : 1;
+  if (r) return r;
+  // no seed within kSeedRing cells (counted as nvol_noseed): the walk starts
+  // from the lowest in-use tetra the grid sampled (a long walk, or the
+  // exhaustive search if it gets stuck, costs less than sending the query
+  // straight to the O(ne) search); 0 (the exhaustive search) when the grid
+  // sampled no tetra in use
+  noseed = true;
+  return fr->seed_any != INT_MAX ? fr->seed_any : 0;
 }
 
 // ---------------------------------------------------------------- surface seeds and node -> tria CSR

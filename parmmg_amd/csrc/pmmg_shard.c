@@ -111,7 +111,11 @@ int pmmg_shard_mark(int np, const double *xyz, int ne, const int *tetv, const do
       if (th[d] < lo[d] || tl[d] > hi[d]) meets = 0;
     tet_map[k] = meets;
     if (meets)
-      for (int i = 0; i < 4; i++) vert_map[v[i] - 1] = 1; /* every writer stores 1 */
+      for (int i = 0; i < 4; i++) {
+        /* several threads may mark one vertex: atomic stores (all store 1) */
+#pragma omp atomic write
+        vert_map[v[i] - 1] = 1;
+      }
   }
   if (bad) return 0;
   counts[0] = number_marks(tet_map, ne);
@@ -175,7 +179,11 @@ int pmmg_shard_mark_cells(int np, const double *xyz, int ne, const int *tetv, co
     }
     tet_map[k] = meets;
     if (meets)
-      for (int i = 0; i < 4; i++) vert_map[v[i] - 1] = 1; /* every writer stores 1 */
+      for (int i = 0; i < 4; i++) {
+        /* several threads may mark one vertex: atomic stores (all store 1) */
+#pragma omp atomic write
+        vert_map[v[i] - 1] = 1;
+      }
   }
   if (bad) return 0;
   counts[0] = number_marks(tet_map, ne);

@@ -291,12 +291,18 @@ struct LaneSlotsD {
 // north_star's bit-exact class) lands in its tetra whatever the path
 // (cfgG: 1 point in 3.9M otherwise).  The neighbour across the face of the
 // smallest coordinate is checked with the reference's own arithmetic.
-__device__ __noinline__ void prefer_strict(const Bg &bg, const double *x, const int4 &ad, int &k, VolLoc *loc) {
+// (inlined: as an out-of-line call its pointer arguments kept the caller's
+// locals in scratch memory, 208 B per lane of k_vol_walk_exact in r03)
+__device__ __forceinline__ void prefer_strict(const Bg &bg, const double *x, const int4 &ad, int &k, VolLoc *loc) {
   if (min4(loc->phi) > kEps) return;
-  int f = 0;
+  int f = 0; // the first smallest coordinate (compile-time indices only: phi stays in registers)
+  double mn = loc->phi[0];
 #pragma unroll
   for (int j = 1; j < 4; j++)
-    if (loc->phi[j] < loc->phi[f]) f = j;
+    if (loc->phi[j] < mn) {
+      mn = loc->phi[j];
+      f = j;
+    }
   const int nb = sel4(ad, f) >> 2;
   if (nb == 0) return;
   const int4 tn = tetv_row(bg, nb);
@@ -391,7 +397,6 @@ __global__ __launch_bounds__(64) void k_vol_walk_exact(Bg bg, const double *qxyz
     const bool fail = active && status != 1;
     const int slot = wave_append(&st->nfb_vol, fail);
     if (fail) fb[slot] = ip;
-    wave_count(&bs, kCntNoSeed, fail && status == 0);
     wave_count(&bs, kCntStuck, fail && status == 2);
     wave_count(&bs, kCntLimit, fail && status == 3);
     wave_stats(&bs, active, status == 1 ? PMMG_HIT_VOL_WALK : 0, steps);
@@ -810,11 +815,12 @@ __global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsign
   int status = 0, steps = 0, k = 0;
   double x[3];
   int4 tv = make_int4(1, 1, 1, 1);
+  bool noseed = false;
   if (active) {
     // streamed once: non-temporal (Morton order: the binning's coordinate
     // copy in processing order when it made one, else the query's own row)
     load_pt_nt(sorted && qs ? qs : qxyz, sorted && qs ? i + 1 : ip, x);
-    k = seed_vol(grid, g, fr, x);
+    k = seed_vol(grid, g, fr, x, noseed);
     if (k == 0) {
       status = 2;
     } else {
@@ -865,6 +871,7 @@ __global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsign
   wave_stats(&sh.bs, active, acc ? PMMG_HIT_VOL_WALK : 0, steps);
   wave_count(&sh.bs, kCntVolQueries, active);
   wave_count(&sh.bs, kCntExact, more);
+  wave_count(&sh.bs, kCntNoSeed, active && noseed);
   // 3. interpolation
   const Sink snk{!sorted, (size_t)(i - __lane_id()), ip};
   if (__any(acc)) {

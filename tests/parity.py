@@ -46,8 +46,9 @@ def make_case(kind=synth.CUBE, n_old=6, n_new=7, metric=synth.F_ANI,
 
 
 def run_gpu(case, sort=None, ctx=None, tet8=False, packed=False, env=None):
-    """env: PMMG_HIP_* settings read when the context is created (test-only
-    path selection, e.g. PMMG_HIP_STAGE=3: the staged Morton path)."""
+    """env: PMMG_HIP_* settings read when the context is created (documented
+    options and test-only path selection, e.g. PMMG_HIP_BINBITS=7: the fine
+    Morton cells auto mode picks for a numbering without coherence)."""
     import os
     bg, new = case["bg"], case["new"]
     own = ctx is None
@@ -119,6 +120,51 @@ def run_dev(ctx, bg, new_xyz, met, fields, pc, hausd, separate=False, packed=Fal
             if b is not None:
                 b.free()
     return out
+
+
+def invmat_failure_case():
+    """A 4-cell cube whose tensors make MMG5_invmat return 0 on every path
+    the reference has for it (rows then left untouched):
+      * vertex tensors u u^T (u = (1, 2, 3): off-diagonals >= MMG5_EPS, det
+        exactly 0) at the interior vertex (3,3,3) and the boundary vertex
+        (0,2,2): the inversion of a vertex tensor fails — interp4bar_ani
+        (src/interpmesh_pmmg.c:258-259) for volume points in its tetra,
+        interp3bar_ani (:177-178) for surface face hits, interp2bar (:98-99)
+        for surface edge hits;
+      * the edge (1,1,1)-(2,1,1) and the boundary edge (1,3,0)-(2,3,0) carry
+        the tensors 0.5 J - I and I (J = all ones; both invert exactly in
+        binary), and a new point sits on each edge's midpoint, where the
+        coordinates are exactly (1/2, 1/2, 0, ...): every vertex inverts, but
+        mint = 1/2 (J - I) + 1/2 I = 1/2 J is singular and the final inversion
+        fails (:107 edge, :187 face, :267 volume).
+    The same tensors go into the metric and into the tensor field."""
+    case = make_case(kind=synth.CUBE, n_old=4, n_new=5, metric=synth.F_ANI,
+                     fields=(synth.F_SCALAR, synth.F_VECTOR, synth.F_TENSOR),
+                     with_ref=False)
+    bg, new = case["bg"], case["new"]
+
+    def vid(i, j, k):  # the cube lattice's vertex numbering (n = 4: 5 per row)
+        v = 1 + i + 5 * j + 25 * k
+        assert np.allclose(bg.xyz[v - 1], np.array([i, j, k]) / 4.0)
+        return v
+
+    J = np.array([1.0, 1.0, 1.0, 1.0, 1.0, 1.0])  # m11 m12 m13 m22 m23 m33
+    I3 = np.array([1.0, 0.0, 0.0, 1.0, 0.0, 1.0])
+    rank1 = np.array([1.0, 2.0, 3.0, 4.0, 6.0, 9.0])  # (1,2,3)(1,2,3)^T
+    special = {vid(3, 3, 3): rank1, vid(0, 2, 2): rank1,
+               vid(1, 1, 1): 0.5 * J - I3, vid(2, 1, 1): I3,
+               vid(1, 3, 0): 0.5 * J - I3, vid(2, 3, 0): I3}
+    for v, t in special.items():
+        case["met"][v - 1] = t
+        case["fields"][2][v - 1] = t
+    # one volume point and one surface point moved onto the two edge midpoints
+    pc = case["pclass"]
+    vol = int(np.nonzero(pc == 1)[0][0])
+    srf = int(np.nonzero((pc == 2) & (new.xyz[:, 2] == 0.0))[0][0])
+    new.xyz[vol] = (0.375, 0.25, 0.25)
+    new.xyz[srf] = (0.375, 0.75, 0.0)
+    case["B"] = O.Background(bg, case["met"], case["fields"], case["hausd"])
+    return case, vol, srf
 
 
 def _same(a, b):

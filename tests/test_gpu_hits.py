@@ -154,3 +154,59 @@ def test_surface_walks_from_one_far_seed(monkeypatch, kind, n_old, n_new):
     assert st["stepmax"] > 10
     if kind == synth.SHELL:
         assert st["nbdy_exhaust"] > 0
+
+
+def two_cubes_case():
+    """Two 16-cell cubes far apart ([0,1]^3 and [10,11]^3) whose tetra 1 is
+    unused (v = 0, its neighbours' adjacency cleared, as MMG leaves a deleted
+    tetra), new points in both cubes, and one volume query at (0, 11, 0):
+    no background tetra within 6 seed cells of it in either the uniform or
+    the quantile-mapped seed grid.  Its walk starts from the lowest in-use
+    tetra the seed grid sampled (never from the unused tetra 1), gets stuck
+    on the cube's boundary, and ends in the exhaustive search: the closest
+    tetra (code 3)."""
+    import dataclasses
+    a = synth.lattice(synth.CUBE, 16)
+    off = a.np
+    ne = a.ne
+    xyz = np.vstack([a.xyz, a.xyz + 10.0])
+    tetv = np.vstack([a.tetv, a.tetv + off]).astype(np.int32)
+    adja = np.vstack([a.adja, np.where(a.adja > 0, a.adja + 4 * ne, 0)]).astype(np.int32)
+    triv = np.vstack([a.triv, a.triv + off]).astype(np.int32)
+    adjt = np.vstack([a.adjt, np.where(a.adjt > 0, a.adjt + 3 * a.nt, 0)]).astype(np.int32)
+    tetv[0] = 0
+    adja[0] = 0
+    adja[(adja >> 2) == 1] = 0
+    bg = dataclasses.replace(a, xyz=xyz, tetv=tetv, adja=adja, triv=triv, adjt=adjt,
+                             isbdy=np.concatenate([a.isbdy, a.isbdy]))
+    b = synth.lattice(synth.CUBE, 5, jitter=0.2, with_trias=False, with_tetra=False)
+    far = np.array([[0.0, 11.0, 0.0]])
+    nxyz = np.vstack([b.xyz, b.xyz + 10.0, far])
+    isbdy = np.concatenate([b.isbdy, b.isbdy, [0]]).astype(np.uint8)
+    new = dataclasses.replace(b, xyz=nxyz, isbdy=isbdy)
+    pc = np.where(isbdy == 1, 2, 1).astype(np.uint8)
+    met = synth.solution(synth.F_ANI, xyz)
+    fs = [synth.solution(synth.F_SCALAR, xyz), synth.solution(synth.F_TENSOR, xyz)]
+    B = O.Background(bg, met, fs, 0.01)
+    # no oracle run: the reference's own walk cannot start on an unused tetra
+    # 1 (src/locate_pmmg.c:795-811 spins to step > ne, then takes the
+    # "closest" tetra 0); check() still verifies every point's acceptance and
+    # values against the oracle's element tests, which skip unused tetra
+    return dict(bg=bg, new=new, met=met, fields=fs, pclass=pc, B=B, hausd=0.01)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [dict(), dict(sort=True), dict(tet8=True)])
+def test_unused_tetra_one_and_empty_seed_neighbourhood(mode):
+    """The last-resort seed of a query with an empty seed neighbourhood is
+    a sampled tetra in use, not tetra 1 (tetra 1 unused made the
+    walk read vertex 0, before the start of the coordinate arrays)."""
+    case = two_cubes_case()
+    gpu = run_gpu(case, **mode)
+    rep = check(case, gpu)
+    st = gpu["stats"]
+    print(rep, {k: st[k] for k in ("nvol", "nvol_noseed", "nvol_exhaust", "nvol_closest", "nvol_stuck")})
+    assert rep["n"] == case["new"].np and rep["class_i"] == rep["class_i_same"]
+    assert st["nvol_noseed"] >= 1
+    assert (gpu["hit"][-1] & 15) == 3
+    assert O.first_accepting_tetra(case["B"], case["new"].xyz[-1]) == 0

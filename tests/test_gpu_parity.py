@@ -5,7 +5,7 @@ contract is documented in tests/parity.py."""
 import numpy as np
 import pytest
 
-from parity import check, make_case, run_gpu
+from parity import check, invmat_failure_case, make_case, run_gpu
 from parmmg_amd import synth
 
 C, S = synth.CUBE, synth.SHELL
@@ -79,18 +79,30 @@ def test_fallback_paths_outside_domain(mode):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["auto", "morton-fine"])
-def test_invmat_failure_leaves_rows_untouched(mode):
-    """MMG5_invmat failure (zero tensor) -> the output row is not written
-    (src/interpmesh_pmmg.c:258-267)."""
-    case = make_case(kind=C, n_old=4, n_new=5, metric=synth.F_ANI, fields=(synth.F_TENSOR,), with_ref=False)
-    case["met"][:40] = 0.0
-    from oracle import oracle as O
-    case["B"] = O.Background(case["bg"], case["met"], case["fields"], case["hausd"])
+@pytest.mark.parametrize("mode", ["auto", "morton-fine", "packed"])
+def test_invmat_failures_leave_rows_untouched(mode):
+    """Every MMG5_invmat failure path of the reference's interpolators
+    leaves the output row untouched (src/interpmesh_pmmg.c:98-107, 177-187,
+    258-267): the oracle's rows stay at their NaN sentinel exactly where
+    invmat returned 0, and the GPU's rows are identical (check() compares
+    every point bit for bit, NaN with NaN)."""
+    case, vol, srf = invmat_failure_case()
     gpu = run_gpu(case, **MODES[mode])
     rep = check(case, gpu)
-    assert np.isnan(gpu["met"]).any(), "expected untouched rows"
-    print(rep)
+    print(rep, gpu["stats"])
+    skip = case["pclass"] == 0
+    met_nan = np.isnan(gpu["met"]).all(axis=1) & ~skip
+    ten_nan = np.isnan(gpu["fields"][2]).all(axis=1) & ~skip
+    assert met_nan.sum() > 2 and ten_nan.sum() > 2
+    for f in gpu["fields"][:2]:  # scalar and vector fields never fail
+        assert not np.isnan(f[~skip]).any()
+    # the final inversion's failure at both midpoints (volume and surface edge)
+    assert met_nan[vol] and ten_nan[vol] and met_nan[srf] and ten_nan[srf]
+    code = gpu["hit"].astype(np.int32) & 15
+    assert code[vol] == 1 and code[srf] == 5  # VOL_WALK, BDY_EDGE
+    # the vertex-tensor failures reach volume, surface-face and surface-edge hits
+    for h in (1, 4, 5):
+        assert (met_nan & (code == h)).any(), h
 
 
 @pytest.mark.gpu

@@ -196,3 +196,37 @@ def test_threaded_driver_matches_sequential():
     np.testing.assert_array_equal(seq["met"][same], mt["met"][same])
     for a, b in zip(seq["fields"], mt["fields"]):
         np.testing.assert_array_equal(a[same], b[same])
+
+
+def test_invmat_failure_case_on_the_oracle():
+    """tests/parity.invmat_failure_case on the oracle alone: every failure
+    path of MMG5_invmat is reached and leaves its rows at the NaN sentinel
+    (src/interpmesh_pmmg.c:98-107, 177-187, 258-267) — the case the GPU test
+    test_invmat_failures_leave_rows_untouched compares against."""
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    from parity import check, invmat_failure_case
+
+    case, vol, srf = invmat_failure_case()
+    new, pc = case["new"], case["pclass"]
+    out = O.run(case["B"], new.xyz, pc, synth.visit_order(new), O.MODE_FRESH)
+    skip = pc == 0
+    met_nan = np.isnan(out["met"]).all(axis=1) & ~skip
+    ten_nan = np.isnan(out["fields"][2]).all(axis=1) & ~skip
+    assert met_nan.sum() > 2 and ten_nan.sum() > 2
+    for f in out["fields"][:2]:
+        assert not np.isnan(f[~skip]).any()
+    assert met_nan[vol] and ten_nan[vol] and met_nan[srf] and ten_nan[srf]
+    assert out["hit"][vol] == 1 and out["hit"][srf] == 5
+    for h in (1, 4, 5):
+        assert (met_nan & (out["hit"] == h)).any(), h
+    # the final inversion fails although every vertex tensor inverts
+    for i in (vol, srf):
+        k = int(out["elem"][i])
+        vv = case["bg"].tetv[k - 1] if out["hit"][i] == 1 else case["bg"].triv[k - 1]
+        for v in vv:
+            assert O.invmat(case["met"][v - 1])[0]
+    # the oracle's own run meets the contract check() applies to the GPU
+    hit = out["hit"].astype(np.int32) | (np.maximum(out["loc"], 0).astype(np.int32) << 4)
+    rep = check(case, dict(met=out["met"], fields=out["fields"], elem=out["elem"], hit=hit.astype(np.int8)))
+    assert rep["n"] == int((~skip).sum()) and rep["exact"] == rep["n"]

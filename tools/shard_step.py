@@ -14,6 +14,9 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+# the measurement build of the module (its PMMG_HIP_* A/B switches; the same
+# kernels as the product library otherwise)
+os.environ.setdefault("PMMG_HIP_SO", os.path.join(ROOT, "parmmg_amd", "libpmmg_hip_measure.so"))
 
 import bench  # noqa: E402
 from parmmg_amd import configs, ranks, shard  # noqa: E402
