@@ -98,7 +98,8 @@ typedef struct {
   float ms_fallback;     /* exhaustive / closest kernels of the volume queries */
   float ms_total;        /* whole call, first to last event */
   float ms_vol_locate;   /* the volume walk kernel alone (part of ms_vol) */
-  int64_t nvol_noseed;   /* volume queries without a seed (empty seed-grid neighbourhood) */
+  int64_t nvol_noseed;   /* volume queries with no seed within 6 seed-grid cells: walked from the lowest
+                            in-use tetra the grid sampled */
   int64_t nvol_stuck;    /* exact volume walks stuck (no eligible neighbour) -> exhaustive */
   int64_t nvol_limit;    /* exact volume walks stopped at maxstep -> exhaustive */
   int64_t seed_map_axes; /* bit d: axis d of the volume seed grid followed the vertex quantiles */

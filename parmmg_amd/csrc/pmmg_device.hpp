@@ -124,6 +124,27 @@ __device__ __forceinline__ int xcd_block() {
   return base + (b >> 3);
 }
 
+// The same in runs of G logical blocks dealt round-robin over the XCDs
+// (G <= 0: xcd_block's contiguous eighths): each XCD still walks spatially
+// adjacent queries within a run, but a costly stretch of the input (the
+// appended points of an Mmg-like numbering, the last sixth of the range) is
+// shared by all eight XCDs instead of landing on one or two of them while the
+// others idle (r04a: 15.0 -> 10.7 resident waves per CU).  Bijective for any n.
+__device__ __forceinline__ int xcd_block_runs(int G) {
+  if (G <= 0) return xcd_block();
+  const int b = blockIdx.x, n = gridDim.x;
+  const int x = b & 7, j = b >> 3;      // the j-th block dispatched to XCD x
+  const int nruns = (n + G - 1) / G;     // runs of G logical blocks (the last one short)
+  const int full = n / (8 * G);          // rounds in which every XCD takes a whole run
+  if (j < full * G) return ((j / G) * 8 + x) * G + j % G;
+  // the tail: the remaining n - 8 G full blocks, in contiguous eighths
+  const int base = 8 * G * full, m = n - base;
+  const int q = m >> 3, r = m & 7;
+  const int jj = j - full * G;
+  (void)nruns;
+  return base + (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + jj;
+}
+
 // Grid-stride iteration over [0, n) split into 8 contiguous chunks, one per
 // XCD (blockIdx % 8), for kernels launched with a fixed grid (a multiple of 8).
 // iters is uniform across a block, so wave-collective code may run per iteration.

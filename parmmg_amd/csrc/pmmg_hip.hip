@@ -54,7 +54,8 @@ namespace {
 // ---------------------------------------------------------------- slot layouts
 
 typedef void (*VolFn)(Bg, const Frame *, const unsigned long long *, int, const double *, const uint8_t *,
-                      const int *, const double *, int, ContEntry *, DevStats *, Slots, int *, int8_t *, int, int);
+                      const int *, const double *, int, ContEntry *, DevStats *, Slots, int *, int8_t *, int, int,
+                      int, int, int);
 
 struct LayoutEntry {
   int c[6];
@@ -199,6 +200,12 @@ struct pmmg_hip_ctx {
   int maxstep = 4096; // longer walks go to the exact continuation / exhaustive kernels (PMMG_HIP_MAXSTEP; the
                       // reference caps at ne)
   int fanmax = kFanMax;    // cone fans longer than this take the O(nt) scan (test-only PMMG_HIP_FANMAX)
+  int dma = 1;           // k_vol's interpolation gathers by LDS DMA (measurement build: PMMG_HIP_DMA=0 keeps
+                         // the register-staged gathers)
+  int pad = 0;           // measurement build, PMMG_HIP_PAD: extra VALU / L1 work per walk step (k_vol)
+  int xcd_run = 64;      // k_vol's blocks dealt to the XCDs in runs of 64 (4096 queries) instead of contiguous
+                         // eighths: r04c at cfg4, volume kernel 3.80 -> 3.50 ms, Mmg-like numbering 5.83 -> 4.14 ms
+                         // (measurement build: PMMG_HIP_XCDRUN, 0 = eighths)
   int filter_steps = 64; // step cap of the fp32 filter walk (then the exact fp64 walk continues from where it
                          // stopped: a query the filter misjudges hands over early instead of cycling through a
                          // 4-entry history for up to maxstep steps); test-only PMMG_HIP_FILTER_STEPS=0 sends every
@@ -538,6 +545,10 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   c->brick = env_int("PMMG_HIP_BRICK", 0);
   c->srf_solo = env_int("PMMG_HIP_SRFSOLO", 0);
   c->set_order = env_int("PMMG_HIP_SETORDER", 0);
+  if (const char *e = getenv("PMMG_HIP_XCDRUN"))
+    if (*e && atoi(e) >= 0) c->xcd_run = atoi(e);
+  c->pad = env_int("PMMG_HIP_PAD", 0);
+  if (const char *e = getenv("PMMG_HIP_DMA")) c->dma = atoi(e) != 0;
 #endif
   return c;
 }
@@ -1048,8 +1059,9 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
                      (const Frame *)fr, (int *)c->xq.p);
   {
     const long long nsamp = ng < bg.ne ? ng : bg.ne;
-    hipLaunchKernelGGL(k_seed_vol, dim3((blocks_for(nsamp, 8192) + 7) & ~7), dim3(kBlock), 0, s, bg, fr, grid, g,
-                       nsamp, c->seed_lanes);
+    // one thread per run of 4 sampled tetra
+    hipLaunchKernelGGL(k_seed_vol, dim3((blocks_for((nsamp + kSeedRun - 1) / kSeedRun, 8192) + 7) & ~7), dim3(kBlock), 0,
+                       s, bg, fr, grid, g, nsamp, c->seed_lanes);
   }
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[EV_PREP], s));
@@ -1116,7 +1128,8 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   hipLaunchKernelGGL(vol_fn, dim3((np_new + 63) / 64), dim3(64), 0, s, bg, (const Frame *)fr,
                      (const unsigned long long *)grid, g, xyz_new, pclass, (const int *)order_v,
                      c->bin_qs ? (const double *)c->qs.p : nullptr, np_new,
-                     (ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->filter_steps, sorted);
+                     (ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->filter_steps, sorted, c->xcd_run,
+                     c->pad, c->dma);
   HIPCK(c, hipEventRecord(c->ev[EV_WALK], s));
   hipLaunchKernelGGL(k_vol_walk_exact, dim3(8 * 64), dim3(64), 0, s, bg, xyz_new, (int *)c->fb_vol.p,
                      (const ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->maxstep);

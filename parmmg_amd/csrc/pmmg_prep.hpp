@@ -158,8 +158,27 @@ __device__ __forceinline__ int quant(double x, const Frame *fr, int d) {
   return __double2int_rn(t);
 }
 
+// Two vertices per thread when xyz is 16-byte aligned: three 16-byte loads
+// and three 8-byte stores (the lanes of a wave stream 3 KiB in, 1.5 KiB out)
+// instead of six single-double loads and six int stores
 __global__ __launch_bounds__(kBlock) void k_quantize(const double *xyz, long long np, const Frame *fr, int *xq) {
-  for (long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x; j < 3 * np; j += (long long)gridDim.x * blockDim.x)
+  const long long nth = (long long)gridDim.x * blockDim.x;
+  if (kXqStride == 3 && ((uintptr_t)xyz & 15) == 0 && ((uintptr_t)xq & 7) == 0) {
+    const long long npair = np / 2;
+    for (long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x; j < npair; j += nth) {
+      const ntd2 *src = reinterpret_cast<const ntd2 *>(xyz) + 3 * j;
+      const ntd2 a = __builtin_nontemporal_load(src), b = __builtin_nontemporal_load(src + 1),
+                 c = __builtin_nontemporal_load(src + 2);
+      int2 *dst = reinterpret_cast<int2 *>(xq) + 3 * j;
+      dst[0] = make_int2(quant(a.x, fr, 0), quant(a.y, fr, 1));
+      dst[1] = make_int2(quant(b.x, fr, 2), quant(b.y, fr, 0));
+      dst[2] = make_int2(quant(c.x, fr, 1), quant(c.y, fr, 2));
+    }
+    if (blockIdx.x == 0 && threadIdx.x < 3 && (np & 1))
+      xq[3 * (np - 1) + threadIdx.x] = quant(xyz[3 * (np - 1) + threadIdx.x], fr, (int)threadIdx.x);
+    return;
+  }
+  for (long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x; j < 3 * np; j += nth)
     xq[kXqStride * (j / 3) + j % 3] = quant(__builtin_nontemporal_load(xyz + j), fr, (int)(j % 3));
 }
 
@@ -264,6 +283,14 @@ __global__ void k_frame_final(Frame *fr, int g, int gs, int gb) {
 constexpr int kSeedRun = 4;
 constexpr unsigned long long kSeedIdMask = (1ULL << 29) - 1; // ids below 2^29 (the adja encoding's limit)
 
+// One thread per run of 4 consecutive tetra (one 128-byte line of packed
+// records): the run's 4 records, then their 16 vertex rows, are all in flight
+// before the first key is computed (r04: one sample per lane took ~6 loop
+// trips of two dependent loads each), the 4 keys are combined in the thread
+// and each distinct cell gets one atomicMin.  The cell position comes from
+// the fixed-point vertex sum in one multiply-add per axis (Frame::sa, sb:
+// the uniform map folded with the fixed-point frame); an axis with a
+// quantile map (Frame::adaptive) goes through seed_pos.
 __global__ __launch_bounds__(kBlock) void k_seed_vol(Bg bg, Frame *fr, unsigned long long *cell, int g,
                                                      long long nsamp, int lanes) {
   constexpr int R = kSeedRun;
@@ -273,41 +300,72 @@ __global__ __launch_bounds__(kBlock) void k_seed_vol(Bg bg, Frame *fr, unsigned 
   int kmin = INT_MAX;
   const long long nruns = (nsamp + R - 1) / R;
   const long long quads = bg.ne / 4;
-  const long long nthreads = nruns * R;
   // XCD-aware: the blocks of XCD x (blockIdx % 8; gridDim is a multiple of
-  // 8) sweep one contiguous eighth of the samples, so the vertex rows shared
-  // by neighbouring tetra are fetched into one L2, not eight
-  const long long per = (nthreads + 8LL * kBlock - 1) / (8LL * kBlock) * kBlock;
-  const long long lo = (blockIdx.x & 7) * per, hi = lo + per < nthreads ? lo + per : nthreads;
+  // 8) take one contiguous eighth of the runs, so the vertex rows shared by
+  // neighbouring tetra are fetched into one L2, not eight
+  const long long per = (nruns + 8LL * kBlock - 1) / (8LL * kBlock) * kBlock;
+  const long long lo = (blockIdx.x & 7) * per, hi = lo + per < nruns ? lo + per : nruns;
   const long long bstride = (long long)(gridDim.x >> 3) * blockDim.x;
-  for (long long s0 = lo + (blockIdx.x >> 3) * (long long)blockDim.x; s0 < hi; s0 += bstride) {
-    const long long s = s0 + threadIdx.x;
-    const long long run = s / R;
-    const int r = (int)(s % R);
+  const int adaptive = fr->adaptive;
+  double sa[3], sb[3];
+#pragma unroll
+  for (int d = 0; d < 3; d++) {
+    sa[d] = (fr->qc[d] - fr->lo[d]) * fr->inv_vol[d];
+    sb[d] = 0.25 * fr->inv_vol[d] / fr->qs;
+  }
+  for (long long run = lo + (blockIdx.x >> 3) * (long long)blockDim.x + threadIdx.x; run < hi; run += bstride) {
     const long long base = 4 * ((run * quads) / (nruns > 0 ? nruns : 1)); // a cache line of tet8 records
-    const int k = (int)(1 + base + r);
-    bool ok = s < hi && k <= bg.ne && r < lanes; // `lanes` of the run's 4 records are sampled
-    int4 tv = make_int4(0, 0, 0, 0);
-    if (ok) {
-      const nti4 rr =
-          __builtin_nontemporal_load(reinterpret_cast<const nti4 *>(bg.tetv + (size_t)(k - 1) * bg.tstride));
-      tv = make_int4(rr.x, rr.y, rr.z, rr.w);
-      ok = tv.x > 0;
+    int4 tv[R];
+    bool ok[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const int k = (int)(1 + base + r);
+      ok[r] = k <= bg.ne && r < lanes; // `lanes` of the run's 4 records are sampled
+      tv[r] = make_int4(0, 0, 0, 0);
+      if (ok[r]) {
+        const nti4 rr =
+            __builtin_nontemporal_load(reinterpret_cast<const nti4 *>(bg.tetv + (size_t)(k - 1) * bg.tstride));
+        tv[r] = make_int4(rr.x, rr.y, rr.z, rr.w);
+      }
     }
-    unsigned long long key = ~0ULL;
-    long long ci = -1;
-    if (ok) {
-      // centroid from the fixed-point copy (12-byte rows)
-      const int *q0 = bg.xq + kXqStride * (size_t)(tv.x - 1), *q1 = bg.xq + kXqStride * (size_t)(tv.y - 1);
-      const int *q2 = bg.xq + kXqStride * (size_t)(tv.z - 1), *q3 = bg.xq + kXqStride * (size_t)(tv.w - 1);
-      double p[3];
-      for (int d = 0; d < 3; d++)
-        p[d] = fr->qc[d] + 0.25 * ((double)q0[d] + (double)q1[d] + (double)q2[d] + (double)q3[d]) / fr->qs;
+    long long sq[R][3]; // 64-bit: clamped coordinates (+-2^30) of vertices outside the sampled frame
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      ok[r] = ok[r] && tv[r].x > 0;
+#pragma unroll
+      for (int d = 0; d < 3; d++) sq[r][d] = 0;
+      if (ok[r]) {
+        const int *q0 = bg.xq + kXqStride * (size_t)(tv[r].x - 1), *q1 = bg.xq + kXqStride * (size_t)(tv[r].y - 1);
+        const int *q2 = bg.xq + kXqStride * (size_t)(tv[r].z - 1), *q3 = bg.xq + kXqStride * (size_t)(tv[r].w - 1);
+        int a0[3], a1[3], a2[3], a3[3];
+#pragma unroll
+        for (int d = 0; d < 3; d++) {
+          a0[d] = q0[d];
+          a1[d] = q1[d];
+          a2[d] = q2[d];
+          a3[d] = q3[d];
+        }
+#pragma unroll
+        for (int d = 0; d < 3; d++) sq[r][d] = ((long long)a0[d] + a1[d]) + ((long long)a2[d] + a3[d]);
+      }
+    }
+    unsigned long long key[R];
+    long long ci[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      key[r] = ~0ULL;
+      ci[r] = -1;
+      if (!ok[r]) continue;
+      const int k = (int)(1 + base + r);
       int c[3];
       unsigned long long off = 0;
       float d2 = 0.f;
+#pragma unroll
       for (int d = 0; d < 3; d++) {
-        const double t = seed_pos(fr, d, p[d], g);
+        // the centroid's position in cells: uniform axes in one multiply-add
+        // on the fixed-point sum (exact in fp64), mapped axes through seed_pos
+        double t = sa[d] + sb[d] * (double)sq[r][d];
+        if ((adaptive >> d) & 1) t = seed_pos(fr, d, fr->qc[d] + 0.25 * (double)sq[r][d] / fr->qs, g);
         c[d] = seed_cell(t, g);
         float f = (float)(t - c[d]);
         f = f < 0.f ? 0.f : (f > 0.999f ? 0.999f : f);
@@ -315,24 +373,24 @@ __global__ __launch_bounds__(kBlock) void k_seed_vol(Bg bg, Frame *fr, unsigned 
         d2 += (f - 0.5f) * (f - 0.5f);
       }
       const unsigned q8 = d2 * 340.f < 255.f ? (unsigned)(d2 * 340.f) : 255u;
-      key = ((unsigned long long)q8 << 56) | (off << 29) | (unsigned)k;
-      ci = c[0] + (long long)g * (c[1] + (long long)g * c[2]);
+      key[r] = ((unsigned long long)q8 << 56) | (off << 29) | (unsigned)k;
+      ci[r] = c[0] + (long long)g * (c[1] + (long long)g * c[2]);
+      kmin = k < kmin ? k : kmin;
     }
-    // combine within the run: the first lane of each distinct cell issues
-    // the atomic with the run's minimum for that cell
-    const int lane = __lane_id(), g0 = lane - r;
-    bool leader = ci >= 0;
-    unsigned long long best = key;
-    for (int o = 0; o < R; o++) {
-      const long long co = __shfl(ci, g0 + o);
-      const unsigned long long ko = __shfl(key, g0 + o);
-      if (co == ci && ci >= 0) {
-        best = ko < best ? ko : best;
-        if (o < r) leader = false;
+    // the run's keys combined per distinct cell: one atomic per cell
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      if (ci[r] < 0) continue;
+      bool first = true;
+      unsigned long long best = key[r];
+#pragma unroll
+      for (int o = 0; o < R; o++) {
+        if (o == r || ci[o] != ci[r]) continue;
+        if (o < r) first = false;
+        best = key[o] < best ? key[o] : best;
       }
+      if (first) atomicMin(&cell[ci[r]], best);
     }
-    if (leader) atomicMin(&cell[ci], best);
-    if (ci >= 0 && k < kmin) kmin = k;
   }
   for (int o = 32; o > 0; o >>= 1) {
     const int u = __shfl_down(kmin, o);

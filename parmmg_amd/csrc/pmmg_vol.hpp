@@ -161,6 +161,22 @@ __device__ __forceinline__ int4 next_slots(const int4 &m, const int4 &tv, const 
   return mn;
 }
 
+// The same on a packed slot map (2 bits per local vertex: slot of local l =
+// bits 2l..2l+1), the fp32 filter walk's form: a lookup is one bit-field
+// extract instead of a select chain
+__device__ __forceinline__ unsigned pslot(unsigned m, int l) { return (m >> (2 * l)) & 3u; }
+__device__ __forceinline__ unsigned next_slots_packed(unsigned m, const int4 &tv, const int4 &tn, int f, int iopp) {
+  const unsigned sf = pslot(m, f);
+  const int ids[4] = {tn.x, tn.y, tn.z, tn.w};
+  unsigned mn = 0u;
+#pragma unroll
+  for (int l = 0; l < 4; l++) {
+    const unsigned s = l == iopp ? sf : pslot(m, idx_in(ids[l], tv));
+    mn |= s << (2 * l);
+  }
+  return mn;
+}
+
 // ---------------------------------------------------------------- fp32 filter walk
 //
 // The walk itself only has to reach the accepting tetra; the reference's
@@ -186,15 +202,18 @@ __device__ __forceinline__ int4 next_slots(const int4 &m, const int4 &tv, const 
 // for a walk whose steps are two dependent gathers each.
 constexpr float kFilterMargin = 1.220703125e-4f; // 2^-13
 
+// (an address-space-3 pointer: the slot offsets are 32-bit LDS arithmetic;
+// through a generic pointer they were 64-bit multiply-adds)
+typedef __attribute__((address_space(3))) float lds_float;
 struct LaneSlotsF { // this lane's view of the wave's slot image [slot*3 + dim][64]
-  float *base;
+  lds_float *base;
   __device__ __forceinline__ void put(int slot, const float *q) const {
 #pragma unroll
-    for (int d = 0; d < 3; d++) base[(slot * 3 + d) * 64] = q[d];
+    for (int d = 0; d < 3; d++) base[(unsigned)(slot * 3 + d) * 64u] = q[d];
   }
   __device__ __forceinline__ void get(int slot, float *q) const {
 #pragma unroll
-    for (int d = 0; d < 3; d++) q[d] = base[(slot * 3 + d) * 64];
+    for (int d = 0; d < 3; d++) q[d] = base[(unsigned)(slot * 3 + d) * 64u];
   }
 };
 
@@ -214,22 +233,54 @@ __device__ __forceinline__ void rel_pt(const int *xq, int v, const int *xqq, flo
   }
 }
 
+// The filter's arithmetic needs no particular rounding (its margin is ~100x
+// its error, and every accepted tetra passes the reference's exact test), so
+// it takes fused multiply-adds: fewer VALU instructions per step (the module is
+// built with -ffp-contract=off for the fp64 paths; fmaf is explicit)
 __device__ __forceinline__ void cross3(const float *a, const float *b, float *c) {
-  c[0] = a[1] * b[2] - a[2] * b[1];
-  c[1] = a[2] * b[0] - a[0] * b[2];
-  c[2] = a[0] * b[1] - a[1] * b[0];
+  c[0] = __builtin_fmaf(a[1], b[2], -(a[2] * b[1]));
+  c[1] = __builtin_fmaf(a[2], b[0], -(a[0] * b[2]));
+  c[2] = __builtin_fmaf(a[0], b[1], -(a[1] * b[0]));
 }
-__device__ __forceinline__ float dot3(const float *a, const float *b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+__device__ __forceinline__ float dot3(const float *a, const float *b) {
+  return __builtin_fmaf(a[0], b[0], __builtin_fmaf(a[1], b[1], a[2] * b[2]));
+}
+
+// the face the walk leaves through: the largest key among the faces with a
+// neighbour (ties: lowest face); only when that neighbour is in the visited
+// history does the full rule (pick_face) run — the same face either way
+template <typename T>
+__device__ __forceinline__ int pick_face_fast(const int4 &ad, const int *hist, const T *key, unsigned rsel) {
+  if (rsel) return pick_face_walk<T>(ad, hist, key, rsel);
+  int f = -1;
+  T best = 0;
+#pragma unroll
+  for (int ff = 0; ff < 4; ff++) {
+    const int iel = sel4(ad, ff) >> 2;
+    if (iel != 0 && (f < 0 || key[ff] > best)) {
+      f = ff;
+      best = key[ff];
+    }
+  }
+  if (f >= 0) {
+    const int iel = sel4(ad, f) >> 2;
+    bool vis = false;
+#pragma unroll
+    for (int h = 0; h < kHist; h++) vis = vis || (hist[h] == iel);
+    if (vis) f = pick_face<T>(ad, hist, key);
+  }
+  return f;
+}
 
 // returns 1 candidate (filter passed), 0 moved (k, tv, ad, m, hist updated),
 // 2 stuck (no eligible neighbour)
-__device__ __forceinline__ int step_f32(const Bg &bg, const int *x, int &k, int4 &tv, int4 &ad, int4 &m, int *hist,
+__device__ __forceinline__ int step_f32(const Bg &bg, const int *x, int &k, int4 &tv, int4 &ad, unsigned &m, int *hist,
                                         const LaneSlotsF &L, unsigned rsel) {
   float q[4][3];
-  L.get(m.x, q[0]);
-  L.get(m.y, q[1]);
-  L.get(m.z, q[2]);
-  L.get(m.w, q[3]);
+  L.get(pslot(m, 0), q[0]);
+  L.get(pslot(m, 1), q[1]);
+  L.get(pslot(m, 2), q[2]);
+  L.get(pslot(m, 3), q[3]);
   float c23[3], c13[3], c12[3], s[4];
   cross3(q[2], q[3], c23);
   cross3(q[1], q[3], c13);
@@ -244,7 +295,7 @@ __device__ __forceinline__ int step_f32(const Bg &bg, const int *x, int &k, int4
   for (int f = 0; f < 4; f++) key[f] = vol < 0.f ? -s[f] : s[f];
   const float kmax = fmaxf(fmaxf(key[0], key[1]), fmaxf(key[2], key[3]));
   if (vol != 0.f && kmax < (float)(kEps + kFilterMargin) * fabsf(vol)) return 1;
-  const int f = pick_face_walk<float>(ad, hist, key, rsel);
+  const int f = pick_face_fast<float>(ad, hist, key, rsel);
   if (f < 0) return 2;
 #pragma unroll
   for (int h = kHist - 1; h > 0; h--) hist[h] = hist[h - 1];
@@ -256,8 +307,8 @@ __device__ __forceinline__ int step_f32(const Bg &bg, const int *x, int &k, int4
   ad = adja_row(bg, k);
   float qn[3];
   rel_pt(bg.xq, sel4(tn, iopp), x, qn);
-  const int sf = sel4(m, f);
-  m = next_slots(m, tv, tn, f, iopp);
+  const int sf = (int)pslot(m, f);
+  m = next_slots_packed(m, tv, tn, f, iopp);
   L.put(sf, qn);
   tv = tn;
   return 0;
@@ -517,13 +568,17 @@ __device__ __forceinline__ void sink_rows(const Slot &sl, const double *r, bool 
 //      live per lane; vertex i+1's loads are issued before vertex i's rows
 //      go through LDS (coop_issue* / coop_land*).  In input order the rows are stored as whole cache lines
 //      through the same LDS image; Morton-binned queries store per lane.
-// The walk's vertex slots and the gather image share one 3 KiB LDS buffer
-// (the phases are sequential within the wave).
+// The walk's vertex slots and the gather image share one 4 KiB LDS buffer
+// (the phases are sequential within the wave).  (r04b measured a third use —
+// an image of the wave's distinct vertices, sorted, for the exact test and the
+// interpolation: 20 % fewer L1 accesses, +23 % VALU for the sort, +10 % time;
+// profiles/r04b/unique_vertex_rows.patch.txt.)
 struct VolShared {
   BlockStats bs;
   union {
     float slots[12 * 64]; // walk: [slot*3 + dim][lane]
-    double img[8 * 64];   // interpolation: 64 rows of up to 6 doubles, or 64 x 8 doubles of packed records
+    double img[12 * 64];  // interpolation: two images of 64 rows of up to 6 doubles (LDS DMA), or one, or 64 x 8
+                          // doubles of packed records
   } u;
 };
 
@@ -579,10 +634,87 @@ __device__ __forceinline__ void coop_land3(double p0, double p1, double p2, doub
   __builtin_amdgcn_wave_barrier();
 }
 
+// The same gathers by LDS DMA (global_load_lds: each lane's piece lands in
+// the image at lane-contiguous positions without passing through VGPRs):
+// the pieces of vertex i + 1 in flight cost no registers, which takes the
+// fused kernel under the next occupancy step.  Two images per wave (vertex
+// i in one, i + 1 in the other); 16-byte pieces of 6-double rows.
+typedef __attribute__((address_space(3))) void lds_void;
+__device__ __forceinline__ void dma_issue6(const double *in, int stride, int myv, double *dst) {
+  const int lane = __lane_id();
+#pragma unroll
+  for (int t = 0; t < 3; t++) {
+    const int q = 64 * t + lane;
+    const int v = __shfl(myv, q / 3);
+    __builtin_amdgcn_global_load_lds((const void *)(in + (size_t)stride * (v - 1) + 2 * (q % 3)),
+                                     (lds_void *)(dst + 128 * t), 16, 0, 0);
+  }
+}
+// the pieces issued before the last n are in LDS (vmcnt counts loads, stores
+// and LDS DMA of the wave in issue order)
+template <int N>
+__device__ __forceinline__ void dma_wait() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+template <int C>
+__device__ __forceinline__ void dma_read(const double *img, double *row) {
+  const int lane = __lane_id();
+#pragma unroll
+  for (int j = 0; j < C; j++) row[j] = img[C * lane + j];
+  wait_lgkm();
+  __builtin_amdgcn_wave_barrier(); // every lane has read its row: the image takes the next vertex
+}
+
+template <int C> // C == 6
+__device__ __forceinline__ void vol_slot_dma(const Slot &sl, bool act, const int4 &v, const double *phi, double *img,
+                                             const Sink &k) {
+  double *ia = img, *ib = img + 384; // two 3 KiB images
+  double r[C];
+  bool ok = act;
+  if constexpr (C == 6) {
+    double mint[6], m[6], mi[6];
+#define PMMG_ACC6(i)                                                                               \
+  do {                                                                                             \
+    ok = invmat(m, mi) && ok;                                                                      \
+    _Pragma("unroll") for (int q = 0; q < 6; q++) mint[q] = (i == 0) ? phi[0] * mi[q] : mint[q] + phi[i] * mi[q]; \
+  } while (0)
+    dma_issue6(sl.in, sl.istride, v.x, ia);
+    dma_issue6(sl.in, sl.istride, v.y, ib);
+    dma_wait<3>();
+    dma_read<6>(ia, m);
+    PMMG_ACC6(0);
+    dma_issue6(sl.in, sl.istride, v.z, ia);
+    dma_wait<3>();
+    dma_read<6>(ib, m);
+    PMMG_ACC6(1);
+    dma_issue6(sl.in, sl.istride, v.w, ib);
+    dma_wait<3>();
+    dma_read<6>(ia, m);
+    PMMG_ACC6(2);
+    dma_wait<0>();
+    dma_read<6>(ib, m);
+    PMMG_ACC6(3);
+    ok = invmat(mint, r) && ok;
+#undef PMMG_ACC6
+  }
+  sink_rows<C>(sl, r, ok, img, k);
+}
+
 // one slot of the wave's queries: rows gathered, interpolated, stored
 template <int C>
 __device__ __forceinline__ void vol_slot(const Slot &sl, bool act, const int4 &v, const double *phi, double *img,
-                                         const Sink &k) {
+                                         const Sink &k, bool dma) {
+  if constexpr (C == 6) { // (12-byte DMA pieces land 16 bytes apart: 3-double rows keep the register path)
+#ifndef PMMG_HIP_MEASURE
+    dma = true; // the product always gathers 6-double rows by DMA (the register path only for the A/B)
+#endif
+    if (dma) {
+      vol_slot_dma<C>(sl, act, v, phi, img, k);
+      return;
+    }
+  }
   if constexpr (C > 0) {
     double r[C];
     bool ok = act;
@@ -792,15 +924,21 @@ __device__ __forceinline__ void vol_interp_packed(const Slots &S, bool acc, cons
 }
 
 template <bool PK, int C0, int C1, int C2, int C3, int C4, int C5>
-__global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsigned long long *grid, int g,
+#ifdef PMMG_KVOL_WAVES // measurement: the volume kernel compiled for this many waves per SIMD (spills allowed)
+#define PMMG_KVOL_OCC __attribute__((amdgpu_waves_per_eu(PMMG_KVOL_WAVES)))
+#else
+#define PMMG_KVOL_OCC
+#endif
+__global__ __launch_bounds__(64) PMMG_KVOL_OCC void k_vol(Bg bg, const Frame *fr, const unsigned long long *grid, int g,
                                             const double *qxyz, const uint8_t *pclass, const int *order,
                                             const double *qs, int np, ContEntry *cont, DevStats *st, Slots S,
-                                            int *elem_out, int8_t *hit_out, int filter_steps, int sorted_order) {
+                                            int *elem_out, int8_t *hit_out, int filter_steps, int sorted_order,
+                                            int xcd_run, int pad, int dma) {
   __shared__ VolShared sh;
   bstats_init(&sh.bs);
   __syncthreads();
-  const LaneSlotsF L{&sh.u.slots[__lane_id()]};
-  const int i = xcd_block() * 64 + threadIdx.x;
+  const LaneSlotsF L{(lds_float *)&sh.u.slots[__lane_id()]};
+  const int i = xcd_block_runs(xcd_run) * 64 + threadIdx.x;
   const bool sorted = sorted_order != 0;
   bool active;
   int ip = 0;
@@ -816,17 +954,44 @@ __global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsign
   double x[3];
   int4 tv = make_int4(1, 1, 1, 1);
   bool noseed = false;
+  // the queries' coordinates, streamed once (non-temporal).  In input order
+  // (and in the binning's processing-order copy) the wave's 64 rows are one
+  // contiguous 1.5 KiB block: two instructions of 16-byte pieces through LDS
+  // touch its 24 sectors once, where three per-lane double loads touched
+  // them three times
+  {
+    const double *qrow = sorted ? qs : qxyz;
+    const long long w0 = (long long)(i - __lane_id());
+    if (qrow && w0 + 64 <= (sorted ? (long long)st->nvol : (long long)np) && ((uintptr_t)qrow & 15) == 0) {
+      const ntd2 *src = reinterpret_cast<const ntd2 *>(qrow + 3 * w0);
+      ntd2 *dst = reinterpret_cast<ntd2 *>(sh.u.slots);
+      const int lane = __lane_id();
+      const ntd2 a = __builtin_nontemporal_load(src + lane);
+      ntd2 b = {0.0, 0.0};
+      if (lane < 32) b = __builtin_nontemporal_load(src + 64 + lane);
+      dst[lane] = a;
+      if (lane < 32) dst[64 + lane] = b;
+      wait_lgkm();
+      __builtin_amdgcn_wave_barrier();
+      const double *row = reinterpret_cast<const double *>(sh.u.slots) + 3 * lane;
+      x[0] = row[0];
+      x[1] = row[1];
+      x[2] = row[2];
+      wait_lgkm();
+      __builtin_amdgcn_wave_barrier(); // the buffer holds the walk's vertex slots next
+    } else if (active) {
+      load_pt_nt(sorted && qs ? qs : qxyz, sorted && qs ? i + 1 : ip, x);
+    }
+  }
   if (active) {
-    // streamed once: non-temporal (Morton order: the binning's coordinate
-    // copy in processing order when it made one, else the query's own row)
-    load_pt_nt(sorted && qs ? qs : qxyz, sorted && qs ? i + 1 : ip, x);
     k = seed_vol(grid, g, fr, x, noseed);
     if (k == 0) {
       status = 2;
     } else {
       const int xq[3] = {quant(x[0], fr, 0), quant(x[1], fr, 1), quant(x[2], fr, 2)};
       tv = tetv_row(bg, k);
-      int4 ad = adja_row(bg, k), m = make_int4(0, 1, 2, 3);
+      int4 ad = adja_row(bg, k);
+      unsigned m = 0xE4u; // local l in slot l
       {
         float q[3];
         rel_pt(bg.xq, tv.x, xq, q);
@@ -847,6 +1012,20 @@ __global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsign
           break;
         }
         ++steps;
+#ifdef PMMG_HIP_MEASURE
+        // measurement build, PMMG_HIP_PAD = v + 65536 t: v extra VALU
+        // instructions and t extra L1 accesses (re-loads of the current
+        // record) per walk step, to price each resource in the step
+        if (pad) {
+          float acc = (float)steps;
+          for (int j = 0; j < (pad & 0xFFFF); j++) asm volatile("v_add_f32 %0, %0, %0" : "+v"(acc));
+          int dummy = 0;
+          for (int j = 0; j < (pad >> 16); j++)
+            dummy += reinterpret_cast<const volatile int *>(bg.tetv + (size_t)(k - 1) * bg.tstride)[j & 3];
+          if (acc == -1.0f && dummy == 0x7FFFFFFF) steps += 0; // keep both chains alive
+          asm volatile("" ::"v"(acc), "v"(dummy));
+        }
+#endif
         const int r = step_f32(bg, xq, k, tv, ad, m, hist, L, walk_rsel(ip, steps));
         if (r != 0) {
           status = r;
@@ -890,12 +1069,12 @@ __global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsign
         for (int s2 = 0; s2 < S.n; s2++) interp_dyn<4>(S.s[s2], ip, vv, loc.phi);
       }
     } else {
-      vol_slot<C0>(S.s[0], acc, loc.v, loc.phi, img, snk);
-      vol_slot<C1>(S.s[1], acc, loc.v, loc.phi, img, snk);
-      vol_slot<C2>(S.s[2], acc, loc.v, loc.phi, img, snk);
-      vol_slot<C3>(S.s[3], acc, loc.v, loc.phi, img, snk);
-      vol_slot<C4>(S.s[4], acc, loc.v, loc.phi, img, snk);
-      vol_slot<C5>(S.s[5], acc, loc.v, loc.phi, img, snk);
+      vol_slot<C0>(S.s[0], acc, loc.v, loc.phi, img, snk, dma != 0);
+      vol_slot<C1>(S.s[1], acc, loc.v, loc.phi, img, snk, dma != 0);
+      vol_slot<C2>(S.s[2], acc, loc.v, loc.phi, img, snk, dma != 0);
+      vol_slot<C3>(S.s[3], acc, loc.v, loc.phi, img, snk, dma != 0);
+      vol_slot<C4>(S.s[4], acc, loc.v, loc.phi, img, snk, dma != 0);
+      vol_slot<C5>(S.s[5], acc, loc.v, loc.phi, img, snk, dma != 0);
     }
     if (acc) {
       if (sorted) { // scattered: cached stores (see wave_store_rows_scat)

@@ -82,7 +82,7 @@ def main():
             k, v = item.split("=")
             if k.lower() == "sort":  # context option: 1 Morton bins, 0 input order
                 sort = v == "1"
-            elif k.lower() in ("sol", "perm", "packed"):  # measurement only: slots / renumbering / packed records
+            elif k.lower() in ("sol", "perm", "packed", "so"):  # measurement only: slots / renumbering / packed records / build
                 pass
             else:
                 os.environ["PMMG_HIP_" + k.upper()] = v
@@ -146,8 +146,12 @@ def parent(args):
     res = {v: {} for v in variants}
     for r in range(args.rounds):
         for spec in variants:
+            env = dict(os.environ)
+            so = dict(item.split("=") for item in spec.split(",") if item).get("so")
+            if so:  # another build of the module for this variant (e.g. the previous commit's, for an A/B)
+                env["PMMG_HIP_SO"] = os.path.join(ROOT, so)
             p = subprocess.run([sys.executable, "-u", os.path.abspath(__file__), "--config", args.config, "--steps",
-                                str(args.steps), "--child", spec], stdout=subprocess.PIPE, text=True)
+                                str(args.steps), "--child", spec], stdout=subprocess.PIPE, text=True, env=env)
             line = [x for x in p.stdout.splitlines() if x.startswith("RESULT ")]
             if p.returncode != 0 or not line:
                 print(p.stdout[-2000:])
