@@ -500,6 +500,82 @@ def graded_leg(args, rank: int, budget_s: float = 60.0) -> dict:
     return out
 
 
+def groups_leg(args, ngroup: int = 10, reps: int = 5, budget_s: float = 30.0) -> dict:
+    """ParMmg's loop over a rank's groups (src/interpmesh_pmmg.c:690): ngroup
+    cfg2-size groups (own copies of the background, solutions and new points
+    in HBM, the new points jittered with their own seeds), timed as one
+    pmmg_hip_locate_interp_groups call against the same groups one
+    pmmg_hip_locate_interp each; the outputs of the groups call are checked
+    bit for bit against the per-group calls', and group 0's against an oracle
+    run (parity)."""
+    w = configs.CFG2
+    ctx = TransferContext(0)
+    gs, hosts = [], []
+    for i in range(ngroup):
+        bg, new, met, fields, pc = build_workload(w, 100 + i)
+        nq = new.np
+        gs.append(dict(xyz=ctx.upload(bg.xyz), tet8=ctx.upload(pack_tet8(bg.tetv, bg.adja)), triv=ctx.upload(bg.triv),
+                       adjt=ctx.upload(bg.adjt), hausd=w.hausd, met=ctx.upload(met),
+                       fields=[ctx.upload(f) for f in fields], xyz_new=ctx.upload(new.xyz), pclass=ctx.upload(pc),
+                       met_out=ctx.empty((nq, w.met_size), np.float64),
+                       fields_out=[ctx.empty((nq, f.shape[1]), np.float64) for f in fields],
+                       elem_out=ctx.empty((nq,), np.int32), hit_out=ctx.empty((nq,), np.int8)))
+        hosts.append((bg, new, met, fields, pc) if i == 0 else None)
+
+    def one_by_one():
+        for g in gs:
+            ctx.set_background_tet8(g["xyz"], g["tet8"], g["triv"], g["adjt"], g["hausd"])
+            ctx.set_solutions(g["met"], g["fields"])
+            ctx.locate_interp(g["xyz_new"], g["pclass"], g["met_out"], g["fields_out"], g["elem_out"], g["hit_out"],
+                              sync=False)
+
+    def download():
+        return [{"elem": g["elem_out"].download(), "hit": g["hit_out"].download(), "met": g["met_out"].download(),
+                 "fields": [f.download() for f in g["fields_out"]]} for g in gs]
+
+    def timed(fn):
+        fn()
+        ctx.sync()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        t_enq = time.perf_counter() - t0
+        ctx.sync()
+        return (time.perf_counter() - t0) / (reps * ngroup), t_enq / (reps * ngroup)
+
+    t_single, e_single = timed(one_by_one)
+    ref_out = download()
+    for g in gs:  # the groups call must write every row again
+        for a in [g["met_out"], g["elem_out"], g["hit_out"]] + g["fields_out"]:
+            a.zero()
+    t_groups, e_groups = timed(lambda: ctx.locate_interp_groups(gs, sync=False))
+    st = ctx.locate_interp_groups(gs, sync=True)
+    out_g = download()
+    same = all(np.array_equal(a[k], b[k], equal_nan=True) for a, b in zip(out_g, ref_out)
+               for k in ("elem", "hit", "met")) and all(
+        np.array_equal(x, y, equal_nan=True) for a, b in zip(out_g, ref_out) for x, y in zip(a["fields"], b["fields"]))
+    npts = int(st.nvol + st.nbdy)
+    lanes = int(os.environ.get("PMMG_HIP_GROUP_LANES", "2"))
+    res = {"what": f"{ngroup} cfg2-size groups (own copies in HBM) in one pmmg_hip_locate_interp_groups call vs one "
+                   "pmmg_hip_locate_interp per group; not the bench value",
+           "groups": ngroup, "lanes": lanes, "points_per_group": npts // ngroup,
+           "ms_per_group_groups_call": round(1e3 * t_groups, 4), "ms_per_group_single_calls": round(1e3 * t_single, 4),
+           "host_enqueue_ms_per_group": {"groups_call": round(1e3 * e_groups, 4), "single_calls": round(1e3 * e_single, 4)},
+           "mpts_per_s_groups_call": round(npts / ngroup / t_groups / 1e6, 1),
+           "bit_identical_to_single_calls": bool(same)}
+    ctx.close()
+    if not args.no_cpu_baseline:
+        from oracle import oracle as O
+        bg, new, met, fields, pc = hosts[0]
+        threads, _ = host_cores()
+        B = O.Background(bg, met, fields, w.hausd)
+        new_t = synth.lattice(w.kind, w.n_new, jitter=w.jitter_new, seed=synth.SEED + 100, with_trias=False)
+        ref = O.run(B, new.xyz, pc, synth.visit_order(new_t), budget_s=budget_s, threads=threads)
+        res["parity_group0"] = parity_report(B, new, pc, out_g[0], ref)
+    log(f"[bench] groups leg: {res}")
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -535,6 +611,8 @@ def main():
                     help="skip the (separately reported) device background snapshot timing")
     ap.add_argument("--no-surface-solo", action="store_true",
                     help="skip the (separately reported) surface branch timed alone")
+    ap.add_argument("--no-groups", action="store_true",
+                    help="skip the (separately reported) 10 cfg2-size groups in one groups call")
     ap.add_argument("--no-graded", action="store_true",
                     help="skip the (separately reported) step on the graded and stretched cfgG meshes")
     args = ap.parse_args()
@@ -761,6 +839,11 @@ def main():
     if not args.no_snapshot and halo_info is None:  # (a shard's cut faces are no boundary trias)
         out["snapshot"] = snapshot_timing(ctx, bg, rank)
     ctx.close()
+    if not args.no_groups and world == 1 and not split:
+        try:
+            out["groups"] = groups_leg(args)
+        except Exception as e:  # reported, never fatal to the bench line
+            out["groups"] = {"error": str(e)}
     if not args.no_graded and world == 1 and not split and args.config == "cfg4":
         try:
             out["graded"] = graded_leg(args, rank)

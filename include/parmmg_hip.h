@@ -178,9 +178,56 @@ int pmmg_hip_locate_interp(pmmg_hip_ctx *ctx, int np_new, const double *xyz_new,
                            double *const *fields_out, int *elem_out,
                            int8_t *hit_out, pmmg_hip_stats *stats, int where);
 
-/* Wait for all work queued on the context; fills the stats of the last
- * PMMG_HIP_DEVICE call.  Returns 1/0. */
+/* Wait for all work queued on the context (groups calls included); fills the
+ * stats of the last PMMG_HIP_DEVICE pmmg_hip_locate_interp call.  Returns 1/0. */
 int pmmg_hip_sync(pmmg_hip_ctx *ctx, pmmg_hip_stats *stats);
+
+/* ---- Many groups in one call ------------------------------------------------
+ * ParMmg transfers group by group (the loop of src/interpmesh_pmmg.c:690 over
+ * up to PMMG_REMESHER_NGRPS_MAX = 100 groups per rank, src/parmmg.h:212);
+ * a group of a few hundred thousand points is launch-bound on one stream.  One
+ * group: the arguments of pmmg_hip_set_background(_tet8) +
+ * pmmg_hip_set_solutions + pmmg_hip_locate_interp, all PMMG_HIP_DEVICE
+ * pointers (same alignment rules). */
+typedef struct {
+  /* background (old group): tet8 != NULL selects packed records, else tetv +
+   * adja (adja NULL: adjacency built on the device, which synchronises); nt <
+   * 0 with triv NULL: boundary trias built on the device (synchronises) */
+  int np, ne, nt;
+  const double *xyz;
+  const int *tet8;
+  const int *tetv, *adja;
+  const int *triv, *adjt;
+  double hausd;
+  /* solutions at the background vertices */
+  int met_size;
+  const double *met;
+  int nfield;
+  const int *field_size;
+  const double *const *fields;
+  /* the new group's points and outputs */
+  int np_new;
+  const double *xyz_new;
+  const uint8_t *pclass;
+  double *met_out;
+  double *const *fields_out;
+  int *elem_out;
+  int8_t *hit_out;
+} pmmg_hip_group;
+
+/* Enqueue the transfer of ngroup groups: group i runs on lane i % L of the
+ * context (L = min(ngroup, PMMG_HIP_GROUP_LANES, default 2); a lane is a
+ * pair of streams with its own work buffers, so the groups of different lanes
+ * overlap on the device).  stats == NULL: the call only enqueues (nothing is
+ * read back; use pmmg_hip_sync before reading outputs).  stats != NULL: the
+ * call waits after each round of L groups and returns the counters summed
+ * over all groups (ms_* summed as well, stepmax the largest, sorted the
+ * number of groups whose queries were Morton-binned).  Results are identical to one
+ * pmmg_hip_locate_interp per group.  Returns 1 if every group was enqueued
+ * (and, with stats, completed), 0 at the first invalid group (the error names
+ * its index; groups before it are enqueued). */
+int pmmg_hip_locate_interp_groups(pmmg_hip_ctx *ctx, int ngroup, const pmmg_hip_group *groups,
+                                  pmmg_hip_stats *stats);
 
 /* ---- Background snapshot on the device -------------------------------------
  * ParMmg rebuilds the background's derived arrays on the host every

@@ -34,6 +34,18 @@ class HipStats(ctypes.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+class HipGroup(ctypes.Structure):
+    """``pmmg_hip_group`` of include/parmmg_hip.h (device pointers)."""
+
+    _fields_ = [
+        ("np", c_int), ("ne", c_int), ("nt", c_int), ("xyz", c_void_p), ("tet8", c_void_p), ("tetv", c_void_p),
+        ("adja", c_void_p), ("triv", c_void_p), ("adjt", c_void_p), ("hausd", c_double),
+        ("met_size", c_int), ("met", c_void_p), ("nfield", c_int), ("field_size", c_void_p), ("fields", c_void_p),
+        ("np_new", c_int), ("xyz_new", c_void_p), ("pclass", c_void_p), ("met_out", c_void_p),
+        ("fields_out", c_void_p), ("elem_out", c_void_p), ("hit_out", c_void_p),
+    ]
+
+
 # C-ABI of include/parmmg_hip.h: name -> (restype, argtypes)
 HIP_API = {
     "pmmg_hip_create": (c_void_p, [c_int, c_int]),
@@ -46,6 +58,7 @@ HIP_API = {
     "pmmg_hip_locate_interp": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                        c_void_p, P(HipStats), c_int]),
     "pmmg_hip_sync": (c_int, [c_void_p, P(HipStats)]),
+    "pmmg_hip_locate_interp_groups": (c_int, [c_void_p, c_int, c_void_p, P(HipStats)]),
     "pmmg_hip_malloc": (c_void_p, [c_void_p, c_int64]),
     "pmmg_hip_free": (c_int, [c_void_p, c_void_p]),
     "pmmg_hip_build_adjacency": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),

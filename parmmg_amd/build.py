@@ -65,7 +65,7 @@ def build_hip(force: bool = False, measure: bool = False) -> str:
     deps = [src, snap, qual, os.path.join(INC, "parmmg_hip.h"), __file__] + [
         os.path.join(CSRC, h) for h in ("pmmg_device.hpp", "pmmg_prep.hpp", "pmmg_vol.hpp", "pmmg_bdy.hpp",
                                         "pmmg_fallback.hpp", "pmmg_snapshot.hpp", "pmmg_quality.hpp",
-                                        "pmmg_brick.hpp")]
+                                        "pmmg_brick.hpp", "pmmg_sort.hpp")]
     if force or _stale(out, deps):
         # max-memory-clause scheduling: the gathers of a step issued as clauses
         # (volume kernel -4.6 % at cfg4, same registers; profiles/r02e/sweep_sched_strategy.txt)

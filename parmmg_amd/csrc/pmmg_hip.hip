@@ -18,7 +18,9 @@
 //                   continuation | interpolation | join | fallbacks
 //   surface stream  (after the order) surface seeds, node->tria CSR, k_bdy
 #include <hip/hip_runtime.h>
-#include <rocprim/device/device_radix_sort.hpp>
+#ifdef PMMG_HIP_MEASURE
+#include <rocprim/device/device_radix_sort.hpp> // the brick renumbering's sort (measurement build)
+#endif
 
 #include <math.h>
 #include <stdarg.h>
@@ -32,6 +34,7 @@
 #include <condition_variable>
 #include <functional>
 #include <mutex>
+#include <string>
 #include <thread>
 #include <type_traits>
 #include <vector>
@@ -41,6 +44,7 @@
 #ifdef PMMG_HIP_MEASURE
 #include "pmmg_brick.hpp" // measurement build only
 #endif
+#include "pmmg_sort.hpp"
 #include "pmmg_vol.hpp"
 #include "pmmg_bdy.hpp"
 #include "pmmg_fallback.hpp"
@@ -54,8 +58,8 @@ namespace {
 // ---------------------------------------------------------------- slot layouts
 
 typedef void (*VolFn)(Bg, const Frame *, const unsigned long long *, int, const double *, const uint8_t *,
-                      const int *, const double *, int, ContEntry *, DevStats *, Slots, int *, int8_t *, int, int,
-                      int, int, int);
+                      const int *, const double *, int, ContEntry *, DevStats *, Slots, int *, int8_t *, int,
+                      const int *, int, int);
 
 struct LayoutEntry {
   int c[6];
@@ -147,18 +151,16 @@ struct pmmg_hip_ctx {
   // work buffers
   DevBuf frame, stats, grid, sgrid, order_v, order_b, cont, xq;
   DevBuf axh;                             // per-axis histograms of the seed grid map (k_axis_hist)
-  DevBuf bkeys, bkeys2, bvals, sort_tmp;  // Morton binning: keys, sorted keys, ids, rocPRIM scratch
+  DevBuf bkeys, bkeys2, bvals, bvals2;    // Morton binning: keys and ids, ping-ponged by the radix sort
+  DevBuf rs_hist, rs_csum;                // the radix sort's digit table and its scan's chunk sums
   // PMMG_HIP_BRICK (measurement only, pmmg_brick.hpp): the background renumbered by bricks
   DevBuf brk_k, brk_k2, brk_v, brk_v2, brk_vinv, brk_tinv, brk_xq, brk_xyz, brk_sol, brk_rec, brk_tmp;
   int brick = 0;
   int set_order = 0; // test-only PMMG_HIP_SETORDER=1 (see k_set_order)
-  int cur_sorted = 0; // the query order of the last call (stats)
   int srf_solo = 0; // test-only PMMG_HIP_SRFSOLO=1: the surface branch waits for the seed grid (its cost alone)
   DevBuf qs;                              // volume query coordinates in processing order (Morton path)
   DevBuf cls_cnt;                         // per-block class counts (surface list compaction)
-  int *h_sorted = nullptr;                // pinned: the coherence test's {sorted, bin_bits}, read back in auto mode
   DevBuf oflag;                           // the coherence test's {sorted, bin_bits} on the device
-  hipEvent_t ev_flag = nullptr;           // its read-back
   DevBuf qmin;                               // tetra quality minimum (pmmg_hip_tetra_qual)
   DevBuf fb_vol, fb_bdy, best, ckey, cidx, bbest, bckey, bcidx;
   // host-mode staging
@@ -200,12 +202,14 @@ struct pmmg_hip_ctx {
   int maxstep = 4096; // longer walks go to the exact continuation / exhaustive kernels (PMMG_HIP_MAXSTEP; the
                       // reference caps at ne)
   int fanmax = kFanMax;    // cone fans longer than this take the O(nt) scan (test-only PMMG_HIP_FANMAX)
-  int dma = 1;           // k_vol's interpolation gathers by LDS DMA (measurement build: PMMG_HIP_DMA=0 keeps
-                         // the register-staged gathers)
   int pad = 0;           // measurement build, PMMG_HIP_PAD: extra VALU / L1 work per walk step (k_vol)
   int xcd_run = 64;      // k_vol's blocks dealt to the XCDs in runs of 64 (4096 queries) instead of contiguous
                          // eighths: r04c at cfg4, volume kernel 3.80 -> 3.50 ms, Mmg-like numbering 5.83 -> 4.14 ms
                          // (measurement build: PMMG_HIP_XCDRUN, 0 = eighths)
+  // pmmg_hip_locate_interp_groups: the context itself is lane 0, lanes[j]
+  // lane j + 1 (same device and options, created at the first groups call)
+  std::vector<pmmg_hip_ctx *> lanes;
+  int group_lanes = 2; // PMMG_HIP_GROUP_LANES
   int filter_steps = 64; // step cap of the fp32 filter walk (then the exact fp64 walk continues from where it
                          // stopped: a query the filter misjudges hands over early instead of cycling through a
                          // 4-entry history for up to maxstep steps); test-only PMMG_HIP_FILTER_STEPS=0 sends every
@@ -240,6 +244,15 @@ static int ensure(pmmg_hip_ctx *c, DevBuf &b, size_t bytes) {
   }
   HIPCK(c, hipMalloc(&b.p, bytes));
   b.cap = bytes;
+  return 1;
+}
+
+// the host-mode copy stream, created at the first host-mode upload (a
+// device-mode context, and every group lane, keeps to two streams: the
+// process has few hardware queues, GPU_MAX_HW_QUEUES = 4 by default, and
+// streams beyond them share one)
+static int copy_stream(pmmg_hip_ctx *c) {
+  if (!c->cstream) HIPCK(c, hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
   return 1;
 }
 
@@ -508,25 +521,19 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   c->device = device;
   c->options = options;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking) != hipSuccess) {
+      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
     fprintf(stderr, "[parmmg_hip] cannot initialise device %d\n", device);
     delete c;
     return nullptr;
   }
   for (int i = 0; i < EV_COUNT; i++) (void)hipEventCreate(&c->ev[i]);
-  (void)hipEventCreateWithFlags(&c->ev_flag, hipEventDisableTiming);
-  if (hipHostMalloc((void **)&c->h_sorted, 2 * sizeof(int), hipHostMallocDefault) != hipSuccess) {
-    fprintf(stderr, "[parmmg_hip] cannot allocate pinned host memory\n");
-    pmmg_hip_destroy(c);
-    return nullptr;
-  }
   // documented options, each clamped to its valid range
   c->tpc = std::min(4096, env_int("PMMG_HIP_TPC", c->tpc));
   c->srf_mult = std::min(4096, env_int("PMMG_HIP_SRFMULT", c->srf_mult));
   c->bin_bits = std::min(7, env_int("PMMG_HIP_BINBITS", c->bin_bits));
   c->verbose = env_int("PMMG_HIP_VERBOSE", 0);
   c->maxstep = env_int("PMMG_HIP_MAXSTEP", c->maxstep);
+  c->group_lanes = std::min(8, env_int("PMMG_HIP_GROUP_LANES", c->group_lanes));
   // test-only path selection (tests/test_gpu_hits.py, tests/test_gpu_parity.py)
   c->fanmax = env_int("PMMG_HIP_FANMAX", c->fanmax);
   c->srf_g = std::min(1024, env_int("PMMG_HIP_SRFG", 0));
@@ -548,13 +555,13 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   if (const char *e = getenv("PMMG_HIP_XCDRUN"))
     if (*e && atoi(e) >= 0) c->xcd_run = atoi(e);
   c->pad = env_int("PMMG_HIP_PAD", 0);
-  if (const char *e = getenv("PMMG_HIP_DMA")) c->dma = atoi(e) != 0;
 #endif
   return c;
 }
 
 void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   if (!c) return;
+  for (pmmg_hip_ctx *l : c->lanes) pmmg_hip_destroy(l);
   (void)hipSetDevice(c->device);
   (void)snap_join(c);
   (void)hipStreamSynchronize(c->stream);
@@ -562,7 +569,7 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   if (c->cstream) (void)hipStreamSynchronize(c->cstream);
   DevBuf *bufs[] = {&c->o_xyz, &c->o_tetv, &c->o_adja, &c->o_triv, &c->o_adjt, &c->o_met, &c->o_rec, &c->frame,
                     &c->stats, &c->grid, &c->sgrid, &c->order_v,
-                    &c->order_b, &c->cont, &c->xq, &c->qs, &c->axh, &c->bkeys, &c->bkeys2, &c->bvals, &c->sort_tmp, &c->oflag, &c->cls_cnt, &c->qmin, &c->fb_vol, &c->fb_bdy,
+                    &c->order_b, &c->cont, &c->xq, &c->qs, &c->axh, &c->bkeys, &c->bkeys2, &c->bvals, &c->bvals2, &c->rs_hist, &c->rs_csum, &c->oflag, &c->cls_cnt, &c->qmin, &c->fb_vol, &c->fb_bdy,
                     &c->best, &c->ckey, &c->cidx, &c->bbest, &c->bckey, &c->bcidx, &c->h_xyz,
                     &c->h_cls, &c->h_met, &c->h_elem, &c->h_hit, &c->brk_k, &c->brk_k2, &c->brk_v, &c->brk_v2,
                     &c->brk_vinv, &c->brk_tinv, &c->brk_xq, &c->brk_xyz, &c->brk_sol, &c->brk_rec, &c->brk_tmp};
@@ -575,8 +582,6 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
     if (c->stage[b]) (void)hipHostFree(c->stage[b]);
     if (c->stage_ev[b]) (void)hipEventDestroy(c->stage_ev[b]);
   }
-  if (c->h_sorted) (void)hipHostFree(c->h_sorted);
-  if (c->ev_flag) (void)hipEventDestroy(c->ev_flag);
   delete c->pool;
   release(c->o_tet4);
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
@@ -797,12 +802,13 @@ int pmmg_hip_set_solutions(pmmg_hip_ctx *c, int met_size, const double *met, int
   }
   // host mode: through the copy stream (beside a deferred snapshot)
   if (met_size) {
-    if (!upload(c, c->o_met, met, sizeof(double) * met_size * np, c->cstream)) return 0;
+    if (!copy_stream(c) || !upload(c, c->o_met, met, sizeof(double) * met_size * np, c->cstream)) return 0;
     c->met = (const double *)c->o_met.p;
   }
   c->o_f.resize(nfield);
   for (int j = 0; j < nfield; j++) {
-    if (!upload(c, c->o_f[j], fields[j], sizeof(double) * field_size[j] * np, c->cstream)) return 0;
+    if (!copy_stream(c) || !upload(c, c->o_f[j], fields[j], sizeof(double) * field_size[j] * np, c->cstream))
+      return 0;
     c->fin[j] = (const double *)c->o_f[j].p;
   }
   HIPCK(c, hipStreamSynchronize(c->cstream));
@@ -850,11 +856,15 @@ int pmmg_hip_set_solutions_packed(pmmg_hip_ctx *c, int met_size, int nfield, con
     c->rec = rec;
     return 1;
   }
-  if (!upload(c, c->o_rec, rec, sizeof(double) * c->rstride * np, c->cstream)) return 0;
+  if (!copy_stream(c) || !upload(c, c->o_rec, rec, sizeof(double) * c->rstride * np, c->cstream)) return 0;
   c->rec = (const double *)c->o_rec.p;
   HIPCK(c, hipStreamSynchronize(c->cstream));
   return 1;
 }
+
+// groups with fewer new points take the input order without the coherence
+// test (their background stays cache-resident; see run_device)
+constexpr int kSmallGroup = 1 << 21;
 
 static int grid_dim(long long n, int per_cell, int gmax) {
   double g = cbrt((double)n / (double)per_cell);
@@ -1020,7 +1030,8 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   unsigned long long *grid = (unsigned long long *)c->grid.p;
   int *sgrid = (int *)c->sgrid.p;
   int *order_v = (int *)c->order_v.p, *order_b = (int *)c->order_b.p;
-  const int force = (c->options & PMMG_HIP_OPT_SORT) ? 1 : (c->options & PMMG_HIP_OPT_NOSORT) ? 0 : -1;
+  int force = (c->options & PMMG_HIP_OPT_SORT) ? 1 : (c->options & PMMG_HIP_OPT_NOSORT) ? 0 : -1;
+  if (force < 0 && np_new < kSmallGroup) force = 0;
 
   // ---- frame (main stream)
   HIPCK(c, hipEventRecord(c->ev[EV_START], s));
@@ -1031,10 +1042,6 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_START], 0));
   hipLaunchKernelGGL(k_coherence, dim3(1), dim3(kBlock), 0, sb, xyz_new, np_new, (int *)c->oflag.p, force,
                      c->bin_bits);
-  if (force < 0) {
-    HIPCK(c, hipMemcpyAsync(c->h_sorted, c->oflag.p, 2 * sizeof(int), hipMemcpyDeviceToHost, sb));
-    HIPCK(c, hipEventRecord(c->ev_flag, sb));
-  }
   hipLaunchKernelGGL(k_reset, dim3(blocks_for(ng > nsg ? ng : nsg, 2048)), dim3(kBlock), 0, s, fr, st, grid, ng,
                      sgrid, nsg);
   hipLaunchKernelGGL(k_bbox, dim3(blocks_for(bg.np / c->bbox_stride + 1, 256)), dim3(kBlock), 0, s, bg.xyz, bg.np, fr,
@@ -1059,45 +1066,57 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
                      (const Frame *)fr, (int *)c->xq.p);
   {
     const long long nsamp = ng < bg.ne ? ng : bg.ne;
-    // one thread per run of 4 sampled tetra
-    hipLaunchKernelGGL(k_seed_vol, dim3((blocks_for((nsamp + kSeedRun - 1) / kSeedRun, 8192) + 7) & ~7), dim3(kBlock), 0,
-                       s, bg, fr, grid, g, nsamp, c->seed_lanes);
+    hipLaunchKernelGGL(k_seed_vol, dim3((blocks_for(nsamp, 8192) + 7) & ~7), dim3(kBlock), 0, s, bg, fr, grid, g,
+                       nsamp, c->seed_lanes);
   }
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[EV_PREP], s));
 
-  int sorted = force, bits = c->bin_bits;
-  if (force < 0) {
-    HIPCK(c, hipEventSynchronize(c->ev_flag));
-    sorted = c->h_sorted[0];
-    bits = c->h_sorted[1];
-  }
-  c->cur_sorted = sorted;
+  // ---- query order (second stream, after the frame): the kernels of both
+  // orders, each gated on k_coherence's flag on the device — no host read.
+  // Forced orders enqueue only theirs; a small group (below kSmallGroup
+  // queries: its background and solutions stay in the Infinity Cache, where
+  // a numbering's locality matters little) takes the input order untested.
+  const int *flag = (const int *)c->oflag.p;
 #ifdef PMMG_HIP_MEASURE
-  if (c->set_order) hipLaunchKernelGGL(k_set_order, dim3(1), dim3(1), 0, s, st, sorted, bits);
+  if (c->set_order) hipLaunchKernelGGL(k_set_order, dim3(1), dim3(1), 0, s, st, force > 0 ? 1 : 0, c->bin_bits);
 #endif
-  if (sorted && np_new > 0) {
+  if (force != 0 && np_new > 0) {
     hipLaunchKernelGGL(k_bin_keys, dim3(blocks_for(np_new, 1024)), dim3(kBlock), 0, sb, xyz_new, pclass, np_new,
-                       (const Frame *)fr, bits, (unsigned *)c->bkeys.p, (int *)c->bvals.p, st);
-    const int key_bits = 3 * bits + 2;
-    size_t tmp = 0;
-    HIPCK(c, rocprim::radix_sort_pairs(nullptr, tmp, (const unsigned *)c->bkeys.p, (unsigned *)c->bkeys2.p,
-                                       (const int *)c->bvals.p, order_v, np_new, 0, key_bits, sb));
-    if (!ensure(c, c->sort_tmp, tmp)) return 0;
-    HIPCK(c, rocprim::radix_sort_pairs(c->sort_tmp.p, tmp, (const unsigned *)c->bkeys.p, (unsigned *)c->bkeys2.p,
-                                       (const int *)c->bvals.p, order_v, np_new, 0, key_bits, sb));
+                       (const Frame *)fr, flag, (unsigned *)c->bkeys.p, (int *)c->bvals.p, st);
+    // stable LSD radix sort of the keys (<= 3 * 7 + 2 bits) in 3 passes of 8 bits (pmmg_sort.hpp)
+    const int ntile = (int)((np_new + kRsTile - 1) / kRsTile);
+    const long long nh = 256LL * ntile;
+    const int nch = (int)((nh + kScanChunk - 1) / kScanChunk);
+    if (!ensure(c, c->bvals2, 4 * nq) || !ensure(c, c->rs_hist, 4 * (size_t)nh) || !ensure(c, c->rs_csum, 4 * (size_t)nch))
+      return 0;
+    unsigned *k0 = (unsigned *)c->bkeys.p, *k1 = (unsigned *)c->bkeys2.p;
+    int *v0 = (int *)c->bvals.p, *v1 = (int *)c->bvals2.p, *hist = (int *)c->rs_hist.p, *csum = (int *)c->rs_csum.p;
+    for (int pass = 0; pass < 3; pass++) {
+      const unsigned *kin = pass == 1 ? k1 : k0;
+      const int *vin = pass == 1 ? v1 : v0;
+      unsigned *kout = pass == 1 ? k0 : k1;
+      int *vout = pass == 1 ? v0 : (pass == 0 ? v1 : order_v);
+      hipLaunchKernelGGL(k_rs_hist, dim3(ntile), dim3(kBlock), 0, sb, kin, np_new, 8 * pass, ntile, hist, flag, 1);
+      hipLaunchKernelGGL(k_rs_scan_local, dim3(nch), dim3(kBlock), 0, sb, hist, (int)nh, csum, flag, 1);
+      hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, sb, csum, nch, (int *)nullptr, flag, 1);
+      hipLaunchKernelGGL(k_rs_scan_add, dim3(nch), dim3(kBlock), 0, sb, hist, (int)nh, (const int *)csum, flag, 1);
+      hipLaunchKernelGGL(k_rs_scatter, dim3(ntile), dim3(kBlock), 0, sb, kin, vin, np_new, 8 * pass, ntile,
+                         (const int *)hist, kout, vout, flag, 1);
+    }
     hipLaunchKernelGGL(k_bin_split, dim3(blocks_for(np_new, 4096)), dim3(kBlock), 0, sb, (const int *)order_v, xyz_new,
-                       np_new, order_b, c->bin_qs ? (double *)c->qs.p : nullptr, (const DevStats *)st);
-  } else if (bg.nt > 0) {
+                       np_new, order_b, c->bin_qs ? (double *)c->qs.p : nullptr, (const DevStats *)st, flag);
+  }
+  if (force != 1 && bg.nt > 0) {
     // input order: the surface points in input order (stable compaction:
     // per-block counts, their scan, the scatter; rocPRIM's select took 0.2 ms
     // longer here, r03o)
     int *bc = (int *)c->cls_cnt.p;
     hipLaunchKernelGGL(k_cls_count, dim3((unsigned)ncls), dim3(kBlock), 0, sb, pclass, (long long)np_new,
-                       (int)PMMG_PT_BDY, bc);
-    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, sb, bc, (int)ncls, &st->nbdy, (const int *)nullptr, 0);
+                       (int)PMMG_PT_BDY, bc, flag, 0);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, sb, bc, (int)ncls, &st->nbdy, flag, 0);
     hipLaunchKernelGGL(k_cls_scatter, dim3((unsigned)ncls), dim3(kBlock), 0, sb, pclass, (long long)np_new,
-                       (int)PMMG_PT_BDY, (const int *)bc, order_b);
+                       (int)PMMG_PT_BDY, (const int *)bc, order_b, flag, 0);
   }
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[EV_ORDER], sb));
@@ -1128,8 +1147,8 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   hipLaunchKernelGGL(vol_fn, dim3((np_new + 63) / 64), dim3(64), 0, s, bg, (const Frame *)fr,
                      (const unsigned long long *)grid, g, xyz_new, pclass, (const int *)order_v,
                      c->bin_qs ? (const double *)c->qs.p : nullptr, np_new,
-                     (ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->filter_steps, sorted, c->xcd_run,
-                     c->pad, c->dma);
+                     (ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->filter_steps, flag, c->xcd_run,
+                     c->pad);
   HIPCK(c, hipEventRecord(c->ev[EV_WALK], s));
   hipLaunchKernelGGL(k_vol_walk_exact, dim3(8 * 64), dim3(64), 0, s, bg, xyz_new, (int *)c->fb_vol.p,
                      (const ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->maxstep);
@@ -1148,6 +1167,8 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
 
 static int collect_stats(pmmg_hip_ctx *c, pmmg_hip_stats *out) {
   DevStats h;
+  int order[2] = {0, 0}; // the call's query order, decided on the device
+  HIPCK(c, hipMemcpy(order, c->oflag.p, sizeof(order), hipMemcpyDeviceToHost));
   std::vector<StatPart> parts(kStatParts);
   HIPCK(c, hipMemcpy(&h, c->stats.p, sizeof(DevStats), hipMemcpyDeviceToHost));
   HIPCK(c, hipMemcpy(parts.data(), (const DevStats *)c->stats.p + 1, kStatParts * sizeof(StatPart),
@@ -1159,7 +1180,7 @@ static int collect_stats(pmmg_hip_ctx *c, pmmg_hip_stats *out) {
     if (pt.stepmax > stepmax) stepmax = pt.stepmax;
   }
   memset(out, 0, sizeof(*out));
-  out->nvol = c->cur_sorted ? (int64_t)h.nvol : (int64_t)cnt[kCntVolQueries];
+  out->nvol = order[0] == 1 ? (int64_t)h.nvol : (int64_t)cnt[kCntVolQueries];
   out->nbdy = h.nbdy;
   out->nvol_walk = (int64_t)cnt[PMMG_HIT_VOL_WALK];
   out->nvol_exhaust = (int64_t)cnt[PMMG_HIT_VOL_EXHAUST];
@@ -1176,7 +1197,7 @@ static int collect_stats(pmmg_hip_ctx *c, pmmg_hip_stats *out) {
   out->steps_total = (int64_t)steps;
   out->stepmax = (int64_t)stepmax;
   out->wave_iters = (int64_t)cnt[kCntWaveIters];
-  out->sorted = c->cur_sorted;
+  out->sorted = order[0] == 1;
   out->nvol_noseed = (int64_t)cnt[kCntNoSeed];
   out->nvol_stuck = (int64_t)cnt[kCntStuck];
   out->nvol_limit = (int64_t)cnt[kCntLimit];
@@ -1207,6 +1228,11 @@ int pmmg_hip_sync(pmmg_hip_ctx *c, pmmg_hip_stats *stats) {
   if (!c) return 0;
   HIPCK(c, hipSetDevice(c->device));
   if (!snap_join(c)) return 0;
+  for (pmmg_hip_ctx *l : c->lanes)
+    if (hipStreamSynchronize(l->stream) != hipSuccess) {
+      set_err(c, "sync: group lane failed: %s", l->err);
+      return 0;
+    }
   HIPCK(c, hipStreamSynchronize(c->stream));
   if (stats && c->pending) return collect_stats(c, stats);
   return 1;
@@ -1300,6 +1326,86 @@ int pmmg_hip_locate_interp(pmmg_hip_ctx *c, int np_new, const double *xyz_new, c
     fprintf(stderr, "[parmmg_hip] host locate: uploads + enqueue %.2f ms, step + hit codes %.2f ms, rows %.2f ms\n",
             1e3 * (t1 - t0), 1e3 * (t2 - t1), 1e3 * (now_s() - t2));
   if (stats) return collect_stats(c, stats);
+  return 1;
+}
+
+// ---- many groups in one call
+
+static void stats_sum(pmmg_hip_stats *a, const pmmg_hip_stats &b) {
+  a->nvol += b.nvol; a->nbdy += b.nbdy;
+  a->nvol_walk += b.nvol_walk; a->nvol_exhaust += b.nvol_exhaust; a->nvol_closest += b.nvol_closest;
+  a->nvol_exact += b.nvol_exact;
+  a->nbdy_face += b.nbdy_face; a->nbdy_edge += b.nbdy_edge; a->nbdy_vertex += b.nbdy_vertex;
+  a->nbdy_wedge += b.nbdy_wedge; a->nbdy_cone += b.nbdy_cone; a->nbdy_exhaust += b.nbdy_exhaust;
+  a->nbdy_stale += b.nbdy_stale; a->nbdy_closest += b.nbdy_closest;
+  a->steps_total += b.steps_total; a->wave_iters += b.wave_iters;
+  a->sorted += b.sorted; // the number of groups whose queries were Morton-binned
+  if (b.stepmax > a->stepmax) a->stepmax = b.stepmax;
+  a->ms_prepare += b.ms_prepare; a->ms_sort += b.ms_sort; a->ms_vol += b.ms_vol; a->ms_bdy += b.ms_bdy;
+  a->ms_fallback += b.ms_fallback; a->ms_total += b.ms_total; a->ms_vol_locate += b.ms_vol_locate;
+  a->nvol_noseed += b.nvol_noseed; a->nvol_stuck += b.nvol_stuck; a->nvol_limit += b.nvol_limit;
+  a->seed_map_axes |= b.seed_map_axes;
+}
+
+static pmmg_hip_ctx *group_lane(pmmg_hip_ctx *c, int j) {
+  if (j == 0) return c;
+  while ((int)c->lanes.size() < j) {
+    pmmg_hip_ctx *l = pmmg_hip_create(c->device, c->options);
+    if (!l) {
+      set_err(c, "locate_interp_groups: cannot create group lane %d", (int)c->lanes.size() + 1);
+      return nullptr;
+    }
+    c->lanes.push_back(l);
+  }
+  return c->lanes[j - 1];
+}
+
+int pmmg_hip_locate_interp_groups(pmmg_hip_ctx *c, int ngroup, const pmmg_hip_group *groups,
+                                  pmmg_hip_stats *stats) {
+  if (!c) return 0;
+  if (stats) memset(stats, 0, sizeof(*stats));
+  if (ngroup <= 0) return 1;
+  if (!groups) {
+    set_err(c, "locate_interp_groups: groups is NULL");
+    return 0;
+  }
+  HIPCK(c, hipSetDevice(c->device));
+  if (!snap_join(c)) return 0;
+  const int L = std::max(1, std::min(ngroup, c->group_lanes));
+  std::vector<pmmg_hip_ctx *> lane(L);
+  for (int j = 0; j < L; j++)
+    if (!(lane[j] = group_lane(c, j))) return 0;
+  for (int r0 = 0; r0 < ngroup; r0 += L) {
+    const int r1 = std::min(ngroup, r0 + L);
+    for (int i = r0; i < r1; i++) {
+      const pmmg_hip_group &g = groups[i];
+      pmmg_hip_ctx *l = lane[i % L];
+      const int ok =
+          (g.tet8 ? set_background_impl(l, g.np, g.xyz, g.ne, nullptr, nullptr, g.tet8, g.nt, g.triv, g.adjt, g.hausd,
+                                        PMMG_HIP_DEVICE)
+                  : (g.tetv && set_background_impl(l, g.np, g.xyz, g.ne, g.tetv, g.adja, nullptr, g.nt, g.triv,
+                                                   g.adjt, g.hausd, PMMG_HIP_DEVICE))) &&
+          pmmg_hip_set_solutions(l, g.met_size, g.met, g.nfield, g.field_size, g.fields, PMMG_HIP_DEVICE) &&
+          pmmg_hip_locate_interp(l, g.np_new, g.xyz_new, g.pclass, g.met_out, g.fields_out, g.elem_out, g.hit_out,
+                                 nullptr, PMMG_HIP_DEVICE);
+      if (!ok) {
+        const std::string why = l->err;
+        set_err(c, "locate_interp_groups: group %d: %s", i, why.c_str());
+        return 0;
+      }
+    }
+    if (stats) // the round's counters, before the lanes take the next groups
+      for (int i = r0; i < r1; i++) {
+        pmmg_hip_ctx *l = lane[i % L];
+        pmmg_hip_stats st;
+        if (!pmmg_hip_sync(l, &st)) {
+          const std::string why = l->err;
+          set_err(c, "locate_interp_groups: group %d: %s", i, why.c_str());
+          return 0;
+        }
+        stats_sum(stats, st);
+      }
+  }
   return 1;
 }
 

@@ -2,11 +2,10 @@
 // (included by pmmg_hip.hip only): state reset, background frame, volume and
 // surface seed grids, and the query order.
 //
-// The input-order coherence test runs on the device (DevStats::sorted); in
-// auto mode the host reads that one flag back while the main stream builds
-// the seed grid, then enqueues either the Morton binning (a rocPRIM radix
-// sort: its kernels cannot be gated on a device flag) or the class compaction
-// of the surface list.  No other result is read back inside a call.
+// The input-order coherence test runs on the device (k_coherence's flag); in
+// auto mode both the Morton binning (pmmg_sort.hpp) and the class compaction
+// of the surface list are enqueued, each gated on that flag, and the volume
+// kernel reads it: nothing is read back inside a call.
 #pragma once
 
 #include "pmmg_device.hpp"
@@ -283,28 +282,30 @@ __global__ void k_frame_final(Frame *fr, int g, int gs, int gb) {
 constexpr int kSeedRun = 4;
 constexpr unsigned long long kSeedIdMask = (1ULL << 29) - 1; // ids below 2^29 (the adja encoding's limit)
 
-// One thread per run of 4 consecutive tetra (one 128-byte line of packed
-// records): the run's 4 records, then their 16 vertex rows, are all in flight
-// before the first key is computed (r04: one sample per lane took ~6 loop
-// trips of two dependent loads each), the 4 keys are combined in the thread
-// and each distinct cell gets one atomicMin.  The cell position comes from
-// the fixed-point vertex sum in one multiply-add per axis (Frame::sa, sb:
-// the uniform map folded with the fixed-point frame); an axis with a
+// One lane per sample, the 4 lanes of a run on consecutive records (their
+// record and vertex loads share sectors: r04e, one thread per run read twice
+// the sectors and took 0.72 ms against 0.25).  The grid-stride loop is
+// unrolled by kSeedBatch: the records of kSeedBatch trips, then their vertex
+// rows, are in flight together before the first key is computed.  The cell
+// position comes from the fixed-point vertex sum in one multiply-add per
+// axis (the uniform map folded with the fixed-point frame); an axis with a
 // quantile map (Frame::adaptive) goes through seed_pos.
+constexpr int kSeedBatch = 3;
 __global__ __launch_bounds__(kBlock) void k_seed_vol(Bg bg, Frame *fr, unsigned long long *cell, int g,
                                                      long long nsamp, int lanes) {
-  constexpr int R = kSeedRun;
+  constexpr int R = kSeedRun, B = kSeedBatch;
   __shared__ int smin;
   if (threadIdx.x == 0) smin = INT_MAX;
   __syncthreads();
   int kmin = INT_MAX;
   const long long nruns = (nsamp + R - 1) / R;
   const long long quads = bg.ne / 4;
+  const long long nthreads = nruns * R;
   // XCD-aware: the blocks of XCD x (blockIdx % 8; gridDim is a multiple of
-  // 8) take one contiguous eighth of the runs, so the vertex rows shared by
-  // neighbouring tetra are fetched into one L2, not eight
-  const long long per = (nruns + 8LL * kBlock - 1) / (8LL * kBlock) * kBlock;
-  const long long lo = (blockIdx.x & 7) * per, hi = lo + per < nruns ? lo + per : nruns;
+  // 8) sweep one contiguous eighth of the samples, so the vertex rows shared
+  // by neighbouring tetra are fetched into one L2, not eight
+  const long long per = (nthreads + 8LL * kBlock - 1) / (8LL * kBlock) * kBlock;
+  const long long lo = (blockIdx.x & 7) * per, hi = lo + per < nthreads ? lo + per : nthreads;
   const long long bstride = (long long)(gridDim.x >> 3) * blockDim.x;
   const int adaptive = fr->adaptive;
   double sa[3], sb[3];
@@ -313,30 +314,34 @@ __global__ __launch_bounds__(kBlock) void k_seed_vol(Bg bg, Frame *fr, unsigned 
     sa[d] = (fr->qc[d] - fr->lo[d]) * fr->inv_vol[d];
     sb[d] = 0.25 * fr->inv_vol[d] / fr->qs;
   }
-  for (long long run = lo + (blockIdx.x >> 3) * (long long)blockDim.x + threadIdx.x; run < hi; run += bstride) {
-    const long long base = 4 * ((run * quads) / (nruns > 0 ? nruns : 1)); // a cache line of tet8 records
-    int4 tv[R];
-    bool ok[R];
+  const int lane = __lane_id(), r = lane % R, g0 = lane - r;
+  for (long long s0 = lo + (blockIdx.x >> 3) * (long long)blockDim.x; s0 < hi; s0 += B * bstride) {
+    int k[B];
+    int4 tv[B];
+    bool ok[B];
 #pragma unroll
-    for (int r = 0; r < R; r++) {
-      const int k = (int)(1 + base + r);
-      ok[r] = k <= bg.ne && r < lanes; // `lanes` of the run's 4 records are sampled
-      tv[r] = make_int4(0, 0, 0, 0);
-      if (ok[r]) {
+    for (int b = 0; b < B; b++) {
+      const long long s = s0 + b * bstride + threadIdx.x;
+      const long long run = s / R;
+      const long long base = 4 * ((run * quads) / (nruns > 0 ? nruns : 1)); // a cache line of tet8 records
+      k[b] = (int)(1 + base + r);
+      ok[b] = s < hi && k[b] <= bg.ne && r < lanes; // `lanes` of the run's 4 records are sampled
+      tv[b] = make_int4(0, 0, 0, 0);
+      if (ok[b]) {
         const nti4 rr =
-            __builtin_nontemporal_load(reinterpret_cast<const nti4 *>(bg.tetv + (size_t)(k - 1) * bg.tstride));
-        tv[r] = make_int4(rr.x, rr.y, rr.z, rr.w);
+            __builtin_nontemporal_load(reinterpret_cast<const nti4 *>(bg.tetv + (size_t)(k[b] - 1) * bg.tstride));
+        tv[b] = make_int4(rr.x, rr.y, rr.z, rr.w);
       }
     }
-    long long sq[R][3]; // 64-bit: clamped coordinates (+-2^30) of vertices outside the sampled frame
+    long long sq[B][3]; // 64-bit: clamped coordinates (+-2^30) of vertices outside the sampled frame
 #pragma unroll
-    for (int r = 0; r < R; r++) {
-      ok[r] = ok[r] && tv[r].x > 0;
+    for (int b = 0; b < B; b++) {
+      ok[b] = ok[b] && tv[b].x > 0;
 #pragma unroll
-      for (int d = 0; d < 3; d++) sq[r][d] = 0;
-      if (ok[r]) {
-        const int *q0 = bg.xq + kXqStride * (size_t)(tv[r].x - 1), *q1 = bg.xq + kXqStride * (size_t)(tv[r].y - 1);
-        const int *q2 = bg.xq + kXqStride * (size_t)(tv[r].z - 1), *q3 = bg.xq + kXqStride * (size_t)(tv[r].w - 1);
+      for (int d = 0; d < 3; d++) sq[b][d] = 0;
+      if (ok[b]) {
+        const int *q0 = bg.xq + kXqStride * (size_t)(tv[b].x - 1), *q1 = bg.xq + kXqStride * (size_t)(tv[b].y - 1);
+        const int *q2 = bg.xq + kXqStride * (size_t)(tv[b].z - 1), *q3 = bg.xq + kXqStride * (size_t)(tv[b].w - 1);
         int a0[3], a1[3], a2[3], a3[3];
 #pragma unroll
         for (int d = 0; d < 3; d++) {
@@ -346,50 +351,46 @@ __global__ __launch_bounds__(kBlock) void k_seed_vol(Bg bg, Frame *fr, unsigned 
           a3[d] = q3[d];
         }
 #pragma unroll
-        for (int d = 0; d < 3; d++) sq[r][d] = ((long long)a0[d] + a1[d]) + ((long long)a2[d] + a3[d]);
+        for (int d = 0; d < 3; d++) sq[b][d] = ((long long)a0[d] + a1[d]) + ((long long)a2[d] + a3[d]);
       }
     }
-    unsigned long long key[R];
-    long long ci[R];
 #pragma unroll
-    for (int r = 0; r < R; r++) {
-      key[r] = ~0ULL;
-      ci[r] = -1;
-      if (!ok[r]) continue;
-      const int k = (int)(1 + base + r);
-      int c[3];
-      unsigned long long off = 0;
-      float d2 = 0.f;
+    for (int b = 0; b < B; b++) {
+      unsigned long long key = ~0ULL;
+      long long ci = -1;
+      if (ok[b]) {
+        int c[3];
+        unsigned long long off = 0;
+        float d2 = 0.f;
 #pragma unroll
-      for (int d = 0; d < 3; d++) {
-        // the centroid's position in cells: uniform axes in one multiply-add
-        // on the fixed-point sum (exact in fp64), mapped axes through seed_pos
-        double t = sa[d] + sb[d] * (double)sq[r][d];
-        if ((adaptive >> d) & 1) t = seed_pos(fr, d, fr->qc[d] + 0.25 * (double)sq[r][d] / fr->qs, g);
-        c[d] = seed_cell(t, g);
-        float f = (float)(t - c[d]);
-        f = f < 0.f ? 0.f : (f > 0.999f ? 0.999f : f);
-        off |= (unsigned long long)(unsigned)(f * 512.f) << (9 * d);
-        d2 += (f - 0.5f) * (f - 0.5f);
+        for (int d = 0; d < 3; d++) {
+          double t = sa[d] + sb[d] * (double)sq[b][d];
+          if ((adaptive >> d) & 1) t = seed_pos(fr, d, fr->qc[d] + 0.25 * (double)sq[b][d] / fr->qs, g);
+          c[d] = seed_cell(t, g);
+          float f = (float)(t - c[d]);
+          f = f < 0.f ? 0.f : (f > 0.999f ? 0.999f : f);
+          off |= (unsigned long long)(unsigned)(f * 512.f) << (9 * d);
+          d2 += (f - 0.5f) * (f - 0.5f);
+        }
+        const unsigned q8 = d2 * 340.f < 255.f ? (unsigned)(d2 * 340.f) : 255u;
+        key = ((unsigned long long)q8 << 56) | (off << 29) | (unsigned)k[b];
+        ci = c[0] + (long long)g * (c[1] + (long long)g * c[2]);
+        kmin = k[b] < kmin ? k[b] : kmin;
       }
-      const unsigned q8 = d2 * 340.f < 255.f ? (unsigned)(d2 * 340.f) : 255u;
-      key[r] = ((unsigned long long)q8 << 56) | (off << 29) | (unsigned)k;
-      ci[r] = c[0] + (long long)g * (c[1] + (long long)g * c[2]);
-      kmin = k < kmin ? k : kmin;
-    }
-    // the run's keys combined per distinct cell: one atomic per cell
-#pragma unroll
-    for (int r = 0; r < R; r++) {
-      if (ci[r] < 0) continue;
-      bool first = true;
-      unsigned long long best = key[r];
+      // combine within the run: the first lane of each distinct cell issues
+      // the atomic with the run's minimum for that cell
+      bool leader = ci >= 0;
+      unsigned long long best = key;
 #pragma unroll
       for (int o = 0; o < R; o++) {
-        if (o == r || ci[o] != ci[r]) continue;
-        if (o < r) first = false;
-        best = key[o] < best ? key[o] : best;
+        const long long co = __shfl(ci, g0 + o);
+        const unsigned long long ko = __shfl(key, g0 + o);
+        if (co == ci && ci >= 0) {
+          best = ko < best ? ko : best;
+          if (o < r) leader = false;
+        }
       }
-      if (first) atomicMin(&cell[ci[r]], best);
+      if (leader) atomicMin(&cell[ci], best);
     }
   }
   for (int o = 32; o > 0; o >>= 1) {
@@ -755,8 +756,12 @@ __global__ __launch_bounds__(kBlock) void k_coherence(const double *xyz, int np,
 // them coalesced) and the surface list.  The radix sort is stable: the order
 // is a deterministic function of the input.
 
+// flag: the order decision {sorted, bits per axis} (k_coherence); the kernel
+// runs only when flag[0] == 1
 __global__ __launch_bounds__(kBlock) void k_bin_keys(const double *xyz, const uint8_t *pclass, int np, const Frame *fr,
-                                                     int bits, unsigned *keys, int *vals, DevStats *st) {
+                                                     const int *flag, unsigned *keys, int *vals, DevStats *st) {
+  if (flag[0] != 1) return;
+  const int bits = flag[1];
   int nv = 0, nb = 0;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < np; i += (long long)gridDim.x * blockDim.x) {
     const int c = pclass[i];
@@ -795,7 +800,8 @@ __global__ __launch_bounds__(kBlock) void k_bin_keys(const double *xyz, const ui
 // sorted ids -> volume list (order_v, in place) + the volume queries'
 // coordinates in that order (qs, when non-null), surface list (order_b)
 __global__ __launch_bounds__(kBlock) void k_bin_split(const int *sorted_ids, const double *xyz, int np, int *order_b,
-                                                      double *qs, const DevStats *st) {
+                                                      double *qs, const DevStats *st, const int *flag) {
+  if (flag[0] != 1) return;
   const int nvol = st->nvol, nbdy = st->nbdy;
   for (long long j = (qs ? 0 : nvol) + blockIdx.x * (long long)blockDim.x + threadIdx.x; j < nvol + nbdy;
        j += (long long)gridDim.x * blockDim.x) {
@@ -836,7 +842,9 @@ __device__ __forceinline__ unsigned cls_bits(const uint8_t *pclass, long long np
   return m;
 }
 
-__global__ __launch_bounds__(kBlock) void k_cls_count(const uint8_t *pclass, long long np, int cls, int *bcnt) {
+__global__ __launch_bounds__(kBlock) void k_cls_count(const uint8_t *pclass, long long np, int cls, int *bcnt,
+                                                      const int *gate, int want) {
+  if (gate_off(gate, want)) return;
   const long long i0 = (long long)blockIdx.x * kScanChunk + (long long)threadIdx.x * kScanItems;
   int tot;
   block_excl_scan(__popc(cls_bits(pclass, np, i0, cls)), &tot);
@@ -844,7 +852,8 @@ __global__ __launch_bounds__(kBlock) void k_cls_count(const uint8_t *pclass, lon
 }
 
 __global__ __launch_bounds__(kBlock) void k_cls_scatter(const uint8_t *pclass, long long np, int cls,
-                                                        const int *boff, int *out) {
+                                                        const int *boff, int *out, const int *gate, int want) {
+  if (gate_off(gate, want)) return;
   const long long i0 = (long long)blockIdx.x * kScanChunk + (long long)threadIdx.x * kScanItems;
   unsigned m = cls_bits(pclass, np, i0, cls);
   int tot;

@@ -1,0 +1,113 @@
+// pmmg_sort.hpp — the Morton binning's sort as device-gated kernels
+// (included by pmmg_hip.hip only).
+//
+// A stable LSD radix sort of (32-bit key, 32-bit value) pairs, 8 bits per
+// pass, whose every kernel returns at once unless *gate == want: the query
+// order of a call is chosen on the device (k_coherence) and both orders'
+// kernels are enqueued, so the call never waits for the flag on the host
+// (rocPRIM's sort, used up to r03, takes its work from host arguments and
+// cannot be skipped from the device).
+//
+// Per pass: k_rs_hist counts the digits of each tile of kRsTile keys (LDS
+// histogram, digit-major table hist[digit][tile]), k_rs_scan_* turns the
+// table into each (digit, tile)'s first output position, and k_rs_scatter
+// ranks each tile's keys stably — sub-tiles of 256 keys in input order, a
+// wave's lanes with equal digits found by 8 ballots — and writes them there.
+#pragma once
+
+#include "pmmg_prep.hpp"
+
+namespace pmmg {
+
+constexpr int kRsItems = 16, kRsTile = kBlock * kRsItems; // keys per tile (one block)
+
+__global__ __launch_bounds__(kBlock) void k_rs_hist(const unsigned *keys, int n, int shift, int ntile, int *hist,
+                                                    const int *gate, int want) {
+  if (gate_off(gate, want)) return;
+  __shared__ int h[256];
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  const long long base = (long long)blockIdx.x * kRsTile;
+#pragma unroll 4
+  for (int j = 0; j < kRsItems; j++) {
+    const long long idx = base + j * kBlock + threadIdx.x;
+    if (idx < n) atomicAdd(&h[(keys[idx] >> shift) & 255u], 1);
+  }
+  __syncthreads();
+  hist[(size_t)threadIdx.x * ntile + blockIdx.x] = h[threadIdx.x];
+}
+
+// exclusive scan of a[0..n) in place: per-chunk scans (chunk sums to
+// csum), the scan of the chunk sums (k_scan_top), their addition
+__global__ __launch_bounds__(kBlock) void k_rs_scan_local(int *a, int n, int *csum, const int *gate, int want) {
+  if (gate_off(gate, want)) return;
+  const long long i0 = (long long)blockIdx.x * kScanChunk + (long long)threadIdx.x * kScanItems;
+  int v[kScanItems], s = 0;
+#pragma unroll
+  for (int j = 0; j < kScanItems; j++) {
+    v[j] = i0 + j < n ? a[i0 + j] : 0;
+    s += v[j];
+  }
+  int tot;
+  int run = block_excl_scan(s, &tot);
+#pragma unroll
+  for (int j = 0; j < kScanItems; j++) {
+    if (i0 + j < n) a[i0 + j] = run;
+    run += v[j];
+  }
+  if (threadIdx.x == 0) csum[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(kBlock) void k_rs_scan_add(int *a, int n, const int *coff, const int *gate, int want) {
+  if (gate_off(gate, want)) return;
+  const long long i0 = (long long)blockIdx.x * kScanChunk + (long long)threadIdx.x * kScanItems;
+  const int o = coff[blockIdx.x];
+#pragma unroll
+  for (int j = 0; j < kScanItems; j++)
+    if (i0 + j < n) a[i0 + j] += o;
+}
+
+__global__ __launch_bounds__(kBlock) void k_rs_scatter(const unsigned *kin, const int *vin, int n, int shift, int ntile,
+                                                       const int *off, unsigned *kout, int *vout, const int *gate,
+                                                       int want) {
+  if (gate_off(gate, want)) return;
+  __shared__ int run[256];     // next output position of each digit for this tile
+  __shared__ int wcnt[4][256]; // keys of each digit in each wave of the current sub-tile
+  run[threadIdx.x] = off[(size_t)threadIdx.x * ntile + blockIdx.x];
+#pragma unroll
+  for (int w = 0; w < 4; w++) wcnt[w][threadIdx.x] = 0;
+  __syncthreads();
+  const int w = threadIdx.x >> 6, lane = __lane_id();
+  const long long base = (long long)blockIdx.x * kRsTile;
+  for (int j = 0; j < kRsItems; j++) {
+    const long long idx = base + j * kBlock + threadIdx.x;
+    const bool ok = idx < n;
+    const unsigned key = ok ? kin[idx] : 0u;
+    const int val = ok ? vin[idx] : 0;
+    const unsigned d = (key >> shift) & 255u;
+    unsigned long long same = __ballot(ok);
+#pragma unroll
+    for (int b = 0; b < 8; b++) {
+      const unsigned long long bb = __ballot((d >> b) & 1u);
+      same &= ((d >> b) & 1u) ? bb : ~bb;
+    }
+    const int rank = __popcll(same & ((1ULL << lane) - 1ULL));
+    if (ok && rank == 0) wcnt[w][d] = __popcll(same);
+    __syncthreads();
+    if (ok) {
+      int pos = run[d] + rank;
+      for (int w2 = 0; w2 < w; w2++) pos += wcnt[w2][d];
+      kout[pos] = key;
+      vout[pos] = val;
+    }
+    __syncthreads();
+    {
+      const int dd = threadIdx.x;
+      run[dd] += wcnt[0][dd] + wcnt[1][dd] + wcnt[2][dd] + wcnt[3][dd];
+      wcnt[0][dd] = wcnt[1][dd] = wcnt[2][dd] = wcnt[3][dd] = 0;
+    }
+    __syncthreads();
+  }
+}
+
+} // namespace pmmg

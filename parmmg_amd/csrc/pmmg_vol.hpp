@@ -15,6 +15,8 @@
 
 namespace pmmg {
 
+__device__ __forceinline__ void wait_lgkm() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
 // a located query: the tetra's vertex ids and the reference's (exact,
 // unsorted) barycentric coordinates
 struct VolLoc {
@@ -273,7 +275,9 @@ __device__ __forceinline__ int pick_face_fast(const int4 &ad, const int *hist, c
 }
 
 // returns 1 candidate (filter passed), 0 moved (k, tv, ad, m, hist updated),
-// 2 stuck (no eligible neighbour)
+// 2 stuck (no eligible neighbour).  (r04f: the neighbour records loaded by
+// lane pairs, one sector access per record, wave-uniform loop: +4 %;
+// profiles/r04f/pair_records.patch.txt.)
 __device__ __forceinline__ int step_f32(const Bg &bg, const int *x, int &k, int4 &tv, int4 &ad, unsigned &m, int *hist,
                                         const LaneSlotsF &L, unsigned rsel) {
   float q[4][3];
@@ -292,7 +296,7 @@ __device__ __forceinline__ int step_f32(const Bg &bg, const int *x, int &k, int4
   const float vol = -((s[0] + s[1]) + (s[2] + s[3]));
   float key[4];
 #pragma unroll
-  for (int f = 0; f < 4; f++) key[f] = vol < 0.f ? -s[f] : s[f];
+  for (int ff = 0; ff < 4; ff++) key[ff] = vol < 0.f ? -s[ff] : s[ff];
   const float kmax = fmaxf(fmaxf(key[0], key[1]), fmaxf(key[2], key[3]));
   if (vol != 0.f && kmax < (float)(kEps + kFilterMargin) * fabsf(vol)) return 1;
   const int f = pick_face_fast<float>(ad, hist, key, rsel);
@@ -458,7 +462,6 @@ __global__ __launch_bounds__(64) void k_vol_walk_exact(Bg bg, const double *qxyz
 
 // ---------------------------------------------------------------- interpolation
 
-__device__ __forceinline__ void wait_lgkm() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // Output rows of one slot for the wave's 64 consecutive queries, written as
 // whole cache lines: each lane puts its row into a wave-private LDS image,
@@ -569,16 +572,18 @@ __device__ __forceinline__ void sink_rows(const Slot &sl, const double *r, bool 
 //      go through LDS (coop_issue* / coop_land*).  In input order the rows are stored as whole cache lines
 //      through the same LDS image; Morton-binned queries store per lane.
 // The walk's vertex slots and the gather image share one 4 KiB LDS buffer
-// (the phases are sequential within the wave).  (r04b measured a third use —
+// (the phases are sequential within the wave).  (r04e: the tensor slots'
+// gathers by LDS DMA, with the next vertex in flight in a second image
+// instead of registers, measured equal; 5 waves per SIMD with 8 VGPRs
+// spilled, +3 %.  r04b measured a third use —
 // an image of the wave's distinct vertices, sorted, for the exact test and the
 // interpolation: 20 % fewer L1 accesses, +23 % VALU for the sort, +10 % time;
 // profiles/r04b/unique_vertex_rows.patch.txt.)
 struct VolShared {
   BlockStats bs;
   union {
-    float slots[12 * 64]; // walk: [slot*3 + dim][lane]
-    double img[12 * 64];  // interpolation: two images of 64 rows of up to 6 doubles (LDS DMA), or one, or 64 x 8
-                          // doubles of packed records
+    float slots[12 * 64]; // walk: the vertex slots [slot*3 + dim][lane]
+    double img[8 * 64]; // interpolation: 64 rows of up to 6 doubles, or 64 x 8 doubles of packed records
   } u;
 };
 
@@ -634,87 +639,10 @@ __device__ __forceinline__ void coop_land3(double p0, double p1, double p2, doub
   __builtin_amdgcn_wave_barrier();
 }
 
-// The same gathers by LDS DMA (global_load_lds: each lane's piece lands in
-// the image at lane-contiguous positions without passing through VGPRs):
-// the pieces of vertex i + 1 in flight cost no registers, which takes the
-// fused kernel under the next occupancy step.  Two images per wave (vertex
-// i in one, i + 1 in the other); 16-byte pieces of 6-double rows.
-typedef __attribute__((address_space(3))) void lds_void;
-__device__ __forceinline__ void dma_issue6(const double *in, int stride, int myv, double *dst) {
-  const int lane = __lane_id();
-#pragma unroll
-  for (int t = 0; t < 3; t++) {
-    const int q = 64 * t + lane;
-    const int v = __shfl(myv, q / 3);
-    __builtin_amdgcn_global_load_lds((const void *)(in + (size_t)stride * (v - 1) + 2 * (q % 3)),
-                                     (lds_void *)(dst + 128 * t), 16, 0, 0);
-  }
-}
-// the pieces issued before the last n are in LDS (vmcnt counts loads, stores
-// and LDS DMA of the wave in issue order)
-template <int N>
-__device__ __forceinline__ void dma_wait() {
-  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-}
-template <int C>
-__device__ __forceinline__ void dma_read(const double *img, double *row) {
-  const int lane = __lane_id();
-#pragma unroll
-  for (int j = 0; j < C; j++) row[j] = img[C * lane + j];
-  wait_lgkm();
-  __builtin_amdgcn_wave_barrier(); // every lane has read its row: the image takes the next vertex
-}
-
-template <int C> // C == 6
-__device__ __forceinline__ void vol_slot_dma(const Slot &sl, bool act, const int4 &v, const double *phi, double *img,
-                                             const Sink &k) {
-  double *ia = img, *ib = img + 384; // two 3 KiB images
-  double r[C];
-  bool ok = act;
-  if constexpr (C == 6) {
-    double mint[6], m[6], mi[6];
-#define PMMG_ACC6(i)                                                                               \
-  do {                                                                                             \
-    ok = invmat(m, mi) && ok;                                                                      \
-    _Pragma("unroll") for (int q = 0; q < 6; q++) mint[q] = (i == 0) ? phi[0] * mi[q] : mint[q] + phi[i] * mi[q]; \
-  } while (0)
-    dma_issue6(sl.in, sl.istride, v.x, ia);
-    dma_issue6(sl.in, sl.istride, v.y, ib);
-    dma_wait<3>();
-    dma_read<6>(ia, m);
-    PMMG_ACC6(0);
-    dma_issue6(sl.in, sl.istride, v.z, ia);
-    dma_wait<3>();
-    dma_read<6>(ib, m);
-    PMMG_ACC6(1);
-    dma_issue6(sl.in, sl.istride, v.w, ib);
-    dma_wait<3>();
-    dma_read<6>(ia, m);
-    PMMG_ACC6(2);
-    dma_wait<0>();
-    dma_read<6>(ib, m);
-    PMMG_ACC6(3);
-    ok = invmat(mint, r) && ok;
-#undef PMMG_ACC6
-  }
-  sink_rows<C>(sl, r, ok, img, k);
-}
-
 // one slot of the wave's queries: rows gathered, interpolated, stored
 template <int C>
 __device__ __forceinline__ void vol_slot(const Slot &sl, bool act, const int4 &v, const double *phi, double *img,
-                                         const Sink &k, bool dma) {
-  if constexpr (C == 6) { // (12-byte DMA pieces land 16 bytes apart: 3-double rows keep the register path)
-#ifndef PMMG_HIP_MEASURE
-    dma = true; // the product always gathers 6-double rows by DMA (the register path only for the A/B)
-#endif
-    if (dma) {
-      vol_slot_dma<C>(sl, act, v, phi, img, k);
-      return;
-    }
-  }
+                                         const Sink &k) {
   if constexpr (C > 0) {
     double r[C];
     bool ok = act;
@@ -924,22 +852,17 @@ __device__ __forceinline__ void vol_interp_packed(const Slots &S, bool acc, cons
 }
 
 template <bool PK, int C0, int C1, int C2, int C3, int C4, int C5>
-#ifdef PMMG_KVOL_WAVES // measurement: the volume kernel compiled for this many waves per SIMD (spills allowed)
-#define PMMG_KVOL_OCC __attribute__((amdgpu_waves_per_eu(PMMG_KVOL_WAVES)))
-#else
-#define PMMG_KVOL_OCC
-#endif
-__global__ __launch_bounds__(64) PMMG_KVOL_OCC void k_vol(Bg bg, const Frame *fr, const unsigned long long *grid, int g,
+__global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsigned long long *grid, int g,
                                             const double *qxyz, const uint8_t *pclass, const int *order,
                                             const double *qs, int np, ContEntry *cont, DevStats *st, Slots S,
-                                            int *elem_out, int8_t *hit_out, int filter_steps, int sorted_order,
-                                            int xcd_run, int pad, int dma) {
+                                            int *elem_out, int8_t *hit_out, int filter_steps,
+                                            const int *order_flag, int xcd_run, int pad) {
   __shared__ VolShared sh;
   bstats_init(&sh.bs);
   __syncthreads();
   const LaneSlotsF L{(lds_float *)&sh.u.slots[__lane_id()]};
   const int i = xcd_block_runs(xcd_run) * 64 + threadIdx.x;
-  const bool sorted = sorted_order != 0;
+  const bool sorted = order_flag[0] == 1; // the call's query order, decided on the device (k_coherence)
   bool active;
   int ip = 0;
   if (sorted) {
@@ -1069,12 +992,12 @@ __global__ __launch_bounds__(64) PMMG_KVOL_OCC void k_vol(Bg bg, const Frame *fr
         for (int s2 = 0; s2 < S.n; s2++) interp_dyn<4>(S.s[s2], ip, vv, loc.phi);
       }
     } else {
-      vol_slot<C0>(S.s[0], acc, loc.v, loc.phi, img, snk, dma != 0);
-      vol_slot<C1>(S.s[1], acc, loc.v, loc.phi, img, snk, dma != 0);
-      vol_slot<C2>(S.s[2], acc, loc.v, loc.phi, img, snk, dma != 0);
-      vol_slot<C3>(S.s[3], acc, loc.v, loc.phi, img, snk, dma != 0);
-      vol_slot<C4>(S.s[4], acc, loc.v, loc.phi, img, snk, dma != 0);
-      vol_slot<C5>(S.s[5], acc, loc.v, loc.phi, img, snk, dma != 0);
+      vol_slot<C0>(S.s[0], acc, loc.v, loc.phi, img, snk);
+      vol_slot<C1>(S.s[1], acc, loc.v, loc.phi, img, snk);
+      vol_slot<C2>(S.s[2], acc, loc.v, loc.phi, img, snk);
+      vol_slot<C3>(S.s[3], acc, loc.v, loc.phi, img, snk);
+      vol_slot<C4>(S.s[4], acc, loc.v, loc.phi, img, snk);
+      vol_slot<C5>(S.s[5], acc, loc.v, loc.phi, img, snk);
     }
     if (acc) {
       if (sorted) { // scattered: cached stores (see wave_store_rows_scat)

@@ -17,7 +17,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from ._native import HipStats, hip_lib, host_lib
+from ._native import HipGroup, HipStats, hip_lib, host_lib
 
 HOST, DEVICE = 0, 1
 PT_SKIP, PT_VOL, PT_BDY = 0, 1, 2
@@ -59,6 +59,11 @@ class DeviceArray:
         if not self.ctx.lib.pmmg_hip_memcpy_d2h(self.ctx.h, _p(out), ctypes.c_void_p(self.ptr), self.nbytes):
             raise RuntimeError(self.ctx.error())
         return out
+
+    def zero(self) -> None:
+        z = np.zeros(self.nbytes, np.uint8)
+        if not self.ctx.lib.pmmg_hip_memcpy_h2d(self.ctx.h, ctypes.c_void_p(self.ptr), _p(z), self.nbytes):
+            raise RuntimeError(self.ctx.error())
 
     def free(self) -> None:
         if self.ptr:
@@ -225,6 +230,40 @@ class TransferContext:
                                                  ctypes.byref(st) if (sync or where == HOST) else None, where),
                  "locate_interp")
         return st if (sync or where == HOST) else None
+
+    def locate_interp_groups(self, groups, sync: bool = True) -> HipStats | None:
+        """pmmg_hip_locate_interp_groups: many groups in one call, device
+        arrays only.  Each group is a dict {xyz, tet8 | (tetv, adja), triv,
+        adjt, hausd, met, fields, xyz_new, pclass, met_out, fields_out[,
+        elem_out, hit_out]}.  sync: wait and return the summed counters;
+        otherwise only enqueue (pmmg_hip_sync before reading outputs)."""
+        G = (HipGroup * max(1, len(groups)))()
+        keep = []
+        for i, g in enumerate(groups):
+            arrays = [g["xyz"], g.get("tet8"), g.get("tetv"), g.get("adja"), g["triv"], g.get("adjt"), g.get("met"),
+                      g["xyz_new"], g["pclass"], g.get("met_out"), g.get("elem_out"), g.get("hit_out")]
+            arrays += list(g.get("fields", [])) + list(g.get("fields_out", []))
+            if not all(a is None or _is_dev(a) for a in arrays):
+                raise ValueError(f"group {i}: locate_interp_groups takes device arrays")
+            fs, fo = list(g.get("fields", [])), list(g.get("fields_out", []))
+            fsz = (ctypes.c_int * max(1, len(fs)))(*[int(f.shape[1]) for f in fs])
+            fpt = (ctypes.c_void_p * max(1, len(fs)))(*[_p(f) for f in fs])
+            opt = (ctypes.c_void_p * max(1, len(fo)))(*[_p(f) for f in fo])
+            keep += [fsz, fpt, opt, arrays]
+            tet = g["tet8"] if g.get("tet8") is not None else g["tetv"]
+            met = g.get("met")
+            v = lambda a: None if a is None else _p(a).value  # noqa: E731
+            G[i] = HipGroup(int(g["xyz"].shape[0]), int(tet.shape[0]), int(g["triv"].shape[0]), v(g["xyz"]),
+                            v(g.get("tet8")), v(g.get("tetv")), v(g.get("adja")), v(g["triv"]), v(g.get("adjt")),
+                            float(g["hausd"]), 0 if met is None else int(met.shape[1]), v(met), len(fs),
+                            ctypes.cast(fsz, ctypes.c_void_p), ctypes.cast(fpt, ctypes.c_void_p),
+                            int(g["xyz_new"].shape[0]), v(g["xyz_new"]), v(g["pclass"]), v(g.get("met_out")),
+                            ctypes.cast(opt, ctypes.c_void_p), v(g.get("elem_out")), v(g.get("hit_out")))
+        self._grp_keep = (G, keep)
+        st = HipStats()
+        self._ck(self.lib.pmmg_hip_locate_interp_groups(self.h, len(groups), ctypes.cast(G, ctypes.c_void_p),
+                                                        ctypes.byref(st) if sync else None), "locate_interp_groups")
+        return st if sync else None
 
     def tetra_qual(self, xyz, tetv, met=None, qual=None):
         """PMMG_tetraQual's MMG3D_tetraQual(mesh, met, 1) on the device
