@@ -275,22 +275,27 @@ def snapshot_timing(ctx, bg, rank: int, reps: int = 3):
     its own, outside the transfer step, checked against the host-built
     arrays the step uses."""
     d_tetv = ctx.upload(bg.tetv)
+    d_tet8 = ctx.empty((bg.ne, 8), np.int32)  # the caller's old-group array, kept across iterations
     times = []
     ok = True
-    for rep in range(reps):
+    for rep in range(reps + 1):  # the first call sizes the context's snapshot scratch (untimed)
+        if rep == reps:
+            d_tet8.zero()  # the checked call writes every record again
         t0 = time.perf_counter()
-        adja, tet8 = ctx.build_adjacency(bg.np, d_tetv, adja=False, tet8=True)
+        adja, tet8 = ctx.build_adjacency(bg.np, d_tetv, adja=False, tet8=True, out=(None, d_tet8))
         t1 = time.perf_counter()
         triv, adjt = ctx.build_boundary(bg.np, tet8=tet8)
         t2 = time.perf_counter()
-        times.append((t1 - t0, t2 - t1))
+        if rep > 0:
+            times.append((t1 - t0, t2 - t1))
         ok = ok and bool(np.array_equal(adjt.download(), bg.adjt))
-        if rep == reps - 1:
+        if rep == reps:
             ok = ok and bool(np.array_equal(tet8.download(), pack_tet8(bg.tetv, bg.adja)))
             ok = ok and bool(np.array_equal(triv.download(), bg.triv))
-        for a in (tet8, triv, adjt):
+        for a in (triv, adjt):
             a.free()
     d_tetv.free()
+    d_tet8.free()
     t_adj = float(np.median([t[0] for t in times]))
     t_bdy = float(np.median([t[1] for t in times]))
     b_adj = bg.ne * (16 + 32)  # tetv in, tet8 records out
@@ -357,12 +362,55 @@ def host_mode_timing(ctx, w, bg, met, fields, q_xyz, q_pc, rank: int, reps: int 
     npts = int(st.nvol + st.nbdy)
     log(f"[bench r{rank}] host-buffer (PCIe-inclusive) call: {1e3 * t:.1f} ms "
         f"(background {1e3 * b:.1f}, solutions {1e3 * s_:.1f}, locate {1e3 * l_:.1f})")
-    return {"what": "one group through host buffers as the C host layer runs it: background (xyz + tetv up, "
-                    "adjacency and boundary trias built on the device), solutions up, queries up + the step + the "
-                    "written rows down; not the bench value",
-            "ms": round(1e3 * t, 2), "ms_background": round(1e3 * b, 2), "ms_solutions": round(1e3 * s_, 2),
-            "ms_locate_interp": round(1e3 * l_, 2), "mpts_per_s": round(npts / t / 1e6, 1),
-            "bytes_up": int(up), "bytes_down": int(down), "pcie_gbps_effective": round((up + down) / t / 1e9, 1)}
+    out = {"what": "one group through host buffers as the C host layer runs it: background (xyz + tetv up, "
+                   "adjacency and boundary trias built on the device), solutions up, queries up + the step + the "
+                   "written rows down; not the bench value",
+           "ms": round(1e3 * t, 2), "ms_background": round(1e3 * b, 2), "ms_solutions": round(1e3 * s_, 2),
+           "ms_locate_interp": round(1e3 * l_, 2), "mpts_per_s": round(npts / t / 1e6, 1),
+           "bytes_up": int(up), "bytes_down": int(down), "pcie_gbps_effective": round((up + down) / t / 1e9, 1)}
+    try:
+        out["iteration2"] = host_mode_iteration2(ctx, w, bg, mo, fo, rank)
+    except Exception as e:  # reported, never fatal to the bench line
+        out["iteration2"] = {"error": str(e)}
+    return out
+
+
+def host_mode_iteration2(ctx, w, bg, mo, fo, rank: int) -> dict:
+    """The next iteration through host buffers (src/libparmmg1.c:653: the
+    adapted group becomes the old group): its background is the new mesh just
+    transferred into (the new points, with the rows the step wrote) and the
+    next new mesh has the first background's points (synthetic stand-in).
+    Timed twice: cold (everything uploaded) and carried (pmmg_hip_keep after
+    the first iteration, pmmg_hip_carry_over: only the connectivity and the
+    next queries go up), outputs compared bit for bit; bytes_up counted by
+    the module."""
+    ctx.keep(0)  # the first iteration's last call (host_mode_timing) stays on the device
+    new_t = synth.lattice(w.kind, w.n_new, jitter=w.jitter_new, seed=synth.SEED, with_trias=False)
+    q2, pc2 = bg.xyz, synth.classes(bg)
+    res = {}
+    outs = {}
+    for mode in ("cold", "carried"):
+        m2 = np.full((q2.shape[0], mo.shape[1]), np.nan)
+        f2 = [np.full((q2.shape[0], f.shape[1]), np.nan) for f in fo]
+        if mode == "carried":
+            ctx.carry_over(0, new_t.np)
+        ctx.bytes_up(reset=True)
+        t0 = time.perf_counter()
+        ctx.set_background(new_t.xyz, new_t.tetv, None, None, None, w.hausd)
+        ctx.set_solutions(mo, fo)
+        st = ctx.locate_interp(q2, pc2, m2, f2)
+        t = time.perf_counter() - t0
+        res[mode] = {"ms": round(1e3 * t, 2), "bytes_up": ctx.bytes_up(reset=True),
+                     "located_points": int(st.nvol + st.nbdy)}
+        outs[mode] = [m2] + f2
+    same = all(np.array_equal(a, b, equal_nan=True) for a, b in zip(outs["cold"], outs["carried"]))
+    res.update({"what": "second iteration through host buffers: background = the new mesh of the first "
+                        f"({new_t.ne} tets, {new_t.np} verts), queries = the first background's points; cold vs "
+                        "carried over from the device (pmmg_hip_keep / pmmg_hip_carry_over)",
+                "bytes_up_saved_frac": round(1 - res["carried"]["bytes_up"] / max(1, res["cold"]["bytes_up"]), 3),
+                "bit_identical": bool(same)})
+    log(f"[bench r{rank}] host-mode iteration 2: {res}")
+    return res
 
 
 def renumbered_timing(ctx, args, w, step_bg, q_xyz, q_pc, d_mo, d_fo, d_elem, d_hit, rank: int, perm, what: str):

@@ -182,6 +182,35 @@ int pmmg_hip_locate_interp(pmmg_hip_ctx *ctx, int np_new, const double *xyz_new,
  * stats of the last PMMG_HIP_DEVICE pmmg_hip_locate_interp call.  Returns 1/0. */
 int pmmg_hip_sync(pmmg_hip_ctx *ctx, pmmg_hip_stats *stats);
 
+/* ---- Carry-over of the new mesh into the next iteration ----------------------
+ * ParMmg's next iteration takes the adapted group as its old group
+ * (src/libparmmg1.c:653 -> PMMG_update_oldGrps, src/grpsplit_pmmg.c:1224-1248):
+ * its vertices are the points this step located and its solutions the rows
+ * this step wrote.  After a PMMG_HIP_HOST pmmg_hip_locate_interp they are
+ * still in HBM:
+ *   pmmg_hip_keep(ctx, slot)    keeps that call's new points and written rows
+ *                               in `slot` (0..1023; no copy)
+ *   pmmg_hip_carry_over(ctx, slot, np, src)
+ *                               arms the next PMMG_HIP_HOST set_background +
+ *                               set_solutions: vertex i+1 of the new background
+ *                               is kept point src[i] (1-based; NULL: the
+ *                               identity, np = the kept count).  Those calls
+ *                               still take the full host arrays, but upload
+ *                               only the vertices with src[i] == 0 (moved in,
+ *                               e.g. by load balancing) and the solution rows
+ *                               the step did not write (skipped points, whose
+ *                               values the caller copies on the host, and
+ *                               MMG5_invmat failures); a metric / field whose
+ *                               size differs from the kept one goes up whole.
+ * pmmg_hip_carry_over(ctx, slot, 0, NULL) drops the slot.  The kept rows
+ * must not have been changed on the host in between; the connectivity always
+ * comes from the host.  Both return 1/0. */
+int pmmg_hip_keep(pmmg_hip_ctx *ctx, int slot);
+int pmmg_hip_carry_over(pmmg_hip_ctx *ctx, int slot, int np, const int *src);
+
+/* Host -> device bytes moved by host-mode calls since the last reset. */
+int64_t pmmg_hip_bytes_up(pmmg_hip_ctx *ctx, int reset);
+
 /* ---- Many groups in one call ------------------------------------------------
  * ParMmg transfers group by group (the loop of src/interpmesh_pmmg.c:690 over
  * up to PMMG_REMESHER_NGRPS_MAX = 100 groups per rank, src/parmmg.h:212);

@@ -59,6 +59,9 @@ HIP_API = {
                                        c_void_p, P(HipStats), c_int]),
     "pmmg_hip_sync": (c_int, [c_void_p, P(HipStats)]),
     "pmmg_hip_locate_interp_groups": (c_int, [c_void_p, c_int, c_void_p, P(HipStats)]),
+    "pmmg_hip_keep": (c_int, [c_void_p, c_int]),
+    "pmmg_hip_carry_over": (c_int, [c_void_p, c_int, c_int, c_void_p]),
+    "pmmg_hip_bytes_up": (c_int64, [c_void_p, c_int]),
     "pmmg_hip_malloc": (c_void_p, [c_void_p, c_int64]),
     "pmmg_hip_free": (c_int, [c_void_p, c_void_p]),
     "pmmg_hip_build_adjacency": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
@@ -121,6 +124,8 @@ HOST_API = {
     "pmmg_copy_metrics_and_fields_point": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int]),
     "pmmg_set_constant_metric": (c_int, [c_void_p]),
     "pmmg_interp_metrics_and_fields": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, P(HipStats)]),
+    "pmmg_interp_metrics_and_fields_carry": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p,
+                                                     P(HipStats)]),
     "pmmg_max_tet_extent": (c_double, [c_int, c_void_p, c_int, c_void_p]),
     "pmmg_shard_mark": (c_int, [c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_double, c_void_p,
                                 c_void_p, P(c_int64)]),

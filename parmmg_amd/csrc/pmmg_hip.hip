@@ -176,6 +176,7 @@ struct pmmg_hip_ctx {
   int stage_i = 0;
   struct Pool *pool = nullptr;
   DevBuf o_tet4; // device copy of a host tetv (input of the device adjacency)
+  SnapCache snap_cache; // the snapshot kernels' scratch (pmmg_snapshot.hip)
   // host mode: the device-built background (adjacency, boundary trias) runs
   // on `stream` in a host thread while set_solutions' uploads go through
   // `cstream` (the DMA engine works beside the snapshot kernels); every other
@@ -206,6 +207,24 @@ struct pmmg_hip_ctx {
   int xcd_run = 64;      // k_vol's blocks dealt to the XCDs in runs of 64 (4096 queries) instead of contiguous
                          // eighths: r04c at cfg4, volume kernel 3.80 -> 3.50 ms, Mmg-like numbering 5.83 -> 4.14 ms
                          // (measurement build: PMMG_HIP_XCDRUN, 0 = eighths)
+  // carry-over (pmmg_hip_keep / pmmg_hip_carry_over): kept[slot] holds the new
+  // points and written rows of a host-mode call; an armed carry (carry_slot
+  // >= 0) feeds the next host-mode set_background / set_solutions from it
+  struct Kept {
+    DevBuf xyz, met;
+    std::vector<DevBuf> f;
+    int np = 0, met_size = 0;
+    std::vector<int> fsize;
+    bool valid = false;
+  };
+  std::vector<Kept> kept;
+  int last_host_np = 0, last_host_met = 0; // the last host-mode locate_interp (what pmmg_hip_keep keeps)
+  std::vector<int> last_host_fsize;
+  int carry_slot = -1, carry_np = 0;
+  bool carry_bg = false;       // set_background took its vertices from the carry
+  std::vector<int> carry_src;  // next vertex i+1 = kept point carry_src[i] (0: host row); empty: identity
+  DevBuf carry_dsrc, carry_need, carry_ids, carry_cnt, carry_rows, carry_bc;
+  int64_t bytes_up = 0; // host -> device bytes of host-mode calls (pmmg_hip_bytes_up)
   // pmmg_hip_locate_interp_groups: the context itself is lane 0, lanes[j]
   // lane j + 1 (same device and options, created at the first groups call)
   std::vector<pmmg_hip_ctx *> lanes;
@@ -380,6 +399,7 @@ static void par_copy(pmmg_hip_ctx *c, void *dst, const void *src, size_t n) {
 // reused as soon as the call returns
 static int h2d(pmmg_hip_ctx *c, void *dst, const void *src, size_t bytes, hipStream_t s) {
   if (bytes == 0) return 1;
+  c->bytes_up += (int64_t)bytes;
   if (bytes < kStageMin) {
     HIPCK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
     return 1;
@@ -584,6 +604,14 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   }
   delete c->pool;
   release(c->o_tet4);
+  pmmg_snap_cache_free(&c->snap_cache);
+  for (auto &k : c->kept) {
+    release(k.xyz);
+    release(k.met);
+    for (auto &b : k.f) release(b);
+  }
+  DevBuf *cb[] = {&c->carry_dsrc, &c->carry_need, &c->carry_ids, &c->carry_cnt, &c->carry_rows, &c->carry_bc};
+  for (DevBuf *b : cb) release(*b);
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->cstream) (void)hipStreamDestroy(c->cstream);
@@ -591,6 +619,176 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
 }
 
 const char *pmmg_hip_last_error(pmmg_hip_ctx *c) { return c ? c->err : "null context"; }
+
+// ---------------------------------------------------------------- carry-over
+//
+// ParMmg's next iteration takes the adapted group as its old group
+// (src/libparmmg1.c:653 -> PMMG_update_oldGrps, src/grpsplit_pmmg.c:1224-1248):
+// its vertices are the new points the transfer step just located and its
+// solutions the rows the step just wrote, both still in HBM after a
+// host-mode call.  pmmg_hip_keep keeps them (the staging buffers are swapped
+// into a slot, no copy); pmmg_hip_carry_over arms the next host-mode
+// set_background / set_solutions to take from the slot every row it holds —
+// vertex i + 1 of the new background is kept point src[i] — and to upload only
+// the rest: vertices not in the slot (src[i] == 0, e.g. moved in by load
+// balancing) and rows the step did not write (skipped points, whose values
+// the caller copies on the host, and MMG5_invmat failures), found on the
+// device by the output sentinel.
+
+static int blocks_for(long long n, int cap);
+
+// to[i] = from[src[i] - 1] (row doubles; src NULL: the identity, to NULL: no
+// copy); need[i] = 1 where the row must come from the host: src[i] == 0, or
+// (check) the kept row is the unwritten sentinel
+__global__ void k_carry_gather(const double *from, int row, const int *src, long long np, double *to, uint8_t *need,
+                               int check) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < np; i += (long long)gridDim.x * blockDim.x) {
+    const long long s = src ? (long long)src[i] : i + 1;
+    bool miss = s <= 0;
+    if (!miss) {
+      const double *f = from + (size_t)row * (size_t)(s - 1);
+      miss = check && (unsigned long long)__double_as_longlong(f[0]) == kSentinel;
+      if (!miss && to)
+        for (int j = 0; j < row; j++) to[(size_t)row * (size_t)i + j] = f[j];
+    }
+    if (miss && need) need[i] = 1;
+  }
+}
+
+// to[ids[k] - 1] = rows[k] (row doubles), k < *n
+__global__ void k_scatter_rows(const double *rows, const int *ids, const int *n, int row, double *to) {
+  for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < *n; k += (long long)gridDim.x * blockDim.x)
+    for (int j = 0; j < row; j++) to[(size_t)row * (size_t)(ids[k] - 1) + j] = rows[(size_t)row * (size_t)k + j];
+}
+
+// host rows ids (1-based) of `host` uploaded and scattered into dst
+static int carry_host_rows(pmmg_hip_ctx *c, const std::vector<int> &ids, const double *host, int row, double *dst) {
+  if (ids.empty()) return 1;
+  std::vector<double> rows((size_t)row * ids.size());
+  for (size_t k = 0; k < ids.size(); k++)
+    memcpy(&rows[(size_t)row * k], host + (size_t)row * (size_t)(ids[k] - 1), sizeof(double) * row);
+  const int n = (int)ids.size();
+  if (!upload(c, c->carry_rows, rows.data(), sizeof(double) * rows.size()) ||
+      !upload(c, c->carry_ids, ids.data(), sizeof(int) * ids.size()) || !upload(c, c->carry_cnt, &n, sizeof(int)))
+    return 0;
+  hipLaunchKernelGGL(k_scatter_rows, dim3(blocks_for(n, 4096)), dim3(kBlock), 0, c->stream,
+                     (const double *)c->carry_rows.p, (const int *)c->carry_ids.p, (const int *)c->carry_cnt.p, row,
+                     dst);
+  HIPCK(c, hipGetLastError());
+  return 1;
+}
+
+static void carry_disarm(pmmg_hip_ctx *c) {
+  c->carry_slot = -1;
+  c->carry_bg = false;
+  c->carry_src.clear();
+}
+
+// set_background, host mode, carry armed: the vertices from the slot
+static int carry_vertices(pmmg_hip_ctx *c, int np, const double *xyz) {
+  pmmg_hip_ctx::Kept &k = c->kept[c->carry_slot];
+  if (np != c->carry_np || c->carry_bg) {
+    set_err(c, "set_background: the armed carry-over is for %d vertices (got %d)%s", c->carry_np, np,
+            c->carry_bg ? " and was taken already" : "");
+    carry_disarm(c);
+    return 0;
+  }
+  if (c->carry_src.empty()) {
+    std::swap(c->o_xyz, k.xyz); // every row is a kept point, in order
+  } else {
+    if (!ensure(c, c->o_xyz, sizeof(double) * 3 * (size_t)np) ||
+        !upload(c, c->carry_dsrc, c->carry_src.data(), sizeof(int) * (size_t)np))
+      return 0;
+    hipLaunchKernelGGL(k_carry_gather, dim3(blocks_for(np, 4096)), dim3(kBlock), 0, c->stream,
+                       (const double *)k.xyz.p, 3, (const int *)c->carry_dsrc.p, (long long)np, (double *)c->o_xyz.p,
+                       (uint8_t *)nullptr, 0);
+    std::vector<int> ids;
+    for (int i = 0; i < np; i++)
+      if (c->carry_src[i] == 0) ids.push_back(i + 1);
+    if (!carry_host_rows(c, ids, xyz, 3, (double *)c->o_xyz.p)) return 0;
+  }
+  c->carry_bg = true;
+  return 1;
+}
+
+// set_solutions, host mode, carry armed: the metric and the fields whose
+// sizes match the kept ones from the slot, their missing rows from the host
+static int carry_solutions(pmmg_hip_ctx *c, int met_size, const double *met, int nfield, const int *field_size,
+                           const double *const *fields) {
+  pmmg_hip_ctx::Kept &k = c->kept[c->carry_slot];
+  const int np = c->carry_np;
+  const bool ident = c->carry_src.empty();
+  hipStream_t s = c->stream;
+  if (!c->carry_bg || np != c->bg.np) {
+    set_err(c, "set_solutions: the armed carry-over needs set_background with its %d vertices first", np);
+    carry_disarm(c);
+    return 0;
+  }
+  const long long ncls = np / kScanChunk + 1;
+  if (!ensure(c, c->carry_need, (size_t)np) || !ensure(c, c->carry_ids, sizeof(int) * (size_t)np) ||
+      !ensure(c, c->carry_cnt, sizeof(int)) || !ensure(c, c->carry_bc, sizeof(int) * (size_t)ncls))
+    return 0;
+  HIPCK(c, hipMemsetAsync(c->carry_need.p, 0, (size_t)np, s));
+  struct Arr { DevBuf *dst; const double *host; int row; };
+  std::vector<Arr> carried;
+  auto take = [&](DevBuf &dst, DevBuf &from, const double *host, int row) -> int {
+    if (ident) {
+      std::swap(dst, from);
+      hipLaunchKernelGGL(k_carry_gather, dim3(blocks_for(np, 4096)), dim3(kBlock), 0, s, (const double *)dst.p, row,
+                         (const int *)nullptr, (long long)np, (double *)nullptr, (uint8_t *)c->carry_need.p, 1);
+    } else {
+      if (!ensure(c, dst, sizeof(double) * row * (size_t)np)) return 0;
+      hipLaunchKernelGGL(k_carry_gather, dim3(blocks_for(np, 4096)), dim3(kBlock), 0, s, (const double *)from.p, row,
+                         (const int *)c->carry_dsrc.p, (long long)np, (double *)dst.p, (uint8_t *)c->carry_need.p, 1);
+    }
+    HIPCK(c, hipGetLastError());
+    carried.push_back(Arr{&dst, host, row});
+    return 1;
+  };
+  // what is not carried goes up whole
+  if (met_size) {
+    if (k.met_size == met_size && k.met.p) {
+      if (!take(c->o_met, k.met, met, met_size)) return 0;
+    } else if (!copy_stream(c) || !upload(c, c->o_met, met, sizeof(double) * met_size * (size_t)np, c->cstream)) {
+      return 0;
+    }
+    c->met = (const double *)c->o_met.p;
+  }
+  c->o_f.resize(nfield);
+  for (int j = 0; j < nfield; j++) {
+    if (j < (int)k.f.size() && k.fsize[j] == field_size[j] && k.f[j].p) {
+      if (!take(c->o_f[j], k.f[j], fields[j], field_size[j])) return 0;
+    } else if (!copy_stream(c) ||
+               !upload(c, c->o_f[j], fields[j], sizeof(double) * field_size[j] * (size_t)np, c->cstream)) {
+      return 0;
+    }
+    c->fin[j] = (const double *)c->o_f[j].p;
+  }
+  if (!carried.empty()) {
+    // the rows to fetch from the host: one list for every carried array
+    const uint8_t *need = (const uint8_t *)c->carry_need.p;
+    int *bc = (int *)c->carry_bc.p;
+    hipLaunchKernelGGL(k_cls_count, dim3((unsigned)ncls), dim3(kBlock), 0, s, need, (long long)np, 1, bc,
+                       (const int *)nullptr, 0);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, s, bc, (int)ncls, (int *)c->carry_cnt.p,
+                       (const int *)nullptr, 0);
+    hipLaunchKernelGGL(k_cls_scatter, dim3((unsigned)ncls), dim3(kBlock), 0, s, need, (long long)np, 1,
+                       (const int *)bc, (int *)c->carry_ids.p, (const int *)nullptr, 0);
+    HIPCK(c, hipGetLastError());
+    int n = 0;
+    HIPCK(c, hipMemcpyAsync(&n, c->carry_cnt.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIPCK(c, hipStreamSynchronize(s));
+    std::vector<int> ids((size_t)n);
+    if (n > 0) HIPCK(c, hipMemcpy(ids.data(), c->carry_ids.p, sizeof(int) * (size_t)n, hipMemcpyDeviceToHost));
+    for (const Arr &a : carried)
+      if (!carry_host_rows(c, ids, a.host, a.row, (double *)a.dst->p)) return 0;
+  }
+  if (c->cstream) HIPCK(c, hipStreamSynchronize(c->cstream));
+  HIPCK(c, hipStreamSynchronize(s));
+  k.valid = false; // its buffers now back the background (or were swapped out)
+  carry_disarm(c);
+  return 1;
+}
 
 // shared body of the two background entry points: tet8 != NULL selects the
 // packed {v[4], adja[4]} records, else the separate tetv / adja arrays.
@@ -627,9 +825,18 @@ static int set_background_impl(pmmg_hip_ctx *c, int np, const double *xyz, int n
   c->bg.hausd = hausd;
   // vertices
   if (dev) {
+    if (c->carry_slot >= 0) {
+      set_err(c, "set_background: a carry-over is armed; it takes host-mode (PMMG_HIP_HOST) calls");
+      carry_disarm(c);
+      return 0;
+    }
     c->bg.xyz = xyz;
   } else {
-    if (!upload(c, c->o_xyz, xyz, sizeof(double) * 3 * (size_t)np)) return 0;
+    if (c->carry_slot >= 0) {
+      if (!carry_vertices(c, np, xyz)) return 0;
+    } else if (!upload(c, c->o_xyz, xyz, sizeof(double) * 3 * (size_t)np)) {
+      return 0;
+    }
     c->bg.xyz = (const double *)c->o_xyz.p;
   }
   // tetra
@@ -685,7 +892,8 @@ static int set_background_impl(pmmg_hip_ctx *c, int np, const double *xyz, int n
   // the device snapshot (PMMG_create_oldGrp's arrays): adjacency, boundary
   // trias, tria adjacency, each on the context stream
   auto snapshot = [c, np, ne, d_tetv, build_bdy, tria_adj]() -> int {
-    if (d_tetv && !pmmg_snap_adjacency(c->stream, np, ne, d_tetv, nullptr, (int *)c->o_tetv.p, c->err, sizeof(c->err))) {
+    if (d_tetv && !pmmg_snap_adjacency(c->stream, np, ne, d_tetv, nullptr, (int *)c->o_tetv.p, &c->snap_cache, c->err,
+                                     sizeof(c->err))) {
       fprintf(stderr, "[parmmg_hip] %s\n", c->err);
       return 0;
     }
@@ -694,11 +902,11 @@ static int set_background_impl(pmmg_hip_ctx *c, int np, const double *xyz, int n
       int cnt = 0, ntb = 0;
       char msg[256];
       pmmg_snap_boundary(c->stream, np, ne, t0, c->bg.tstride, a0, c->bg.tstride, nullptr, 0, &cnt, nullptr, nullptr,
-                         msg, sizeof(msg)); // counts (fails on capacity 0 when there are trias)
+                         &c->snap_cache, msg, sizeof(msg)); // counts (fails on capacity 0 when there are trias)
       if (!ensure(c, c->o_triv, sizeof(int) * 3 * (size_t)cnt) || !ensure(c, c->o_adjt, sizeof(int) * 3 * (size_t)cnt))
         return 0;
       if (!pmmg_snap_boundary(c->stream, np, ne, t0, c->bg.tstride, a0, c->bg.tstride, nullptr, cnt, &ntb,
-                              (int *)c->o_triv.p, (int *)c->o_adjt.p, c->err, sizeof(c->err))) {
+                              (int *)c->o_triv.p, (int *)c->o_adjt.p, &c->snap_cache, c->err, sizeof(c->err))) {
         fprintf(stderr, "[parmmg_hip] %s\n", c->err);
         return 0;
       }
@@ -708,7 +916,7 @@ static int set_background_impl(pmmg_hip_ctx *c, int np, const double *xyz, int n
     }
     if (tria_adj) {
       if (!ensure(c, c->o_adjt, sizeof(int) * 3 * (size_t)c->bg.nt)) return 0;
-      if (!pmmg_snap_tria_adjacency(c->stream, np, c->bg.nt, c->bg.triv, (int *)c->o_adjt.p, c->err,
+      if (!pmmg_snap_tria_adjacency(c->stream, np, c->bg.nt, c->bg.triv, (int *)c->o_adjt.p, &c->snap_cache, c->err,
                                     sizeof(c->err))) {
         fprintf(stderr, "[parmmg_hip] %s\n", c->err);
         return 0;
@@ -796,10 +1004,16 @@ int pmmg_hip_set_solutions(pmmg_hip_ctx *c, int met_size, const double *met, int
   c->rec = nullptr;
   c->rstride = 0;
   if (where == PMMG_HIP_DEVICE) {
+    if (c->carry_slot >= 0) {
+      set_err(c, "set_solutions: a carry-over is armed; it takes host-mode (PMMG_HIP_HOST) calls");
+      carry_disarm(c);
+      return 0;
+    }
     c->met = met;
     for (int j = 0; j < nfield; j++) c->fin[j] = fields[j];
     return 1;
   }
+  if (c->carry_slot >= 0) return carry_solutions(c, met_size, met, nfield, field_size, fields);
   // host mode: through the copy stream (beside a deferred snapshot)
   if (met_size) {
     if (!copy_stream(c) || !upload(c, c->o_met, met, sizeof(double) * met_size * np, c->cstream)) return 0;
@@ -863,8 +1077,11 @@ int pmmg_hip_set_solutions_packed(pmmg_hip_ctx *c, int met_size, int nfield, con
 }
 
 // groups with fewer new points take the input order without the coherence
-// test (their background stays cache-resident; see run_device)
-constexpr int kSmallGroup = 1 << 21;
+// test: their background stays in the caches, and the binning costs more
+// than a numbering's locality (r04g, shuffled numberings: cfg2's 205k points
+// 0.19 ms per call in input order, 0.31 Morton-binned; cfg3's 4.1M points
+// 2.74 vs 1.89 ms)
+constexpr int kSmallGroup = 1 << 20;
 
 static int grid_dim(long long n, int per_cell, int gmax) {
   double g = cbrt((double)n / (double)per_cell);
@@ -1082,9 +1299,8 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   if (c->set_order) hipLaunchKernelGGL(k_set_order, dim3(1), dim3(1), 0, s, st, force > 0 ? 1 : 0, c->bin_bits);
 #endif
   if (force != 0 && np_new > 0) {
-    hipLaunchKernelGGL(k_bin_keys, dim3(blocks_for(np_new, 1024)), dim3(kBlock), 0, sb, xyz_new, pclass, np_new,
-                       (const Frame *)fr, flag, (unsigned *)c->bkeys.p, (int *)c->bvals.p, st);
-    // stable LSD radix sort of the keys (<= 3 * 7 + 2 bits) in 3 passes of 8 bits (pmmg_sort.hpp)
+    // stable LSD radix sort of the keys (<= 3 * 7 + 2 bits) in 3 passes of 8 bits (pmmg_sort.hpp); the key
+    // kernel writes the first pass's digit table
     const int ntile = (int)((np_new + kRsTile - 1) / kRsTile);
     const long long nh = 256LL * ntile;
     const int nch = (int)((nh + kScanChunk - 1) / kScanChunk);
@@ -1092,12 +1308,15 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
       return 0;
     unsigned *k0 = (unsigned *)c->bkeys.p, *k1 = (unsigned *)c->bkeys2.p;
     int *v0 = (int *)c->bvals.p, *v1 = (int *)c->bvals2.p, *hist = (int *)c->rs_hist.p, *csum = (int *)c->rs_csum.p;
+    hipLaunchKernelGGL(k_bin_keys, dim3(ntile), dim3(kBlock), 0, sb, xyz_new, pclass, np_new, (const Frame *)fr, flag,
+                       k0, v0, st, kRsTile, ntile, hist);
     for (int pass = 0; pass < 3; pass++) {
       const unsigned *kin = pass == 1 ? k1 : k0;
       const int *vin = pass == 1 ? v1 : v0;
       unsigned *kout = pass == 1 ? k0 : k1;
       int *vout = pass == 1 ? v0 : (pass == 0 ? v1 : order_v);
-      hipLaunchKernelGGL(k_rs_hist, dim3(ntile), dim3(kBlock), 0, sb, kin, np_new, 8 * pass, ntile, hist, flag, 1);
+      if (pass > 0)
+        hipLaunchKernelGGL(k_rs_hist, dim3(ntile), dim3(kBlock), 0, sb, kin, np_new, 8 * pass, ntile, hist, flag, 1);
       hipLaunchKernelGGL(k_rs_scan_local, dim3(nch), dim3(kBlock), 0, sb, hist, (int)nh, csum, flag, 1);
       hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, sb, csum, nch, (int *)nullptr, flag, 1);
       hipLaunchKernelGGL(k_rs_scan_add, dim3(nch), dim3(kBlock), 0, sb, hist, (int)nh, (const int *)csum, flag, 1);
@@ -1325,8 +1544,75 @@ int pmmg_hip_locate_interp(pmmg_hip_ctx *c, int np_new, const double *xyz_new, c
   if (c->verbose)
     fprintf(stderr, "[parmmg_hip] host locate: uploads + enqueue %.2f ms, step + hit codes %.2f ms, rows %.2f ms\n",
             1e3 * (t1 - t0), 1e3 * (t2 - t1), 1e3 * (now_s() - t2));
+  c->last_host_np = np_new; // what pmmg_hip_keep can keep
+  c->last_host_met = c->met_size;
+  c->last_host_fsize = c->fsize;
   if (stats) return collect_stats(c, stats);
   return 1;
+}
+
+// ---- carry-over entry points (see "carry-over" above)
+
+int pmmg_hip_keep(pmmg_hip_ctx *c, int slot) {
+  if (!c) return 0;
+  if (slot < 0 || slot >= 1024) {
+    set_err(c, "keep: slot %d out of [0, 1024)", slot);
+    return 0;
+  }
+  if (c->last_host_np <= 0) {
+    set_err(c, "keep: no host-mode pmmg_hip_locate_interp to keep since the last keep");
+    return 0;
+  }
+  if ((int)c->kept.size() <= slot) c->kept.resize(slot + 1);
+  pmmg_hip_ctx::Kept &k = c->kept[slot];
+  std::swap(k.xyz, c->h_xyz);
+  k.met_size = c->last_host_met;
+  if (k.met_size) std::swap(k.met, c->h_met);
+  k.fsize = c->last_host_fsize;
+  k.f.resize(k.fsize.size());
+  for (size_t j = 0; j < k.f.size(); j++) std::swap(k.f[j], c->h_f[j]);
+  k.np = c->last_host_np;
+  k.valid = true;
+  c->last_host_np = 0;
+  return 1;
+}
+
+int pmmg_hip_carry_over(pmmg_hip_ctx *c, int slot, int np, const int *src) {
+  if (!c) return 0;
+  if (np == 0) { // drop the slot
+    if (slot >= 0 && slot < (int)c->kept.size()) c->kept[slot].valid = false;
+    if (c->carry_slot == slot) carry_disarm(c);
+    return 1;
+  }
+  if (slot < 0 || slot >= (int)c->kept.size() || !c->kept[slot].valid) {
+    set_err(c, "carry_over: slot %d holds nothing (pmmg_hip_keep after a host-mode call)", slot);
+    return 0;
+  }
+  const pmmg_hip_ctx::Kept &k = c->kept[slot];
+  if (np <= 0 || (!src && np != k.np)) {
+    set_err(c, "carry_over: %d vertices for %d kept points without a map", np, k.np);
+    return 0;
+  }
+  c->carry_src.clear();
+  if (src) {
+    for (int i = 0; i < np; i++)
+      if (src[i] < 0 || src[i] > k.np) {
+        set_err(c, "carry_over: src[%d] = %d out of [0, %d]", i, src[i], k.np);
+        return 0;
+      }
+    c->carry_src.assign(src, src + np);
+  }
+  c->carry_slot = slot;
+  c->carry_np = np;
+  c->carry_bg = false;
+  return 1;
+}
+
+int64_t pmmg_hip_bytes_up(pmmg_hip_ctx *c, int reset) {
+  if (!c) return -1;
+  const int64_t b = c->bytes_up;
+  if (reset) c->bytes_up = 0;
+  return b;
 }
 
 // ---- many groups in one call
@@ -1429,7 +1715,7 @@ int pmmg_hip_build_adjacency(pmmg_hip_ctx *c, int np, int ne, const int *tetv, i
     set_err(c, "build_adjacency: device arrays must be 16-byte aligned");
     return 0;
   }
-  return pmmg_snap_adjacency(c->stream, np, ne, tetv, adja, tet8, c->err, sizeof(c->err));
+  return pmmg_snap_adjacency(c->stream, np, ne, tetv, adja, tet8, &c->snap_cache, c->err, sizeof(c->err));
 }
 
 int pmmg_hip_tetra_qual(pmmg_hip_ctx *c, int np, const double *xyz, int ne, const int *tetv, int met_size,
@@ -1522,7 +1808,7 @@ int pmmg_hip_build_boundary(pmmg_hip_ctx *c, int np, int ne, const int *tet8, co
     return 0;
   }
   return pmmg_snap_boundary(c->stream, np, ne, t0, packed ? 2 : 1, a0, packed ? 2 : 1, tref, cap, nt, triv, adjt,
-                            c->err, sizeof(c->err));
+                            &c->snap_cache, c->err, sizeof(c->err));
 }
 
 void *pmmg_hip_malloc(pmmg_hip_ctx *c, int64_t bytes) {

@@ -166,8 +166,8 @@ static void stats_add(pmmg_hip_stats *a, const pmmg_hip_stats *b) {
   a->seed_map_axes |= b->seed_map_axes;
 }
 
-int pmmg_interp_metrics_and_fields(pmmg_hip_ctx *ctx, int ngrp, const pmmg_old_group *old, pmmg_new_group *grp,
-                                   int input_met, pmmg_hip_stats *stats) {
+static int interp_groups(pmmg_hip_ctx *ctx, int ngrp, const pmmg_old_group *old, pmmg_new_group *grp, int input_met,
+                         int keep, int carried, const int *const *src, pmmg_hip_stats *stats) {
   if (!ctx) {
     fprintf(stderr, "[parmmg_host] no HIP context: the transfer step has no CPU fallback\n");
     return 0;
@@ -182,14 +182,31 @@ int pmmg_interp_metrics_and_fields(pmmg_hip_ctx *ctx, int ngrp, const pmmg_old_g
     if (input_met != 1) {
       ismet = 0;
     } else if (g->hsiz > 0.0) {
-      if (!pmmg_set_constant_metric(g)) { ier = 0; continue; }
+      if (!pmmg_set_constant_metric(g)) {
+        if (keep) pmmg_hip_carry_over(ctx, ig, 0, NULL);
+        ier = 0;
+        continue;
+      }
       ismet = 0;
     }
-    if (!ismet && o->nfield == 0) continue; /* nothing to do */
-    if (ismet && (o->met_size == 0 || g->met_size != o->met_size || !g->met)) { ier = 0; continue; }
+    /* a group left out drops what was kept for it (its next old group is
+     * not this call's output) */
+    if (!ismet && o->nfield == 0) { /* nothing to do */
+      if (keep) pmmg_hip_carry_over(ctx, ig, 0, NULL);
+      continue;
+    }
+    if (ismet && (o->met_size == 0 || g->met_size != o->met_size || !g->met)) {
+      if (keep) pmmg_hip_carry_over(ctx, ig, 0, NULL);
+      ier = 0;
+      continue;
+    }
     uint8_t *pclass = (uint8_t *)malloc((size_t)g->np + 1);
     if (!pclass) { ier = 0; continue; }
     pmmg_classify_points(g, pclass);
+    /* the previous iteration's new group ig, kept on the device: carried
+     * unless nothing was kept for it (then it goes up whole) */
+    if (carried && !pmmg_hip_carry_over(ctx, ig, o->np, src ? src[ig] : NULL))
+      fprintf(stderr, "[parmmg_host] group %d: no carry-over (%s), uploading it\n", ig, pmmg_hip_last_error(ctx));
     /* the background: adjacency and boundary trias are built on the device
      * when the caller does not hand them over (set_background, adja / triv
      * NULL) */
@@ -202,8 +219,21 @@ int pmmg_interp_metrics_and_fields(pmmg_hip_ctx *ctx, int ngrp, const pmmg_old_g
       ok = pmmg_hip_locate_interp(ctx, g->np, g->xyz, pclass, ismet ? g->met : NULL, g->field, g->elem, g->hit,
                                   &st, PMMG_HIP_HOST);
     if (ok && stats) stats_add(stats, &st);
+    if (ok && keep) ok = pmmg_hip_keep(ctx, ig);
+    if (!ok && keep) pmmg_hip_carry_over(ctx, ig, 0, NULL);
     if (!ok) ier = 0;
     free(pclass);
   }
   return ier;
+}
+
+int pmmg_interp_metrics_and_fields(pmmg_hip_ctx *ctx, int ngrp, const pmmg_old_group *old, pmmg_new_group *grp,
+                                   int input_met, pmmg_hip_stats *stats) {
+  return interp_groups(ctx, ngrp, old, grp, input_met, 0, 0, NULL, stats);
+}
+
+int pmmg_interp_metrics_and_fields_carry(pmmg_hip_ctx *ctx, int ngrp, const pmmg_old_group *old,
+                                         pmmg_new_group *grp, int input_met, int carried, const int *const *src,
+                                         pmmg_hip_stats *stats) {
+  return interp_groups(ctx, ngrp, old, grp, input_met, 1, carried, src, stats);
 }

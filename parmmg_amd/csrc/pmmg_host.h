@@ -93,6 +93,20 @@ int pmmg_set_constant_metric(pmmg_new_group *g);
 int pmmg_interp_metrics_and_fields(pmmg_hip_ctx *ctx, int ngrp, const pmmg_old_group *old, pmmg_new_group *grp,
                                    int input_met, pmmg_hip_stats *stats);
 
+/* The same over the iterations of a run (src/libparmmg1.c:653: the adapted
+ * groups become the next old groups): every group's new points and the rows
+ * the step wrote stay on the device (pmmg_hip_keep, slot = group index), and
+ * with carried = 1 old group ig IS the previous call's new group ig — its
+ * vertex i+1 is that group's point src[ig][i] (1-based, 0: not carried, e.g.
+ * moved in by load balancing; src or src[ig] NULL: the same numbering) — so
+ * only its connectivity and the rows the device does not hold go up
+ * (pmmg_hip_carry_over).  A group whose previous rows are not kept (it was
+ * skipped, or its point count changed without a map) goes up whole.  The
+ * kept rows must not have been modified on the host in between. */
+int pmmg_interp_metrics_and_fields_carry(pmmg_hip_ctx *ctx, int ngrp, const pmmg_old_group *old,
+                                         pmmg_new_group *grp, int input_met, int carried, const int *const *src,
+                                         pmmg_hip_stats *stats);
+
 /* ---- halo shards of a background group (pmmg_shard.c) ----
  * All arrays in the "row r = entity r+1" layout of parmmg_hip.h. */
 

@@ -757,13 +757,24 @@ __global__ __launch_bounds__(kBlock) void k_coherence(const double *xyz, int np,
 // is a deterministic function of the input.
 
 // flag: the order decision {sorted, bits per axis} (k_coherence); the kernel
-// runs only when flag[0] == 1
+// runs only when flag[0] == 1.  One block per radix-sort tile (tile_keys
+// keys, pmmg_sort.hpp): besides the keys it writes the tile's histogram of
+// the first 8-bit digit (hist[digit * ntile + tile]), the first pass's table.
 __global__ __launch_bounds__(kBlock) void k_bin_keys(const double *xyz, const uint8_t *pclass, int np, const Frame *fr,
-                                                     const int *flag, unsigned *keys, int *vals, DevStats *st) {
+                                                     const int *flag, unsigned *keys, int *vals, DevStats *st,
+                                                     int tile_keys, int ntile, int *hist) {
   if (flag[0] != 1) return;
   const int bits = flag[1];
+  __shared__ int h[kBlock];
+  __shared__ int sv, sb;
+  h[threadIdx.x] = 0;
+  if (threadIdx.x == 0) sv = sb = 0;
+  __syncthreads();
   int nv = 0, nb = 0;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < np; i += (long long)gridDim.x * blockDim.x) {
+  const long long base = (long long)blockIdx.x * tile_keys;
+  for (int e = threadIdx.x; e < tile_keys; e += kBlock) {
+    const long long i = base + e;
+    if (i >= np) break;
     const int c = pclass[i];
     unsigned cls = 2u;
     uint32_t q[3] = {0u, 0u, 0u};
@@ -776,12 +787,11 @@ __global__ __launch_bounds__(kBlock) void k_bin_keys(const double *xyz, const ui
         q[d] = (uint32_t)cell_coord(xyz[3 * i + d], fr->lo[d], fr->inv_bin[d], 1 << kBinBitsAxis) >>
                (kBinBitsAxis - bits);
     }
-    keys[i] = (cls << (3 * bits)) | (expand10(q[0]) << 2) | (expand10(q[1]) << 1) | expand10(q[2]);
+    const unsigned key = (cls << (3 * bits)) | (expand10(q[0]) << 2) | (expand10(q[1]) << 1) | expand10(q[2]);
+    keys[i] = key;
     vals[i] = (int)(i + 1);
+    atomicAdd(&h[key & 255u], 1);
   }
-  __shared__ int sv, sb;
-  if (threadIdx.x == 0) sv = sb = 0;
-  __syncthreads();
   for (int o = 32; o > 0; o >>= 1) {
     nv += __shfl_down(nv, o);
     nb += __shfl_down(nb, o);
@@ -791,6 +801,7 @@ __global__ __launch_bounds__(kBlock) void k_bin_keys(const double *xyz, const ui
     atomicAdd(&sb, nb);
   }
   __syncthreads();
+  hist[(size_t)threadIdx.x * ntile + blockIdx.x] = h[threadIdx.x];
   if (threadIdx.x == 0) {
     if (sv) atomicAdd(&st->nvol, sv);
     if (sb) atomicAdd(&st->nbdy, sb);

@@ -23,8 +23,13 @@
 // id — count with atomics, exclusive scan, scatter {other ids, code} — then
 // each face (edge) scans its own bucket (~24 faces per vertex in a tetra
 // mesh) for its twin.  The match is a pure function of the connectivity, so
-// the result does not depend on the atomic order.  Everything is a stream of
-// the connectivity plus small L2-resident bucket scans: HBM-bound.
+// the result does not depend on the atomic order.  Tetra faces (r04): the
+// counting atomics are combined per wave (consecutive tetra share their
+// smallest vertex), and the twins are found bucket by bucket — a block loads
+// the buckets of 64 consecutive vertices into LDS with one coalesced read and
+// every face scans its bucket there, writing its adjacency entry (r03: one
+// thread per tetra scanning two buckets in HBM, 9.3 of the 22 ms, latency-
+// bound).  Scratch buffers are kept by the context (SnapCache).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -82,22 +87,48 @@ __device__ __forceinline__ bool tet_ids_ok(const int4 &t, int np) {
   return ok;
 }
 
-// rank[k] = {slot of the s0 faces (3 consecutive), slot of the s1 face}
-__global__ __launch_bounds__(kB) void k_face_count(const int4 *tetv, int ne, int np, int *cnt, int2 *rank,
-                                                   int *err) {
-  const int k = blockIdx.x * kB + threadIdx.x;
-  if (k >= ne) return;
-  const int4 t = tetv[k];
-  if (!tet_ids_ok(t, np)) {
-    atomicOr(err, kErrIds);
-    rank[k] = make_int2(-1, -1);
-    return;
+// cnt[idx] += val for the active lanes, returning each lane's old value plus
+// the contributions of the lower lanes with the same idx: lanes with equal
+// idx share one atomic (up to kAggRounds distinct idx per wave; the rest
+// issue their own)
+constexpr int kAggRounds = 6;
+__device__ __forceinline__ int wave_add(int *cnt, int idx, int val, bool act) {
+  const int lane = __lane_id();
+  unsigned long long todo = __ballot(act);
+  int res = 0;
+#pragma unroll 1
+  for (int r = 0; r < kAggRounds && todo; r++) {
+    const int leader = __ffsll((long long)todo) - 1;
+    const int li = __shfl(idx, leader);
+    const unsigned long long m = __ballot(act && idx == li) & todo;
+    int old = 0;
+    if (lane == leader) old = atomicAdd(&cnt[li], val * __popcll(m));
+    old = __shfl(old, leader);
+    if ((m >> lane) & 1ULL) res = old + val * __popcll(m & ((1ULL << lane) - 1ULL));
+    todo &= ~m;
   }
-  int i0, i1;
+  if ((todo >> lane) & 1ULL) res = atomicAdd(&cnt[idx], val);
+  return res;
+}
+
+// rank[k] = {slot of the s0 faces (3 consecutive), slot of the s1 face};
+// the vertex half of the tet8 record goes out here (the adjacency half is
+// written face by face by k_face_match)
+__global__ __launch_bounds__(kB) void k_face_count(const int4 *tetv, int ne, int np, int *cnt, int2 *rank,
+                                                   int4 *tet8, int *err) {
+  const int k = blockIdx.x * kB + threadIdx.x;
+  const bool in = k < ne;
+  const int4 t = in ? tetv[k] : make_int4(1, 2, 3, 4);
+  const bool ok = in && tet_ids_ok(t, np);
+  if (in && !ok) atomicOr(err, kErrIds);
+  int i0 = 0, i1 = 1;
   two_smallest(t, i0, i1);
-  const int r0 = atomicAdd(&cnt[sel(t, i0) - 1], 3);
-  const int r1 = atomicAdd(&cnt[sel(t, i1) - 1], 1);
-  rank[k] = make_int2(r0, r1);
+  const int r0 = wave_add(cnt, sel(t, i0) - 1, 3, ok);
+  const int r1 = wave_add(cnt, sel(t, i1) - 1, 1, ok);
+  if (in) {
+    rank[k] = ok ? make_int2(r0, r1) : make_int2(-1, -1);
+    if (tet8) tet8[2 * (size_t)k] = t;
+  }
 }
 
 __global__ __launch_bounds__(kB) void k_face_scatter(const int4 *tetv, int ne, const int *off, const int2 *rank,
@@ -121,47 +152,57 @@ __global__ __launch_bounds__(kB) void k_face_scatter(const int4 *tetv, int ne, c
   }
 }
 
-// one thread per tetra: the 4 twins, one adjacency row (and one tet8 record)
-__global__ __launch_bounds__(kB) void k_face_match(const int4 *tetv, int ne, int np, const int *off, const int *cnt,
-                                                   const int4 *bucket, int4 *adja, int4 *tet8, int *err) {
-  const int k = blockIdx.x * kB + threadIdx.x;
-  if (k >= ne) return;
-  const int4 t = tetv[k];
-  int code[4] = {0, 0, 0, 0};
-  if (tet_ids_ok(t, np)) { // invalid tetra were flagged by k_face_count
-    int i0, i1;
-    two_smallest(t, i0, i1);
-    int fb[4], fc[4], found[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      int a;
-      face_ids(t, i, a, fb[i], fc[i]);
+// The buckets of kMatchVerts consecutive vertices per block (contiguous
+// entries), staged in LDS when they fit in kMatchCap entries, else scanned
+// in place; every face writes its entry of the adjacency: its twin's code, 0
+// on the boundary.  Invalid tetra (flagged by k_face_count) have no faces in
+// the buckets: their rows are zeroed by k_face_invalid.
+constexpr int kMatchVerts = 64, kMatchCap = 2048;
+__global__ __launch_bounds__(kB) void k_face_match(int np, const int *off, const int *cnt, const int4 *bucket,
+                                                   int *adja, int *tet8, int *err) {
+  __shared__ int4 ent[kMatchCap];
+  __shared__ int loff[kMatchVerts + 1];
+  const int v0 = blockIdx.x * kMatchVerts, nv = min(kMatchVerts, np - v0);
+  if (threadIdx.x <= nv) loff[threadIdx.x] = threadIdx.x < nv ? off[v0 + threadIdx.x] : off[v0 + nv - 1] + cnt[v0 + nv - 1];
+  __syncthreads();
+  const int e0 = loff[0], n = loff[nv] - e0;
+  const bool staged = n <= kMatchCap;
+  if (staged)
+    for (int j = threadIdx.x; j < n; j += kB) ent[j] = bucket[e0 + j];
+  __syncthreads();
+  const int4 *src = staged ? ent : bucket + e0;
+  int bad = 0;
+  for (int j = threadIdx.x; j < n; j += kB) {
+    // the bucket of entry j: the last local offset <= j
+    int lo = 0, hi = nv; // loff[lo] - e0 <= j < loff[hi] - e0
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (loff[mid] - e0 <= j) lo = mid;
+      else hi = mid;
     }
-    // bucket of s0: the three faces other than i0; bucket of s1: face i0
-#pragma unroll
-    for (int pass = 0; pass < 2; pass++) {
-      const int v = pass == 0 ? sel(t, i0) : sel(t, i1);
-      const int lo = off[v - 1], n = cnt[v - 1];
-      for (int j = 0; j < n; j++) {
-        const int4 e = bucket[lo + j];
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-          if ((i == i0) != (pass == 1)) continue;
-          if (e.x == fb[i] && e.y == fc[i] && e.z != 4 * (k + 1) + i) {
-            if (!found[i]) code[i] = e.z;
-            found[i]++;
-          }
-        }
+    const int b0 = loff[lo] - e0, b1 = loff[lo + 1] - e0;
+    const int4 me = src[j];
+    int twin = 0, found = 0;
+    for (int q = b0; q < b1; q++) {
+      const int4 o = src[q];
+      if (q != j && o.x == me.x && o.y == me.y) {
+        if (!found) twin = o.z;
+        found++;
       }
     }
-    if (found[0] > 1 || found[1] > 1 || found[2] > 1 || found[3] > 1) atomicOr(err, kErrNonManifold);
+    bad |= found > 1;
+    const size_t k = (size_t)(me.z >> 2) - 1, i = (size_t)(me.z & 3);
+    if (adja) adja[4 * k + i] = twin;
+    if (tet8) tet8[8 * k + 4 + i] = twin;
   }
-  const int4 row = make_int4(code[0], code[1], code[2], code[3]);
-  if (adja) adja[k] = row;
-  if (tet8) {
-    tet8[2 * (size_t)k] = t;
-    tet8[2 * (size_t)k + 1] = row;
-  }
+  if (bad) atomicOr(err, kErrNonManifold);
+}
+
+__global__ __launch_bounds__(kB) void k_face_invalid(int ne, const int2 *rank, int4 *adja, int4 *tet8) {
+  const int k = blockIdx.x * kB + threadIdx.x;
+  if (k >= ne || rank[k].x >= 0) return;
+  if (adja) adja[k] = make_int4(0, 0, 0, 0);
+  if (tet8) tet8[2 * (size_t)k + 1] = make_int4(0, 0, 0, 0);
 }
 
 // ---- boundary trias
@@ -260,20 +301,33 @@ __global__ __launch_bounds__(kB) void k_edge_match(const int *triv, int nt, cons
 
 int blocks(long long n) { return (int)((n + kB - 1) / kB > 0 ? (n + kB - 1) / kB : 1); }
 
+// device scratch: slot i of the context's cache (grown, never shrunk), or a
+// temporary freed at the end of the call when there is no cache
 struct Scratch {
-  static constexpr int kMax = 16;
-  void *p[kMax] = {};
-  int n = 0;
+  SnapCache *cache;
+  void *tmp[SnapCache::kSlots] = {};
+  explicit Scratch(SnapCache *c) : cache(c) {}
   ~Scratch() {
-    for (int i = 0; i < n; i++) (void)hipFree(p[i]);
+    for (void *q : tmp)
+      if (q) (void)hipFree(q);
   }
   template <class T>
-  T *get(size_t count) {
-    if (n >= kMax) return nullptr;
-    void *q = nullptr;
-    if (hipMalloc(&q, count * sizeof(T) > 0 ? count * sizeof(T) : 16) != hipSuccess) return nullptr;
-    p[n++] = q;
-    return static_cast<T *>(q);
+  T *get(int slot, size_t count) {
+    const size_t bytes = count * sizeof(T) > 0 ? count * sizeof(T) : 16;
+    if (cache) {
+      if (cache->cap[slot] < bytes) {
+        if (cache->p[slot]) (void)hipFree(cache->p[slot]);
+        cache->p[slot] = nullptr;
+        cache->cap[slot] = 0;
+        if (hipMalloc(&cache->p[slot], bytes) != hipSuccess) return nullptr;
+        cache->cap[slot] = bytes;
+      }
+      return static_cast<T *>(cache->p[slot]);
+    }
+    if (tmp[slot]) (void)hipFree(tmp[slot]);
+    tmp[slot] = nullptr;
+    if (hipMalloc(&tmp[slot], bytes) != hipSuccess) return nullptr;
+    return static_cast<T *>(tmp[slot]);
   }
 };
 
@@ -286,10 +340,11 @@ struct Scratch {
     }                                                                                               \
   } while (0)
 
+constexpr int kSlotScan = SnapCache::kSlots - 1;
 int exclusive_scan(Scratch &S, const int *in, int *out, int n, hipStream_t s, char *msg, size_t msglen) {
   size_t tb = 0;
   SCK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, n, s));
-  void *tmp = S.get<char>(tb);
+  void *tmp = S.get<char>(kSlotScan, tb);
   if (!tmp) { snprintf(msg, msglen, "out of device memory (scan)"); return 0; }
   SCK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, in, out, n, s));
   return 1;
@@ -297,13 +352,13 @@ int exclusive_scan(Scratch &S, const int *in, int *out, int n, hipStream_t s, ch
 
 } // namespace
 
-int pmmg_snap_adjacency(hipStream_t s, int np, int ne, const int *tetv, int *adja, int *tet8, char *msg,
-                        size_t msglen) {
-  Scratch S;
+int pmmg_snap_adjacency(hipStream_t s, int np, int ne, const int *tetv, int *adja, int *tet8, SnapCache *cache,
+                        char *msg, size_t msglen) {
+  Scratch S(cache);
   const long long nf = 4LL * ne;
-  int *cnt = S.get<int>((size_t)np), *off = S.get<int>((size_t)np), *err = S.get<int>(1);
-  int2 *rank = S.get<int2>((size_t)ne);
-  int4 *bucket = S.get<int4>((size_t)nf);
+  int *cnt = S.get<int>(0, (size_t)np), *off = S.get<int>(1, (size_t)np), *err = S.get<int>(2, 1);
+  int2 *rank = S.get<int2>(3, (size_t)ne);
+  int4 *bucket = S.get<int4>(4, (size_t)nf);
   if (!cnt || !off || !rank || !err || !bucket) {
     snprintf(msg, msglen, "build_adjacency: out of device memory (%lld faces)", nf);
     return 0;
@@ -311,11 +366,14 @@ int pmmg_snap_adjacency(hipStream_t s, int np, int ne, const int *tetv, int *adj
   SCK(hipMemsetAsync(cnt, 0, sizeof(int) * (size_t)np, s));
   SCK(hipMemsetAsync(err, 0, sizeof(int), s));
   const int4 *tv = reinterpret_cast<const int4 *>(tetv);
-  hipLaunchKernelGGL(k_face_count, dim3(blocks(ne)), dim3(kB), 0, s, tv, ne, np, cnt, rank, err);
+  hipLaunchKernelGGL(k_face_count, dim3(blocks(ne)), dim3(kB), 0, s, tv, ne, np, cnt, rank,
+                     reinterpret_cast<int4 *>(tet8), err);
   if (!exclusive_scan(S, cnt, off, np, s, msg, msglen)) return 0;
   hipLaunchKernelGGL(k_face_scatter, dim3(blocks(ne)), dim3(kB), 0, s, tv, ne, off, rank, bucket);
-  hipLaunchKernelGGL(k_face_match, dim3(blocks(ne)), dim3(kB), 0, s, tv, ne, np, off, cnt, bucket,
-                     reinterpret_cast<int4 *>(adja), reinterpret_cast<int4 *>(tet8), err);
+  hipLaunchKernelGGL(k_face_match, dim3((np + kMatchVerts - 1) / kMatchVerts), dim3(kB), 0, s, np, off, cnt, bucket,
+                     adja, tet8, err);
+  hipLaunchKernelGGL(k_face_invalid, dim3(blocks(ne)), dim3(kB), 0, s, ne, rank, reinterpret_cast<int4 *>(adja),
+                     reinterpret_cast<int4 *>(tet8));
   SCK(hipGetLastError());
   int h_err = 0;
   SCK(hipMemcpyAsync(&h_err, err, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -325,13 +383,23 @@ int pmmg_snap_adjacency(hipStream_t s, int np, int ne, const int *tetv, int *adj
   return 1;
 }
 
-int pmmg_snap_tria_adjacency(hipStream_t s, int np, int nt, const int *triv, int *adjt, char *msg, size_t msglen) {
+void pmmg_snap_cache_free(SnapCache *c) {
+  if (!c) return;
+  for (int i = 0; i < SnapCache::kSlots; i++) {
+    if (c->p[i]) (void)hipFree(c->p[i]);
+    c->p[i] = nullptr;
+    c->cap[i] = 0;
+  }
+}
+
+int pmmg_snap_tria_adjacency(hipStream_t s, int np, int nt, const int *triv, int *adjt, SnapCache *cache, char *msg,
+                             size_t msglen) {
   if (nt == 0) return 1;
-  Scratch S;
+  Scratch S(cache);
   const long long nedge = 3LL * nt;
-  int *cnt = S.get<int>((size_t)np), *off = S.get<int>((size_t)np), *rank = S.get<int>((size_t)nedge);
-  int2 *bucket = S.get<int2>((size_t)nedge);
-  int *err = S.get<int>(1);
+  int *cnt = S.get<int>(0, (size_t)np), *off = S.get<int>(1, (size_t)np), *rank = S.get<int>(3, (size_t)nedge);
+  int2 *bucket = S.get<int2>(4, (size_t)nedge);
+  int *err = S.get<int>(2, 1);
   if (!cnt || !off || !rank || !bucket || !err) {
     snprintf(msg, msglen, "tria adjacency: out of device memory");
     return 0;
@@ -354,9 +422,10 @@ int pmmg_snap_tria_adjacency(hipStream_t s, int np, int nt, const int *triv, int
 }
 
 int pmmg_snap_boundary(hipStream_t s, int np, int ne, const int *tetv, int tstride, const int *adja, int astride,
-                       const int *tref, int cap, int *nt_out, int *triv, int *adjt, char *msg, size_t msglen) {
-  Scratch S;
-  int *nb = S.get<int>((size_t)ne), *toff = S.get<int>((size_t)ne);
+                       const int *tref, int cap, int *nt_out, int *triv, int *adjt, SnapCache *cache, char *msg,
+                       size_t msglen) {
+  Scratch S(cache);
+  int *nb = S.get<int>(5, (size_t)ne), *toff = S.get<int>(6, (size_t)ne);
   if (!nb || !toff) { snprintf(msg, msglen, "build_boundary: out of device memory"); return 0; }
   const int4 *tv = reinterpret_cast<const int4 *>(tetv), *ad = reinterpret_cast<const int4 *>(adja);
   hipLaunchKernelGGL(k_bdy_count, dim3(blocks(ne)), dim3(kB), 0, s, ad, astride, tref, ne, nb);
@@ -371,7 +440,7 @@ int pmmg_snap_boundary(hipStream_t s, int np, int ne, const int *tetv, int tstri
   if (nt == 0) return 1;
   hipLaunchKernelGGL(k_bdy_write, dim3(blocks(ne)), dim3(kB), 0, s, tv, tstride, ad, astride, tref, ne, toff, triv);
   SCK(hipGetLastError());
-  if (adjt && !pmmg_snap_tria_adjacency(s, np, nt, triv, adjt, msg, msglen)) return 0;
+  if (adjt && !pmmg_snap_tria_adjacency(s, np, nt, triv, adjt, cache, msg, msglen)) return 0;
   SCK(hipStreamSynchronize(s));
   return 1;
 }

@@ -9,10 +9,10 @@
 // cannot be skipped from the device).
 //
 // Per pass: k_rs_hist counts the digits of each tile of kRsTile keys (LDS
-// histogram, digit-major table hist[digit][tile]), k_rs_scan_* turns the
-// table into each (digit, tile)'s first output position, and k_rs_scatter
-// ranks each tile's keys stably — sub-tiles of 256 keys in input order, a
-// wave's lanes with equal digits found by 8 ballots — and writes them there.
+// histogram, digit-major table hist[digit][tile]; the first pass's table
+// comes from the key kernel, k_bin_keys), k_rs_scan_* turns the table into
+// each (digit, tile)'s first output position, and k_rs_scatter sorts each
+// tile stably by digit in LDS and writes the digits' runs there.
 #pragma once
 
 #include "pmmg_prep.hpp"
@@ -67,23 +67,45 @@ __global__ __launch_bounds__(kBlock) void k_rs_scan_add(int *a, int n, const int
     if (i0 + j < n) a[i0 + j] += o;
 }
 
+// One tile per block: the tile's keys are first ranked stably by digit into
+// LDS (sub-tiles of 256 keys in input order; a wave's lanes with equal digits
+// found by 8 ballots), then written out in that order, so consecutive threads
+// store consecutive positions of one digit's run (r04g: ranking straight to
+// global memory wrote every key as an isolated 4-byte store, 0.44 ms per pass
+// of 20M random keys).
 __global__ __launch_bounds__(kBlock) void k_rs_scatter(const unsigned *kin, const int *vin, int n, int shift, int ntile,
                                                        const int *off, unsigned *kout, int *vout, const int *gate,
                                                        int want) {
   if (gate_off(gate, want)) return;
-  __shared__ int run[256];     // next output position of each digit for this tile
-  __shared__ int wcnt[4][256]; // keys of each digit in each wave of the current sub-tile
-  run[threadIdx.x] = off[(size_t)threadIdx.x * ntile + blockIdx.x];
-#pragma unroll
-  for (int w = 0; w < 4; w++) wcnt[w][threadIdx.x] = 0;
-  __syncthreads();
-  const int w = threadIdx.x >> 6, lane = __lane_id();
+  __shared__ unsigned lk[kRsTile]; // the tile, sorted by digit (stable)
+  __shared__ int lv[kRsTile];
+  __shared__ int run[256];         // next local position of each digit
+  __shared__ int gdelta[256];      // global position - local position of each digit's keys
+  __shared__ int wcnt[4][256];     // keys of each digit in each wave of the current sub-tile
+  const int t = threadIdx.x, w = t >> 6, lane = __lane_id();
   const long long base = (long long)blockIdx.x * kRsTile;
+  const int cnt = (int)(n - base < kRsTile ? n - base : kRsTile);
+  // the tile's digit counts, their exclusive scan
+  run[t] = 0;
+#pragma unroll
+  for (int q = 0; q < 4; q++) wcnt[q][t] = 0;
+  __syncthreads();
   for (int j = 0; j < kRsItems; j++) {
-    const long long idx = base + j * kBlock + threadIdx.x;
-    const bool ok = idx < n;
-    const unsigned key = ok ? kin[idx] : 0u;
-    const int val = ok ? vin[idx] : 0;
+    const int e = j * kBlock + t;
+    if (e < cnt) atomicAdd(&run[(kin[base + e] >> shift) & 255u], 1);
+  }
+  __syncthreads();
+  int tot;
+  const int lstart = block_excl_scan(run[t], &tot);
+  __syncthreads();
+  run[t] = lstart;
+  gdelta[t] = off[(size_t)t * ntile + blockIdx.x] - lstart;
+  __syncthreads();
+  for (int j = 0; j < kRsItems; j++) {
+    const int e = j * kBlock + t;
+    const bool ok = e < cnt;
+    const unsigned key = ok ? kin[base + e] : 0u;
+    const int val = ok ? vin[base + e] : 0;
     const unsigned d = (key >> shift) & 255u;
     unsigned long long same = __ballot(ok);
 #pragma unroll
@@ -97,16 +119,19 @@ __global__ __launch_bounds__(kBlock) void k_rs_scatter(const unsigned *kin, cons
     if (ok) {
       int pos = run[d] + rank;
       for (int w2 = 0; w2 < w; w2++) pos += wcnt[w2][d];
-      kout[pos] = key;
-      vout[pos] = val;
+      lk[pos] = key;
+      lv[pos] = val;
     }
     __syncthreads();
-    {
-      const int dd = threadIdx.x;
-      run[dd] += wcnt[0][dd] + wcnt[1][dd] + wcnt[2][dd] + wcnt[3][dd];
-      wcnt[0][dd] = wcnt[1][dd] = wcnt[2][dd] = wcnt[3][dd] = 0;
-    }
+    run[t] += wcnt[0][t] + wcnt[1][t] + wcnt[2][t] + wcnt[3][t];
+    wcnt[0][t] = wcnt[1][t] = wcnt[2][t] = wcnt[3][t] = 0;
     __syncthreads();
+  }
+  for (int e = t; e < cnt; e += kBlock) {
+    const unsigned key = lk[e];
+    const int pos = gdelta[(key >> shift) & 255u] + e;
+    kout[pos] = key;
+    vout[pos] = lv[e];
   }
 }
 

@@ -176,11 +176,12 @@ class TransferContext:
                                                        float(hausd), where), "set_background_tet8")
 
     # ------------------------------------------------------------------ background snapshot
-    def build_adjacency(self, npt: int, tetv: DeviceArray, adja: bool = True, tet8: bool = True):
-        """Device-side MMG3D_hashTetra: (adja, tet8) DeviceArrays (None when not requested)."""
+    def build_adjacency(self, npt: int, tetv: DeviceArray, adja: bool = True, tet8: bool = True, out=None):
+        """Device-side MMG3D_hashTetra: (adja, tet8) DeviceArrays (None when
+        not requested); out = (adja, tet8) arrays to fill instead of new ones."""
         ne = tetv.shape[0]
-        a = self.empty((ne, 4), np.int32) if adja else None
-        t = self.empty((ne, 8), np.int32) if tet8 else None
+        a = (out[0] if out and out[0] is not None else self.empty((ne, 4), np.int32)) if adja else None
+        t = (out[1] if out and out[1] is not None else self.empty((ne, 8), np.int32)) if tet8 else None
         self._ck(self.lib.pmmg_hip_build_adjacency(self.h, int(npt), ne, _p(tetv), _p(a), _p(t)), "build_adjacency")
         return a, t
 
@@ -264,6 +265,22 @@ class TransferContext:
         self._ck(self.lib.pmmg_hip_locate_interp_groups(self.h, len(groups), ctypes.cast(G, ctypes.c_void_p),
                                                         ctypes.byref(st) if sync else None), "locate_interp_groups")
         return st if sync else None
+
+    def keep(self, slot: int = 0) -> None:
+        """pmmg_hip_keep: the last host-mode call's new points and written rows
+        stay on the device in `slot` (the next iteration's background)."""
+        self._ck(self.lib.pmmg_hip_keep(self.h, int(slot)), "keep")
+
+    def carry_over(self, slot: int, npt: int, src=None) -> None:
+        """pmmg_hip_carry_over: the next host-mode set_background /
+        set_solutions take vertex i+1 from kept point src[i] (1-based, 0: from
+        the host arrays; None: the identity)."""
+        s = None if src is None else np.ascontiguousarray(src, np.int32)
+        self._ck(self.lib.pmmg_hip_carry_over(self.h, int(slot), int(npt), _p(s)), "carry_over")
+
+    def bytes_up(self, reset: bool = False) -> int:
+        """host -> device bytes of host-mode calls (pmmg_hip_bytes_up)"""
+        return int(self.lib.pmmg_hip_bytes_up(self.h, int(reset)))
 
     def tetra_qual(self, xyz, tetv, met=None, qual=None):
         """PMMG_tetraQual's MMG3D_tetraQual(mesh, met, 1) on the device
@@ -380,17 +397,34 @@ class _Groups:
             self.keep += [fsz, fpt, gpt]
 
 
-def interp_metrics_and_fields(ctx: TransferContext, old_groups, new_groups, input_met: int = 1):
+def interp_metrics_and_fields(ctx: TransferContext, old_groups, new_groups, input_met: int = 1, carry=None):
     """PMMG_interpMetricsAndFields over groups (src/interpmesh_pmmg.c:663-741)
     through the C host layer (pmmg_interp_metrics_and_fields).  The new
     groups' ``met`` / ``fields`` arrays are filled in place; per-group
     ``hsiz`` > 0 replaces the metric by a constant (MMG3D_Set_constantSize).
+    carry: None (plain call), or (carried, src) for
+    pmmg_interp_metrics_and_fields_carry — the new groups stay on the device,
+    and with carried the old groups are the previous call's new groups (src:
+    None, or per group None / the 1-based map of its vertices onto them).
     Returns (ier, stats)."""
     G = _Groups(old_groups, new_groups)
     st = HipStats()
-    ier = host_lib().pmmg_interp_metrics_and_fields(ctx.h, len(old_groups), ctypes.cast(G.olds, ctypes.c_void_p),
-                                                    ctypes.cast(G.news, ctypes.c_void_p), int(input_met),
-                                                    ctypes.byref(st))
+    if carry is None:
+        ier = host_lib().pmmg_interp_metrics_and_fields(ctx.h, len(old_groups), ctypes.cast(G.olds, ctypes.c_void_p),
+                                                        ctypes.cast(G.news, ctypes.c_void_p), int(input_met),
+                                                        ctypes.byref(st))
+        return ier, st
+    carried, src = carry
+    maps = None
+    if src is not None:
+        arrs = [None if m is None else np.ascontiguousarray(m, np.int32) for m in src]
+        maps = (ctypes.c_void_p * max(1, len(arrs)))(*[None if a is None else _p(a).value for a in arrs])
+        G.keep.append(arrs)
+    ier = host_lib().pmmg_interp_metrics_and_fields_carry(ctx.h, len(old_groups), ctypes.cast(G.olds, ctypes.c_void_p),
+                                                          ctypes.cast(G.news, ctypes.c_void_p), int(input_met),
+                                                          int(bool(carried)),
+                                                          None if maps is None else ctypes.cast(maps, ctypes.c_void_p),
+                                                          ctypes.byref(st))
     return ier, st
 
 

@@ -60,6 +60,39 @@ def test_snapshot_of_a_shuffled_numbering():
         np.testing.assert_array_equal(adja.download(), expect)
 
 
+def _host_adjacency(tetv):
+    """MMG3D_hashTetra's result by a dictionary of sorted faces (face i opposite vertex i)."""
+    faces = {}
+    for k, t in enumerate(tetv.tolist()):
+        for i in range(4):
+            faces.setdefault(tuple(sorted(t[:i] + t[i + 1:])), []).append(4 * (k + 1) + i)
+    adja = np.zeros(tetv.shape, np.int32)
+    for codes in faces.values():
+        if len(codes) == 2:
+            a, b = codes
+            adja[a // 4 - 1, a % 4], adja[b // 4 - 1, b % 4] = b, a
+    return adja
+
+
+@pytest.mark.gpu
+def test_snapshot_of_a_high_valence_vertex():
+    """A star of tetra around one vertex (vertex 1, the smallest id, in every
+    tetra): its face bucket holds 3 faces per tetra, more than the match
+    kernel stages in LDS for a block of vertices, so that block scans its
+    buckets in place."""
+    bg = synth.lattice(synth.SHELL, 12)
+    r = np.linalg.norm(bg.xyz - bg.xyz.mean(0), axis=1)
+    outer = bg.triv[(r[bg.triv - 1] > np.median(r)).all(axis=1)]
+    assert 3 * outer.shape[0] > 2048  # pmmg_snapshot.hip kMatchCap
+    tetv = np.hstack([np.ones((outer.shape[0], 1), np.int32), outer + 1]).astype(np.int32)
+    with TransferContext(0) as ctx:
+        adja, tet8 = ctx.build_adjacency(bg.np + 1, ctx.upload(np.ascontiguousarray(tetv)))
+        expect = _host_adjacency(tetv)
+        np.testing.assert_array_equal(adja.download(), expect)
+        np.testing.assert_array_equal(tet8.download(), pack_tet8(tetv, expect))
+        assert (expect[:, 0] == 0).all() and (expect[:, 1:] > 0).all()  # the outer faces, the star's inner faces
+
+
 @pytest.mark.gpu
 def test_snapshot_rejects_invalid_connectivity():
     bg = synth.lattice(synth.CUBE, 2)
