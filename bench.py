@@ -603,7 +603,7 @@ def groups_leg(args, ngroup: int = 10, reps: int = 5, budget_s: float = 30.0) ->
                for k in ("elem", "hit", "met")) and all(
         np.array_equal(x, y, equal_nan=True) for a, b in zip(out_g, ref_out) for x, y in zip(a["fields"], b["fields"]))
     npts = int(st.nvol + st.nbdy)
-    lanes = int(os.environ.get("PMMG_HIP_GROUP_LANES", "2"))
+    lanes = int(os.environ.get("PMMG_HIP_GROUP_LANES", "4"))
     res = {"what": f"{ngroup} cfg2-size groups (own copies in HBM) in one pmmg_hip_locate_interp_groups call vs one "
                    "pmmg_hip_locate_interp per group; not the bench value",
            "groups": ngroup, "lanes": lanes, "points_per_group": npts // ngroup,

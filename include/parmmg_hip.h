@@ -107,8 +107,8 @@ typedef struct {
 
 /* Options (bit flags) for pmmg_hip_create.  Default: Morton-bin the queries
  * unless a sampled test on the device finds the input numbering already
- * spatially coherent (median distance between consecutive points < 4 mean
- * spacings). */
+ * spatially coherent (3 in 4 consecutive points closer than 4 mean
+ * spacings), and groups of fewer than 2^20 new points keep their input order. */
 #define PMMG_HIP_OPT_NOSORT 1   /* always process queries in input order */
 #define PMMG_HIP_OPT_SORT   2   /* always Morton-bin the queries */
 
@@ -245,7 +245,7 @@ typedef struct {
 } pmmg_hip_group;
 
 /* Enqueue the transfer of ngroup groups: group i runs on lane i % L of the
- * context (L = min(ngroup, PMMG_HIP_GROUP_LANES, default 2); a lane is a
+ * context (L = min(ngroup, PMMG_HIP_GROUP_LANES, default 4); a lane is a
  * pair of streams with its own work buffers, so the groups of different lanes
  * overlap on the device).  stats == NULL: the call only enqueues (nothing is
  * read back; use pmmg_hip_sync before reading outputs).  stats != NULL: the

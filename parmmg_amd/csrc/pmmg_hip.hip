@@ -228,7 +228,8 @@ struct pmmg_hip_ctx {
   // pmmg_hip_locate_interp_groups: the context itself is lane 0, lanes[j]
   // lane j + 1 (same device and options, created at the first groups call)
   std::vector<pmmg_hip_ctx *> lanes;
-  int group_lanes = 2; // PMMG_HIP_GROUP_LANES
+  int group_lanes = 4; // PMMG_HIP_GROUP_LANES (r04i, 10 cfg2-size groups: 1 / 2 / 4 lanes 0.165 / 0.125 / 0.108 ms per group)
+  struct Pool *lane_pool = nullptr; // host threads enqueueing the other lanes' groups
   int filter_steps = 64; // step cap of the fp32 filter walk (then the exact fp64 walk continues from where it
                          // stopped: a query the filter misjudges hands over early instead of cycling through a
                          // 4-entry history for up to maxstep steps); test-only PMMG_HIP_FILTER_STEPS=0 sends every
@@ -581,6 +582,7 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
 
 void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   if (!c) return;
+  delete c->lane_pool;
   for (pmmg_hip_ctx *l : c->lanes) pmmg_hip_destroy(l);
   (void)hipSetDevice(c->device);
   (void)snap_join(c);
@@ -1646,6 +1648,34 @@ static pmmg_hip_ctx *group_lane(pmmg_hip_ctx *c, int j) {
   return c->lanes[j - 1];
 }
 
+// one lane's share of a groups call: groups j, j + L, j + 2L, ... enqueued in
+// order (each waited for and its counters summed when stats are wanted)
+static int lane_groups(pmmg_hip_ctx *l, int j, int L, int ngroup, const pmmg_hip_group *groups, bool want,
+                       pmmg_hip_stats *sum, int *bad) {
+  if (hipSetDevice(l->device) != hipSuccess) {
+    *bad = j;
+    return 0;
+  }
+  for (int i = j; i < ngroup; i += L) {
+    const pmmg_hip_group &g = groups[i];
+    const int ok =
+        (g.tet8 ? set_background_impl(l, g.np, g.xyz, g.ne, nullptr, nullptr, g.tet8, g.nt, g.triv, g.adjt, g.hausd,
+                                      PMMG_HIP_DEVICE)
+                : (g.tetv && set_background_impl(l, g.np, g.xyz, g.ne, g.tetv, g.adja, nullptr, g.nt, g.triv, g.adjt,
+                                                 g.hausd, PMMG_HIP_DEVICE))) &&
+        pmmg_hip_set_solutions(l, g.met_size, g.met, g.nfield, g.field_size, g.fields, PMMG_HIP_DEVICE) &&
+        pmmg_hip_locate_interp(l, g.np_new, g.xyz_new, g.pclass, g.met_out, g.fields_out, g.elem_out, g.hit_out,
+                               nullptr, PMMG_HIP_DEVICE);
+    pmmg_hip_stats st;
+    if (!ok || (want && !pmmg_hip_sync(l, &st))) {
+      *bad = i;
+      return 0;
+    }
+    if (want) stats_sum(sum, st);
+  }
+  return 1;
+}
+
 int pmmg_hip_locate_interp_groups(pmmg_hip_ctx *c, int ngroup, const pmmg_hip_group *groups,
                                   pmmg_hip_stats *stats) {
   if (!c) return 0;
@@ -1661,37 +1691,32 @@ int pmmg_hip_locate_interp_groups(pmmg_hip_ctx *c, int ngroup, const pmmg_hip_gr
   std::vector<pmmg_hip_ctx *> lane(L);
   for (int j = 0; j < L; j++)
     if (!(lane[j] = group_lane(c, j))) return 0;
-  for (int r0 = 0; r0 < ngroup; r0 += L) {
-    const int r1 = std::min(ngroup, r0 + L);
-    for (int i = r0; i < r1; i++) {
-      const pmmg_hip_group &g = groups[i];
-      pmmg_hip_ctx *l = lane[i % L];
-      const int ok =
-          (g.tet8 ? set_background_impl(l, g.np, g.xyz, g.ne, nullptr, nullptr, g.tet8, g.nt, g.triv, g.adjt, g.hausd,
-                                        PMMG_HIP_DEVICE)
-                  : (g.tetv && set_background_impl(l, g.np, g.xyz, g.ne, g.tetv, g.adja, nullptr, g.nt, g.triv,
-                                                   g.adjt, g.hausd, PMMG_HIP_DEVICE))) &&
-          pmmg_hip_set_solutions(l, g.met_size, g.met, g.nfield, g.field_size, g.fields, PMMG_HIP_DEVICE) &&
-          pmmg_hip_locate_interp(l, g.np_new, g.xyz_new, g.pclass, g.met_out, g.fields_out, g.elem_out, g.hit_out,
-                                 nullptr, PMMG_HIP_DEVICE);
-      if (!ok) {
-        const std::string why = l->err;
-        set_err(c, "locate_interp_groups: group %d: %s", i, why.c_str());
-        return 0;
-      }
+  // every lane enqueues its groups from its own host thread (the enqueue of
+  // ~25 launches per group is the host's share of a small group)
+  std::vector<pmmg_hip_stats> sums(L);
+  std::vector<int> bad(L, -1), ok(L, 1);
+  for (auto &x : sums) memset(&x, 0, sizeof(x));
+  if (L > 1 && !c->lane_pool) c->lane_pool = new Pool(c->group_lanes - 1);
+  auto work = [&](size_t a, size_t e) {
+    for (size_t j = a; j < e; j++)
+      ok[j] = lane_groups(lane[j], (int)j, L, ngroup, groups, stats != nullptr, &sums[j], &bad[j]);
+  };
+  if (L > 1) c->lane_pool->run((size_t)L, (size_t)L, work);
+  else work(0, 1);
+  HIPCK(c, hipSetDevice(c->device));
+  int first = -1, fl = 0;
+  for (int j = 0; j < L; j++)
+    if (!ok[j] && (first < 0 || bad[j] < first)) {
+      first = bad[j];
+      fl = j;
     }
-    if (stats) // the round's counters, before the lanes take the next groups
-      for (int i = r0; i < r1; i++) {
-        pmmg_hip_ctx *l = lane[i % L];
-        pmmg_hip_stats st;
-        if (!pmmg_hip_sync(l, &st)) {
-          const std::string why = l->err;
-          set_err(c, "locate_interp_groups: group %d: %s", i, why.c_str());
-          return 0;
-        }
-        stats_sum(stats, st);
-      }
+  if (first >= 0) {
+    const std::string why = lane[fl]->err;
+    set_err(c, "locate_interp_groups: group %d: %s", first, why.c_str());
+    return 0;
   }
+  if (stats)
+    for (int j = 0; j < L; j++) stats_sum(stats, sums[j]);
   return 1;
 }
 

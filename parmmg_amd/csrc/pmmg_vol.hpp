@@ -939,11 +939,11 @@ __global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsign
         // measurement build, PMMG_HIP_PAD = v + 65536 t: v extra VALU
         // instructions and t extra L1 accesses (re-loads of the current
         // record) per walk step, to price each resource in the step
-        if (pad) {
+        if (pad & 0x1FFFFFFF) {
           float acc = (float)steps;
           for (int j = 0; j < (pad & 0xFFFF); j++) asm volatile("v_add_f32 %0, %0, %0" : "+v"(acc));
           int dummy = 0;
-          for (int j = 0; j < (pad >> 16); j++)
+          for (int j = 0; j < ((pad >> 16) & 0x1FFF); j++)
             dummy += reinterpret_cast<const volatile int *>(bg.tetv + (size_t)(k - 1) * bg.tstride)[j & 3];
           if (acc == -1.0f && dummy == 0x7FFFFFFF) steps += 0; // keep both chains alive
           asm volatile("" ::"v"(acc), "v"(dummy));
@@ -975,7 +975,15 @@ __global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsign
   wave_count(&sh.bs, kCntExact, more);
   wave_count(&sh.bs, kCntNoSeed, active && noseed);
   // 3. interpolation
+#ifdef PMMG_HIP_MEASURE
+  // measurement build: PMMG_HIP_PAD bit 30 — Morton order stores whole lines
+  // at the processing position (wrong rows, the scattered stores' price);
+  // bit 29 — no row stores in Morton order
+  const Sink snk{!sorted || ((pad >> 30) & 1), (size_t)(i - __lane_id()), ip};
+  if (sorted && ((pad >> 29) & 1)) acc = false;
+#else
   const Sink snk{!sorted, (size_t)(i - __lane_id()), ip};
+#endif
   if (__any(acc)) {
     if (!acc) { // idle lanes gather a valid row, never stored
       loc.v = make_int4(1, 1, 1, 1);

@@ -142,9 +142,10 @@ def test_full_size_cfg3_sample_against_oracle_and_determinism():
 def test_query_order_detection(n):
     """Input order is kept for a lattice numbering whatever its row length
     (n=127: 128^3 points, a row length an evenly strided sample would alias
-    with), and Morton binning is chosen for a shuffled numbering of a group
-    of at least 2^20 points (n=39: 64k points, a small group, keeps the input
-    order untested: kSmallGroup); results are the same either way."""
+    with) and for an Mmg-like one, and Morton binning is chosen for a
+    shuffled numbering of a group of at least 2^20 points (n=39: 64k points,
+    a small group, keeps the input order untested: kSmallGroup); results are
+    the same either way."""
     case = make_case(kind=C, n_old=8, n_new=n, with_ref=False)
     a = run_gpu(case)
     assert a["stats"]["sorted"] == 0
@@ -158,3 +159,11 @@ def test_query_order_detection(n):
     assert b["stats"]["sorted"] == (1 if case["new"].np >= 1 << 20 else 0)
     np.testing.assert_array_equal(b["elem"], a["elem"][perm])
     np.testing.assert_array_equal(b["met"], a["met"][perm])
+    # an Mmg-like numbering (the inserted sixth appended) keeps its input order
+    perm = synth.mmg_like_perm(case["new"].np)
+    mmg = dict(case)
+    mmg["new"] = dataclasses.replace(case["new"], xyz=np.ascontiguousarray(case["new"].xyz[perm]))
+    mmg["pclass"] = np.ascontiguousarray(case["pclass"][perm])
+    m = run_gpu(mmg)
+    assert m["stats"]["sorted"] == 0
+    np.testing.assert_array_equal(m["elem"], a["elem"][perm])

@@ -12,10 +12,10 @@ from parmmg_amd import synth
 from parmmg_amd.transfer import TransferContext, pack_tet8
 
 C, S = synth.CUBE, synth.SHELL
-GROUPS = [dict(kind=C, n_old=6, n_new=7), dict(kind=S, n_old=8, n_new=10),
+GROUPS = [dict(kind=C, n_old=6, n_new=7), dict(kind=S, n_old=8, n_new=12),
           dict(kind=C, n_old=5, n_new=9, metric=None, fields=(synth.F_TENSOR, synth.F_AFFINE_VEC)),
           dict(kind=C, n_old=7, n_new=5, metric=synth.F_ISO, fields=(synth.F_SCALAR,)),
-          dict(kind=S, n_old=6, n_new=9, metric=synth.F_ISO, fields=(synth.F_SCALAR, synth.F_AFFINE))]
+          dict(kind=S, n_old=12, n_new=8, metric=synth.F_ISO, fields=(synth.F_SCALAR, synth.F_AFFINE))]
 
 
 def _device_group(ctx, case, tet8=True):
