@@ -112,7 +112,7 @@ __device__ __forceinline__ int bdy_query(const Bg &bg, const Frame *fr, const in
 // slowed the volume kernel beside them (profiles/r03y).
 __global__ __launch_bounds__(kBlock) void k_bdy(Bg bg, const Frame *fr, const int *sgrid, int gs, const double *qxyz,
                                                 const int *order, Slots S, int *elem_out, int8_t *hit_out, int *fb,
-                                                DevStats *st, int maxstep, int dyn) {
+                                                DevStats *st, int maxstep, int dyn, FbInit fi) {
   __shared__ BlockStats bs;
   bstats_init(&bs);
   __syncthreads();
@@ -139,7 +139,10 @@ __global__ __launch_bounds__(kBlock) void k_bdy(Bg bg, const Frame *fr, const in
       hit = bdy_query(bg, fr, sgrid, gs, qxyz, ip, S, elem_out, hit_out, maxstep, steps);
     }
     int slot = wave_append(&st->nfb_bdy, active && hit == 0);
-    if (active && hit == 0) fb[slot] = ip;
+    if (active && hit == 0) {
+      fb[slot] = ip;
+      fi.at(slot);
+    }
     wave_stats(&bs, active, hit, steps);
   }
   __syncthreads();

@@ -18,21 +18,6 @@ namespace pmmg {
 
 constexpr int kQB = 128; // fallback queries staged in LDS per pass
 
-__global__ void k_fallback_init(int *best, int *cidx, unsigned long long *ckey, const int *count, int *bbest,
-                                int *bcidx, unsigned long long *bckey, const int *bcount) {
-  const int n = count ? *count : 0, nb = bcount ? *bcount : 0;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    best[i] = INT_MAX;
-    cidx[i] = INT_MAX;
-    ckey[i] = ~0ULL;
-  }
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += gridDim.x * blockDim.x) {
-    bbest[i] = INT_MAX;
-    bcidx[i] = INT_MAX;
-    bckey[i] = ~0ULL;
-  }
-}
-
 // lowest-index tetra accepting each fallback query (locate_pmmg.c:743-762)
 __global__ __launch_bounds__(kBlock) void k_vol_exhaust_accept(Bg bg, const double *qxyz, const int *fb,
                                                                const DevStats *st, int *best) {

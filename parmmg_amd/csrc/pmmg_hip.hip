@@ -1109,9 +1109,6 @@ static void launch_vol_fallbacks(pmmg_hip_ctx *c, const Slots &S, const double *
   const Bg &bg = c->bg;
   hipStream_t s = c->stream;
   DevStats *st = (DevStats *)c->stats.p;
-  hipLaunchKernelGGL(k_fallback_init, dim3(64), dim3(kBlock), 0, s, (int *)c->best.p, (int *)c->cidx.p,
-                     (unsigned long long *)c->ckey.p, (const int *)&st->nfb_vol, nullptr, nullptr, nullptr,
-                     (const int *)nullptr);
   const int fgrid = 1024;
   hipLaunchKernelGGL(k_vol_exhaust_accept, dim3(fgrid), dim3(kBlock), 0, s, bg, xyz_new, (const int *)c->fb_vol.p, st,
                      (int *)c->best.p);
@@ -1126,9 +1123,6 @@ static void launch_bdy_fallbacks(pmmg_hip_ctx *c, hipStream_t s, const Slots &S,
                                  int *elem_out, int8_t *hit_out) {
   const Bg &bg = c->bg;
   DevStats *st = (DevStats *)c->stats.p;
-  hipLaunchKernelGGL(k_fallback_init, dim3(64), dim3(kBlock), 0, s, nullptr, nullptr, nullptr, (const int *)nullptr,
-                     (int *)c->bbest.p, (int *)c->bcidx.p, (unsigned long long *)c->bckey.p,
-                     (const int *)&st->nfb_bdy);
   for (int pass = 0; pass < 3; pass++)
     hipLaunchKernelGGL(k_bdy_exhaust, dim3(256), dim3(kBlock), 0, s, bg, xyz_new, (const int *)c->fb_bdy.p, st,
                        (int *)c->bbest.p, (unsigned long long *)c->bckey.p, pass, (int *)c->bcidx.p);
@@ -1352,7 +1346,8 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     // second, nearly empty round doubled the surface branch alone)
     hipLaunchKernelGGL(k_bdy, dim3(8 * blocks_for((np_new + 7) / 8, c->bdy_bpx)), dim3(kBlock), 0, sb, bg,
                        (const Frame *)fr, (const int *)sgrid, gs, xyz_new, (const int *)order_b, S, elem_out, hit_out,
-                       (int *)c->fb_bdy.p, st, c->maxstep, c->bdy_dyn);
+                       (int *)c->fb_bdy.p, st, c->maxstep, c->bdy_dyn,
+                       FbInit{(int *)c->bbest.p, (int *)c->bcidx.p, (unsigned long long *)c->bckey.p});
     launch_bdy_fallbacks(c, sb, S, xyz_new, elem_out, hit_out);
     HIPCK(c, hipGetLastError());
   }
@@ -1372,7 +1367,8 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
                      c->pad);
   HIPCK(c, hipEventRecord(c->ev[EV_WALK], s));
   hipLaunchKernelGGL(k_vol_walk_exact, dim3(8 * 64), dim3(64), 0, s, bg, xyz_new, (int *)c->fb_vol.p,
-                     (const ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->maxstep);
+                     (const ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->maxstep,
+                     FbInit{(int *)c->best.p, (int *)c->cidx.p, (unsigned long long *)c->ckey.p});
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[EV_VOL], s));
   // ---- exhaustive fallbacks of the volume queries (lists and counts on the

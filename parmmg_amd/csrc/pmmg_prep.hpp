@@ -27,6 +27,19 @@ struct DevStats {
   int bdy_next[8];      // k_bdy: per-XCD work counters (the next unclaimed surface query of each eighth)
 };
 
+// the exhaustive searches' per-query state, initialised where a query joins
+// a fallback list (no separate init launch): best accepting element, closest
+// key, lowest index at that key
+struct FbInit {
+  int *best, *cidx;
+  unsigned long long *ckey;
+  __device__ __forceinline__ void at(int slot) const {
+    best[slot] = INT_MAX;
+    cidx[slot] = INT_MAX;
+    ckey[slot] = ~0ULL;
+  }
+};
+
 constexpr int kStatParts = 256;
 // extra counter slots next to the PMMG_HIT_* codes (1..11)
 constexpr int kCntVolQueries = 12; // volume queries seen by the walk

@@ -421,7 +421,7 @@ __device__ __forceinline__ int walk_exact(const Bg &bg, const double *x, int ip,
 // count is read on the device.
 __global__ __launch_bounds__(64) void k_vol_walk_exact(Bg bg, const double *qxyz, int *fb, const ContEntry *cont,
                                                        DevStats *st, Slots S, int *elem_out, int8_t *hit_out,
-                                                       int maxstep) {
+                                                       int maxstep, FbInit fi) {
   __shared__ BlockStats bs;
   __shared__ double slot_img[12 * 64];
   const LaneSlotsD L{&slot_img[__lane_id()]};
@@ -451,7 +451,10 @@ __global__ __launch_bounds__(64) void k_vol_walk_exact(Bg bg, const double *qxyz
     }
     const bool fail = active && status != 1;
     const int slot = wave_append(&st->nfb_vol, fail);
-    if (fail) fb[slot] = ip;
+    if (fail) {
+      fb[slot] = ip;
+      fi.at(slot);
+    }
     wave_count(&bs, kCntStuck, fail && status == 2);
     wave_count(&bs, kCntLimit, fail && status == 3);
     wave_stats(&bs, active, status == 1 ? PMMG_HIT_VOL_WALK : 0, steps);
