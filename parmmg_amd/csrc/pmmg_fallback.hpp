@@ -18,9 +18,40 @@ namespace pmmg {
 
 constexpr int kQB = 128; // fallback queries staged in LDS per pass
 
+// distance from x to the tria's centroid, in the arithmetic of the closest
+// tria search (locate_pmmg.c:400-416): x - sum_v p_v / 3, component by component
+__device__ __forceinline__ double centroid_dist(const double *x, const TriGeom &t) {
+  double d[3] = {x[0], x[1], x[2]};
+  for (int v = 0; v < 3; v++)
+    for (int c = 0; c < 3; c++) d[c] -= t.p[v][c] / 3.0;
+  double nrm = 0;
+  for (int c = 0; c < 3; c++) nrm += d[c] * d[c];
+  return sqrt(nrm);
+}
+
+// Exhaustive searches of the queries the walks did not settle, in two
+// launches per class: a scan over every element gives each query its
+// lowest-index accepting element (best) and its closest key (ckey); a second
+// scan finds the lowest index at that key (cidx) for the queries nothing
+// accepted, and the last block to finish it interpolates every query of the
+// list (r04: the scan passes and the finish were four launches; a small
+// group's step is a chain of ~20 launches of a few microseconds each).
+
+// the last block of a grid to pass this point (after its device-scope
+// atomics) gets true: the other blocks' results are then visible to it
+__device__ __forceinline__ bool last_block(unsigned *done) {
+  __threadfence();
+  __shared__ bool last;
+  if (threadIdx.x == 0) last = atomicAdd(done, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (last) __threadfence();
+  return last;
+}
+
 // lowest-index tetra accepting each fallback query (locate_pmmg.c:743-762)
-__global__ __launch_bounds__(kBlock) void k_vol_exhaust_accept(Bg bg, const double *qxyz, const int *fb,
-                                                               const DevStats *st, int *best) {
+// and the closest tetra's key, argmin |bary_min| * vol (:453-458)
+__global__ __launch_bounds__(kBlock) void k_vol_exhaust_scan(Bg bg, const double *qxyz, const int *fb,
+                                                             const DevStats *st, int *best, unsigned long long *ckey) {
   __shared__ double sx[kQB][3];
   const int nfb = st->nfb_vol;
   for (int q0 = 0; q0 < nfb; q0 += kQB) {
@@ -36,37 +67,26 @@ __global__ __launch_bounds__(kBlock) void k_vol_exhaust_accept(Bg bg, const doub
       load_pt(bg.xyz, tv.y, p1);
       load_pt(bg.xyz, tv.z, p2);
       load_pt(bg.xyz, tv.w, p3);
-      double lo[3], hi[3];
-      for (int d = 0; d < 3; d++) {
-        lo[d] = fmin(fmin(p0[d], p1[d]), fmin(p2[d], p3[d]));
-        hi[d] = fmax(fmax(p0[d], p1[d]), fmax(p2[d], p3[d]));
-        // an accepted point has every barycentric coordinate > -EPS, so it
-        // lies inside the tetra's bbox inflated by 3 EPS of its extent
-        double pad = 8.0 * kEps * (hi[d] - lo[d]) + 1e-300;
-        lo[d] -= pad;
-        hi[d] += pad;
-      }
       for (int j = 0; j < nq; j++) {
-        const double *x = sx[j];
-        if (x[0] < lo[0] || x[0] > hi[0] || x[1] < lo[1] || x[1] > hi[1] || x[2] < lo[2] || x[2] > hi[2]) continue;
-        if (best[q0 + j] <= k) continue;
         double b[4];
-        tet_bary(x, p0, p1, p2, p3, b);
-        if (min4(b) > -kEps) atomicMin(&best[q0 + j], k);
+        const double vol = tet_bary(sx[j], p0, p1, p2, p3, b);
+        const double bmin = min4(b);
+        if (bmin > -kEps && best[q0 + j] > k) atomicMin(&best[q0 + j], k);
+        atomicMin(&ckey[q0 + j], dkey(fabs(bmin) * vol));
       }
     }
   }
 }
 
-// closest tetra of queries nobody accepts: argmin |bary_min| * vol
-// (locate_pmmg.c:453-458); pass 0 finds the minimum value, pass 1 the lowest
-// index reaching it
-__global__ __launch_bounds__(kBlock) void k_vol_exhaust_closest(Bg bg, const double *qxyz, const int *fb,
-                                                                const DevStats *st, const int *best,
-                                                                unsigned long long *ckey, int pass, int *cidx) {
+// the lowest index at the closest key (queries nothing accepted), then, in
+// the last block, every query of the list located and interpolated
+__global__ __launch_bounds__(kBlock) void k_vol_exhaust_pick(Bg bg, const double *qxyz, const int *fb, DevStats *st,
+                                                             const int *best, const unsigned long long *ckey,
+                                                             int *cidx, Slots S, int *elem_out, int8_t *hit_out) {
   __shared__ double sx[kQB][3];
   __shared__ int sneed[kQB];
   const int nfb = st->nfb_vol;
+  if (nfb == 0) return;
   for (int q0 = 0; q0 < nfb; q0 += kQB) {
     int nq = min(kQB, nfb - q0);
     __syncthreads();
@@ -89,20 +109,13 @@ __global__ __launch_bounds__(kBlock) void k_vol_exhaust_closest(Bg bg, const dou
       for (int j = 0; j < nq; j++) {
         if (!sneed[j]) continue;
         double b[4];
-        double vol = tet_bary(sx[j], p0, p1, p2, p3, b);
-        unsigned long long key = dkey(fabs(min4(b)) * vol);
-        if (pass == 0) atomicMin(&ckey[q0 + j], key);
-        else if (key == ckey[q0 + j]) atomicMin(&cidx[q0 + j], k);
+        const double vol = tet_bary(sx[j], p0, p1, p2, p3, b);
+        if (dkey(fabs(min4(b)) * vol) == ckey[q0 + j]) atomicMin(&cidx[q0 + j], k);
       }
     }
   }
-}
-
-__global__ __launch_bounds__(kBlock) void k_vol_finish(Bg bg, const double *qxyz, const int *fb, DevStats *st,
-                                                       const int *best, const int *cidx, Slots S, int *elem_out,
-                                                       int8_t *hit_out) {
-  const int nfb = st->nfb_vol;
-  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nfb; j += gridDim.x * blockDim.x) {
+  if (!last_block(&st->fb_done[0])) return;
+  for (int j = threadIdx.x; j < nfb; j += blockDim.x) {
     int ip = fb[j];
     double x[3];
     load_pt(qxyz, ip, x);
@@ -111,7 +124,7 @@ __global__ __launch_bounds__(kBlock) void k_vol_finish(Bg bg, const double *qxyz
       k = best[j];
       hit = PMMG_HIT_VOL_EXHAUST;
     } else {
-      k = cidx[j];
+      k = atomicOr(&cidx[j], 0); // the other blocks' atomicMin results
       hit = PMMG_HIT_VOL_CLOSEST;
     }
     if (k == INT_MAX || k <= 0) continue;
@@ -131,10 +144,10 @@ __global__ __launch_bounds__(kBlock) void k_vol_finish(Bg bg, const double *qxyz
   }
 }
 
-// surface: pass 0 lowest-index accepting tria (locate_pmmg.c:483-503), pass 1
-// minimum centroid distance, pass 2 lowest index reaching it (:400-416)
-__global__ __launch_bounds__(kBlock) void k_bdy_exhaust(Bg bg, const double *qxyz, const int *fb, const DevStats *st,
-                                                        int *best, unsigned long long *ckey, int pass, int *cidx) {
+// surface: the lowest-index accepting tria (locate_pmmg.c:483-503) and the
+// minimum centroid distance (:400-416) in one scan
+__global__ __launch_bounds__(kBlock) void k_bdy_exhaust_scan(Bg bg, const double *qxyz, const int *fb,
+                                                             const DevStats *st, int *best, unsigned long long *ckey) {
   __shared__ double sx[kQB][3];
   const int nfb = st->nfb_bdy;
   for (int q0 = 0; q0 < nfb; q0 += kQB) {
@@ -148,34 +161,43 @@ __global__ __launch_bounds__(kBlock) void k_bdy_exhaust(Bg bg, const double *qxy
       tri_load(bg, k, t);
       for (int j = 0; j < nq; j++) {
         const double *x = sx[j];
-        if (pass == 0) {
-          if (best[q0 + j] <= k) continue;
+        if (best[q0 + j] > k) {
           double b[3];
           double dist = tri_bary(x, t.p, t.q, t.n, b);
           double bmin = fmin(b[0], fmin(b[1], b[2]));
           if (bmin > -kEps && !(fabs(dist) > bg.hausd)) atomicMin(&best[q0 + j], k);
-        } else {
-          if (best[q0 + j] != INT_MAX) continue;
-          double d[3] = {x[0], x[1], x[2]};
-          for (int v = 0; v < 3; v++)
-            for (int c = 0; c < 3; c++) d[c] -= t.p[v][c] / 3.0;
-          double nrm = 0;
-          for (int c = 0; c < 3; c++) nrm += d[c] * d[c];
-          nrm = sqrt(nrm);
-          unsigned long long key = dkey(nrm);
-          if (pass == 1) atomicMin(&ckey[q0 + j], key);
-          else if (key == ckey[q0 + j]) atomicMin(&cidx[q0 + j], k);
         }
+        atomicMin(&ckey[q0 + j], dkey(centroid_dist(x, t)));
       }
     }
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_bdy_finish(Bg bg, const double *qxyz, const int *fb, DevStats *st,
-                                                       const int *best, const int *cidx, Slots S, int *elem_out,
-                                                       int8_t *hit_out) {
+// the lowest index at the minimum distance (queries nothing accepted), then,
+// in the last block, every query of the list interpolated
+__global__ __launch_bounds__(kBlock) void k_bdy_exhaust_pick(Bg bg, const double *qxyz, const int *fb, DevStats *st,
+                                                             const int *best, const unsigned long long *ckey,
+                                                             int *cidx, Slots S, int *elem_out, int8_t *hit_out) {
+  __shared__ double sx[kQB][3];
   const int nfb = st->nfb_bdy;
-  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nfb; j += gridDim.x * blockDim.x) {
+  if (nfb == 0) return;
+  for (int q0 = 0; q0 < nfb; q0 += kQB) {
+    int nq = min(kQB, nfb - q0);
+    __syncthreads();
+    for (int j = threadIdx.x; j < nq; j += blockDim.x) load_pt(qxyz, fb[q0 + j], sx[j]);
+    __syncthreads();
+    for (int k = 1 + blockIdx.x * blockDim.x + threadIdx.x; k <= bg.nt; k += gridDim.x * blockDim.x) {
+      if (bg.triv[3 * (size_t)(k - 1)] <= 0) continue;
+      TriGeom t;
+      tri_load(bg, k, t);
+      for (int j = 0; j < nq; j++) {
+        if (best[q0 + j] != INT_MAX) continue;
+        if (dkey(centroid_dist(sx[j], t)) == ckey[q0 + j]) atomicMin(&cidx[q0 + j], k);
+      }
+    }
+  }
+  if (!last_block(&st->fb_done[1])) return;
+  for (int j = threadIdx.x; j < nfb; j += blockDim.x) {
     int ip = fb[j];
     double x[3];
     load_pt(qxyz, ip, x);
@@ -188,7 +210,7 @@ __global__ __launch_bounds__(kBlock) void k_bdy_finish(Bg bg, const double *qxyz
       tri_load(bg, k, t);
       tri_bary(x, t.p, t.q, t.n, phi);
     } else {
-      k = cidx[j];
+      k = atomicOr(&cidx[j], 0); // the other blocks' atomicMin results
       if (k == INT_MAX || k <= 0) continue;
       tri_load(bg, k, t);
       // stale re-evaluation (locate_pmmg.c:505-509): vertices and area of the

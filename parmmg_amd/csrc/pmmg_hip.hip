@@ -1100,7 +1100,6 @@ static int blocks_for(long long n, int cap) {
   return (int)b;
 }
 
-// exhaustive fallbacks; every kernel reads its list's count on the device
 // exhaustive fallbacks of the volume queries (main stream, after the exact
 // continuation) and of the surface queries (surface stream, after k_bdy): the
 // lists and their counts live on the device, every kernel reads its count
@@ -1110,24 +1109,22 @@ static void launch_vol_fallbacks(pmmg_hip_ctx *c, const Slots &S, const double *
   hipStream_t s = c->stream;
   DevStats *st = (DevStats *)c->stats.p;
   const int fgrid = 1024;
-  hipLaunchKernelGGL(k_vol_exhaust_accept, dim3(fgrid), dim3(kBlock), 0, s, bg, xyz_new, (const int *)c->fb_vol.p, st,
-                     (int *)c->best.p);
-  for (int pass = 0; pass < 2; pass++)
-    hipLaunchKernelGGL(k_vol_exhaust_closest, dim3(fgrid), dim3(kBlock), 0, s, bg, xyz_new, (const int *)c->fb_vol.p,
-                       st, (const int *)c->best.p, (unsigned long long *)c->ckey.p, pass, (int *)c->cidx.p);
-  hipLaunchKernelGGL(k_vol_finish, dim3(64), dim3(kBlock), 0, s, bg, xyz_new, (const int *)c->fb_vol.p, st,
-                     (const int *)c->best.p, (const int *)c->cidx.p, S, elem_out, hit_out);
+  hipLaunchKernelGGL(k_vol_exhaust_scan, dim3(fgrid), dim3(kBlock), 0, s, bg, xyz_new, (const int *)c->fb_vol.p, st,
+                     (int *)c->best.p, (unsigned long long *)c->ckey.p);
+  hipLaunchKernelGGL(k_vol_exhaust_pick, dim3(fgrid), dim3(kBlock), 0, s, bg, xyz_new, (const int *)c->fb_vol.p, st,
+                     (const int *)c->best.p, (const unsigned long long *)c->ckey.p, (int *)c->cidx.p, S, elem_out,
+                     hit_out);
 }
 
 static void launch_bdy_fallbacks(pmmg_hip_ctx *c, hipStream_t s, const Slots &S, const double *xyz_new,
                                  int *elem_out, int8_t *hit_out) {
   const Bg &bg = c->bg;
   DevStats *st = (DevStats *)c->stats.p;
-  for (int pass = 0; pass < 3; pass++)
-    hipLaunchKernelGGL(k_bdy_exhaust, dim3(256), dim3(kBlock), 0, s, bg, xyz_new, (const int *)c->fb_bdy.p, st,
-                       (int *)c->bbest.p, (unsigned long long *)c->bckey.p, pass, (int *)c->bcidx.p);
-  hipLaunchKernelGGL(k_bdy_finish, dim3(64), dim3(kBlock), 0, s, bg, xyz_new, (const int *)c->fb_bdy.p, st,
-                     (const int *)c->bbest.p, (const int *)c->bcidx.p, S, elem_out, hit_out);
+  hipLaunchKernelGGL(k_bdy_exhaust_scan, dim3(256), dim3(kBlock), 0, s, bg, xyz_new, (const int *)c->fb_bdy.p, st,
+                     (int *)c->bbest.p, (unsigned long long *)c->bckey.p);
+  hipLaunchKernelGGL(k_bdy_exhaust_pick, dim3(256), dim3(kBlock), 0, s, bg, xyz_new, (const int *)c->fb_bdy.p, st,
+                     (const int *)c->bbest.p, (const unsigned long long *)c->bckey.p, (int *)c->bcidx.p, S, elem_out,
+                     hit_out);
 }
 
 #ifdef PMMG_HIP_MEASURE
@@ -1249,20 +1246,20 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   // ---- frame (main stream)
   HIPCK(c, hipEventRecord(c->ev[EV_START], s));
   // the coherence test first, on the second stream beside the frame kernels
-  // (it reads only the queries; its flag is read back in auto mode while the
-  // main stream builds the seed grid, so the host has enqueued the rest of the
-  // call long before the device needs it)
-  HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_START], 0));
-  hipLaunchKernelGGL(k_coherence, dim3(1), dim3(kBlock), 0, sb, xyz_new, np_new, (int *)c->oflag.p, force,
-                     c->bin_bits);
+  // (it reads only the queries); a forced order's flag is written by k_reset
+  if (force < 0) {
+    HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_START], 0));
+    hipLaunchKernelGGL(k_coherence, dim3(1), dim3(kBlock), 0, sb, xyz_new, np_new, (int *)c->oflag.p, force,
+                       c->bin_bits);
+  }
   hipLaunchKernelGGL(k_reset, dim3(blocks_for(ng > nsg ? ng : nsg, 2048)), dim3(kBlock), 0, s, fr, st, grid, ng,
-                     sgrid, nsg);
+                     sgrid, nsg, (int *)c->oflag.p, force, c->bin_bits);
+  // bbox (its last block finalises the frame), axis histograms (the last
+  // block builds the seed grid's axis maps)
   hipLaunchKernelGGL(k_bbox, dim3(blocks_for(bg.np / c->bbox_stride + 1, 256)), dim3(kBlock), 0, s, bg.xyz, bg.np, fr,
-                     c->bbox_stride);
-  hipLaunchKernelGGL(k_frame_final, dim3(1), dim3(1), 0, s, fr, g, gs, gb);
-  hipLaunchKernelGGL(k_axis_hist, dim3(kHistBlocks), dim3(kBlock), 0, s, bg.xyz, bg.np, (const Frame *)fr,
-                     c->hist_stride, (int *)c->axh.p);
-  hipLaunchKernelGGL(k_axis_map, dim3(3), dim3(kBlock), 0, s, (const int *)c->axh.p, fr, g);
+                     c->bbox_stride, g, gs, gb);
+  hipLaunchKernelGGL(k_axis_hist, dim3(kHistBlocks), dim3(kBlock), 0, s, bg.xyz, bg.np, fr, c->hist_stride,
+                     (int *)c->axh.p, g);
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[EV_FRAME], s));
 

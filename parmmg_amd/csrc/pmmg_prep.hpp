@@ -25,6 +25,7 @@ struct DevStats {
   int bin_bits;         // Morton bits per axis of the binning keys (read back with `sorted`)
   int pad;
   int bdy_next[8];      // k_bdy: per-XCD work counters (the next unclaimed surface query of each eighth)
+  unsigned fb_done[2];  // blocks done with the last exhaustive pass (volume, surface): the last one finishes
 };
 
 // the exhaustive searches' per-query state, initialised where a query joins
@@ -137,6 +138,7 @@ struct Frame {
   double qc[3], qs; // fixed-point frame of the walk's vertex copy
   int adaptive;     // bit d: axis d of the volume seed grid follows map[d]
   int seed_any;     // the lowest in-use tetra the seed grid sampled (INT_MAX: none): the last-resort seed
+  unsigned bbox_done, hist_done; // blocks done (the last block of k_bbox / k_axis_hist finishes the frame / map)
   float map[3][kMapBins + 1]; // map[d][b] = share of the vertices below bin b's lower edge
 };
 
@@ -196,8 +198,10 @@ __global__ __launch_bounds__(kBlock) void k_quantize(const double *xyz, long lon
 
 // one launch initialises the per-call state: frame accumulators, counters,
 // seed grids
+// (and writes the order flag of a forced order, when k_coherence is not
+// launched: force >= 0)
 __global__ __launch_bounds__(kBlock) void k_reset(Frame *fr, DevStats *st, unsigned long long *grid, long long ng,
-                                                  int *sgrid, long long nsg) {
+                                                  int *sgrid, long long nsg, int *flag, int force, int force_bits) {
   const long long tid = blockIdx.x * (long long)blockDim.x + threadIdx.x, nth = (long long)gridDim.x * blockDim.x;
   if (tid == 0) {
     for (int d = 0; d < 3; d++) {
@@ -206,6 +210,11 @@ __global__ __launch_bounds__(kBlock) void k_reset(Frame *fr, DevStats *st, unsig
     }
     fr->adaptive = 0;
     fr->seed_any = INT_MAX;
+    fr->bbox_done = fr->hist_done = 0u;
+    if (force >= 0) {
+      flag[0] = force;
+      flag[1] = force_bits;
+    }
     unsigned int *w = reinterpret_cast<unsigned int *>(st);
     for (size_t j = 0; j < sizeof(DevStats) / 4; j++) w[j] = 0u;
   }
@@ -222,7 +231,12 @@ __global__ __launch_bounds__(kBlock) void k_reset(Frame *fr, DevStats *st, unsig
 // of the first and last vertex: the frame only sizes the seed / bin grids,
 // whose cell lookups clamp, so a sampled bbox costs at most slightly longer
 // walks for the few points outside it
-__global__ __launch_bounds__(kBlock) void k_bbox(const double *xyz, int np, Frame *fr, int stride) {
+__device__ void frame_final(Frame *fr, int g, int gs, int gb);
+
+// the last block to finish also finalises the frame (one launch less per
+// call; the other blocks' atomics are read back atomically)
+__global__ __launch_bounds__(kBlock) void k_bbox(const double *xyz, int np, Frame *fr, int stride, int g, int gs,
+                                                 int gb) {
   __shared__ unsigned long long slo[3][kBlock / 64], shi[3][kBlock / 64];
   unsigned long long lo[3] = {~0ULL, ~0ULL, ~0ULL}, hi[3] = {0ULL, 0ULL, 0ULL};
   const long long ns = ((long long)np + stride - 1) / stride + 2;
@@ -264,12 +278,21 @@ __global__ __launch_bounds__(kBlock) void k_bbox(const double *xyz, int np, Fram
     atomicMin(&fr->key_lo[d], a);
     atomicMax(&fr->key_hi[d], b);
   }
+  __threadfence();
+  __shared__ bool last;
+  if (threadIdx.x == 0) last = atomicAdd(&fr->bbox_done, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (last && threadIdx.x == 0) {
+    __threadfence();
+    frame_final(fr, g, gs, gb);
+  }
 }
 
-__global__ void k_frame_final(Frame *fr, int g, int gs, int gb) {
+__device__ void frame_final(Frame *fr, int g, int gs, int gb) {
   double emax = 0.0;
   for (int d = 0; d < 3; d++) {
-    double lo = dunkey(fr->key_lo[d]), hi = dunkey(fr->key_hi[d]);
+    // (atomic reads: the other blocks' atomicMin / atomicMax results)
+    double lo = dunkey(atomicOr(&fr->key_lo[d], 0ULL)), hi = dunkey(atomicOr(&fr->key_hi[d], 0ULL));
     double ext = hi - lo;
     fr->lo[d] = lo;
     fr->ext[d] = ext;
@@ -591,7 +614,11 @@ __global__ __launch_bounds__(kBlock) void k_scan_top(int *bsum, int nb, int *tot
 // of an every-256th sample on its x = 0 plane and mapped a uniform axis);
 // vertices outside the (sampled) frame are left out, not clamped into the
 // edge bins.  H[block][d][bin] (kHistBlocks blocks, no atomics outside LDS)
-__global__ __launch_bounds__(kBlock) void k_axis_hist(const double *xyz, int np, const Frame *fr, int stride, int *H) {
+__device__ void axis_map(const int *H, Frame *fr, int g, int d);
+
+// the last block to finish turns the histograms into the three axes' maps
+// (one launch less per call)
+__global__ __launch_bounds__(kBlock) void k_axis_hist(const double *xyz, int np, Frame *fr, int stride, int *H, int g) {
   __shared__ int h[3][kMapBins];
   for (int j = threadIdx.x; j < 3 * kMapBins; j += kBlock) (&h[0][0])[j] = 0;
   __syncthreads();
@@ -611,6 +638,16 @@ __global__ __launch_bounds__(kBlock) void k_axis_hist(const double *xyz, int np,
   }
   __syncthreads();
   for (int j = threadIdx.x; j < 3 * kMapBins; j += kBlock) H[(size_t)blockIdx.x * 3 * kMapBins + j] = (&h[0][0])[j];
+  __threadfence();
+  __shared__ bool last;
+  if (threadIdx.x == 0) last = atomicAdd(&fr->hist_done, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  for (int d = 0; d < 3; d++) {
+    axis_map(H, fr, g, d);
+    __syncthreads();
+  }
 }
 
 // one block per axis: counts -> quantile map, adaptive bit.  The test is on
@@ -618,9 +655,8 @@ __global__ __launch_bounds__(kBlock) void k_axis_hist(const double *xyz, int np,
 // (one uniform cell's slab) against the mean slab, g * max / total.  Bins
 // finer than a cell cannot decide it (a lattice's coordinates fill only the
 // bins its planes fall into).
-__global__ __launch_bounds__(kBlock) void k_axis_map(const int *H, Frame *fr, int g) {
+__device__ void axis_map(const int *H, Frame *fr, int g, int d) {
   constexpr int R = kMapBins / kBlock; // bins per thread
-  const int d = blockIdx.x;
   __shared__ int cum[kMapBins + 1]; // cum[b] = vertices in bins [0, b)
   int cnt[R], s = 0;
 #pragma unroll

@@ -42,6 +42,17 @@ namespace {
 
 constexpr int kB = 256;
 
+// XCD-contiguous block order: hardware deals workgroup b to XCD b % 8; the
+// logical block returned gives XCD x the contiguous range [x n / 8, (x + 1)
+// n / 8), so the bucket / adjacency lines a tetra range writes fill in one
+// XCD's L2 instead of being written in parts from all eight (bijective)
+__device__ __forceinline__ long long xcd_blk() {
+  const long long b = blockIdx.x, n = gridDim.x;
+  const long long x = b & 7, q = n >> 3, r = n & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+}
+
+
 __constant__ int kIdirS[4][3] = {{1, 2, 3}, {0, 3, 2}, {0, 1, 3}, {0, 2, 1}};
 
 __device__ __forceinline__ int sel(const int4 &t, int i) { return i == 0 ? t.x : (i == 1 ? t.y : (i == 2 ? t.z : t.w)); }
@@ -116,7 +127,7 @@ __device__ __forceinline__ int wave_add(int *cnt, int idx, int val, bool act) {
 // written face by face by k_face_match)
 __global__ __launch_bounds__(kB) void k_face_count(const int4 *tetv, int ne, int np, int *cnt, int2 *rank,
                                                    int4 *tet8, int *err) {
-  const int k = blockIdx.x * kB + threadIdx.x;
+  const int k = (int)(xcd_blk() * kB + threadIdx.x);
   const bool in = k < ne;
   const int4 t = in ? tetv[k] : make_int4(1, 2, 3, 4);
   const bool ok = in && tet_ids_ok(t, np);
@@ -133,7 +144,7 @@ __global__ __launch_bounds__(kB) void k_face_count(const int4 *tetv, int ne, int
 
 __global__ __launch_bounds__(kB) void k_face_scatter(const int4 *tetv, int ne, const int *off, const int2 *rank,
                                                      int4 *bucket) {
-  const int k = blockIdx.x * kB + threadIdx.x;
+  const int k = (int)(xcd_blk() * kB + threadIdx.x);
   if (k >= ne) return;
   const int2 r = rank[k];
   if (r.x < 0) return;
@@ -162,7 +173,7 @@ __global__ __launch_bounds__(kB) void k_face_match(int np, const int *off, const
                                                    int *adja, int *tet8, int *err) {
   __shared__ int4 ent[kMatchCap];
   __shared__ int loff[kMatchVerts + 1];
-  const int v0 = blockIdx.x * kMatchVerts, nv = min(kMatchVerts, np - v0);
+  const int v0 = (int)xcd_blk() * kMatchVerts, nv = min(kMatchVerts, np - v0);
   if (threadIdx.x <= nv) loff[threadIdx.x] = threadIdx.x < nv ? off[v0 + threadIdx.x] : off[v0 + nv - 1] + cnt[v0 + nv - 1];
   __syncthreads();
   const int e0 = loff[0], n = loff[nv] - e0;
