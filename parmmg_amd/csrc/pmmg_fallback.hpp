@@ -38,9 +38,13 @@ __device__ __forceinline__ double centroid_dist(const double *x, const TriGeom &
 // group's step is a chain of ~20 launches of a few microseconds each).
 
 // the last block of a grid to pass this point (after its device-scope
-// atomics) gets true: the other blocks' results are then visible to it
+// atomics) gets true: the other blocks' results are then visible to it.  The
+// barrier before the ticket: every wave of the block has issued its atomics
+// (r04l: without it a block's later waves could still be scanning when the
+// last block read the results — 4 surface points left unprocessed, once)
 __device__ __forceinline__ bool last_block(unsigned *done) {
   __threadfence();
+  __syncthreads();
   __shared__ bool last;
   if (threadIdx.x == 0) last = atomicAdd(done, 1u) == gridDim.x - 1;
   __syncthreads();

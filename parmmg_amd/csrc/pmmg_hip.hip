@@ -1254,12 +1254,12 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   }
   hipLaunchKernelGGL(k_reset, dim3(blocks_for(ng > nsg ? ng : nsg, 2048)), dim3(kBlock), 0, s, fr, st, grid, ng,
                      sgrid, nsg, (int *)c->oflag.p, force, c->bin_bits);
-  // bbox (its last block finalises the frame), axis histograms (the last
-  // block builds the seed grid's axis maps)
+  // bbox (its last block finalises the frame), the seed grid's axis maps
   hipLaunchKernelGGL(k_bbox, dim3(blocks_for(bg.np / c->bbox_stride + 1, 256)), dim3(kBlock), 0, s, bg.xyz, bg.np, fr,
                      c->bbox_stride, g, gs, gb);
-  hipLaunchKernelGGL(k_axis_hist, dim3(kHistBlocks), dim3(kBlock), 0, s, bg.xyz, bg.np, fr, c->hist_stride,
-                     (int *)c->axh.p, g);
+  hipLaunchKernelGGL(k_axis_hist, dim3(kHistBlocks), dim3(kBlock), 0, s, bg.xyz, bg.np, (const Frame *)fr,
+                     c->hist_stride, (int *)c->axh.p);
+  hipLaunchKernelGGL(k_axis_map, dim3(3), dim3(kBlock), 0, s, (const int *)c->axh.p, fr, g);
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[EV_FRAME], s));
 

@@ -138,7 +138,7 @@ struct Frame {
   double qc[3], qs; // fixed-point frame of the walk's vertex copy
   int adaptive;     // bit d: axis d of the volume seed grid follows map[d]
   int seed_any;     // the lowest in-use tetra the seed grid sampled (INT_MAX: none): the last-resort seed
-  unsigned bbox_done, hist_done; // blocks done (the last block of k_bbox / k_axis_hist finishes the frame / map)
+  unsigned bbox_done; // blocks done (the last block of k_bbox finalises the frame)
   float map[3][kMapBins + 1]; // map[d][b] = share of the vertices below bin b's lower edge
 };
 
@@ -210,7 +210,7 @@ __global__ __launch_bounds__(kBlock) void k_reset(Frame *fr, DevStats *st, unsig
     }
     fr->adaptive = 0;
     fr->seed_any = INT_MAX;
-    fr->bbox_done = fr->hist_done = 0u;
+    fr->bbox_done = 0u;
     if (force >= 0) {
       flag[0] = force;
       flag[1] = force_bits;
@@ -279,6 +279,7 @@ __global__ __launch_bounds__(kBlock) void k_bbox(const double *xyz, int np, Fram
     atomicMax(&fr->key_hi[d], b);
   }
   __threadfence();
+  __syncthreads(); // every wave's atomics issued before the ticket
   __shared__ bool last;
   if (threadIdx.x == 0) last = atomicAdd(&fr->bbox_done, 1u) == gridDim.x - 1;
   __syncthreads();
@@ -614,11 +615,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_top(int *bsum, int nb, int *tot
 // of an every-256th sample on its x = 0 plane and mapped a uniform axis);
 // vertices outside the (sampled) frame are left out, not clamped into the
 // edge bins.  H[block][d][bin] (kHistBlocks blocks, no atomics outside LDS)
-__device__ void axis_map(const int *H, Frame *fr, int g, int d);
-
-// the last block to finish turns the histograms into the three axes' maps
-// (one launch less per call)
-__global__ __launch_bounds__(kBlock) void k_axis_hist(const double *xyz, int np, Frame *fr, int stride, int *H, int g) {
+__global__ __launch_bounds__(kBlock) void k_axis_hist(const double *xyz, int np, const Frame *fr, int stride, int *H) {
   __shared__ int h[3][kMapBins];
   for (int j = threadIdx.x; j < 3 * kMapBins; j += kBlock) (&h[0][0])[j] = 0;
   __syncthreads();
@@ -638,16 +635,6 @@ __global__ __launch_bounds__(kBlock) void k_axis_hist(const double *xyz, int np,
   }
   __syncthreads();
   for (int j = threadIdx.x; j < 3 * kMapBins; j += kBlock) H[(size_t)blockIdx.x * 3 * kMapBins + j] = (&h[0][0])[j];
-  __threadfence();
-  __shared__ bool last;
-  if (threadIdx.x == 0) last = atomicAdd(&fr->hist_done, 1u) == gridDim.x - 1;
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
-  for (int d = 0; d < 3; d++) {
-    axis_map(H, fr, g, d);
-    __syncthreads();
-  }
 }
 
 // one block per axis: counts -> quantile map, adaptive bit.  The test is on
@@ -655,8 +642,11 @@ __global__ __launch_bounds__(kBlock) void k_axis_hist(const double *xyz, int np,
 // (one uniform cell's slab) against the mean slab, g * max / total.  Bins
 // finer than a cell cannot decide it (a lattice's coordinates fill only the
 // bins its planes fall into).
-__device__ void axis_map(const int *H, Frame *fr, int g, int d) {
+// (r04k: the map built by the histogram kernel's last block, one launch
+// less, took the three axes in turn: preparation +0.08 ms at cfg4)
+__global__ __launch_bounds__(kBlock) void k_axis_map(const int *H, Frame *fr, int g) {
   constexpr int R = kMapBins / kBlock; // bins per thread
+  const int d = blockIdx.x;
   __shared__ int cum[kMapBins + 1]; // cum[b] = vertices in bins [0, b)
   int cnt[R], s = 0;
 #pragma unroll
