@@ -541,8 +541,19 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   pmmg_hip_ctx *c = new pmmg_hip_ctx();
   c->device = device;
   c->options = options;
+  // the second stream (query order, then the surface branch) at the highest
+  // priority: k_bdy's blocks are dispatched ahead of the volume kernel's
+  // instead of trailing it (r04o trace: the surface branch ended 0.17 ms after
+  // the volume kernel, the end of the step); measurement build:
+  // PMMG_HIP_SRFPRIO=0 for the default priority
+  int prio_lo = 0, prio_hi = 0;
+  (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+#ifdef PMMG_HIP_MEASURE
+  if (const char *e = getenv("PMMG_HIP_SRFPRIO"))
+    if (*e == '0') prio_hi = prio_lo;
+#endif
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
+      hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess) {
     fprintf(stderr, "[parmmg_hip] cannot initialise device %d\n", device);
     delete c;
     return nullptr;
@@ -1301,7 +1312,8 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
       return 0;
     unsigned *k0 = (unsigned *)c->bkeys.p, *k1 = (unsigned *)c->bkeys2.p;
     int *v0 = (int *)c->bvals.p, *v1 = (int *)c->bvals2.p, *hist = (int *)c->rs_hist.p, *csum = (int *)c->rs_csum.p;
-    hipLaunchKernelGGL(k_bin_keys, dim3(ntile), dim3(kBlock), 0, sb, xyz_new, pclass, np_new, (const Frame *)fr, flag,
+    const int tgrid = std::min(ntile, kRsGrid);
+    hipLaunchKernelGGL(k_bin_keys, dim3(tgrid), dim3(kBlock), 0, sb, xyz_new, pclass, np_new, (const Frame *)fr, flag,
                        k0, v0, st, kRsTile, ntile, hist);
     for (int pass = 0; pass < 3; pass++) {
       const unsigned *kin = pass == 1 ? k1 : k0;
@@ -1309,11 +1321,11 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
       unsigned *kout = pass == 1 ? k0 : k1;
       int *vout = pass == 1 ? v0 : (pass == 0 ? v1 : order_v);
       if (pass > 0)
-        hipLaunchKernelGGL(k_rs_hist, dim3(ntile), dim3(kBlock), 0, sb, kin, np_new, 8 * pass, ntile, hist, flag, 1);
+        hipLaunchKernelGGL(k_rs_hist, dim3(tgrid), dim3(kBlock), 0, sb, kin, np_new, 8 * pass, ntile, hist, flag, 1);
       hipLaunchKernelGGL(k_rs_scan_local, dim3(nch), dim3(kBlock), 0, sb, hist, (int)nh, csum, flag, 1);
       hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, sb, csum, nch, (int *)nullptr, flag, 1);
       hipLaunchKernelGGL(k_rs_scan_add, dim3(nch), dim3(kBlock), 0, sb, hist, (int)nh, (const int *)csum, flag, 1);
-      hipLaunchKernelGGL(k_rs_scatter, dim3(ntile), dim3(kBlock), 0, sb, kin, vin, np_new, 8 * pass, ntile,
+      hipLaunchKernelGGL(k_rs_scatter, dim3(tgrid), dim3(kBlock), 0, sb, kin, vin, np_new, 8 * pass, ntile,
                          (const int *)hist, kout, vout, flag, 1);
     }
     hipLaunchKernelGGL(k_bin_split, dim3(blocks_for(np_new, 4096)), dim3(kBlock), 0, sb, (const int *)order_v, xyz_new,

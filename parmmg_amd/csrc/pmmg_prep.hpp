@@ -799,9 +799,10 @@ __global__ __launch_bounds__(kBlock) void k_coherence(const double *xyz, int np,
 // is a deterministic function of the input.
 
 // flag: the order decision {sorted, bits per axis} (k_coherence); the kernel
-// runs only when flag[0] == 1.  One block per radix-sort tile (tile_keys
-// keys, pmmg_sort.hpp): besides the keys it writes the tile's histogram of
-// the first 8-bit digit (hist[digit * ntile + tile]), the first pass's table.
+// runs only when flag[0] == 1.  Blocks loop over the radix sort's tiles
+// (tile_keys keys, pmmg_sort.hpp): besides the keys it writes each tile's
+// histogram of the first 8-bit digit (hist[digit * ntile + tile]), the first
+// pass's table.
 __global__ __launch_bounds__(kBlock) void k_bin_keys(const double *xyz, const uint8_t *pclass, int np, const Frame *fr,
                                                      const int *flag, unsigned *keys, int *vals, DevStats *st,
                                                      int tile_keys, int ntile, int *hist) {
@@ -813,7 +814,8 @@ __global__ __launch_bounds__(kBlock) void k_bin_keys(const double *xyz, const ui
   if (threadIdx.x == 0) sv = sb = 0;
   __syncthreads();
   int nv = 0, nb = 0;
-  const long long base = (long long)blockIdx.x * tile_keys;
+  for (int tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
+  const long long base = (long long)tile * tile_keys;
   for (int e = threadIdx.x; e < tile_keys; e += kBlock) {
     const long long i = base + e;
     if (i >= np) break;
@@ -834,6 +836,11 @@ __global__ __launch_bounds__(kBlock) void k_bin_keys(const double *xyz, const ui
     vals[i] = (int)(i + 1);
     atomicAdd(&h[key & 255u], 1);
   }
+  __syncthreads();
+  hist[(size_t)threadIdx.x * ntile + tile] = h[threadIdx.x];
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  }
   for (int o = 32; o > 0; o >>= 1) {
     nv += __shfl_down(nv, o);
     nb += __shfl_down(nb, o);
@@ -843,7 +850,6 @@ __global__ __launch_bounds__(kBlock) void k_bin_keys(const double *xyz, const ui
     atomicAdd(&sb, nb);
   }
   __syncthreads();
-  hist[(size_t)threadIdx.x * ntile + blockIdx.x] = h[threadIdx.x];
   if (threadIdx.x == 0) {
     if (sv) atomicAdd(&st->nvol, sv);
     if (sb) atomicAdd(&st->nbdy, sb);

@@ -21,20 +21,29 @@ namespace pmmg {
 
 constexpr int kRsItems = 16, kRsTile = kBlock * kRsItems; // keys per tile (one block)
 
+// The tile kernels loop over tiles (grid <= kRsGrid blocks): gated off, a
+// launch is then a few hundred empty blocks instead of one per tile (r04o:
+// 5000 empty blocks of the 38 KB-LDS scatter took 0.22 ms of CU slots beside
+// the seed grid)
+constexpr int kRsGrid = 1024;
+
 __global__ __launch_bounds__(kBlock) void k_rs_hist(const unsigned *keys, int n, int shift, int ntile, int *hist,
                                                     const int *gate, int want) {
   if (gate_off(gate, want)) return;
   __shared__ int h[256];
-  h[threadIdx.x] = 0;
-  __syncthreads();
-  const long long base = (long long)blockIdx.x * kRsTile;
+  for (int tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const long long base = (long long)tile * kRsTile;
 #pragma unroll 4
-  for (int j = 0; j < kRsItems; j++) {
-    const long long idx = base + j * kBlock + threadIdx.x;
-    if (idx < n) atomicAdd(&h[(keys[idx] >> shift) & 255u], 1);
+    for (int j = 0; j < kRsItems; j++) {
+      const long long idx = base + j * kBlock + threadIdx.x;
+      if (idx < n) atomicAdd(&h[(keys[idx] >> shift) & 255u], 1);
+    }
+    __syncthreads();
+    hist[(size_t)threadIdx.x * ntile + tile] = h[threadIdx.x];
+    __syncthreads();
   }
-  __syncthreads();
-  hist[(size_t)threadIdx.x * ntile + blockIdx.x] = h[threadIdx.x];
 }
 
 // exclusive scan of a[0..n) in place: per-chunk scans (chunk sums to
@@ -83,7 +92,8 @@ __global__ __launch_bounds__(kBlock) void k_rs_scatter(const unsigned *kin, cons
   __shared__ int gdelta[256];      // global position - local position of each digit's keys
   __shared__ int wcnt[4][256];     // keys of each digit in each wave of the current sub-tile
   const int t = threadIdx.x, w = t >> 6, lane = __lane_id();
-  const long long base = (long long)blockIdx.x * kRsTile;
+  for (int tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
+  const long long base = (long long)tile * kRsTile;
   const int cnt = (int)(n - base < kRsTile ? n - base : kRsTile);
   // the tile's digit counts, their exclusive scan
   run[t] = 0;
@@ -99,7 +109,7 @@ __global__ __launch_bounds__(kBlock) void k_rs_scatter(const unsigned *kin, cons
   const int lstart = block_excl_scan(run[t], &tot);
   __syncthreads();
   run[t] = lstart;
-  gdelta[t] = off[(size_t)t * ntile + blockIdx.x] - lstart;
+  gdelta[t] = off[(size_t)t * ntile + tile] - lstart;
   __syncthreads();
   for (int j = 0; j < kRsItems; j++) {
     const int e = j * kBlock + t;
@@ -132,6 +142,8 @@ __global__ __launch_bounds__(kBlock) void k_rs_scatter(const unsigned *kin, cons
     const int pos = gdelta[(key >> shift) & 255u] + e;
     kout[pos] = key;
     vout[pos] = lv[e];
+  }
+  __syncthreads(); // the tile's LDS is free for the next tile
   }
 }
 

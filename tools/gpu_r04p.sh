@@ -1,0 +1,13 @@
+#!/bin/bash
+# r04p: staged Morton order (records in processing order + k_vol_unstage):
+# GPU suite, shuffled / Mmg-like / forced-bin sweeps at cfg4 and cfg3
+set -o pipefail
+export TMPDIR=/tmp
+OUT=gpurun_out/${TAG:-r04p}
+mkdir -p $OUT
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1 \
+&& tail -2 $OUT/pytest.log \
+&& timeout -k 10 900 python3 -u tools/sweep.py --config cfg4 --rounds 2 --steps 3 --variants "sort=0;perm=shuffle;sort=1;perm=mmg,sort=1" > $OUT/sweep.txt 2>&1 \
+&& cat $OUT/sweep.txt \
+&& timeout -k 10 600 python3 -u tools/sweep.py --config cfg3 --rounds 2 --steps 3 --variants "sort=0;perm=shuffle" > $OUT/sweep_cfg3.txt 2>&1 \
+&& cat $OUT/sweep_cfg3.txt
