@@ -13,7 +13,9 @@
  * is checked against known answers (affine fields are reproduced by the P1
  * interpolation, a constant tensor by the inverse-tensor interpolation) and
  * the device-built background (adjacency / boundary trias not handed over)
- * must give bit-identical outputs.  Exit status 0 = pass.
+ * must give bit-identical outputs, as must the many-groups call
+ * (pmmg_hip_locate_interp_groups) and a second iteration carried over from
+ * the device (pmmg_interp_metrics_and_fields_carry).  Exit status 0 = pass.
  */
 #include <math.h>
 #include <stdint.h>
@@ -250,6 +252,186 @@ static void device_checks(pmmg_hip_ctx *ctx) {
   }
 }
 
+/* device allocations of one check, freed together */
+typedef struct {
+  void *p[64];
+  int n;
+} dev_list;
+
+static void *dev_up(pmmg_hip_ctx *ctx, dev_list *L, const void *src, size_t bytes) {
+  void *d = pmmg_hip_malloc(ctx, (int64_t)bytes);
+  if (d && src && !pmmg_hip_memcpy_h2d(ctx, d, src, (int64_t)bytes)) d = NULL;
+  if (d && L->n < 64) L->p[L->n++] = d;
+  return d;
+}
+
+static void dev_free(pmmg_hip_ctx *ctx, dev_list *L) {
+  for (int i = 0; i < L->n; i++) pmmg_hip_free(ctx, L->p[i]);
+  L->n = 0;
+}
+
+static double *nan_rows(size_t n) {
+  double *a = malloc(sizeof(double) * n);
+  for (size_t i = 0; i < n; i++) a[i] = NAN;
+  return a;
+}
+
+/* pmmg_hip_locate_interp_groups: two groups in device memory, one call —
+ * bit-identical to the host layer's one call per group */
+static void groups_checks(pmmg_hip_ctx *ctx) {
+  group G[2];
+  make_group(&G[0], 6, 7, 21);
+  make_group(&G[1], 5, 8, 22);
+  CHECK(run(ctx, G, 2, 0) == 1, "host-layer transfer failed: %s", pmmg_hip_last_error(ctx));
+  static const int fsz[3] = {1, 3, 6};
+  dev_list L = {{0}, 0};
+  pmmg_hip_group dg[2];
+  const double *din[2][3];
+  double *dout[2][3];
+  for (int ig = 0; ig < 2; ig++) {
+    group *g = &G[ig];
+    const size_t ne = (size_t)g->bg.ne, nq = (size_t)g->nw.np;
+    int *tet8 = malloc(sizeof(int) * 8 * ne);
+    for (size_t k = 0; k < ne; k++) {
+      memcpy(tet8 + 8 * k, g->bg.tetv + 4 * k, 16);
+      memcpy(tet8 + 8 * k + 4, g->bg.adja + 4 * k, 16);
+    }
+    pmmg_new_group ng = {0};
+    ng.np = g->nw.np;
+    ng.ne = g->nw.ne;
+    ng.xyz = g->nw.xyz;
+    ng.tag = g->tag;
+    ng.tetv = g->nw.tetv;
+    uint8_t *pc = malloc(nq);
+    pmmg_classify_points(&ng, pc);
+    double *n6 = nan_rows(6 * nq), *n3 = nan_rows(3 * nq), *n1 = nan_rows(nq);
+    int *z4 = calloc(nq, sizeof(int));
+    din[ig][0] = dev_up(ctx, &L, g->fs, sizeof(double) * g->bg.np);
+    din[ig][1] = dev_up(ctx, &L, g->fv, sizeof(double) * 3 * g->bg.np);
+    din[ig][2] = dev_up(ctx, &L, g->ft, sizeof(double) * 6 * g->bg.np);
+    dout[ig][0] = dev_up(ctx, &L, n1, sizeof(double) * nq);
+    dout[ig][1] = dev_up(ctx, &L, n3, sizeof(double) * 3 * nq);
+    dout[ig][2] = dev_up(ctx, &L, n6, sizeof(double) * 6 * nq);
+    memset(&dg[ig], 0, sizeof(dg[ig]));
+    dg[ig].np = g->bg.np;
+    dg[ig].ne = g->bg.ne;
+    dg[ig].nt = g->bg.nt;
+    dg[ig].xyz = dev_up(ctx, &L, g->bg.xyz, sizeof(double) * 3 * g->bg.np);
+    dg[ig].tet8 = dev_up(ctx, &L, tet8, sizeof(int) * 8 * ne);
+    dg[ig].triv = dev_up(ctx, &L, g->bg.triv, sizeof(int) * 3 * g->bg.nt);
+    dg[ig].adjt = dev_up(ctx, &L, g->bg.adjt, sizeof(int) * 3 * g->bg.nt);
+    dg[ig].hausd = 0.01;
+    dg[ig].met_size = 6;
+    dg[ig].met = dev_up(ctx, &L, g->met, sizeof(double) * 6 * g->bg.np);
+    dg[ig].nfield = 3;
+    dg[ig].field_size = fsz;
+    dg[ig].fields = din[ig];
+    dg[ig].np_new = g->nw.np;
+    dg[ig].xyz_new = dev_up(ctx, &L, g->nw.xyz, sizeof(double) * 3 * nq);
+    dg[ig].pclass = dev_up(ctx, &L, pc, nq);
+    dg[ig].met_out = dev_up(ctx, &L, n6, sizeof(double) * 6 * nq);
+    dg[ig].fields_out = dout[ig];
+    dg[ig].elem_out = dev_up(ctx, &L, z4, sizeof(int) * nq);
+    dg[ig].hit_out = dev_up(ctx, &L, z4, nq);
+    free(tet8); free(pc); free(n6); free(n3); free(n1); free(z4);
+  }
+  pmmg_hip_stats st;
+  CHECK(pmmg_hip_locate_interp_groups(ctx, 2, dg, &st) == 1, "groups call failed: %s", pmmg_hip_last_error(ctx));
+  for (int ig = 0; ig < 2; ig++) {
+    group *g = &G[ig];
+    const size_t nq = (size_t)g->nw.np;
+    double *m = malloc(48 * nq), *fs = malloc(8 * nq), *fv = malloc(24 * nq), *ft = malloc(48 * nq);
+    int *el = malloc(4 * nq);
+    int8_t *ht = malloc(nq);
+    pmmg_hip_memcpy_d2h(ctx, m, dg[ig].met_out, 48 * (int64_t)nq);
+    pmmg_hip_memcpy_d2h(ctx, fs, dout[ig][0], 8 * (int64_t)nq);
+    pmmg_hip_memcpy_d2h(ctx, fv, dout[ig][1], 24 * (int64_t)nq);
+    pmmg_hip_memcpy_d2h(ctx, ft, dout[ig][2], 48 * (int64_t)nq);
+    pmmg_hip_memcpy_d2h(ctx, el, dg[ig].elem_out, 4 * (int64_t)nq);
+    pmmg_hip_memcpy_d2h(ctx, ht, dg[ig].hit_out, (int64_t)nq);
+    /* NaN rows compare bit for bit: both sides start from the same NaN */
+    CHECK(memcmp(m, g->omet, 48 * nq) == 0 && memcmp(fs, g->ofs, 8 * nq) == 0 && memcmp(fv, g->ofv, 24 * nq) == 0 &&
+              memcmp(ft, g->oft, 48 * nq) == 0 && memcmp(el, g->elem, 4 * nq) == 0 && memcmp(ht, g->hit, nq) == 0,
+          "group %d: the groups call differs from the host layer", ig);
+    free(m); free(fs); free(fv); free(ft); free(el); free(ht);
+  }
+  dev_free(ctx, &L);
+  free_group(&G[0]);
+  free_group(&G[1]);
+}
+
+/* pmmg_interp_metrics_and_fields_carry: the second iteration fed from the
+ * rows kept on the device equals a cold call on a fresh context, with fewer
+ * bytes up */
+static void carry_checks(pmmg_hip_ctx *ctx) {
+  group G;
+  make_group(&G, 6, 7, 31);
+  static const int fsz[3] = {1, 3, 6};
+  /* iteration 1: G.bg -> G.nw, kept */
+  pmmg_old_group o1 = {0};
+  pmmg_new_group n1 = {0};
+  const double *fin1[3] = {G.fs, G.fv, G.ft};
+  double *fout1[3] = {G.ofs, G.ofv, G.oft};
+  const size_t nq = (size_t)G.nw.np;
+  for (size_t i = 0; i < 6 * nq; i++) G.omet[i] = G.oft[i] = NAN;
+  for (size_t i = 0; i < nq; i++) G.ofs[i] = NAN;
+  for (size_t i = 0; i < 3 * nq; i++) G.ofv[i] = NAN;
+  o1.np = G.bg.np; o1.ne = G.bg.ne; o1.nt = G.bg.nt; o1.xyz = G.bg.xyz; o1.tetv = G.bg.tetv; o1.adja = G.bg.adja;
+  o1.triv = G.bg.triv; o1.adjt = G.bg.adjt; o1.hausd = 0.01; o1.met_size = 6; o1.met = G.met; o1.nfield = 3;
+  o1.field_size = fsz; o1.field = fin1;
+  n1.np = G.nw.np; n1.ne = G.nw.ne; n1.xyz = G.nw.xyz; n1.tag = G.tag; n1.tetv = G.nw.tetv; n1.met_size = 6;
+  n1.met = G.omet; n1.field = fout1; n1.ani = 1;
+  pmmg_hip_stats st;
+  CHECK(pmmg_interp_metrics_and_fields_carry(ctx, 1, &o1, &n1, 1, 0, NULL, &st) == 1, "iteration 1: %s",
+        pmmg_hip_last_error(ctx));
+  /* the skipped (MG_REQ) rows as PMMG_copyMetricsAndFields_point fills them */
+  for (size_t i = 0; i < nq; i++)
+    if (G.tag[i] & PMMG_TAG_REQ) {
+      for (int c = 0; c < 6; c++) G.omet[6 * i + c] = G.oft[6 * i + c] = 0.5 + c;
+      G.ofs[i] = -1.0;
+      for (int c = 0; c < 3; c++) G.ofv[3 * i + c] = 2.0;
+    }
+  /* iteration 2: old group = G.nw with those rows, new group = another lattice */
+  mesh nx = make_mesh(SYNTH_CUBE, 5, 0.2, 33);
+  const size_t nq2 = (size_t)nx.np;
+  uint16_t *tag2 = calloc(nq2, sizeof(uint16_t));
+  for (size_t i = 0; i < nq2; i++) tag2[i] = nx.isbdy[i] ? PMMG_TAG_BDY : 0;
+  pmmg_old_group o2 = {0};
+  const double *fin2[3] = {G.ofs, G.ofv, G.oft};
+  o2.np = G.nw.np; o2.ne = G.nw.ne; o2.nt = -1; o2.xyz = G.nw.xyz; o2.tetv = G.nw.tetv; o2.hausd = 0.01;
+  o2.met_size = 6; o2.met = G.omet; o2.nfield = 3; o2.field_size = fsz; o2.field = fin2;
+  double *res[2][4];
+  int64_t up[2];
+  for (int pass = 0; pass < 2; pass++) { /* 0: carried, 1: cold on a fresh context */
+    pmmg_hip_ctx *c = pass == 0 ? ctx : pmmg_hip_create(0, 0);
+    res[pass][0] = nan_rows(6 * nq2); res[pass][1] = nan_rows(nq2); res[pass][2] = nan_rows(3 * nq2);
+    res[pass][3] = nan_rows(6 * nq2);
+    double *fo[3] = {res[pass][1], res[pass][2], res[pass][3]};
+    pmmg_new_group n2 = {0};
+    n2.np = nx.np; n2.ne = nx.ne; n2.xyz = nx.xyz; n2.tag = tag2; n2.tetv = nx.tetv; n2.met_size = 6;
+    n2.met = res[pass][0]; n2.field = fo; n2.ani = 1;
+    pmmg_hip_bytes_up(c, 1);
+    const int ok = pass == 0 ? pmmg_interp_metrics_and_fields_carry(c, 1, &o2, &n2, 1, 1, NULL, &st)
+                             : pmmg_interp_metrics_and_fields(c, 1, &o2, &n2, 1, &st);
+    CHECK(ok == 1, "iteration 2 (%s): %s", pass == 0 ? "carried" : "cold", pmmg_hip_last_error(c));
+    up[pass] = pmmg_hip_bytes_up(c, 0);
+    if (pass == 1) pmmg_hip_destroy(c);
+  }
+  const size_t sz[4] = {48 * nq2, 8 * nq2, 24 * nq2, 48 * nq2};
+  int same = 1;
+  for (int a = 0; a < 4; a++) same = same && memcmp(res[0][a], res[1][a], sz[a]) == 0;
+  CHECK(same, "the carried iteration differs from the cold one");
+  const int64_t rows = (int64_t)nq * (24 + 48 + 8 + 24 + 48);
+  CHECK(up[0] <= up[1] - rows / 2, "carried iteration uploaded %lld bytes, cold %lld", (long long)up[0],
+        (long long)up[1]);
+  printf("test_c_abi: carried iteration %lld bytes up, cold %lld\n", (long long)up[0], (long long)up[1]);
+  for (int p = 0; p < 2; p++)
+    for (int a = 0; a < 4; a++) free(res[p][a]);
+  free(tag2);
+  free_mesh(&nx);
+  free_group(&G);
+}
+
 /* the reference's libexamples/adaptation_example0 cube read by the C Medit
  * reader (cube.mesh, cube-met.sol, cube-solphys.sol), transferred to its
  * tetra centroids (volume points: P1 values = mean of the 4 vertex values)
@@ -356,6 +538,8 @@ int main(int argc, char **argv) {
   } else {
     CHECK(ctx != NULL, "pmmg_hip_create(0) failed");
     if (ctx) device_checks(ctx);
+    if (ctx) groups_checks(ctx);
+    if (ctx) carry_checks(ctx);
     if (ctx) fixture_checks(ctx, fixtures);
     pmmg_hip_destroy(ctx);
     printf("test_c_abi: host-only and device checks %s\n", failures ? "FAILED" : "passed");

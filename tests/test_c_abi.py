@@ -35,6 +35,7 @@ def test_c_program_on_the_gpu():
     print(p.stdout)
     assert p.returncode == 0, p.stdout
     assert "host-only and device checks passed" in p.stdout
+    assert "test_c_abi: carried iteration" in p.stdout
     assert "reference cube fixture (12 tetra, 24 points) transferred, 0 wrong values" in p.stdout
 
 
