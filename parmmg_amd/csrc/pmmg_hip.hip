@@ -1274,11 +1274,10 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[EV_FRAME], s));
 
-  // ---- query order (second stream, concurrent with the seed grid): the
-  // coherence test runs first; in auto mode its flag is read back while the
-  // main stream builds the seed grid (the host waits ~0.1 ms, the device does
-  // not), then either the Morton binning (sorted) or the stable class
-  // compaction of the surface points (input order) is enqueued
+  // ---- query order (second stream, concurrent with the seed grid), after
+  // the frame.  (r04: the axis maps moved here beside the fixed-point copy
+  // cost 10 groups 0.11 -> 0.25 ms per group and the 8-way rank +0.02 ms for
+  // -0.0 at cfg4, `profiles/r04s`: not kept)
   HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_FRAME], 0));
   HIPCK(c, hipGetLastError());
 
