@@ -24,17 +24,20 @@
 // each face (edge) scans its own bucket (~24 faces per vertex in a tetra
 // mesh) for its twin.  The match is a pure function of the connectivity, so
 // the result does not depend on the atomic order.  Tetra faces (r04): the
-// counting atomics are combined per wave (consecutive tetra share their
-// smallest vertex), and the twins are found bucket by bucket — a block loads
-// the buckets of 64 consecutive vertices into LDS with one coalesced read and
-// every face scans its bucket there, writing its adjacency entry (r03: one
-// thread per tetra scanning two buckets in HBM, 9.3 of the 22 ms, latency-
-// bound).  Scratch buffers are kept by the context (SnapCache).
+// counting atomics are combined per wave (one atomic per distinct vertex, all
+// in one instruction), the bucket entries are 12 bytes, and the twins are
+// found bucket by bucket — a block loads the buckets of 24 consecutive
+// vertices into LDS with one coalesced read and the faces meet in an LDS hash
+// table, each writing its adjacency entry (r03: one thread per tetra scanning
+// two buckets in HBM, 9.3 of the 22 ms, latency-bound).  Scratch buffers are
+// kept by the context (SnapCache).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
 #include <stdint.h>
 #include <stdio.h>
+
+#include <algorithm>
 
 #include "pmmg_snapshot.hpp"
 
@@ -98,28 +101,53 @@ __device__ __forceinline__ bool tet_ids_ok(const int4 &t, int np) {
   return ok;
 }
 
-// cnt[idx] += val for the active lanes, returning each lane's old value plus
-// the contributions of the lower lanes with the same idx: lanes with equal
-// idx share one atomic (up to kAggRounds distinct idx per wave; the rest
-// issue their own)
-constexpr int kAggRounds = 6;
-__device__ __forceinline__ int wave_add(int *cnt, int idx, int val, bool act) {
+// cnt[idx] += val for the active lanes (idx >= 0), each lane getting the old
+// value plus the contributions of the lanes before it with the same idx.  The
+// wave's {idx, lane} keys are bitonic-sorted across the lanes (wave_runs), the
+// first lane of every run of equal idx issues the run's atomic — all runs in
+// one instruction — and the ranks go back to the lanes they belong to by
+// ds_permute (run_rank).  k_face_count issues its two reservations' atomics
+// together: one round trip per wave.  (r04: the previous form took up to 7
+// dependent atomic round trips per wave, one per distinct idx; the count
+// kernel was latency-bound on them at 6.8 ms for 101M tetra.)
+struct WaveRun {
+  unsigned long long key; // this lane's sorted {idx, lane}
+  int h, n;               // first lane of its run; the run's length (at the first lane)
+  bool head, valid;
+};
+constexpr unsigned long long kIdle = ~0ULL >> 6; // sorts after every idx, lane bits kept distinct
+
+__device__ __forceinline__ WaveRun wave_runs(int idx, bool act) {
   const int lane = __lane_id();
-  unsigned long long todo = __ballot(act);
-  int res = 0;
-#pragma unroll 1
-  for (int r = 0; r < kAggRounds && todo; r++) {
-    const int leader = __ffsll((long long)todo) - 1;
-    const int li = __shfl(idx, leader);
-    const unsigned long long m = __ballot(act && idx == li) & todo;
-    int old = 0;
-    if (lane == leader) old = atomicAdd(&cnt[li], val * __popcll(m));
-    old = __shfl(old, leader);
-    if ((m >> lane) & 1ULL) res = old + val * __popcll(m & ((1ULL << lane) - 1ULL));
-    todo &= ~m;
+  unsigned long long key = ((act ? (unsigned long long)(unsigned)idx : kIdle) << 6) | (unsigned)lane;
+#pragma unroll
+  for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const unsigned long long o = __shfl_xor(key, j);
+      const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
+      key = keep_min ? (o < key ? o : key) : (o > key ? o : key);
+    }
   }
-  if ((todo >> lane) & 1ULL) res = atomicAdd(&cnt[idx], val);
-  return res;
+  WaveRun w;
+  w.key = key;
+  const unsigned long long sid = key >> 6, prev = __shfl_up(sid, 1);
+  w.valid = sid != kIdle;
+  w.head = w.valid && (lane == 0 || prev != sid);
+  const unsigned long long heads = __ballot(w.head), nvalid = __popcll(__ballot(w.valid));
+  const unsigned long long le = lane == 63 ? ~0ULL : ((2ULL << lane) - 1ULL);
+  w.h = 63 - __clzll((long long)(heads & le)); // valid lanes only
+  const unsigned long long after = heads & ~le;
+  w.n = (after ? __ffsll((long long)after) - 1 : (int)nvalid) - lane;
+  return w;
+}
+
+// `old`: the atomic's result at the run's first lane
+__device__ __forceinline__ int run_rank(const WaveRun &w, int old, int val) {
+  const int lane = __lane_id();
+  old = __shfl(old, w.valid ? w.h : lane);
+  // back to the lane the key came from (a push: every lane receives exactly one value)
+  return __builtin_amdgcn_ds_permute((int)(w.key & 63) << 2, old + val * (lane - w.h));
 }
 
 // rank[k] = {slot of the s0 faces (3 consecutive), slot of the s1 face};
@@ -134,8 +162,11 @@ __global__ __launch_bounds__(kB) void k_face_count(const int4 *tetv, int ne, int
   if (in && !ok) atomicOr(err, kErrIds);
   int i0 = 0, i1 = 1;
   two_smallest(t, i0, i1);
-  const int r0 = wave_add(cnt, sel(t, i0) - 1, 3, ok);
-  const int r1 = wave_add(cnt, sel(t, i1) - 1, 1, ok);
+  const WaveRun w0 = wave_runs(sel(t, i0) - 1, ok), w1 = wave_runs(sel(t, i1) - 1, ok);
+  int o0 = 0, o1 = 0;
+  if (w0.head) o0 = atomicAdd(&cnt[(int)(w0.key >> 6)], 3 * w0.n);
+  if (w1.head) o1 = atomicAdd(&cnt[(int)(w1.key >> 6)], w1.n);
+  const int r0 = run_rank(w0, o0, 3), r1 = run_rank(w1, o1, 1);
   if (in) {
     rank[k] = ok ? make_int2(r0, r1) : make_int2(-1, -1);
     if (tet8) tet8[2 * (size_t)k] = t;
@@ -143,7 +174,7 @@ __global__ __launch_bounds__(kB) void k_face_count(const int4 *tetv, int ne, int
 }
 
 __global__ __launch_bounds__(kB) void k_face_scatter(const int4 *tetv, int ne, const int *off, const int2 *rank,
-                                                     int4 *bucket) {
+                                                     int3 *bucket) {
   const int k = (int)(xcd_blk() * kB + threadIdx.x);
   if (k >= ne) return;
   const int2 r = rank[k];
@@ -151,15 +182,16 @@ __global__ __launch_bounds__(kB) void k_face_scatter(const int4 *tetv, int ne, c
   const int4 t = tetv[k];
   int i0, i1;
   two_smallest(t, i0, i1);
+  const int o0 = off[sel(t, i0) - 1] + r.x, o1 = off[sel(t, i1) - 1] + r.y;
   int n = 0;
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     int a, b, c;
     face_ids(t, i, a, b, c);
     // code of this face in the reference encoding: 4*k + i with k 1-based
-    const int4 e = make_int4(b, c, 4 * (k + 1) + i, 0);
-    if (i == i0) bucket[off[a - 1] + r.y] = e; // face opposite s0: bucket of s1
-    else bucket[off[a - 1] + r.x + n++] = e;
+    const int3 e = make_int3(b, c, 4 * (k + 1) + i);
+    if (i == i0) bucket[o1] = e; // face opposite s0: bucket of s1
+    else bucket[o0 + n++] = e;
   }
 }
 
@@ -168,47 +200,149 @@ __global__ __launch_bounds__(kB) void k_face_scatter(const int4 *tetv, int ne, c
 // in place; every face writes its entry of the adjacency: its twin's code, 0
 // on the boundary.  Invalid tetra (flagged by k_face_count) have no faces in
 // the buckets: their rows are zeroed by k_face_invalid.
-constexpr int kMatchVerts = 64, kMatchCap = 2048;
-__global__ __launch_bounds__(kB) void k_face_match(int np, const int *off, const int *cnt, const int4 *bucket,
-                                                   int *adja, int *tet8, int *err) {
-  __shared__ int4 ent[kMatchCap];
-  __shared__ int loff[kMatchVerts + 1];
-  const int v0 = (int)xcd_blk() * kMatchVerts, nv = min(kMatchVerts, np - v0);
-  if (threadIdx.x <= nv) loff[threadIdx.x] = threadIdx.x < nv ? off[v0 + threadIdx.x] : off[v0 + nv - 1] + cnt[v0 + nv - 1];
+//
+// r04: in LDS the twins meet in a hash table keyed by {bucket, b, c} — each
+// entry probes ~1-2 slots — instead of every entry scanning its whole bucket
+// (~24 entries of 16 bytes: 6.7 ms of LDS reads for 404M faces at cfg4).
+// The later of two twins finds the earlier in the table and pairs them with a
+// compare-and-swap on the earlier's mate; a third face with the same key
+// finds the mate taken (non-manifold).  Blocks whose buckets exceed
+// kMatchCap entries scan them in place.
+constexpr int kMatchVerts = 24, kMatchCap = 768, kHashSlots = 1024; // 17 KB of LDS: 8 blocks per CU
+__device__ __forceinline__ int bucket_of(const int *loff, int nv, int e0, int j) {
+  int lo = 0, hi = nv; // loff[lo] - e0 <= j < loff[hi] - e0
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (loff[mid] - e0 <= j) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ void put_adja(int *adja, int *tet8, int code, int twin) {
+  const size_t k = (size_t)(code >> 2) - 1, i = (size_t)(code & 3);
+  if (adja) adja[4 * k + i] = twin;
+  if (tet8) tet8[8 * k + 4 + i] = twin;
+}
+
+// Persistent blocks (r04): the blocks of XCD x walk the chunks of kMatchVerts
+// vertices in [x n / 8, (x + 1) n / 8); the offsets of the chunk after next
+// and the entries of the next chunk are loaded while the current one is
+// matched in LDS (one block per chunk waited for two dependent round trips,
+// offsets then entries, with ~8 blocks per CU: 3.3 ms at cfg4).  The loads
+// are unconditional (clamped indices) so that the compiler's wait for the
+// current entries leaves the next ones in flight.
+static_assert(kMatchCap == 3 * kB, "three entries per thread (registers E0..E2)");
+
+// offset t (0..nv) of the chunk starting at vertex v0: off[v0 + t], or the
+// total past the last vertex; clamped loads, garbage for t > nv
+__device__ __forceinline__ int chunk_off(const int *off, const int *cnt, int np, int v0, int t) {
+  const int v = min(v0 + t, np - 1);
+  const int a = off[v], b = cnt[v];
+  return v0 + t < np ? a : a + b;
+}
+
+__global__ __launch_bounds__(kB) void k_face_match(int np, const int *off, const int *cnt, const int3 *bucket,
+                                                   long long nf, int *adja, int *tet8, int *err) {
+  __shared__ int3 ent[kMatchCap];         // {b, c, code}
+  __shared__ unsigned char lb[kMatchCap]; // local bucket
+  __shared__ int slot[kHashSlots], mate[kMatchCap];
+  __shared__ int loffs[2][kMatchVerts + 1];
+  const int t = threadIdx.x;
+  const int nchunk = (np + kMatchVerts - 1) / kMatchVerts;
+  const int x = blockIdx.x & 7, per = gridDim.x >> 3;
+  const int cend = (int)((long long)(x + 1) * nchunk / 8);
+  int c = (int)((long long)x * nchunk / 8) + (blockIdx.x >> 3);
+  const long long last = nf > 0 ? nf - 1 : 0;
+  auto nverts = [&](int cc) { return cc < cend ? min(kMatchVerts, np - cc * kMatchVerts) : 0; };
+  auto load_off = [&](int cc) { return chunk_off(off, cnt, np, min(cc, nchunk - 1) * kMatchVerts, t); };
+  // entries t, t + kB, t + 2 kB of chunk cc (its offsets in lo), clamped
+  auto load_ent = [&](const int *lo, int cc, int3 &a, int3 &b, int3 &d) {
+    const int nv = nverts(cc), e0 = lo[0], n = nv > 0 ? lo[nv] - e0 : 0;
+    auto at = [&](int j) { return bucket[min((long long)e0 + (j < n && n <= kMatchCap ? j : 0), last)]; };
+    a = at(t);
+    b = at(t + kB);
+    d = at(t + 2 * kB);
+  };
+  int bad = 0, cur = 0;
+  if (t <= kMatchVerts) loffs[0][t] = load_off(c);
+  int L = load_off(c + per);
   __syncthreads();
-  const int e0 = loff[0], n = loff[nv] - e0;
-  const bool staged = n <= kMatchCap;
-  if (staged)
-    for (int j = threadIdx.x; j < n; j += kB) ent[j] = bucket[e0 + j];
-  __syncthreads();
-  const int4 *src = staged ? ent : bucket + e0;
-  int bad = 0;
-  for (int j = threadIdx.x; j < n; j += kB) {
-    // the bucket of entry j: the last local offset <= j
-    int lo = 0, hi = nv; // loff[lo] - e0 <= j < loff[hi] - e0
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (loff[mid] - e0 <= j) lo = mid;
-      else hi = mid;
-    }
-    const int b0 = loff[lo] - e0, b1 = loff[lo + 1] - e0;
-    const int4 me = src[j];
-    int twin = 0, found = 0;
-    for (int q = b0; q < b1; q++) {
-      const int4 o = src[q];
-      if (q != j && o.x == me.x && o.y == me.y) {
-        if (!found) twin = o.z;
-        found++;
+  int3 E0, E1, E2;
+  load_ent(loffs[0], c, E0, E1, E2);
+  for (; c < cend; c += per) {
+    const int c1 = c + per, nv = nverts(c);
+    if (t <= kMatchVerts) loffs[cur ^ 1][t] = L;
+    __syncthreads();
+    const int *lo = loffs[cur];
+    const int e0 = lo[0], n = lo[nv] - e0;
+    int3 N0, N1, N2;
+    load_ent(loffs[cur ^ 1], c1, N0, N1, N2);
+    L = load_off(c1 + per);
+    if (n <= kMatchCap) {
+      auto stage = [&](int j, const int3 &e) {
+        if (j < n) {
+          ent[j] = e;
+          lb[j] = (unsigned char)bucket_of(lo, nv, e0, j);
+          mate[j] = -1;
+        }
+      };
+      stage(t, E0);
+      stage(t + kB, E1);
+      stage(t + 2 * kB, E2);
+      for (int h = t; h < kHashSlots; h += kB) slot[h] = -1;
+      __syncthreads();
+      for (int j = t; j < n; j += kB) {
+        const int3 me = ent[j];
+        const int mb = lb[j];
+        unsigned h = ((unsigned)mb * 0x9E3779B1u) ^ ((unsigned)me.x * 0x85EBCA77u) ^ ((unsigned)me.y * 0xC2B2AE3Du);
+        h = (h ^ (h >> 15)) & (kHashSlots - 1);
+        for (;;) {
+          const int q = atomicCAS(&slot[h], -1, j);
+          if (q < 0) break; // first of its key: inserted
+          const int3 o = ent[q];
+          if (o.x == me.x && o.y == me.y && lb[q] == mb) {
+            if (atomicCAS(&mate[q], -1, j) == -1) mate[j] = q;
+            else bad = 1; // a third face with this key
+            break;
+          }
+          h = (h + 1) & (kHashSlots - 1);
+        }
+      }
+      __syncthreads();
+      for (int j = t; j < n; j += kB) {
+        const int m = mate[j];
+        put_adja(adja, tet8, ent[j].z, m >= 0 ? ent[m].z : 0);
+      }
+    } else {
+      const int3 *src = bucket + e0;
+      for (int j = t; j < n; j += kB) {
+        const int b = bucket_of(lo, nv, e0, j);
+        const int b0 = lo[b] - e0, b1 = lo[b + 1] - e0;
+        const int3 me = src[j];
+        int twin = 0, found = 0;
+        for (int q = b0; q < b1; q++) {
+          const int3 o = src[q];
+          if (q != j && o.x == me.x && o.y == me.y) {
+            if (!found) twin = o.z;
+            found++;
+          }
+        }
+        bad |= found > 1;
+        put_adja(adja, tet8, me.z, twin);
       }
     }
-    bad |= found > 1;
-    const size_t k = (size_t)(me.z >> 2) - 1, i = (size_t)(me.z & 3);
-    if (adja) adja[4 * k + i] = twin;
-    if (tet8) tet8[8 * k + 4 + i] = twin;
+    E0 = N0;
+    E1 = N1;
+    E2 = N2;
+    cur ^= 1;
+    __syncthreads(); // the LDS of this chunk is reused by the next
   }
   if (bad) atomicOr(err, kErrNonManifold);
 }
 
+// (r04: writing the twins in bucket order and the rows by a per-tetra gather
+// took 0.3 ms longer than the match's own 4-byte stores)
 __global__ __launch_bounds__(kB) void k_face_invalid(int ne, const int2 *rank, int4 *adja, int4 *tet8) {
   const int k = blockIdx.x * kB + threadIdx.x;
   if (k >= ne || rank[k].x >= 0) return;
@@ -230,21 +364,68 @@ __device__ __forceinline__ bool bdy_face(int code, int k, const int *tref) {
   return tref && tref[k] > tref[(code >> 2) - 1];
 }
 
-__global__ __launch_bounds__(kB) void k_bdy_count(const int4 *adja, int astride, const int *tref, int ne, int *nb) {
-  const int k = blockIdx.x * kB + threadIdx.x;
-  if (k >= ne) return;
-  const int4 a = adja[(size_t)k * astride];
-  nb[k] = bdy_face(a.x, k, tref) + bdy_face(a.y, k, tref) + bdy_face(a.z, k, tref) + bdy_face(a.w, k, tref);
+__device__ __forceinline__ int bdy_faces(const int4 &a, int k, const int *tref) {
+  return bdy_face(a.x, k, tref) + bdy_face(a.y, k, tref) + bdy_face(a.z, k, tref) + bdy_face(a.w, k, tref);
 }
 
-__global__ __launch_bounds__(kB) void k_bdy_write(const int4 *tetv, int tstride, const int4 *adja, int astride,
-                                                  const int *tref, int ne, const int *toff, int *triv) {
+// block-wide exclusive prefix of v (kB threads), and the block's total
+__device__ __forceinline__ int block_prefix(int v, int *wsum, int &total) {
+  const int lane = __lane_id(), w = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(x, d);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  int before = 0;
+  total = 0;
+#pragma unroll
+  for (int j = 0; j < kB / 64; j++) {
+    before += j < w ? wsum[j] : 0;
+    total += wsum[j];
+  }
+  __syncthreads();
+  return before + x - v;
+}
+
+// Pass 1 over the tetra (r04): per block of kB tetra, its boundary faces'
+// count and its tetra with any, compacted in tetra order into the block's
+// own kB slots of cand (boundary tetra are few: pass 2 reads only those
+// instead of every tetra's adjacency again; r03 wrote and scanned a count per
+// tetra, then re-read all of them)
+__global__ __launch_bounds__(kB) void k_bdy_count(const int4 *adja, int astride, const int *tref, int ne, int *cand,
+                                                  int *btot, int *bcnt) {
+  __shared__ int wsum[kB / 64];
   const int k = blockIdx.x * kB + threadIdx.x;
-  if (k >= ne) return;
-  const int4 a = adja[(size_t)k * astride];
-  if (!tref && a.x && a.y && a.z && a.w) return;
+  const int nb = k < ne ? bdy_faces(adja[(size_t)k * astride], k, tref) : 0;
+  int ncand = 0;
+  const int pos = block_prefix(nb > 0, wsum, ncand);
+  if (nb > 0) cand[(size_t)blockIdx.x * kB + pos] = k;
+  int tot = 0;
+  (void)block_prefix(nb, wsum, tot);
+  if (threadIdx.x == 0) {
+    btot[blockIdx.x] = tot;
+    bcnt[blockIdx.x] = ncand;
+  }
+}
+
+// Pass 2: the trias of a block's candidate tetra at the block's offset
+__global__ __launch_bounds__(kB) void k_bdy_write(const int4 *tetv, int tstride, const int4 *adja, int astride,
+                                                  const int *tref, const int *cand, const int *bcnt, const int *boff,
+                                                  int *triv) {
+  __shared__ int wsum[kB / 64];
+  const int n = bcnt[blockIdx.x];
+  if (n == 0) return; // block-uniform
+  const bool in = (int)threadIdx.x < n;
+  const int k = in ? cand[(size_t)blockIdx.x * kB + threadIdx.x] : 0;
+  const int4 a = in ? adja[(size_t)k * astride] : make_int4(1, 1, 1, 1);
+  const int nb = in ? bdy_faces(a, k, tref) : 0;
+  int tot = 0;
+  int pos = boff[blockIdx.x] + block_prefix(nb, wsum, tot);
+  if (!in) return;
   const int4 t = tetv[(size_t)k * tstride];
-  int pos = toff[k];
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     if (!bdy_face(sel(a, i), k, tref)) continue;
@@ -369,7 +550,7 @@ int pmmg_snap_adjacency(hipStream_t s, int np, int ne, const int *tetv, int *adj
   const long long nf = 4LL * ne;
   int *cnt = S.get<int>(0, (size_t)np), *off = S.get<int>(1, (size_t)np), *err = S.get<int>(2, 1);
   int2 *rank = S.get<int2>(3, (size_t)ne);
-  int4 *bucket = S.get<int4>(4, (size_t)nf);
+  int3 *bucket = S.get<int3>(4, (size_t)nf); // {b, c, code} of every face
   if (!cnt || !off || !rank || !err || !bucket) {
     snprintf(msg, msglen, "build_adjacency: out of device memory (%lld faces)", nf);
     return 0;
@@ -381,8 +562,12 @@ int pmmg_snap_adjacency(hipStream_t s, int np, int ne, const int *tetv, int *adj
                      reinterpret_cast<int4 *>(tet8), err);
   if (!exclusive_scan(S, cnt, off, np, s, msg, msglen)) return 0;
   hipLaunchKernelGGL(k_face_scatter, dim3(blocks(ne)), dim3(kB), 0, s, tv, ne, off, rank, bucket);
-  hipLaunchKernelGGL(k_face_match, dim3((np + kMatchVerts - 1) / kMatchVerts), dim3(kB), 0, s, np, off, cnt, bucket,
-                     adja, tet8, err);
+  if (np > 0) {
+    // 8 blocks per CU (17 KB of LDS each) on 256 CUs, a multiple of 8
+    const int nchunk = (np + kMatchVerts - 1) / kMatchVerts;
+    const int grid = std::max(8, std::min(8 * 256, (nchunk + 7) / 8 * 8));
+    hipLaunchKernelGGL(k_face_match, dim3(grid), dim3(kB), 0, s, np, off, cnt, bucket, nf, adja, tet8, err);
+  }
   hipLaunchKernelGGL(k_face_invalid, dim3(blocks(ne)), dim3(kB), 0, s, ne, rank, reinterpret_cast<int4 *>(adja),
                      reinterpret_cast<int4 *>(tet8));
   SCK(hipGetLastError());
@@ -436,20 +621,23 @@ int pmmg_snap_boundary(hipStream_t s, int np, int ne, const int *tetv, int tstri
                        const int *tref, int cap, int *nt_out, int *triv, int *adjt, SnapCache *cache, char *msg,
                        size_t msglen) {
   Scratch S(cache);
-  int *nb = S.get<int>(5, (size_t)ne), *toff = S.get<int>(6, (size_t)ne);
-  if (!nb || !toff) { snprintf(msg, msglen, "build_boundary: out of device memory"); return 0; }
+  const int nblk = blocks(ne);
+  int *cand = S.get<int>(5, (size_t)nblk * kB), *bs = S.get<int>(6, 3 * (size_t)nblk);
+  if (!cand || !bs) { snprintf(msg, msglen, "build_boundary: out of device memory"); return 0; }
+  int *btot = bs, *bcnt = bs + nblk, *boff = bs + 2 * (size_t)nblk;
   const int4 *tv = reinterpret_cast<const int4 *>(tetv), *ad = reinterpret_cast<const int4 *>(adja);
-  hipLaunchKernelGGL(k_bdy_count, dim3(blocks(ne)), dim3(kB), 0, s, ad, astride, tref, ne, nb);
-  if (!exclusive_scan(S, nb, toff, ne, s, msg, msglen)) return 0;
+  hipLaunchKernelGGL(k_bdy_count, dim3(nblk), dim3(kB), 0, s, ad, astride, tref, ne, cand, btot, bcnt);
+  if (!exclusive_scan(S, btot, boff, nblk, s, msg, msglen)) return 0;
   int last[2] = {0, 0};
-  SCK(hipMemcpyAsync(&last[0], toff + ne - 1, sizeof(int), hipMemcpyDeviceToHost, s));
-  SCK(hipMemcpyAsync(&last[1], nb + ne - 1, sizeof(int), hipMemcpyDeviceToHost, s));
+  SCK(hipMemcpyAsync(&last[0], boff + nblk - 1, sizeof(int), hipMemcpyDeviceToHost, s));
+  SCK(hipMemcpyAsync(&last[1], btot + nblk - 1, sizeof(int), hipMemcpyDeviceToHost, s));
   SCK(hipStreamSynchronize(s));
   const int nt = last[0] + last[1];
   *nt_out = nt;
   if (nt > cap) { snprintf(msg, msglen, "build_boundary: %d boundary trias exceed the capacity %d", nt, cap); return 0; }
   if (nt == 0) return 1;
-  hipLaunchKernelGGL(k_bdy_write, dim3(blocks(ne)), dim3(kB), 0, s, tv, tstride, ad, astride, tref, ne, toff, triv);
+  hipLaunchKernelGGL(k_bdy_write, dim3(nblk), dim3(kB), 0, s, tv, tstride, ad, astride, tref, (const int *)cand,
+                     (const int *)bcnt, (const int *)boff, triv);
   SCK(hipGetLastError());
   if (adjt && !pmmg_snap_tria_adjacency(s, np, nt, triv, adjt, cache, msg, msglen)) return 0;
   SCK(hipStreamSynchronize(s));

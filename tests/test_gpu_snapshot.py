@@ -78,8 +78,8 @@ def _host_adjacency(tetv):
 def test_snapshot_of_a_high_valence_vertex():
     """A star of tetra around one vertex (vertex 1, the smallest id, in every
     tetra): its face bucket holds 3 faces per tetra, more than the match
-    kernel stages in LDS for a block of vertices, so that block scans its
-    buckets in place."""
+    kernel stages in LDS for a block of vertices (kMatchCap, 768 entries), so
+    that block scans its buckets in place."""
     bg = synth.lattice(synth.SHELL, 12)
     r = np.linalg.norm(bg.xyz - bg.xyz.mean(0), axis=1)
     outer = bg.triv[(r[bg.triv - 1] > np.median(r)).all(axis=1)]
@@ -91,6 +91,52 @@ def test_snapshot_of_a_high_valence_vertex():
         np.testing.assert_array_equal(adja.download(), expect)
         np.testing.assert_array_equal(tet8.download(), pack_tet8(tetv, expect))
         assert (expect[:, 0] == 0).all() and (expect[:, 1:] > 0).all()  # the outer faces, the star's inner faces
+
+
+_IDIR = np.array([[1, 2, 3], [0, 3, 2], [0, 1, 3], [0, 2, 1]])
+
+
+def _host_tria_adjacency(triv):
+    """MMG3D_hashTria's adjt: edge j (opposite local vertex j) paired only
+    when exactly two trias share it"""
+    edges = {}
+    for t, tri in enumerate(triv.tolist()):
+        for j in range(3):
+            edges.setdefault(tuple(sorted((tri[(j + 1) % 3], tri[(j + 2) % 3]))), []).append(3 * (t + 1) + j)
+    adjt = np.zeros(triv.shape, np.int32)
+    for codes in edges.values():
+        if len(codes) == 2:
+            a, b = codes
+            adjt[a // 3 - 1, a % 3], adjt[b // 3 - 1, b % 3] = b, a
+    return adjt
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("use_tet8", [True, False])
+def test_snapshot_boundary_of_a_multi_material_mesh(use_tet8):
+    """With tetra references the boundary trias are the faces without a
+    neighbour and the interface faces seen from the larger reference
+    (MMG5_chkBdryTria's rule restated in pmmg_snapshot.hip), in (tetra, face)
+    order, oriented by MMG5_idir."""
+    bg = synth.lattice(synth.CUBE, 6)
+    cx = bg.xyz[bg.tetv - 1, 0].mean(axis=1)
+    tref = (np.floor(3 * (cx - cx.min()) / np.ptp(cx) * 0.999) + 1).astype(np.int32)
+    assert len(set(tref.tolist())) == 3
+    nbr = np.maximum(bg.adja // 4 - 1, 0)
+    keep = (bg.adja == 0) | (tref[:, None] > tref[nbr])
+    k, i = np.nonzero(keep)
+    expect = bg.tetv[k[:, None], _IDIR[i]].astype(np.int32)
+    assert expect.shape[0] > bg.nt  # interface faces beside the outer boundary
+    with TransferContext(0) as ctx:
+        tetv = ctx.upload(bg.tetv)
+        adja, tet8 = ctx.build_adjacency(bg.np, tetv)
+        d_tref = ctx.upload(tref)
+        if use_tet8:
+            triv, adjt = ctx.build_boundary(bg.np, tet8=tet8, tref=d_tref)
+        else:
+            triv, adjt = ctx.build_boundary(bg.np, tetv=tetv, adja=adja, tref=d_tref)
+        np.testing.assert_array_equal(triv.download(), expect)
+        np.testing.assert_array_equal(adjt.download(), _host_tria_adjacency(expect))
 
 
 @pytest.mark.gpu
