@@ -230,6 +230,9 @@ struct pmmg_hip_ctx {
   std::vector<pmmg_hip_ctx *> lanes;
   int group_lanes = 4; // PMMG_HIP_GROUP_LANES (r04i, 10 cfg2-size groups: 1 / 2 / 4 lanes 0.165 / 0.125 / 0.108 ms per group)
   struct Pool *lane_pool = nullptr; // host threads enqueueing the other lanes' groups
+  int lane_streams = 2; // a group lane's streams: 2 = its surface stream at normal priority, 1 = the surface
+                        // branch on the main stream, 3 = the surface stream at the highest priority as in a
+                        // single call (measurement build: PMMG_HIP_LANE_STREAMS)
   int filter_steps = 64; // step cap of the fp32 filter walk (then the exact fp64 walk continues from where it
                          // stopped: a query the filter misjudges hands over early instead of cycling through a
                          // 4-entry history for up to maxstep steps); test-only PMMG_HIP_FILTER_STEPS=0 sends every
@@ -587,6 +590,7 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   if (const char *e = getenv("PMMG_HIP_XCDRUN"))
     if (*e && atoi(e) >= 0) c->xcd_run = atoi(e);
   c->pad = env_int("PMMG_HIP_PAD", 0);
+  c->lane_streams = std::max(1, std::min(3, env_int("PMMG_HIP_LANE_STREAMS", c->lane_streams)));
 #endif
   return c;
 }
@@ -625,7 +629,7 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   }
   DevBuf *cb[] = {&c->carry_dsrc, &c->carry_need, &c->carry_ids, &c->carry_cnt, &c->carry_rows, &c->carry_bc};
   for (DevBuf *b : cb) release(*b);
-  if (c->stream2) (void)hipStreamDestroy(c->stream2);
+  if (c->stream2 && c->stream2 != c->stream) (void)hipStreamDestroy(c->stream2);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->cstream) (void)hipStreamDestroy(c->cstream);
   delete c;
@@ -1646,6 +1650,16 @@ static pmmg_hip_ctx *group_lane(pmmg_hip_ctx *c, int j) {
     if (!l) {
       set_err(c, "locate_interp_groups: cannot create group lane %d", (int)c->lanes.size() + 1);
       return nullptr;
+    }
+    if (c->lane_streams != 3) {
+      (void)hipStreamDestroy(l->stream2);
+      l->stream2 = l->stream;
+      if (c->lane_streams == 2 && hipStreamCreateWithFlags(&l->stream2, hipStreamNonBlocking) != hipSuccess) {
+        l->stream2 = l->stream;
+        set_err(c, "locate_interp_groups: cannot create a stream for group lane %d", (int)c->lanes.size() + 1);
+        pmmg_hip_destroy(l);
+        return nullptr;
+      }
     }
     c->lanes.push_back(l);
   }

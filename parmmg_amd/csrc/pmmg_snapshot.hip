@@ -37,7 +37,6 @@
 #include <stdint.h>
 #include <stdio.h>
 
-#include <algorithm>
 
 #include "pmmg_snapshot.hpp"
 
@@ -106,8 +105,8 @@ __device__ __forceinline__ bool tet_ids_ok(const int4 &t, int np) {
 // wave's {idx, lane} keys are bitonic-sorted across the lanes (wave_runs), the
 // first lane of every run of equal idx issues the run's atomic — all runs in
 // one instruction — and the ranks go back to the lanes they belong to by
-// ds_permute (run_rank).  k_face_count issues its two reservations' atomics
-// together: one round trip per wave.  (r04: the previous form took up to 7
+// ds_permute (run_rank).  k_face_scatter issues its two reservations'
+// atomics together: one round trip per wave.  (r04: the previous form took up to 7
 // dependent atomic round trips per wave, one per distinct idx; the count
 // kernel was latency-bound on them at 6.8 ms for 101M tetra.)
 struct WaveRun {
@@ -150,11 +149,13 @@ __device__ __forceinline__ int run_rank(const WaveRun &w, int old, int val) {
   return __builtin_amdgcn_ds_permute((int)(w.key & 63) << 2, old + val * (lane - w.h));
 }
 
-// rank[k] = {slot of the s0 faces (3 consecutive), slot of the s1 face};
-// the vertex half of the tet8 record goes out here (the adjacency half is
-// written face by face by k_face_match)
-__global__ __launch_bounds__(kB) void k_face_count(const int4 *tetv, int ne, int np, int *cnt, int2 *rank,
-                                                   int4 *tet8, int *err) {
+// The bucket sizes: per tetra, 3 faces in the bucket of its smallest vertex,
+// 1 in that of the second smallest, counted with no-return atomics (r04: the
+// slots themselves are taken in k_face_scatter, so nothing waits on these
+// atomics and no per-tetra rank goes through memory).  The vertex half of
+// the tet8 record goes out here (the adjacency half is written face by face
+// by k_face_match).
+__global__ __launch_bounds__(kB) void k_face_count(const int4 *tetv, int ne, int np, int *cnt, int4 *tet8, int *err) {
   const int k = (int)(xcd_blk() * kB + threadIdx.x);
   const bool in = k < ne;
   const int4 t = in ? tetv[k] : make_int4(1, 2, 3, 4);
@@ -163,26 +164,34 @@ __global__ __launch_bounds__(kB) void k_face_count(const int4 *tetv, int ne, int
   int i0 = 0, i1 = 1;
   two_smallest(t, i0, i1);
   const WaveRun w0 = wave_runs(sel(t, i0) - 1, ok), w1 = wave_runs(sel(t, i1) - 1, ok);
-  int o0 = 0, o1 = 0;
-  if (w0.head) o0 = atomicAdd(&cnt[(int)(w0.key >> 6)], 3 * w0.n);
-  if (w1.head) o1 = atomicAdd(&cnt[(int)(w1.key >> 6)], w1.n);
-  const int r0 = run_rank(w0, o0, 3), r1 = run_rank(w1, o1, 1);
-  if (in) {
-    rank[k] = ok ? make_int2(r0, r1) : make_int2(-1, -1);
-    if (tet8) tet8[2 * (size_t)k] = t;
-  }
+  if (w0.head) atomicAdd(&cnt[(int)(w0.key >> 6)], 3 * w0.n);
+  if (w1.head) atomicAdd(&cnt[(int)(w1.key >> 6)], w1.n);
+  if (in && tet8) tet8[2 * (size_t)k] = t;
 }
 
-__global__ __launch_bounds__(kB) void k_face_scatter(const int4 *tetv, int ne, const int *off, const int2 *rank,
-                                                     int3 *bucket) {
+// The faces into their buckets: slots taken from the buckets' cursors
+// (initialised to the offsets) with one atomic round trip per wave.  An
+// invalid tetra (flagged by k_face_count) gets a zero adjacency row here and
+// has no faces in the buckets.
+__global__ __launch_bounds__(kB) void k_face_scatter(const int4 *tetv, int ne, int np, int *cursor, int3 *bucket,
+                                                     int4 *adja, int4 *tet8) {
   const int k = (int)(xcd_blk() * kB + threadIdx.x);
-  if (k >= ne) return;
-  const int2 r = rank[k];
-  if (r.x < 0) return;
-  const int4 t = tetv[k];
-  int i0, i1;
+  const bool in = k < ne;
+  const int4 t = in ? tetv[k] : make_int4(1, 2, 3, 4);
+  const bool ok = in && tet_ids_ok(t, np);
+  int i0 = 0, i1 = 1;
   two_smallest(t, i0, i1);
-  const int o0 = off[sel(t, i0) - 1] + r.x, o1 = off[sel(t, i1) - 1] + r.y;
+  const WaveRun w0 = wave_runs(sel(t, i0) - 1, ok), w1 = wave_runs(sel(t, i1) - 1, ok);
+  int c0 = 0, c1 = 0;
+  if (w0.head) c0 = atomicAdd(&cursor[(int)(w0.key >> 6)], 3 * w0.n);
+  if (w1.head) c1 = atomicAdd(&cursor[(int)(w1.key >> 6)], w1.n);
+  const int o0 = run_rank(w0, c0, 3), o1 = run_rank(w1, c1, 1);
+  if (!in) return;
+  if (!ok) {
+    if (adja) adja[k] = make_int4(0, 0, 0, 0);
+    if (tet8) tet8[2 * (size_t)k + 1] = make_int4(0, 0, 0, 0);
+    return;
+  }
   int n = 0;
 #pragma unroll
   for (int i = 0; i < 4; i++) {
@@ -199,7 +208,7 @@ __global__ __launch_bounds__(kB) void k_face_scatter(const int4 *tetv, int ne, c
 // entries), staged in LDS when they fit in kMatchCap entries, else scanned
 // in place; every face writes its entry of the adjacency: its twin's code, 0
 // on the boundary.  Invalid tetra (flagged by k_face_count) have no faces in
-// the buckets: their rows are zeroed by k_face_invalid.
+// the buckets: their rows are zeroed by k_face_scatter.
 //
 // r04: in LDS the twins meet in a hash table keyed by {bucket, b, c} — each
 // entry probes ~1-2 slots — instead of every entry scanning its whole bucket
@@ -225,130 +234,73 @@ __device__ __forceinline__ void put_adja(int *adja, int *tet8, int code, int twi
   if (tet8) tet8[8 * k + 4 + i] = twin;
 }
 
-// Persistent blocks (r04): the blocks of XCD x walk the chunks of kMatchVerts
-// vertices in [x n / 8, (x + 1) n / 8); the offsets of the chunk after next
-// and the entries of the next chunk are loaded while the current one is
-// matched in LDS (one block per chunk waited for two dependent round trips,
-// offsets then entries, with ~8 blocks per CU: 3.3 ms at cfg4).  The loads
-// are unconditional (clamped indices) so that the compiler's wait for the
-// current entries leaves the next ones in flight.
-static_assert(kMatchCap == 3 * kB, "three entries per thread (registers E0..E2)");
-
-// offset t (0..nv) of the chunk starting at vertex v0: off[v0 + t], or the
-// total past the last vertex; clamped loads, garbage for t > nv
-__device__ __forceinline__ int chunk_off(const int *off, const int *cnt, int np, int v0, int t) {
-  const int v = min(v0 + t, np - 1);
-  const int a = off[v], b = cnt[v];
-  return v0 + t < np ? a : a + b;
-}
-
+// One block per chunk of kMatchVerts vertices, in XCD-contiguous order.
+// (r04: persistent blocks loading the next chunk's entries while matching
+// the current one took 3.79 against 3.30 ms, r04u.)
 __global__ __launch_bounds__(kB) void k_face_match(int np, const int *off, const int *cnt, const int3 *bucket,
-                                                   long long nf, int *adja, int *tet8, int *err) {
+                                                   int *adja, int *tet8, int *err) {
   __shared__ int3 ent[kMatchCap];         // {b, c, code}
   __shared__ unsigned char lb[kMatchCap]; // local bucket
   __shared__ int slot[kHashSlots], mate[kMatchCap];
-  __shared__ int loffs[2][kMatchVerts + 1];
-  const int t = threadIdx.x;
-  const int nchunk = (np + kMatchVerts - 1) / kMatchVerts;
-  const int x = blockIdx.x & 7, per = gridDim.x >> 3;
-  const int cend = (int)((long long)(x + 1) * nchunk / 8);
-  int c = (int)((long long)x * nchunk / 8) + (blockIdx.x >> 3);
-  const long long last = nf > 0 ? nf - 1 : 0;
-  auto nverts = [&](int cc) { return cc < cend ? min(kMatchVerts, np - cc * kMatchVerts) : 0; };
-  auto load_off = [&](int cc) { return chunk_off(off, cnt, np, min(cc, nchunk - 1) * kMatchVerts, t); };
-  // entries t, t + kB, t + 2 kB of chunk cc (its offsets in lo), clamped
-  auto load_ent = [&](const int *lo, int cc, int3 &a, int3 &b, int3 &d) {
-    const int nv = nverts(cc), e0 = lo[0], n = nv > 0 ? lo[nv] - e0 : 0;
-    auto at = [&](int j) { return bucket[min((long long)e0 + (j < n && n <= kMatchCap ? j : 0), last)]; };
-    a = at(t);
-    b = at(t + kB);
-    d = at(t + 2 * kB);
-  };
-  int bad = 0, cur = 0;
-  if (t <= kMatchVerts) loffs[0][t] = load_off(c);
-  int L = load_off(c + per);
+  __shared__ int loff[kMatchVerts + 1];
+  const int v0 = (int)xcd_blk() * kMatchVerts, nv = min(kMatchVerts, np - v0);
+  if (threadIdx.x <= nv) loff[threadIdx.x] = threadIdx.x < nv ? off[v0 + threadIdx.x] : off[v0 + nv - 1] + cnt[v0 + nv - 1];
   __syncthreads();
-  int3 E0, E1, E2;
-  load_ent(loffs[0], c, E0, E1, E2);
-  for (; c < cend; c += per) {
-    const int c1 = c + per, nv = nverts(c);
-    if (t <= kMatchVerts) loffs[cur ^ 1][t] = L;
+  const int e0 = loff[0], n = loff[nv] - e0;
+  int bad = 0;
+  if (n <= kMatchCap) {
+    for (int j = threadIdx.x; j < n; j += kB) {
+      ent[j] = bucket[e0 + j];
+      lb[j] = (unsigned char)bucket_of(loff, nv, e0, j);
+      mate[j] = -1;
+    }
+    for (int h = threadIdx.x; h < kHashSlots; h += kB) slot[h] = -1;
     __syncthreads();
-    const int *lo = loffs[cur];
-    const int e0 = lo[0], n = lo[nv] - e0;
-    int3 N0, N1, N2;
-    load_ent(loffs[cur ^ 1], c1, N0, N1, N2);
-    L = load_off(c1 + per);
-    if (n <= kMatchCap) {
-      auto stage = [&](int j, const int3 &e) {
-        if (j < n) {
-          ent[j] = e;
-          lb[j] = (unsigned char)bucket_of(lo, nv, e0, j);
-          mate[j] = -1;
+    for (int j = threadIdx.x; j < n; j += kB) {
+      const int3 me = ent[j];
+      const int mb = lb[j];
+      unsigned h = ((unsigned)mb * 0x9E3779B1u) ^ ((unsigned)me.x * 0x85EBCA77u) ^ ((unsigned)me.y * 0xC2B2AE3Du);
+      h = (h ^ (h >> 15)) & (kHashSlots - 1);
+      for (;;) {
+        const int q = atomicCAS(&slot[h], -1, j);
+        if (q < 0) break; // first of its key: inserted
+        const int3 o = ent[q];
+        if (o.x == me.x && o.y == me.y && lb[q] == mb) {
+          if (atomicCAS(&mate[q], -1, j) == -1) mate[j] = q;
+          else bad = 1; // a third face with this key
+          break;
         }
-      };
-      stage(t, E0);
-      stage(t + kB, E1);
-      stage(t + 2 * kB, E2);
-      for (int h = t; h < kHashSlots; h += kB) slot[h] = -1;
-      __syncthreads();
-      for (int j = t; j < n; j += kB) {
-        const int3 me = ent[j];
-        const int mb = lb[j];
-        unsigned h = ((unsigned)mb * 0x9E3779B1u) ^ ((unsigned)me.x * 0x85EBCA77u) ^ ((unsigned)me.y * 0xC2B2AE3Du);
-        h = (h ^ (h >> 15)) & (kHashSlots - 1);
-        for (;;) {
-          const int q = atomicCAS(&slot[h], -1, j);
-          if (q < 0) break; // first of its key: inserted
-          const int3 o = ent[q];
-          if (o.x == me.x && o.y == me.y && lb[q] == mb) {
-            if (atomicCAS(&mate[q], -1, j) == -1) mate[j] = q;
-            else bad = 1; // a third face with this key
-            break;
-          }
-          h = (h + 1) & (kHashSlots - 1);
-        }
-      }
-      __syncthreads();
-      for (int j = t; j < n; j += kB) {
-        const int m = mate[j];
-        put_adja(adja, tet8, ent[j].z, m >= 0 ? ent[m].z : 0);
-      }
-    } else {
-      const int3 *src = bucket + e0;
-      for (int j = t; j < n; j += kB) {
-        const int b = bucket_of(lo, nv, e0, j);
-        const int b0 = lo[b] - e0, b1 = lo[b + 1] - e0;
-        const int3 me = src[j];
-        int twin = 0, found = 0;
-        for (int q = b0; q < b1; q++) {
-          const int3 o = src[q];
-          if (q != j && o.x == me.x && o.y == me.y) {
-            if (!found) twin = o.z;
-            found++;
-          }
-        }
-        bad |= found > 1;
-        put_adja(adja, tet8, me.z, twin);
+        h = (h + 1) & (kHashSlots - 1);
       }
     }
-    E0 = N0;
-    E1 = N1;
-    E2 = N2;
-    cur ^= 1;
-    __syncthreads(); // the LDS of this chunk is reused by the next
+    __syncthreads();
+    for (int j = threadIdx.x; j < n; j += kB) {
+      const int m = mate[j];
+      put_adja(adja, tet8, ent[j].z, m >= 0 ? ent[m].z : 0);
+    }
+  } else {
+    const int3 *src = bucket + e0;
+    for (int j = threadIdx.x; j < n; j += kB) {
+      const int b = bucket_of(loff, nv, e0, j);
+      const int b0 = loff[b] - e0, b1 = loff[b + 1] - e0;
+      const int3 me = src[j];
+      int twin = 0, found = 0;
+      for (int q = b0; q < b1; q++) {
+        const int3 o = src[q];
+        if (q != j && o.x == me.x && o.y == me.y) {
+          if (!found) twin = o.z;
+          found++;
+        }
+      }
+      bad |= found > 1;
+      put_adja(adja, tet8, me.z, twin);
+    }
   }
   if (bad) atomicOr(err, kErrNonManifold);
 }
 
 // (r04: writing the twins in bucket order and the rows by a per-tetra gather
 // took 0.3 ms longer than the match's own 4-byte stores)
-__global__ __launch_bounds__(kB) void k_face_invalid(int ne, const int2 *rank, int4 *adja, int4 *tet8) {
-  const int k = blockIdx.x * kB + threadIdx.x;
-  if (k >= ne || rank[k].x >= 0) return;
-  if (adja) adja[k] = make_int4(0, 0, 0, 0);
-  if (tet8) tet8[2 * (size_t)k + 1] = make_int4(0, 0, 0, 0);
-}
 
 // ---- boundary trias
 //
@@ -400,14 +352,13 @@ __global__ __launch_bounds__(kB) void k_bdy_count(const int4 *adja, int astride,
   __shared__ int wsum[kB / 64];
   const int k = blockIdx.x * kB + threadIdx.x;
   const int nb = k < ne ? bdy_faces(adja[(size_t)k * astride], k, tref) : 0;
-  int ncand = 0;
-  const int pos = block_prefix(nb > 0, wsum, ncand);
-  if (nb > 0) cand[(size_t)blockIdx.x * kB + pos] = k;
+  // one prefix over {candidate flag, face count} (<= 256 and <= 1024 per block)
   int tot = 0;
-  (void)block_prefix(nb, wsum, tot);
+  const int pos = block_prefix(((nb > 0) << 16) | nb, wsum, tot) >> 16;
+  if (nb > 0) cand[(size_t)blockIdx.x * kB + pos] = k;
   if (threadIdx.x == 0) {
-    btot[blockIdx.x] = tot;
-    bcnt[blockIdx.x] = ncand;
+    btot[blockIdx.x] = tot & 0xFFFF;
+    bcnt[blockIdx.x] = tot >> 16;
   }
 }
 
@@ -549,27 +500,23 @@ int pmmg_snap_adjacency(hipStream_t s, int np, int ne, const int *tetv, int *adj
   Scratch S(cache);
   const long long nf = 4LL * ne;
   int *cnt = S.get<int>(0, (size_t)np), *off = S.get<int>(1, (size_t)np), *err = S.get<int>(2, 1);
-  int2 *rank = S.get<int2>(3, (size_t)ne);
+  int *cursor = S.get<int>(3, (size_t)np);
   int3 *bucket = S.get<int3>(4, (size_t)nf); // {b, c, code} of every face
-  if (!cnt || !off || !rank || !err || !bucket) {
+  if (!cnt || !off || !cursor || !err || !bucket) {
     snprintf(msg, msglen, "build_adjacency: out of device memory (%lld faces)", nf);
     return 0;
   }
   SCK(hipMemsetAsync(cnt, 0, sizeof(int) * (size_t)np, s));
   SCK(hipMemsetAsync(err, 0, sizeof(int), s));
   const int4 *tv = reinterpret_cast<const int4 *>(tetv);
-  hipLaunchKernelGGL(k_face_count, dim3(blocks(ne)), dim3(kB), 0, s, tv, ne, np, cnt, rank,
-                     reinterpret_cast<int4 *>(tet8), err);
+  hipLaunchKernelGGL(k_face_count, dim3(blocks(ne)), dim3(kB), 0, s, tv, ne, np, cnt, reinterpret_cast<int4 *>(tet8),
+                     err);
   if (!exclusive_scan(S, cnt, off, np, s, msg, msglen)) return 0;
-  hipLaunchKernelGGL(k_face_scatter, dim3(blocks(ne)), dim3(kB), 0, s, tv, ne, off, rank, bucket);
-  if (np > 0) {
-    // 8 blocks per CU (17 KB of LDS each) on 256 CUs, a multiple of 8
-    const int nchunk = (np + kMatchVerts - 1) / kMatchVerts;
-    const int grid = std::max(8, std::min(8 * 256, (nchunk + 7) / 8 * 8));
-    hipLaunchKernelGGL(k_face_match, dim3(grid), dim3(kB), 0, s, np, off, cnt, bucket, nf, adja, tet8, err);
-  }
-  hipLaunchKernelGGL(k_face_invalid, dim3(blocks(ne)), dim3(kB), 0, s, ne, rank, reinterpret_cast<int4 *>(adja),
-                     reinterpret_cast<int4 *>(tet8));
+  SCK(hipMemcpyAsync(cursor, off, sizeof(int) * (size_t)np, hipMemcpyDeviceToDevice, s));
+  hipLaunchKernelGGL(k_face_scatter, dim3(blocks(ne)), dim3(kB), 0, s, tv, ne, np, cursor, bucket,
+                     reinterpret_cast<int4 *>(adja), reinterpret_cast<int4 *>(tet8));
+  hipLaunchKernelGGL(k_face_match, dim3((np + kMatchVerts - 1) / kMatchVerts), dim3(kB), 0, s, np, off, cnt, bucket,
+                     adja, tet8, err);
   SCK(hipGetLastError());
   int h_err = 0;
   SCK(hipMemcpyAsync(&h_err, err, sizeof(int), hipMemcpyDeviceToHost, s));
