@@ -136,6 +136,8 @@ struct pmmg_hip_ctx {
   int options = 0;
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr; // surface branch, concurrent with the volume walk
+  hipStream_t stream2_hi = nullptr; // the same at the highest priority, for calls of >= kSmallGroup queries
+  bool srf_prio = true;             // (not for group lanes; see run_device)
   char err[512] = {0};
   Bg bg{};
   int met_size = 0;
@@ -230,9 +232,10 @@ struct pmmg_hip_ctx {
   std::vector<pmmg_hip_ctx *> lanes;
   int group_lanes = 4; // PMMG_HIP_GROUP_LANES (r04i, 10 cfg2-size groups: 1 / 2 / 4 lanes 0.165 / 0.125 / 0.108 ms per group)
   struct Pool *lane_pool = nullptr; // host threads enqueueing the other lanes' groups
-  int lane_streams = 2; // a group lane's streams: 2 = its surface stream at normal priority, 1 = the surface
-                        // branch on the main stream, 3 = the surface stream at the highest priority as in a
-                        // single call (measurement build: PMMG_HIP_LANE_STREAMS)
+  int lane_streams = 2; // a group lane's streams: 2 = its own surface stream, 1 = the surface branch on the
+                        // main stream (measurement build: PMMG_HIP_LANE_STREAMS)
+  int lane0 = 1; // the context itself is the groups call's lane 0 (measurement build: PMMG_HIP_LANE0=0 uses
+                 // lane contexts only)
   int filter_steps = 64; // step cap of the fp32 filter walk (then the exact fp64 walk continues from where it
                          // stopped: a query the filter misjudges hands over early instead of cycling through a
                          // 4-entry history for up to maxstep steps); test-only PMMG_HIP_FILTER_STEPS=0 sends every
@@ -535,7 +538,7 @@ int pmmg_hip_device_count(void) {
   return n;
 }
 
-pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
+static pmmg_hip_ctx *create_ctx(int device, int options, bool srf_prio) {
   int n = pmmg_hip_device_count();
   if (n <= 0 || device < 0 || device >= n) {
     fprintf(stderr, "[parmmg_hip] no HIP device %d (visible: %d)\n", device, n);
@@ -544,19 +547,13 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   pmmg_hip_ctx *c = new pmmg_hip_ctx();
   c->device = device;
   c->options = options;
-  // the second stream (query order, then the surface branch) at the highest
-  // priority: k_bdy's blocks are dispatched ahead of the volume kernel's
-  // instead of trailing it (r04o trace: the surface branch ended 0.17 ms after
-  // the volume kernel, the end of the step); measurement build:
-  // PMMG_HIP_SRFPRIO=0 for the default priority
-  int prio_lo = 0, prio_hi = 0;
-  (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
 #ifdef PMMG_HIP_MEASURE
   if (const char *e = getenv("PMMG_HIP_SRFPRIO"))
-    if (*e == '0') prio_hi = prio_lo;
+    if (*e == '0') srf_prio = false;
 #endif
+  c->srf_prio = srf_prio;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess) {
+      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
     fprintf(stderr, "[parmmg_hip] cannot initialise device %d\n", device);
     delete c;
     return nullptr;
@@ -590,10 +587,13 @@ pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
   if (const char *e = getenv("PMMG_HIP_XCDRUN"))
     if (*e && atoi(e) >= 0) c->xcd_run = atoi(e);
   c->pad = env_int("PMMG_HIP_PAD", 0);
-  c->lane_streams = std::max(1, std::min(3, env_int("PMMG_HIP_LANE_STREAMS", c->lane_streams)));
+  c->lane_streams = env_int("PMMG_HIP_LANE_STREAMS", c->lane_streams) == 1 ? 1 : 2;
+  c->lane0 = env_int("PMMG_HIP_LANE0", 1) ? 1 : 0;
 #endif
   return c;
 }
+
+pmmg_hip_ctx *pmmg_hip_create(int device, int options) { return create_ctx(device, options, true); }
 
 void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   if (!c) return;
@@ -603,6 +603,7 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   (void)snap_join(c);
   (void)hipStreamSynchronize(c->stream);
   (void)hipStreamSynchronize(c->stream2);
+  if (c->stream2_hi) (void)hipStreamSynchronize(c->stream2_hi);
   if (c->cstream) (void)hipStreamSynchronize(c->cstream);
   DevBuf *bufs[] = {&c->o_xyz, &c->o_tetv, &c->o_adja, &c->o_triv, &c->o_adjt, &c->o_met, &c->o_rec, &c->frame,
                     &c->stats, &c->grid, &c->sgrid, &c->order_v,
@@ -630,6 +631,7 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   DevBuf *cb[] = {&c->carry_dsrc, &c->carry_need, &c->carry_ids, &c->carry_cnt, &c->carry_rows, &c->carry_bc};
   for (DevBuf *b : cb) release(*b);
   if (c->stream2 && c->stream2 != c->stream) (void)hipStreamDestroy(c->stream2);
+  if (c->stream2_hi) (void)hipStreamDestroy(c->stream2_hi);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->cstream) (void)hipStreamDestroy(c->cstream);
   delete c;
@@ -1200,6 +1202,24 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
                       double *const *fields_out, int *elem_out, int8_t *hit_out) {
   Bg bg = c->bg;
   hipStream_t s = c->stream, sb = c->stream2;
+  // A large call runs its second stream (query order, then the surface
+  // branch) at the highest priority: k_bdy's blocks are dispatched ahead of
+  // the volume kernel's instead of trailing it (r04o trace: the surface branch
+  // ended 0.17 ms after the volume kernel, the end of the step; -0.08 ms at
+  // cfg4).  Created on the first such call and dropped by a groups call: a
+  // high-priority stream anywhere in the process slowed the groups call's
+  // lanes from 0.095 to 0.15-0.19 ms per cfg2-size group (r04x).  The second
+  // stream always waits for the main stream's first event, so a call may use
+  // either.
+  if (c->srf_prio && np_new >= kSmallGroup) {
+    if (!c->stream2_hi) {
+      int prio_lo = 0, prio_hi = 0;
+      (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+      if (hipStreamCreateWithPriority(&c->stream2_hi, hipStreamNonBlocking, prio_hi) != hipSuccess)
+        c->stream2_hi = nullptr;
+    }
+    if (c->stream2_hi) sb = c->stream2_hi;
+  }
   Slots S{};
   S.n = 0;
   S.has_met = c->met_size ? 1 : 0;
@@ -1646,20 +1666,14 @@ static void stats_sum(pmmg_hip_stats *a, const pmmg_hip_stats &b) {
 static pmmg_hip_ctx *group_lane(pmmg_hip_ctx *c, int j) {
   if (j == 0) return c;
   while ((int)c->lanes.size() < j) {
-    pmmg_hip_ctx *l = pmmg_hip_create(c->device, c->options);
+    pmmg_hip_ctx *l = create_ctx(c->device, c->options, false);
     if (!l) {
       set_err(c, "locate_interp_groups: cannot create group lane %d", (int)c->lanes.size() + 1);
       return nullptr;
     }
-    if (c->lane_streams != 3) {
+    if (c->lane_streams == 1) {
       (void)hipStreamDestroy(l->stream2);
       l->stream2 = l->stream;
-      if (c->lane_streams == 2 && hipStreamCreateWithFlags(&l->stream2, hipStreamNonBlocking) != hipSuccess) {
-        l->stream2 = l->stream;
-        set_err(c, "locate_interp_groups: cannot create a stream for group lane %d", (int)c->lanes.size() + 1);
-        pmmg_hip_destroy(l);
-        return nullptr;
-      }
     }
     c->lanes.push_back(l);
   }
@@ -1705,10 +1719,15 @@ int pmmg_hip_locate_interp_groups(pmmg_hip_ctx *c, int ngroup, const pmmg_hip_gr
   }
   HIPCK(c, hipSetDevice(c->device));
   if (!snap_join(c)) return 0;
+  if (c->stream2_hi) { // (see run_device)
+    HIPCK(c, hipStreamSynchronize(c->stream2_hi));
+    HIPCK(c, hipStreamDestroy(c->stream2_hi));
+    c->stream2_hi = nullptr;
+  }
   const int L = std::max(1, std::min(ngroup, c->group_lanes));
   std::vector<pmmg_hip_ctx *> lane(L);
   for (int j = 0; j < L; j++)
-    if (!(lane[j] = group_lane(c, j))) return 0;
+    if (!(lane[j] = group_lane(c, j + 1 - c->lane0))) return 0;
   // every lane enqueues its groups from its own host thread (the enqueue of
   // ~25 launches per group is the host's share of a small group)
   std::vector<pmmg_hip_stats> sums(L);
