@@ -10,8 +10,8 @@
  * tensor).  Medit stores a 3D tensor as m11 m12 m22 m13 m23 m33 and MMG5
  * keeps m11 m12 m13 m22 m23 m33 in memory: entries 2 and 3 are swapped on
  * read, as Mmg's MMG5_loadSolAtVertices does.  Arrays use the C-ABI's "row r =
- * entity r+1" layout (include/parmmg_hip.h).  Binary .meshb / .solb files are
- * not read (error).
+ * entity r+1" layout (include/parmmg_hip.h).  Binary .meshb / .solb files
+ * (GMF versions 1-3, either byte order) are read too (pmmg_medit.c).
  */
 #ifndef PMMG_MEDIT_H
 #define PMMG_MEDIT_H
