@@ -587,7 +587,7 @@ static pmmg_hip_ctx *create_ctx(int device, int options, bool srf_prio) {
   if (const char *e = getenv("PMMG_HIP_XCDRUN"))
     if (*e && atoi(e) >= 0) c->xcd_run = atoi(e);
   c->pad = env_int("PMMG_HIP_PAD", 0);
-  c->lane_streams = env_int("PMMG_HIP_LANE_STREAMS", c->lane_streams) == 1 ? 1 : 2;
+  c->lane_streams = std::max(1, std::min(3, env_int("PMMG_HIP_LANE_STREAMS", c->lane_streams)));
   c->lane0 = env_int("PMMG_HIP_LANE0", 1) ? 1 : 0;
 #endif
   return c;
@@ -1675,6 +1675,16 @@ static pmmg_hip_ctx *group_lane(pmmg_hip_ctx *c, int j) {
       (void)hipStreamDestroy(l->stream2);
       l->stream2 = l->stream;
     }
+#ifdef PMMG_HIP_MEASURE
+    if (c->lane_streams == 3) { // both of a lane's streams at the highest priority
+      int lo = 0, hi = 0;
+      (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+      (void)hipStreamDestroy(l->stream);
+      (void)hipStreamDestroy(l->stream2);
+      (void)hipStreamCreateWithPriority(&l->stream, hipStreamNonBlocking, hi);
+      (void)hipStreamCreateWithPriority(&l->stream2, hipStreamNonBlocking, hi);
+    }
+#endif
     c->lanes.push_back(l);
   }
   return c->lanes[j - 1];
