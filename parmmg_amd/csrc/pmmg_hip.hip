@@ -136,8 +136,8 @@ struct pmmg_hip_ctx {
   int options = 0;
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr; // surface branch, concurrent with the volume walk
-  hipStream_t stream2_hi = nullptr; // the same at the highest priority, for calls of >= kSmallGroup queries
-  bool srf_prio = true;             // (not for group lanes; see run_device)
+  hipStream_t stream2_hi = nullptr; // measurement build, PMMG_HIP_SRFPRIO=1: the same at the highest priority,
+  bool srf_prio = false;            // for calls of >= kSmallGroup queries (see run_device)
   char err[512] = {0};
   Bg bg{};
   int met_size = 0;
@@ -234,6 +234,7 @@ struct pmmg_hip_ctx {
   struct Pool *lane_pool = nullptr; // host threads enqueueing the other lanes' groups
   int lane_streams = 2; // a group lane's streams: 2 = its own surface stream, 1 = the surface branch on the
                         // main stream (measurement build: PMMG_HIP_LANE_STREAMS)
+  int bdy_first = 0; // measurement build, PMMG_HIP_BDYFIRST=1: the volume kernel waits for the surface branch
   int lane0 = 1; // the context itself is the groups call's lane 0 (measurement build: PMMG_HIP_LANE0=0 uses
                  // lane contexts only)
   int filter_steps = 64; // step cap of the fp32 filter walk (then the exact fp64 walk continues from where it
@@ -549,9 +550,10 @@ static pmmg_hip_ctx *create_ctx(int device, int options, bool srf_prio) {
   c->options = options;
 #ifdef PMMG_HIP_MEASURE
   if (const char *e = getenv("PMMG_HIP_SRFPRIO"))
-    if (*e == '0') srf_prio = false;
+    if (*e == '1') c->srf_prio = srf_prio;
+#else
+  (void)srf_prio;
 #endif
-  c->srf_prio = srf_prio;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
     fprintf(stderr, "[parmmg_hip] cannot initialise device %d\n", device);
@@ -589,6 +591,7 @@ static pmmg_hip_ctx *create_ctx(int device, int options, bool srf_prio) {
   c->pad = env_int("PMMG_HIP_PAD", 0);
   c->lane_streams = std::max(1, std::min(3, env_int("PMMG_HIP_LANE_STREAMS", c->lane_streams)));
   c->lane0 = env_int("PMMG_HIP_LANE0", 1) ? 1 : 0;
+  c->bdy_first = env_int("PMMG_HIP_BDYFIRST", 0);
 #endif
   return c;
 }
@@ -1202,15 +1205,15 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
                       double *const *fields_out, int *elem_out, int8_t *hit_out) {
   Bg bg = c->bg;
   hipStream_t s = c->stream, sb = c->stream2;
-  // A large call runs its second stream (query order, then the surface
-  // branch) at the highest priority: k_bdy's blocks are dispatched ahead of
-  // the volume kernel's instead of trailing it (r04o trace: the surface branch
-  // ended 0.17 ms after the volume kernel, the end of the step; -0.08 ms at
-  // cfg4).  Created on the first such call and dropped by a groups call: a
-  // high-priority stream anywhere in the process slowed the groups call's
-  // lanes from 0.095 to 0.15-0.19 ms per cfg2-size group (r04x).  The second
-  // stream always waits for the main stream's first event, so a call may use
-  // either.
+  // Measurement build (PMMG_HIP_SRFPRIO=1): a large call runs its second
+  // stream (query order, then the surface branch) at the highest priority, so
+  // k_bdy's blocks are dispatched ahead of the volume kernel's instead of
+  // trailing it (r04o trace: the surface branch ended 0.17 ms after the
+  // volume kernel; cfg4 -0.06 ms, r04zh).  Not in the product: once a
+  // high-priority stream has existed in the process — even destroyed — the
+  // groups call's lanes run at 0.22-0.33 instead of 0.095 ms per cfg2-size
+  // group (r04x, r04zg).  The second stream always waits for the main
+  // stream's first event, so a call may use either.
   if (c->srf_prio && np_new >= kSmallGroup) {
     if (!c->stream2_hi) {
       int prio_lo = 0, prio_hi = 0;
@@ -1389,6 +1392,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   if (c->brick > 0 && !brick_renumber(c, s, bg, S, fr, g)) return 0;
 #endif
   HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_ORDER], 0));
+  if (c->bdy_first) HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_BDY1], 0));
   HIPCK(c, hipEventRecord(c->ev[EV_VOL0], s));
   // ---- volume (main stream): walk + exact test + interpolation in one
   // kernel, then the exact continuation of the few queries it did not settle
