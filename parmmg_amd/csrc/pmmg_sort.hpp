@@ -76,74 +76,91 @@ __global__ __launch_bounds__(kBlock) void k_rs_scan_add(int *a, int n, const int
     if (i0 + j < n) a[i0 + j] += o;
 }
 
-// One tile per block: the tile's keys are first ranked stably by digit into
-// LDS (sub-tiles of 256 keys in input order; a wave's lanes with equal digits
-// found by 8 ballots), then written out in that order, so consecutive threads
-// store consecutive positions of one digit's run (r04g: ranking straight to
-// global memory wrote every key as an isolated 4-byte store, 0.44 ms per pass
-// of 20M random keys).
+// One tile per block: the tile's keys are ranked stably by digit into LDS,
+// then written out in that order, so consecutive threads store consecutive
+// positions of one digit's run (r04g: ranking straight to global memory
+// wrote every key as an isolated 4-byte store, 0.44 ms per pass of 20M
+// random keys).  r04: each wave ranks its own 1024 consecutive keys (16
+// chunks of 64, held in registers: one global read) with per-wave digit
+// counters in LDS that only the wave itself touches, so the ranking needs
+// no barrier; one block scan over {digit, wave} then gives every key its
+// place — 4 barriers per tile instead of ~50 (the tile's keys were read
+// twice and each chunk of 256 ranked between three barriers: 160-180 µs per
+// pass of 20M keys, 366 beside the seed grid, r04v2 trace).
 __global__ __launch_bounds__(kBlock) void k_rs_scatter(const unsigned *kin, const int *vin, int n, int shift, int ntile,
                                                        const int *off, unsigned *kout, int *vout, const int *gate,
                                                        int want) {
+  static_assert(kBlock == 256, "one thread per digit");
   if (gate_off(gate, want)) return;
+  constexpr int kWaveKeys = kRsTile / (kBlock / 64); // consecutive keys ranked by one wave
   __shared__ unsigned lk[kRsTile]; // the tile, sorted by digit (stable)
   __shared__ int lv[kRsTile];
-  __shared__ int run[256];         // next local position of each digit
-  __shared__ int gdelta[256];      // global position - local position of each digit's keys
-  __shared__ int wcnt[4][256];     // keys of each digit in each wave of the current sub-tile
+  __shared__ int wdig[kBlock / 64][256]; // a wave's digit counts, then its keys' first local position per digit
+  __shared__ int gdelta[256];            // global position - local position of each digit's keys
   const int t = threadIdx.x, w = t >> 6, lane = __lane_id();
+  const unsigned long long below = (1ULL << lane) - 1ULL;
   for (int tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
-  const long long base = (long long)tile * kRsTile;
-  const int cnt = (int)(n - base < kRsTile ? n - base : kRsTile);
-  // the tile's digit counts, their exclusive scan
-  run[t] = 0;
+    const long long base = (long long)tile * kRsTile;
+    const int cnt = (int)(n - base < kRsTile ? n - base : kRsTile);
 #pragma unroll
-  for (int q = 0; q < 4; q++) wcnt[q][t] = 0;
-  __syncthreads();
-  for (int j = 0; j < kRsItems; j++) {
-    const int e = j * kBlock + t;
-    if (e < cnt) atomicAdd(&run[(kin[base + e] >> shift) & 255u], 1);
-  }
-  __syncthreads();
-  int tot;
-  const int lstart = block_excl_scan(run[t], &tot);
-  __syncthreads();
-  run[t] = lstart;
-  gdelta[t] = off[(size_t)t * ntile + tile] - lstart;
-  __syncthreads();
-  for (int j = 0; j < kRsItems; j++) {
-    const int e = j * kBlock + t;
-    const bool ok = e < cnt;
-    const unsigned key = ok ? kin[base + e] : 0u;
-    const int val = ok ? vin[base + e] : 0;
-    const unsigned d = (key >> shift) & 255u;
-    unsigned long long same = __ballot(ok);
-#pragma unroll
-    for (int b = 0; b < 8; b++) {
-      const unsigned long long bb = __ballot((d >> b) & 1u);
-      same &= ((d >> b) & 1u) ? bb : ~bb;
-    }
-    const int rank = __popcll(same & ((1ULL << lane) - 1ULL));
-    if (ok && rank == 0) wcnt[w][d] = __popcll(same);
+    for (int q = 0; q < kBlock / 64; q++) wdig[q][t] = 0;
     __syncthreads();
-    if (ok) {
-      int pos = run[d] + rank;
-      for (int w2 = 0; w2 < w; w2++) pos += wcnt[w2][d];
-      lk[pos] = key;
-      lv[pos] = val;
+    unsigned key[kRsItems];
+    int val[kRsItems], rk[kRsItems];
+#pragma unroll
+    for (int j = 0; j < kRsItems; j++) {
+      const int e = w * kWaveKeys + j * 64 + lane;
+      key[j] = e < cnt ? kin[base + e] : 0u;
+      val[j] = e < cnt ? vin[base + e] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < kRsItems; j++) {
+      const bool ok = w * kWaveKeys + j * 64 + lane < cnt;
+      const unsigned d = (key[j] >> shift) & 255u;
+      unsigned long long same = __ballot(ok);
+#pragma unroll
+      for (int b = 0; b < 8; b++) {
+        const unsigned long long bb = __ballot((d >> b) & 1u);
+        same &= ((d >> b) & 1u) ? bb : ~bb;
+      }
+      const int r = __popcll(same & below);
+      const int prior = wdig[w][d]; // (this wave's counter: read by every lane before its first lane writes it)
+      rk[j] = prior + r;
+      if (ok && r == 0) wdig[w][d] = prior + __popcll(same);
     }
     __syncthreads();
-    run[t] += wcnt[0][t] + wcnt[1][t] + wcnt[2][t] + wcnt[3][t];
-    wcnt[0][t] = wcnt[1][t] = wcnt[2][t] = wcnt[3][t] = 0;
+    int c[kBlock / 64], tot_d = 0;
+#pragma unroll
+    for (int q = 0; q < kBlock / 64; q++) {
+      c[q] = wdig[q][t];
+      tot_d += c[q];
+    }
+    int tot;
+    const int dstart = block_excl_scan(tot_d, &tot);
+    int acc = dstart;
+#pragma unroll
+    for (int q = 0; q < kBlock / 64; q++) {
+      wdig[q][t] = acc;
+      acc += c[q];
+    }
+    gdelta[t] = off[(size_t)t * ntile + tile] - dstart;
     __syncthreads();
-  }
-  for (int e = t; e < cnt; e += kBlock) {
-    const unsigned key = lk[e];
-    const int pos = gdelta[(key >> shift) & 255u] + e;
-    kout[pos] = key;
-    vout[pos] = lv[e];
-  }
-  __syncthreads(); // the tile's LDS is free for the next tile
+#pragma unroll
+    for (int j = 0; j < kRsItems; j++) {
+      if (w * kWaveKeys + j * 64 + lane < cnt) {
+        const int pos = wdig[w][(key[j] >> shift) & 255u] + rk[j];
+        lk[pos] = key[j];
+        lv[pos] = val[j];
+      }
+    }
+    __syncthreads();
+    for (int e = t; e < cnt; e += kBlock) {
+      const unsigned k = lk[e];
+      const int pos = gdelta[(k >> shift) & 255u] + e;
+      kout[pos] = k;
+      vout[pos] = lv[e];
+    }
+    __syncthreads(); // the tile's LDS is free for the next tile
   }
 }
 
