@@ -3,7 +3,7 @@
 # run the sorted order, the shuffled step, its kernel trace
 set -o pipefail
 export TMPDIR=/tmp
-OUT=gpurun_out/${TAG:-r04zm}
+OUT=gpurun_out/${TAG:-r04zn}
 mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests/test_gpu_edge.py tests/test_gpu_parity.py tests/test_gpu_groups.py -x -q --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1 \
 && tail -2 $OUT/pytest.log \
