@@ -178,7 +178,11 @@ static int b_keyword(bfile *B, long long *kw, long long *next) {
   return *kw == kGmfEnd || b_pos(B, next);
 }
 
-static int b_skip_to(bfile *B, long long next) { return next > 0 && fseeko(B->f, (off_t)next, SEEK_SET) == 0; }
+/* forward only: a corrupted position pointing back would loop forever */
+static int b_skip_to(bfile *B, long long next) {
+  const long long at = (long long)ftello(B->f);
+  return at >= 0 && next > at && next <= B->size && fseeko(B->f, (off_t)next, SEEK_SET) == 0;
+}
 
 static int read_mesh_binary(const char *path, pmmg_medit_mesh *m, char *err, int errlen) {
   bfile B;

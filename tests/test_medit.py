@@ -202,6 +202,11 @@ def test_binary_files_rejected(tmp_path):
     (tmp_path / "junk.meshb").write_bytes(b"MeshVersionFormatted 2\n")
     with pytest.raises(ValueError, match="not a binary Medit"):
         medit.read_mesh_c(str(tmp_path / "junk.meshb"))
+    # an unknown block whose next-keyword position points back: rejected, not looped over
+    loop = np.array([1, 2, GMF_CORNERS, 8], "<i4").tobytes()
+    (tmp_path / "loop.meshb").write_bytes(loop)
+    with pytest.raises(ValueError, match="malformed"):
+        medit.read_mesh_c(str(tmp_path / "loop.meshb"))
     (tmp_path / "d2.meshb").write_bytes(raw[:8] + np.array([GMF_DIM, 20, 2], "<i4").tobytes() + raw[20:])
     with pytest.raises(ValueError, match="dimension"):
         medit.read_mesh_c(str(tmp_path / "d2.meshb"))
