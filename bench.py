@@ -468,10 +468,9 @@ def renumbered_timing(ctx, args, w, step_bg, q_xyz, q_pc, d_mo, d_fo, d_elem, d_
 def surface_solo(ctx, step_bg, q_xyz, q_pc, d_mo, d_fo, d_elem, d_hit, device: int, reps: int = 5) -> dict:
     """The surface branch (k_seed_srf + k_bdy + its fallbacks, second
     stream) timed alone: the same call with every volume point marked
-    skipped, the branch starting beside the seed grid kernels of the main
-    stream as in the step (the figure with the GPU to itself needs the
-    measurement build: tools/surface_solo.py).  In the full step it overlaps
-    the volume kernel."""
+    skipped, the branch starting after the seed grid kernels of the main
+    stream as in a large call's step.  In the full step it overlaps the
+    volume kernel."""
     pc = np.where(q_pc == 2, 2, 0).astype(np.uint8)
     d_pc = ctx.upload(pc)
     ms_bdy, ms_tot = [], []
@@ -484,8 +483,8 @@ def surface_solo(ctx, step_bg, q_xyz, q_pc, d_mo, d_fo, d_elem, d_hit, device: i
             ms_tot.append(st.ms_total)
     d_pc.free()
     return {"what": "surface branch alone (volume points skipped): HIP events of the surface stream, "
-                    "starting beside the seed grid as in the step",
-            "surface_points": int(st.nbdy), "ms_beside_seed_grid": round(float(np.median(ms_bdy)), 4),
+                    "starting after the seed grid as in a large call's step",
+            "surface_points": int(st.nbdy), "ms_branch": round(float(np.median(ms_bdy)), 4),
             "ms_call": round(float(np.median(ms_tot)), 4)}
 
 

@@ -159,7 +159,9 @@ struct pmmg_hip_ctx {
   DevBuf brk_k, brk_k2, brk_v, brk_v2, brk_vinv, brk_tinv, brk_xq, brk_xyz, brk_sol, brk_rec, brk_tmp;
   int brick = 0;
   int set_order = 0; // test-only PMMG_HIP_SETORDER=1 (see k_set_order)
-  int srf_solo = 0; // test-only PMMG_HIP_SRFSOLO=1: the surface branch waits for the seed grid (its cost alone)
+  int srf_solo = -1; // the surface branch waits for the seed grid: -1 in calls of >= kSmallGroup queries (r04zo,
+                     // cfg4: the seed grid ran at 455 instead of 261 us beside k_bdy; step 4.24 -> 4.13 ms,
+                     // Mmg-like 5.01 -> 4.93, shuffled =), 1 always, 0 never (PMMG_HIP_SRFSOLO)
   DevBuf qs;                              // volume query coordinates in processing order (Morton path)
   DevBuf cls_cnt;                         // per-block class counts (surface list compaction)
   DevBuf oflag;                           // the coherence test's {sorted, bin_bits} on the device
@@ -584,7 +586,7 @@ static pmmg_hip_ctx *create_ctx(int device, int options, bool srf_prio) {
   c->bdy_bpx = env_int("PMMG_HIP_BDYBPX", c->bdy_bpx);
   c->bin_qs = env_int("PMMG_HIP_BINQS", 2) == 1;
   c->brick = env_int("PMMG_HIP_BRICK", 0);
-  c->srf_solo = env_int("PMMG_HIP_SRFSOLO", 0);
+  c->srf_solo = env_int("PMMG_HIP_SRFSOLO", -1);
   c->set_order = env_int("PMMG_HIP_SETORDER", 0);
   if (const char *e = getenv("PMMG_HIP_XCDRUN"))
     if (*e && atoi(e) >= 0) c->xcd_run = atoi(e);
@@ -1372,7 +1374,8 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   HIPCK(c, hipEventRecord(c->ev[EV_ORDER], sb));
 
   // ---- surface branch (second stream, after the order): seeds, k_bdy
-  if (c->srf_solo) HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_PREP], 0));
+  if (c->srf_solo > 0 || (c->srf_solo < 0 && np_new >= kSmallGroup))
+    HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_PREP], 0));
   HIPCK(c, hipEventRecord(c->ev[EV_BDY0], sb));
   if (bg.nt > 0) {
     hipLaunchKernelGGL(k_seed_srf, dim3(blocks_for(bg.nt, 4096)), dim3(kBlock), 0, sb, bg, (const Frame *)fr, sgrid,
