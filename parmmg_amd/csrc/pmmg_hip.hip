@@ -1297,11 +1297,13 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   // bbox (its last block finalises the frame), the seed grid's axis maps
   hipLaunchKernelGGL(k_bbox, dim3(blocks_for(bg.np / c->bbox_stride + 1, 256)), dim3(kBlock), 0, s, bg.xyz, bg.np, fr,
                      c->bbox_stride, g, gs, gb);
+  // the second stream needs the frame only (lo, inv_bin, inv_srf), not the
+  // axis maps (r04: EV_FRAME moved here from after k_axis_map)
+  HIPCK(c, hipEventRecord(c->ev[EV_FRAME], s));
   hipLaunchKernelGGL(k_axis_hist, dim3(kHistBlocks), dim3(kBlock), 0, s, bg.xyz, bg.np, (const Frame *)fr,
                      c->hist_stride, (int *)c->axh.p);
   hipLaunchKernelGGL(k_axis_map, dim3(3), dim3(kBlock), 0, s, (const int *)c->axh.p, fr, g);
   HIPCK(c, hipGetLastError());
-  HIPCK(c, hipEventRecord(c->ev[EV_FRAME], s));
 
   // ---- query order (second stream, concurrent with the seed grid), after
   // the frame.  (r04: the axis maps moved here beside the fixed-point copy
