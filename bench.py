@@ -400,8 +400,16 @@ def host_mode_iteration2(ctx, w, bg, mo, fo, rank: int) -> dict:
         ctx.set_solutions(mo, fo)
         st = ctx.locate_interp(q2, pc2, m2, f2)
         t = time.perf_counter() - t0
+        sd = st.as_dict()
         res[mode] = {"ms": round(1e3 * t, 2), "bytes_up": ctx.bytes_up(reset=True),
-                     "located_points": int(st.nvol + st.nbdy)}
+                     "located_points": int(st.nvol + st.nbdy),
+                     # the walks' hand-overs and the exhaustive searches they needed
+                     "locate_stats": {k: sd[k] for k in ("nvol", "nbdy", "nvol_exact", "nvol_stuck", "nvol_limit",
+                                                         "nvol_noseed", "nvol_exhaust", "nvol_closest",
+                                                         "nbdy_exhaust", "nbdy_stale", "nbdy_closest", "stepmax")},
+                     "device_ms": {"step_total": round(float(st.ms_total), 3),
+                                   "volume_fallback": round(float(st.ms_fallback), 3),
+                                   "surface_branch": round(float(st.ms_bdy), 3)}}
         outs[mode] = [m2] + f2
     same = all(np.array_equal(a, b, equal_nan=True) for a, b in zip(outs["cold"], outs["carried"]))
     res.update({"what": "second iteration through host buffers: background = the new mesh of the first "

@@ -202,9 +202,12 @@ int pmmg_hip_sync(pmmg_hip_ctx *ctx, pmmg_hip_stats *stats);
  *                               values the caller copies on the host, and
  *                               MMG5_invmat failures); a metric / field whose
  *                               size differs from the kept one goes up whole.
- * pmmg_hip_carry_over(ctx, slot, 0, NULL) drops the slot.  The kept rows
- * must not have been changed on the host in between; the connectivity always
- * comes from the host.  Both return 1/0. */
+ * pmmg_hip_carry_over(ctx, slot, 0, NULL) drops the slot and frees its device
+ * buffers.  A carry consumes its slot (keep again for the next iteration);
+ * any failure of the armed set_background / set_solutions disarms it, and an
+ * armed carry rejects pmmg_hip_set_solutions_packed and PMMG_HIP_DEVICE
+ * calls.  The kept rows must not have been changed on the host in between;
+ * the connectivity always comes from the host.  Both return 1/0. */
 int pmmg_hip_keep(pmmg_hip_ctx *ctx, int slot);
 int pmmg_hip_carry_over(pmmg_hip_ctx *ctx, int slot, int np, const int *src);
 
@@ -252,7 +255,9 @@ typedef struct {
  * call waits after each round of L groups and returns the counters summed
  * over all groups (ms_* summed as well, stepmax the largest, sorted the
  * number of groups whose queries were Morton-binned).  Results are identical to one
- * pmmg_hip_locate_interp per group.  Returns 1 if every group was enqueued
+ * pmmg_hip_locate_interp per group.  The lanes are contexts of their own
+ * (lane 0 enqueues on ctx's streams): ctx's background, solutions and armed
+ * carry-over are left as they were.  Returns 1 if every group was enqueued
  * (and, with stats, completed), 0 at the first invalid group (the error names
  * its index; groups before it are enqueued). */
 int pmmg_hip_locate_interp_groups(pmmg_hip_ctx *ctx, int ngroup, const pmmg_hip_group *groups,

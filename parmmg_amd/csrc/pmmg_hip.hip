@@ -7,7 +7,8 @@
 //                                                             acceptance + interpolation), k_vol_walk_exact
 //   PMMG_interp4bar_*        src/interpmesh_pmmg.c:206-270 -> vol_slot / vol_interp_packed in k_vol (pmmg_vol.hpp)
 //   PMMG_locatePointBdy      src/locate_pmmg.c:587-723     -> k_bdy (locate + interpolate)  (pmmg_bdy.hpp)
-//   exhaustive / closest     src/locate_pmmg.c:477-515, 737-770 -> k_*_exhaust*, k_*_finish (pmmg_fallback.hpp)
+//   exhaustive / closest     src/locate_pmmg.c:477-515, 737-770 -> k_*_exhaust_accept, k_*_exhaust_closest
+//                                                             (pmmg_fallback.hpp)
 // Device arithmetic: pmmg_device.hpp; preparation and query order:
 // pmmg_prep.hpp.
 //
@@ -166,7 +167,8 @@ struct pmmg_hip_ctx {
   DevBuf cls_cnt;                         // per-block class counts (surface list compaction)
   DevBuf oflag;                           // the coherence test's {sorted, bin_bits} on the device
   DevBuf qmin;                               // tetra quality minimum (pmmg_hip_tetra_qual)
-  DevBuf fb_vol, fb_bdy, best, ckey, cidx, bbest, bckey, bcidx;
+  DevBuf fb_vol, fb_bdy, best, nac, cres, bbest, bnac, bcres; // exhaustive searches: fallback lists, lowest
+  DevBuf fbp_vol, fbp_bdy; // accepting element, unaccepted lists, closest results and range minima (FbPart)
   // host-mode staging
   DevBuf h_xyz, h_cls, h_met, h_elem, h_hit;
   std::vector<DevBuf> h_f;
@@ -229,16 +231,19 @@ struct pmmg_hip_ctx {
   std::vector<int> carry_src;  // next vertex i+1 = kept point carry_src[i] (0: host row); empty: identity
   DevBuf carry_dsrc, carry_need, carry_ids, carry_cnt, carry_rows, carry_bc;
   int64_t bytes_up = 0; // host -> device bytes of host-mode calls (pmmg_hip_bytes_up)
-  // pmmg_hip_locate_interp_groups: the context itself is lane 0, lanes[j]
-  // lane j + 1 (same device and options, created at the first groups call)
+  // pmmg_hip_locate_interp_groups: lanes[j] is lane j (same device and
+  // options, created at the first groups call); lane 0 enqueues on this
+  // context's own streams (no extra hardware queue) but has its own state, so
+  // a groups call leaves this context's background and solutions as they were
   std::vector<pmmg_hip_ctx *> lanes;
+  bool borrowed_streams = false; // a lane 0: stream / stream2 belong to its parent
   int group_lanes = 4; // PMMG_HIP_GROUP_LANES (r04i, 10 cfg2-size groups: 1 / 2 / 4 lanes 0.165 / 0.125 / 0.108 ms per group)
   struct Pool *lane_pool = nullptr; // host threads enqueueing the other lanes' groups
   int lane_streams = 2; // a group lane's streams: 2 = its own surface stream, 1 = the surface branch on the
                         // main stream (measurement build: PMMG_HIP_LANE_STREAMS)
   int bdy_first = 0; // measurement build, PMMG_HIP_BDYFIRST=1: the volume kernel waits for the surface branch
-  int lane0 = 1; // the context itself is the groups call's lane 0 (measurement build: PMMG_HIP_LANE0=0 uses
-                 // lane contexts only)
+  int lane0 = 1; // lane 0 enqueues on this context's streams (measurement build: PMMG_HIP_LANE0=0 gives it
+                 // streams of its own)
   int filter_steps = 64; // step cap of the fp32 filter walk (then the exact fp64 walk continues from where it
                          // stopped: a query the filter misjudges hands over early instead of cycling through a
                          // 4-entry history for up to maxstep steps); test-only PMMG_HIP_FILTER_STEPS=0 sends every
@@ -541,7 +546,9 @@ int pmmg_hip_device_count(void) {
   return n;
 }
 
-static pmmg_hip_ctx *create_ctx(int device, int options, bool srf_prio) {
+// share != NULL: a group lane that enqueues on share's two streams (its
+// own buffers, events and state; the streams are not destroyed with it)
+static pmmg_hip_ctx *create_ctx(int device, int options, bool srf_prio, pmmg_hip_ctx *share = nullptr) {
   int n = pmmg_hip_device_count();
   if (n <= 0 || device < 0 || device >= n) {
     fprintf(stderr, "[parmmg_hip] no HIP device %d (visible: %d)\n", device, n);
@@ -556,8 +563,14 @@ static pmmg_hip_ctx *create_ctx(int device, int options, bool srf_prio) {
 #else
   (void)srf_prio;
 #endif
-  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
+  if (share) {
+    c->stream = share->stream;
+    c->stream2 = share->stream2;
+    c->borrowed_streams = true;
+  }
+  if (hipSetDevice(device) != hipSuccess ||
+      (!share && (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+                  hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess))) {
     fprintf(stderr, "[parmmg_hip] cannot initialise device %d\n", device);
     delete c;
     return nullptr;
@@ -613,7 +626,7 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   DevBuf *bufs[] = {&c->o_xyz, &c->o_tetv, &c->o_adja, &c->o_triv, &c->o_adjt, &c->o_met, &c->o_rec, &c->frame,
                     &c->stats, &c->grid, &c->sgrid, &c->order_v,
                     &c->order_b, &c->cont, &c->xq, &c->qs, &c->axh, &c->bkeys, &c->bkeys2, &c->bvals, &c->bvals2, &c->rs_hist, &c->rs_csum, &c->oflag, &c->cls_cnt, &c->qmin, &c->fb_vol, &c->fb_bdy,
-                    &c->best, &c->ckey, &c->cidx, &c->bbest, &c->bckey, &c->bcidx, &c->h_xyz,
+                    &c->best, &c->nac, &c->cres, &c->bbest, &c->bnac, &c->bcres, &c->fbp_vol, &c->fbp_bdy, &c->h_xyz,
                     &c->h_cls, &c->h_met, &c->h_elem, &c->h_hit, &c->brk_k, &c->brk_k2, &c->brk_v, &c->brk_v2,
                     &c->brk_vinv, &c->brk_tinv, &c->brk_xq, &c->brk_xyz, &c->brk_sol, &c->brk_rec, &c->brk_tmp};
   for (DevBuf *b : bufs) release(*b);
@@ -635,9 +648,11 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   }
   DevBuf *cb[] = {&c->carry_dsrc, &c->carry_need, &c->carry_ids, &c->carry_cnt, &c->carry_rows, &c->carry_bc};
   for (DevBuf *b : cb) release(*b);
-  if (c->stream2 && c->stream2 != c->stream) (void)hipStreamDestroy(c->stream2);
+  if (!c->borrowed_streams) {
+    if (c->stream2 && c->stream2 != c->stream) (void)hipStreamDestroy(c->stream2);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+  }
   if (c->stream2_hi) (void)hipStreamDestroy(c->stream2_hi);
-  if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->cstream) (void)hipStreamDestroy(c->cstream);
   delete c;
 }
@@ -717,19 +732,26 @@ static int carry_vertices(pmmg_hip_ctx *c, int np, const double *xyz) {
     carry_disarm(c);
     return 0;
   }
+  k.valid = false; // the slot is consumed by this carry, whatever happens next (a swapped-out
+                   // buffer must never feed a later carry of the same slot)
   if (c->carry_src.empty()) {
     std::swap(c->o_xyz, k.xyz); // every row is a kept point, in order
   } else {
     if (!ensure(c, c->o_xyz, sizeof(double) * 3 * (size_t)np) ||
-        !upload(c, c->carry_dsrc, c->carry_src.data(), sizeof(int) * (size_t)np))
+        !upload(c, c->carry_dsrc, c->carry_src.data(), sizeof(int) * (size_t)np)) {
+      carry_disarm(c);
       return 0;
+    }
     hipLaunchKernelGGL(k_carry_gather, dim3(blocks_for(np, 4096)), dim3(kBlock), 0, c->stream,
                        (const double *)k.xyz.p, 3, (const int *)c->carry_dsrc.p, (long long)np, (double *)c->o_xyz.p,
                        (uint8_t *)nullptr, 0);
     std::vector<int> ids;
     for (int i = 0; i < np; i++)
       if (c->carry_src[i] == 0) ids.push_back(i + 1);
-    if (!carry_host_rows(c, ids, xyz, 3, (double *)c->o_xyz.p)) return 0;
+    if (!carry_host_rows(c, ids, xyz, 3, (double *)c->o_xyz.p)) {
+      carry_disarm(c);
+      return 0;
+    }
   }
   c->carry_bg = true;
   return 1;
@@ -737,8 +759,19 @@ static int carry_vertices(pmmg_hip_ctx *c, int np, const double *xyz) {
 
 // set_solutions, host mode, carry armed: the metric and the fields whose
 // sizes match the kept ones from the slot, their missing rows from the host
+static int carry_solutions_body(pmmg_hip_ctx *c, int met_size, const double *met, int nfield, const int *field_size,
+                                const double *const *fields);
+
+// every way out of an armed set_solutions disarms the carry
 static int carry_solutions(pmmg_hip_ctx *c, int met_size, const double *met, int nfield, const int *field_size,
                            const double *const *fields) {
+  const int ok = carry_solutions_body(c, met_size, met, nfield, field_size, fields);
+  carry_disarm(c);
+  return ok;
+}
+
+static int carry_solutions_body(pmmg_hip_ctx *c, int met_size, const double *met, int nfield, const int *field_size,
+                                const double *const *fields) {
   pmmg_hip_ctx::Kept &k = c->kept[c->carry_slot];
   const int np = c->carry_np;
   const bool ident = c->carry_src.empty();
@@ -1084,6 +1117,12 @@ int pmmg_hip_set_solutions_packed(pmmg_hip_ctx *c, int met_size, int nfield, con
     set_err(c, "set_solutions_packed: call pmmg_hip_set_background first");
     return 0;
   }
+  if (c->carry_slot >= 0) {
+    set_err(c, "set_solutions_packed: a carry-over is armed; it takes pmmg_hip_set_solutions (the kept rows are "
+               "per-solution arrays)");
+    carry_disarm(c);
+    return 0;
+  }
   c->met_size = met_size;
   c->nfield = nfield;
   c->fsize.assign(field_size, field_size + nfield);
@@ -1130,23 +1169,22 @@ static void launch_vol_fallbacks(pmmg_hip_ctx *c, const Slots &S, const double *
   const Bg &bg = c->bg;
   hipStream_t s = c->stream;
   DevStats *st = (DevStats *)c->stats.p;
-  const int fgrid = 1024;
-  hipLaunchKernelGGL(k_vol_exhaust_scan, dim3(fgrid), dim3(kBlock), 0, s, bg, xyz_new, (const int *)c->fb_vol.p, st,
-                     (int *)c->best.p, (unsigned long long *)c->ckey.p);
-  hipLaunchKernelGGL(k_vol_exhaust_pick, dim3(fgrid), dim3(kBlock), 0, s, bg, xyz_new, (const int *)c->fb_vol.p, st,
-                     (const int *)c->best.p, (const unsigned long long *)c->ckey.p, (int *)c->cidx.p, S, elem_out,
-                     hit_out);
+  const int *fb = (const int *)c->fb_vol.p;
+  hipLaunchKernelGGL(k_vol_exhaust_accept, dim3(kFbGridVol), dim3(kBlock), 0, s, bg, xyz_new, fb, st,
+                     (int *)c->best.p, (int *)c->nac.p, S, elem_out, hit_out);
+  hipLaunchKernelGGL(k_vol_exhaust_closest, dim3(kFbGridVol), dim3(kBlock), 0, s, bg, xyz_new, fb, st,
+                     (const int *)c->nac.p, (FbPart *)c->fbp_vol.p, (int *)c->cres.p, S, elem_out, hit_out);
 }
 
 static void launch_bdy_fallbacks(pmmg_hip_ctx *c, hipStream_t s, const Slots &S, const double *xyz_new,
                                  int *elem_out, int8_t *hit_out) {
   const Bg &bg = c->bg;
   DevStats *st = (DevStats *)c->stats.p;
-  hipLaunchKernelGGL(k_bdy_exhaust_scan, dim3(256), dim3(kBlock), 0, s, bg, xyz_new, (const int *)c->fb_bdy.p, st,
-                     (int *)c->bbest.p, (unsigned long long *)c->bckey.p);
-  hipLaunchKernelGGL(k_bdy_exhaust_pick, dim3(256), dim3(kBlock), 0, s, bg, xyz_new, (const int *)c->fb_bdy.p, st,
-                     (const int *)c->bbest.p, (const unsigned long long *)c->bckey.p, (int *)c->bcidx.p, S, elem_out,
-                     hit_out);
+  const int *fb = (const int *)c->fb_bdy.p;
+  hipLaunchKernelGGL(k_bdy_exhaust_accept, dim3(kFbGridBdy), dim3(kBlock), 0, s, bg, xyz_new, fb, st,
+                     (int *)c->bbest.p, (int *)c->bnac.p, S, elem_out, hit_out);
+  hipLaunchKernelGGL(k_bdy_exhaust_closest, dim3(kFbGridBdy), dim3(kBlock), 0, s, bg, xyz_new, fb, st,
+                     (const int *)c->bnac.p, (FbPart *)c->fbp_bdy.p, (int *)c->bcres.p, S, elem_out, hit_out);
 }
 
 #ifdef PMMG_HIP_MEASURE
@@ -1200,9 +1238,10 @@ static int brick_renumber(pmmg_hip_ctx *c, hipStream_t s, const Bg &bg, const Sl
 #endif
 
 // The pipeline of one call on device pointers.  It enqueues its kernels on
-// the context's two streams; in auto order mode it reads one flag back (the
-// coherence test's, pinned, while the main stream builds the seed grid) to
-// choose between the Morton binning and the input-order compaction.
+// the context's two streams and reads nothing back: in auto order mode both
+// the Morton binning and the input-order compaction are enqueued, each gated
+// on the coherence test's flag on the device (r04), and every fallback kernel
+// reads its list's count on the device.
 static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const uint8_t *pclass, double *met_out,
                       double *const *fields_out, int *elem_out, int8_t *hit_out) {
   Bg bg = c->bg;
@@ -1268,8 +1307,10 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
       !ensure(c, c->bkeys, 4 * nq) || !ensure(c, c->bkeys2, 4 * nq) || !ensure(c, c->bvals, 4 * nq) ||
       !ensure(c, c->qs, 24 * nq) || !ensure(c, c->cls_cnt, 4 * (size_t)ncls) || 
       !ensure(c, c->fb_vol, 4 * nq) || !ensure(c, c->fb_bdy, 4 * nq) || !ensure(c, c->best, 4 * nq) ||
-      !ensure(c, c->ckey, 8 * nq) || !ensure(c, c->cidx, 4 * nq) || !ensure(c, c->bbest, 4 * nq) ||
-      !ensure(c, c->bckey, 8 * nq) || !ensure(c, c->bcidx, 4 * nq))
+      !ensure(c, c->nac, 4 * nq) || !ensure(c, c->cres, 4 * nq) || !ensure(c, c->bbest, 4 * nq) ||
+      !ensure(c, c->bnac, 4 * nq) || !ensure(c, c->bcres, 4 * nq) ||
+      !ensure(c, c->fbp_vol, sizeof(FbPart) * (size_t)kFbPartCap) ||
+      !ensure(c, c->fbp_bdy, sizeof(FbPart) * 256 * (size_t)kFbGridBdy))
     return 0;
   if (!ensure(c, c->xq, sizeof(int) * kXqStride * (size_t)bg.np) || !ensure(c, c->oflag, 2 * sizeof(int)) ||
       !ensure(c, c->axh, sizeof(int) * 3 * kMapBins * (size_t)kHistBlocks))
@@ -1387,7 +1428,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     hipLaunchKernelGGL(k_bdy, dim3(8 * blocks_for((np_new + 7) / 8, c->bdy_bpx)), dim3(kBlock), 0, sb, bg,
                        (const Frame *)fr, (const int *)sgrid, gs, xyz_new, (const int *)order_b, S, elem_out, hit_out,
                        (int *)c->fb_bdy.p, st, c->maxstep, c->bdy_dyn,
-                       FbInit{(int *)c->bbest.p, (int *)c->bcidx.p, (unsigned long long *)c->bckey.p});
+                       FbInit{(int *)c->bbest.p});
     launch_bdy_fallbacks(c, sb, S, xyz_new, elem_out, hit_out);
     HIPCK(c, hipGetLastError());
   }
@@ -1409,7 +1450,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   HIPCK(c, hipEventRecord(c->ev[EV_WALK], s));
   hipLaunchKernelGGL(k_vol_walk_exact, dim3(8 * 64), dim3(64), 0, s, bg, xyz_new, (int *)c->fb_vol.p,
                      (const ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->maxstep,
-                     FbInit{(int *)c->best.p, (int *)c->cidx.p, (unsigned long long *)c->ckey.p});
+                     FbInit{(int *)c->best.p});
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[EV_VOL], s));
   // ---- exhaustive fallbacks of the volume queries (lists and counts on the
@@ -1618,8 +1659,22 @@ int pmmg_hip_keep(pmmg_hip_ctx *c, int slot) {
 
 int pmmg_hip_carry_over(pmmg_hip_ctx *c, int slot, int np, const int *src) {
   if (!c) return 0;
-  if (np == 0) { // drop the slot
-    if (slot >= 0 && slot < (int)c->kept.size()) c->kept[slot].valid = false;
+  if (np == 0) { // drop the slot and free its device buffers
+    if (c->carry_slot == slot && c->carry_bg) {
+      set_err(c, "carry_over: slot %d is being carried (set_background took it, set_solutions has not run)", slot);
+      return 0;
+    }
+    if (slot >= 0 && slot < (int)c->kept.size()) {
+      pmmg_hip_ctx::Kept &k = c->kept[slot];
+      HIPCK(c, hipSetDevice(c->device));
+      if (!snap_join(c)) return 0;
+      HIPCK(c, hipStreamSynchronize(c->stream));
+      release(k.xyz);
+      release(k.met);
+      for (auto &b : k.f) release(b);
+      k.f.clear();
+      k.valid = false;
+    }
     if (c->carry_slot == slot) carry_disarm(c);
     return 1;
   }
@@ -1673,19 +1728,19 @@ static void stats_sum(pmmg_hip_stats *a, const pmmg_hip_stats &b) {
 }
 
 static pmmg_hip_ctx *group_lane(pmmg_hip_ctx *c, int j) {
-  if (j == 0) return c;
-  while ((int)c->lanes.size() < j) {
-    pmmg_hip_ctx *l = create_ctx(c->device, c->options, false);
+  while ((int)c->lanes.size() <= j) {
+    const bool first = c->lanes.empty();
+    pmmg_hip_ctx *l = create_ctx(c->device, c->options, false, first && c->lane0 ? c : nullptr);
     if (!l) {
-      set_err(c, "locate_interp_groups: cannot create group lane %d", (int)c->lanes.size() + 1);
+      set_err(c, "locate_interp_groups: cannot create group lane %d", (int)c->lanes.size());
       return nullptr;
     }
-    if (c->lane_streams == 1) {
+    if (c->lane_streams == 1 && !l->borrowed_streams) {
       (void)hipStreamDestroy(l->stream2);
       l->stream2 = l->stream;
     }
 #ifdef PMMG_HIP_MEASURE
-    if (c->lane_streams == 3) { // both of a lane's streams at the highest priority
+    if (c->lane_streams == 3 && !l->borrowed_streams) { // both of a lane's streams at the highest priority
       int lo = 0, hi = 0;
       (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
       (void)hipStreamDestroy(l->stream);
@@ -1696,7 +1751,7 @@ static pmmg_hip_ctx *group_lane(pmmg_hip_ctx *c, int j) {
 #endif
     c->lanes.push_back(l);
   }
-  return c->lanes[j - 1];
+  return c->lanes[j];
 }
 
 // one lane's share of a groups call: groups j, j + L, j + 2L, ... enqueued in
@@ -1718,7 +1773,7 @@ static int lane_groups(pmmg_hip_ctx *l, int j, int L, int ngroup, const pmmg_hip
         pmmg_hip_locate_interp(l, g.np_new, g.xyz_new, g.pclass, g.met_out, g.fields_out, g.elem_out, g.hit_out,
                                nullptr, PMMG_HIP_DEVICE);
     pmmg_hip_stats st;
-    if (!ok || (want && !pmmg_hip_sync(l, &st))) {
+    if (!ok || (want && (hipStreamSynchronize(l->stream) != hipSuccess || !collect_stats(l, &st)))) {
       *bad = i;
       return 0;
     }
@@ -1746,7 +1801,7 @@ int pmmg_hip_locate_interp_groups(pmmg_hip_ctx *c, int ngroup, const pmmg_hip_gr
   const int L = std::max(1, std::min(ngroup, c->group_lanes));
   std::vector<pmmg_hip_ctx *> lane(L);
   for (int j = 0; j < L; j++)
-    if (!(lane[j] = group_lane(c, j + 1 - c->lane0))) return 0;
+    if (!(lane[j] = group_lane(c, j))) return 0;
   // every lane enqueues its groups from its own host thread (the enqueue of
   // ~25 launches per group is the host's share of a small group)
   std::vector<pmmg_hip_stats> sums(L);

@@ -25,20 +25,16 @@ struct DevStats {
   int bin_bits;         // Morton bits per axis of the binning keys (read back with `sorted`)
   int pad;
   int bdy_next[8];      // k_bdy: per-XCD work counters (the next unclaimed surface query of each eighth)
-  unsigned fb_done[2];  // blocks done with the last exhaustive pass (volume, surface): the last one finishes
+  int nac_vol, nac_bdy; // fallback queries no element accepted (the closest searches' lists)
+  unsigned fb_done[4];  // blocks done with an exhaustive kernel (volume accept / closest, surface accept /
+                        // closest): the last one finishes
 };
 
 // the exhaustive searches' per-query state, initialised where a query joins
-// a fallback list (no separate init launch): best accepting element, closest
-// key, lowest index at that key
+// a fallback list (no separate init launch): the lowest accepting element
 struct FbInit {
-  int *best, *cidx;
-  unsigned long long *ckey;
-  __device__ __forceinline__ void at(int slot) const {
-    best[slot] = INT_MAX;
-    cidx[slot] = INT_MAX;
-    ckey[slot] = ~0ULL;
-  }
+  int *best;
+  __device__ __forceinline__ void at(int slot) const { best[slot] = INT_MAX; }
 };
 
 constexpr int kStatParts = 256;

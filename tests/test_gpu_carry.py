@@ -126,3 +126,44 @@ def test_carry_over_errors_and_dropped_slots():
         ctx.carry_over(3, 0)  # dropped
         with pytest.raises(RuntimeError, match="holds nothing"):
             ctx.carry_over(3, B.np)
+
+
+@pytest.mark.gpu
+def test_carry_consumes_its_slot_and_disarms_on_failure():
+    """the identity carry swaps the kept vertex buffer into the
+    background, so the slot is consumed at once — a later carry of it fails
+    instead of feeding the previous background's vertices; an armed carry
+    rejects set_solutions_packed; a failed armed call disarms."""
+    from parmmg_amd.transfer import pack_solutions
+    case = make_case(kind=C, n_old=5, n_new=6, fields=(synth.F_SCALAR,), with_ref=False)
+    B = case["new"]
+    bg = case["bg"]
+    with TransferContext(0) as ctx:
+        def first_iteration():
+            ctx.set_background(bg.xyz, bg.tetv, bg.adja, bg.triv, bg.adjt, case["hausd"])
+            ctx.set_solutions(case["met"], case["fields"])
+            ctx.locate_interp(B.xyz, case["pclass"], np.zeros((B.np, 6)), [np.zeros((B.np, 1))])
+            ctx.keep(1)
+
+        first_iteration()
+        mo, fo = np.zeros((B.np, 6)), [np.zeros((B.np, 1))]
+        ctx.carry_over(1, B.np)
+        ctx.set_background(B.xyz, B.tetv, None, None, None, case["hausd"])  # takes the slot's vertices
+        with pytest.raises(RuntimeError, match="carry-over is armed"):
+            ctx.set_solutions_packed(pack_solutions(mo, fo), 6, [1])
+        with pytest.raises(RuntimeError, match="holds nothing"):
+            ctx.carry_over(1, B.np)  # consumed by the set_background above
+        # disarmed: a plain set_solutions uploads again and the context works
+        ctx.set_solutions(mo, fo)
+        first_iteration()
+        ctx.carry_over(1, B.np)
+        with pytest.raises(RuntimeError, match="armed carry-over is for"):
+            ctx.set_background(B.xyz[:-1].copy(), B.tetv, None, None, None, case["hausd"])  # wrong size: disarms
+        # disarmed without touching the slot: plain host calls work, and the
+        # slot can still be carried
+        ctx.set_background(bg.xyz, bg.tetv, bg.adja, bg.triv, bg.adjt, case["hausd"])
+        ctx.set_solutions(case["met"], case["fields"])
+        ctx.carry_over(1, B.np)
+        ctx.carry_over(1, 0)  # dropped (its buffers freed)
+        with pytest.raises(RuntimeError, match="holds nothing"):
+            ctx.carry_over(1, B.np)

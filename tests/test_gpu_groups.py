@@ -95,3 +95,28 @@ def test_groups_invalid_group_reports_its_index(cases):
         # the context stays usable
         ctx.locate_interp_groups(gs[:1])
         _same(_download(gs[0]), run_gpu(cases[0], tet8=True))
+
+
+@pytest.mark.gpu
+def test_groups_call_leaves_the_context_background(cases):
+    """the groups call's lane 0 used to be the context itself, so a
+    later single call ran against the last group's arrays.  The lanes are
+    contexts of their own now: a single call after a groups call still uses
+    the context's own (host-mode) background and solutions."""
+    case = cases[1]
+    with TransferContext(0) as ctx:
+        bg = case["bg"]
+        ctx.set_background(bg.xyz, bg.tetv, bg.adja, bg.triv, bg.adjt, case["hausd"])
+        ctx.set_solutions(case["met"], case["fields"])
+        gs = [_device_group(ctx, c) for c in cases[:3]]
+        ctx.locate_interp_groups(gs, sync=True)
+        new = case["new"]
+        npn = new.np
+        mo = np.full((npn, case["met"].shape[1]), np.nan)
+        fo = [np.full((npn, f.shape[1]), np.nan) for f in case["fields"]]
+        el, hit = np.zeros(npn, np.int32), np.zeros(npn, np.int8)
+        ctx.locate_interp(new.xyz, case["pclass"], mo, fo, el, hit)
+        out = dict(met=mo, fields=fo, elem=el, hit=hit)
+        _same(out, run_gpu(case, tet8=False))
+        rep = check(case, out)
+        assert rep["class_i"] == rep["class_i_same"]
