@@ -192,14 +192,18 @@ def parity_report(B, new, pclass, gpu, ref) -> dict:
     return out
 
 
-def allgather_timing(ri, d_mo, d_fo, d_elem, d_hit, sh, counts, rank: int, reps: int = 3):
+def allgather_timing(ri, ctx, d_mo, d_fo, d_elem, d_hit, sh, counts, rank: int, reps: int = 3):
     """Split modes: collect every rank's located elements (mapped to group
     ids: a halo shard's local ids through its tet_gid / tria_gid), hit codes
-    and interpolated rows on every rank (ranks.allgather_rows: RCCL
-    all_gather_into_tensor over xGMI), timed on its own after the timed steps
-    (reported separately; ParMmg itself consumes the results
-    per rank).  Returns the report and the gathered (rows, elem, hit) as host
-    arrays in rank order."""
+    and interpolated rows on every rank, timed on its own after the timed
+    steps (reported separately; ParMmg itself consumes the
+    results per rank).  With RCCL (backend nccl) through the module's C-ABI
+    collective (pmmg_hip_comm_init + pmmg_hip_allgather_points: one
+    ncclAllGather of packed records over xGMI), checked against
+    torch.distributed's all_gather_into_tensor of the same arrays
+    (ranks.allgather_rows, also the path of a gloo rehearsal, whose ranks
+    share one GPU and cannot form an RCCL communicator).  Returns the report
+    and the gathered (rows, elem, hit) as host arrays in rank order."""
     import torch
 
     rows = torch.cat([d_mo] + list(d_fo), dim=1)
@@ -208,23 +212,57 @@ def allgather_timing(ri, d_mo, d_fo, d_elem, d_hit, sh, counts, rank: int, reps:
     if sh is not None:
         elem = sh.to_group_elem(elem, (hit & 15) >= 4)
     eh = torch.from_numpy(np.stack([elem.astype(np.int32), hit.astype(np.int32)], axis=1)).to(rows.device)
-    times = []
-    for _ in range(reps):
-        ranks.barrier(ri)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        g_rows = ranks.allgather_rows(ri, rows, counts)
-        g_eh = ranks.allgather_rows(ri, eh, counts)
-        torch.cuda.synchronize()
-        times.append(ranks.max_over_ranks(ri, time.perf_counter() - t0))
+
+    def timed(fn):
+        ts = []
+        out = None
+        for _ in range(reps):
+            ranks.barrier(ri)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            out = fn()
+            torch.cuda.synchronize()
+            ts.append(ranks.max_over_ranks(ri, time.perf_counter() - t0))
+        return float(np.median(ts)), out
+
+    t_torch, (g_rows, g_eh) = timed(lambda: (ranks.allgather_rows(ri, rows, counts),
+                                             ranks.allgather_rows(ri, eh, counts)))
     nbytes = sum(counts) * (rows.shape[1] * 8 + 8)
-    t = float(np.median(times))
-    log(f"[bench r{rank}] all-gather of {nbytes / 1e9:.2f} GB: {1e3 * t:.2f} ms")
-    rep = {"what": "RCCL all-gather of {group elem id, hit code, K doubles} per point, not part of the step",
-           "ms": round(1e3 * t, 3), "bytes": int(nbytes), "gbps": round(nbytes / t / 1e9, 1),
-           "rows": int(g_rows.shape[0])}
     g_eh = g_eh.cpu().numpy()
-    return rep, (g_rows.cpu().numpy(), g_eh[:, 0].copy(), g_eh[:, 1].astype(np.int8))
+    g_rows_np, g_elem, g_hit = g_rows.cpu().numpy(), g_eh[:, 0].copy(), g_eh[:, 1].astype(np.int8)
+    rep = {"what": "all-gather of {group elem id, hit code, K doubles} per point, not part of the step",
+           "bytes": int(nbytes), "rows": int(g_rows.shape[0]),
+           "torch_all_gather_ms": round(1e3 * t_torch, 3)}
+    if ri.backend == "nccl":
+        try:
+            dev = rows.device
+            uid = [TransferContext.comm_unique_id() if rank == 0 else None]
+            ranks.broadcast_object(ri, uid)
+            ctx.comm_init(ri.world, rank, uid[0])
+            n_all = int(sum(counts))
+            d_elem_g = torch.from_numpy(elem.astype(np.int32)).to(dev)
+            outs = [torch.empty((n_all, a.shape[1]), dtype=torch.float64, device=dev) for a in [d_mo] + list(d_fo)]
+            e_all = torch.empty((n_all,), dtype=torch.int32, device=dev)
+            h_all = torch.empty((n_all,), dtype=torch.int8, device=dev)
+            t_c, _ = timed(lambda: ctx.allgather_points(counts, [d_mo] + list(d_fo), outs, d_elem_g, e_all, d_hit,
+                                                        h_all))
+            c_rows = torch.cat(outs, dim=1).cpu().numpy()
+            same = bool(np.array_equal(c_rows, g_rows_np, equal_nan=True)
+                        and np.array_equal(e_all.cpu().numpy(), g_elem) and np.array_equal(h_all.cpu().numpy(), g_hit))
+            rep.update({"path": "C-ABI pmmg_hip_allgather_points (one ncclAllGather of packed records)",
+                        "ms": round(1e3 * t_c, 3), "gbps": round(nbytes / t_c / 1e9, 1),
+                        "matches_torch_all_gather": same})
+            if same:
+                g_rows_np, g_elem, g_hit = c_rows, e_all.cpu().numpy(), h_all.cpu().numpy()
+        except Exception as e:  # reported; the torch path's results stand
+            rep.update({"path": "torch.distributed all_gather_into_tensor (C-ABI collective failed)",
+                        "c_abi_error": str(e), "ms": round(1e3 * t_torch, 3),
+                        "gbps": round(nbytes / t_torch / 1e9, 1)})
+    else:
+        rep.update({"path": f"torch.distributed all_gather_into_tensor ({ri.backend} rehearsal)",
+                    "ms": round(1e3 * t_torch, 3), "gbps": round(nbytes / t_torch / 1e9, 1)})
+    log(f"[bench r{rank}] all-gather of {nbytes / 1e9:.2f} GB: {rep}")
+    return rep, (g_rows_np, g_elem, g_hit)
 
 
 def split_parity(w, bg, met, fields, new, pclass, shards, gathered, budget_s: float) -> dict:
@@ -785,7 +823,7 @@ def main():
     agg = ranks.aggregate(ri, npts, elapsed, args.steps)
     gather = gathered = None
     if split:
-        gather, gathered = allgather_timing(ri, d_mo, d_fo, d_elem, d_hit, sh, counts, rank)
+        gather, gathered = allgather_timing(ri, ctx, d_mo, d_fo, d_elem, d_hit, sh, counts, rank)
         npts = agg["points_per_step"]  # the whole problem: bytes per point below are per problem point
     ms_per_step = agg["ms_per_step"]
     value = agg["mpts_per_s"]

@@ -314,10 +314,11 @@ int pmmg_hip_tetra_qual(pmmg_hip_ctx *ctx, int np, const double *xyz, int ne,
  * RS = (met_size + sum field_size) rounded up to even.  The module's
  * preferred HBM layout (one 128-byte line per vertex for up to 16 doubles:
  * one gather per vertex instead of one per solution); a shim builds it in the
- * pass that packs MMG5_Point.c.  Supported: at most 16 doubles, no tensor
- * across doubles 8/9 (the order metric, scalar, vector, tensor of BASELINE's
- * aniso configs is), the compiled slot layouts; otherwise 0 is returned and
- * pmmg_hip_set_solutions takes the arrays.  Device records: 16-byte aligned.
+ * pass that packs MMG5_Point.c.  Supported: at most 16 doubles in the
+ * compiled slot layouts (BASELINE's configs: metric, scalar, vector, tensor;
+ * iso metric + scalars); otherwise 0 is returned and pmmg_hip_set_solutions
+ * takes the arrays.  Device records: 16-byte aligned (RS * 8 bytes apart: a
+ * 128-byte-aligned base puts a 16-double record on one cache line).
  * Returns 1/0. */
 int pmmg_hip_set_solutions_packed(pmmg_hip_ctx *ctx, int met_size, int nfield,
                                   const int *field_size, const double *rec, int where);
@@ -350,6 +351,36 @@ int pmmg_hip_compute_wgt_mesh(pmmg_hip_ctx *ctx, int np, const double *xyz, int 
 int pmmg_hip_compute_wgt_faces(pmmg_hip_ctx *ctx, int np, const double *xyz,
                                const int *tetv, int nface, const int *face,
                                int met_size, const double *met, double *wgt);
+
+/* ---- One group split over the GPUs of a node -------------
+ * One process per GPU (ParMmg's MPI ranks; GPU = node-local rank,
+ * src/parmmg.c:121).  Each rank transfers its part of the group's new points
+ * (its own pmmg_hip_locate_interp, against a replicated or halo-sharded
+ * background), then the located element ids, hit codes and interpolated rows
+ * of every part are collected on every rank with one RCCL all-gather over
+ * xGMI.  ParMmg's only process boundary is MPI (src/libparmmg1.c:831); a shim
+ * creates the communicator with MPI:
+ *     char id[PMMG_HIP_COMM_ID_BYTES];
+ *     if (rank == 0) pmmg_hip_comm_unique_id(id);
+ *     MPI_Bcast(id, PMMG_HIP_COMM_ID_BYTES, MPI_BYTE, 0, comm_node);
+ *     pmmg_hip_comm_init(ctx, nranks, rank, id);       (collective)
+ * or hands over an ncclComm_t it owns (pmmg_hip_comm_attach).  RCCL
+ * (librccl.so.1) is loaded at the first of these calls.  Returns 1/0. */
+#define PMMG_HIP_COMM_ID_BYTES 128
+int pmmg_hip_comm_unique_id(void *id);
+int pmmg_hip_comm_init(pmmg_hip_ctx *ctx, int nranks, int rank, const void *id);
+int pmmg_hip_comm_attach(pmmg_hip_ctx *ctx, void *nccl_comm, int nranks, int rank);
+
+/* All-gather of the parts' results (collective over the communicator):
+ * counts[nranks] points per rank (rank order), this rank's part in
+ * rows[s] (slot_size[s] doubles per point: the metric / field rows
+ * pmmg_hip_locate_interp wrote), elem, hit (both optional, NULL on every
+ * rank or on none); outputs rows_all[s], elem_all, hit_all hold the parts
+ * concatenated in rank order (sum counts points).  Device pointers;
+ * returns when the outputs are written.  Returns 1/0. */
+int pmmg_hip_allgather_points(pmmg_hip_ctx *ctx, const int64_t *counts, int nslot, const int *slot_size,
+                              const double *const *rows, double *const *rows_all, const int *elem, int *elem_all,
+                              const int8_t *hit, int8_t *hit_all);
 
 /* Device memory helpers for callers that keep data resident (bench, shims
  * that reuse buffers across iterations). */

@@ -76,6 +76,11 @@ HIP_API = {
                                     P(c_double)]),
     "pmmg_hip_memcpy_h2d": (c_int, [c_void_p, c_void_p, c_void_p, c_int64]),
     "pmmg_hip_memcpy_d2h": (c_int, [c_void_p, c_void_p, c_void_p, c_int64]),
+    "pmmg_hip_comm_unique_id": (c_int, [c_void_p]),
+    "pmmg_hip_comm_init": (c_int, [c_void_p, c_int, c_int, c_void_p]),
+    "pmmg_hip_comm_attach": (c_int, [c_void_p, c_void_p, c_int, c_int]),
+    "pmmg_hip_allgather_points": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                          c_void_p, c_void_p]),
     "pmmg_hip_last_error": (c_char_p, [c_void_p]),
     "pmmg_hip_device_count": (c_int, []),
 }

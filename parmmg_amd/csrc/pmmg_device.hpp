@@ -343,6 +343,7 @@ __device__ __forceinline__ void load6(const double *p, double *m) {
 // stores keep them from displacing the gathered background rows in L2.
 typedef double ntd2 __attribute__((ext_vector_type(2)));
 typedef int nti4 __attribute__((ext_vector_type(4)));
+typedef int nti2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void nt_store(double *p, double v) { __builtin_nontemporal_store(v, p); }
 __device__ __forceinline__ void nt_store2(double *p, double a, double b) {
   ntd2 v = {a, b};

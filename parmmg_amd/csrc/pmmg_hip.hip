@@ -51,6 +51,7 @@
 #include "pmmg_fallback.hpp"
 #include "pmmg_snapshot.hpp"
 #include "pmmg_quality.hpp"
+#include "pmmg_comm.hpp"
 
 using namespace pmmg;
 
@@ -64,17 +65,21 @@ typedef void (*VolFn)(Bg, const Frame *, const unsigned long long *, int, const 
 
 struct LayoutEntry {
   int c[6];
-  VolFn fn;        // one array per solution (the reference's layout)
-  VolFn fn_packed; // packed per-vertex records (null: layout not packable)
+  VolFn fn;         // one array per solution (the reference's layout)
+  VolFn fn_packed;  // packed per-vertex records, one pass (null: layout not packable)
+  VolFn fn_packed2; // the same in two passes over the record halves (null: not splittable)
 };
 
-template <int A, int B, int C, int D, int E, int F>
+template <int NP, int A, int B, int C, int D, int E, int F>
 constexpr VolFn packed_fn() {
-  if constexpr (PackedLayout<A, B, C, D, E, F>::valid()) return k_vol<true, A, B, C, D, E, F>;
+  using L = PackedLayout<A, B, C, D, E, F>;
+  if constexpr (L::valid() && L::passes_ok(NP)) return k_vol<NP, A, B, C, D, E, F>;
   else return nullptr;
 }
 
-#define PMMG_LAYOUT(a, b, c, d, e, f) {{a, b, c, d, e, f}, k_vol<false, a, b, c, d, e, f>, packed_fn<a, b, c, d, e, f>()}
+#define PMMG_LAYOUT(a, b, c, d, e, f)                                                                    \
+  {{a, b, c, d, e, f}, k_vol<0, a, b, c, d, e, f>, packed_fn<1, a, b, c, d, e, f>(),                    \
+   packed_fn<2, a, b, c, d, e, f>()}
 // common slot layouts (metric first): aniso metric + scalar/vector/tensor
 // (BASELINE cfg3/cfg4, libexamples cube-solphys.sol), iso metric + scalars
 // (cfg2, cfg5), metric only; anything else runs the runtime-layout variant
@@ -86,16 +91,21 @@ const LayoutEntry kLayouts[] = {
 };
 #undef PMMG_LAYOUT
 
-VolFn pick_layout(const Slots &S) {
+// passes: packed records' gather passes (1 or 2; the other is taken when the
+// layout allows only it)
+VolFn pick_layout(const Slots &S, int passes = 1) {
   for (const LayoutEntry &e : kLayouts) {
     int n = 0;
     while (n < 6 && e.c[n] > 0) n++;
     if (n != S.n) continue;
     bool ok = true;
     for (int j = 0; j < n; j++) ok = ok && (S.s[j].code == e.c[j]);
-    if (ok) return S.rec ? e.fn_packed : e.fn;
+    if (!ok) continue;
+    if (!S.rec) return e.fn;
+    VolFn a = passes == 2 ? e.fn_packed2 : e.fn_packed, b = passes == 2 ? e.fn_packed : e.fn_packed2;
+    return a ? a : b;
   }
-  return S.rec ? nullptr : k_vol<false, -1, 0, 0, 0, 0, 0>;
+  return S.rec ? nullptr : k_vol<0, -1, 0, 0, 0, 0, 0>;
 }
 
 
@@ -163,6 +173,10 @@ struct pmmg_hip_ctx {
   int srf_solo = -1; // the surface branch waits for the seed grid: -1 in calls of >= kSmallGroup queries (r04zo,
                      // cfg4: the seed grid ran at 455 instead of 261 us beside k_bdy; step 4.24 -> 4.13 ms,
                      // Mmg-like 5.01 -> 4.93, shuffled =), 1 always, 0 never (PMMG_HIP_SRFSOLO)
+  // the seed grids left clean by the previous call (its last kernels refill
+  // them while the other stream finishes): k_reset skips what is clean
+  void *grid_clean_p = nullptr, *sgrid_clean_p = nullptr;
+  long long grid_clean_n = 0, sgrid_clean_n = 0;
   DevBuf qs;                              // volume query coordinates in processing order (Morton path)
   DevBuf cls_cnt;                         // per-block class counts (surface list compaction)
   DevBuf oflag;                           // the coherence test's {sorted, bin_bits} on the device
@@ -193,6 +207,8 @@ struct pmmg_hip_ctx {
   int verbose = 0; // PMMG_HIP_VERBOSE: host-mode transfer timings on stderr
   int tpc = 8;        // background tetra per volume seed cell (PMMG_HIP_TPC)
   int seed_lanes = 4;  // sampled tetra per seed run of 4 records (PMMG_HIP_SEEDLANES, 1..4)
+  int seed_v0 = 0;     // measurement build, PMMG_HIP_SEEDV0=1: a sample's first vertex instead of its centroid
+  int pack_passes = 1; // packed records gathered in 1 or 2 passes over the record (PMMG_HIP_PACKPASS)
   int bbox_stride = 64;  // the frame's bbox samples np / n vertices (PMMG_HIP_BBOX; r03o: 64 instead of 16 and
   int hist_stride = 256; // 256 instead of 64 for the axis histograms: preparation -0.15 ms at cfg4, same walks)
   int bdy_bpx = 512;     // k_bdy blocks per XCD at most (PMMG_HIP_BDYBPX)
@@ -237,6 +253,12 @@ struct pmmg_hip_ctx {
   // a groups call leaves this context's background and solutions as they were
   std::vector<pmmg_hip_ctx *> lanes;
   bool borrowed_streams = false; // a lane 0: stream / stream2 belong to its parent
+  // the split of a group over the node's GPUs (pmmg_comm.hpp): an RCCL
+  // communicator, owned (pmmg_hip_comm_init) or the caller's (attach)
+  ncclComm_t comm = nullptr;
+  bool comm_owned = false;
+  int comm_rank = 0, comm_size = 0;
+  DevBuf ag_send, ag_recv, ag_off;
   int group_lanes = 4; // PMMG_HIP_GROUP_LANES (r04i, 10 cfg2-size groups: 1 / 2 / 4 lanes 0.165 / 0.125 / 0.108 ms per group)
   struct Pool *lane_pool = nullptr; // host threads enqueueing the other lanes' groups
   int lane_streams = 2; // a group lane's streams: 2 = its own surface stream, 1 = the surface branch on the
@@ -531,6 +553,14 @@ __global__ void k_fill64(unsigned long long *a, long long n, unsigned long long 
   for (long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x; j < n; j += (long long)gridDim.x * blockDim.x)
     a[j] = v;
 }
+__global__ void k_fill32(int *a, long long n, int v) {
+  for (long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x; j < n; j += (long long)gridDim.x * blockDim.x)
+    a[j] = v;
+}
+// seed grids of at least this many cells are refilled at the end of the call
+// that used them; smaller ones (a small group's chain of launches is its
+// cost) are cleared by k_reset
+constexpr long long kRefillCells = 1LL << 20;
 
 static int env_int(const char *name, int def) { // positive values only
   const char *e = getenv(name);
@@ -586,6 +616,7 @@ static pmmg_hip_ctx *create_ctx(int device, int options, bool srf_prio, pmmg_hip
   // test-only path selection (tests/test_gpu_hits.py, tests/test_gpu_parity.py)
   c->fanmax = env_int("PMMG_HIP_FANMAX", c->fanmax);
   c->srf_g = std::min(1024, env_int("PMMG_HIP_SRFG", 0));
+  c->pack_passes = env_int("PMMG_HIP_PACKPASS", c->pack_passes) == 2 ? 2 : 1; // packed records: gather passes
   c->bg.fanmax = c->fanmax; // every kernel's Bg copy carries it
   c->filter_steps = c->filter_steps < c->maxstep ? c->filter_steps : c->maxstep;
   if (const char *e = getenv("PMMG_HIP_FILTER_STEPS"))
@@ -593,6 +624,7 @@ static pmmg_hip_ctx *create_ctx(int device, int options, bool srf_prio, pmmg_hip
 #ifdef PMMG_HIP_MEASURE
   // A/B switches of the measurement build (libpmmg_hip_measure.so, tools/)
   c->seed_lanes = std::min(4, env_int("PMMG_HIP_SEEDLANES", c->seed_lanes));
+  c->seed_v0 = env_int("PMMG_HIP_SEEDV0", 0) == 1;
   c->bbox_stride = env_int("PMMG_HIP_BBOX", c->bbox_stride);
   c->hist_stride = env_int("PMMG_HIP_HIST", c->hist_stride);
   c->bdy_dyn = env_int("PMMG_HIP_BDYDYN", 2) == 1;
@@ -646,8 +678,10 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
     release(k.met);
     for (auto &b : k.f) release(b);
   }
-  DevBuf *cb[] = {&c->carry_dsrc, &c->carry_need, &c->carry_ids, &c->carry_cnt, &c->carry_rows, &c->carry_bc};
+  DevBuf *cb[] = {&c->carry_dsrc, &c->carry_need, &c->carry_ids, &c->carry_cnt, &c->carry_rows, &c->carry_bc,
+                  &c->ag_send, &c->ag_recv, &c->ag_off};
   for (DevBuf *b : cb) release(*b);
+  if (c->comm && c->comm_owned && rccl().ok) (void)rccl().commDestroy(c->comm);
   if (!c->borrowed_streams) {
     if (c->stream2 && c->stream2 != c->stream) (void)hipStreamDestroy(c->stream2);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1105,7 +1139,7 @@ int pmmg_hip_set_solutions_packed(pmmg_hip_ctx *c, int met_size, int nfield, con
   }
   if (K == 0 || !packed_supported(met_size, nfield, field_size)) {
     set_err(c, "set_solutions_packed: slot layout not supported by the packed records (at most 16 doubles, a "
-               "tensor not across doubles 8 / 9, a compiled layout); use pmmg_hip_set_solutions");
+               "compiled layout); use pmmg_hip_set_solutions");
     return 0;
   }
   if (where == PMMG_HIP_DEVICE && ((uintptr_t)rec & 15)) {
@@ -1290,7 +1324,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
       off += S.s[j].code;
     }
   }
-  const VolFn vol_fn = pick_layout(S);
+  const VolFn vol_fn = pick_layout(S, c->pack_passes);
   if (!vol_fn) {
     set_err(c, "locate_interp: no packed-record kernel for this slot layout");
     return 0;
@@ -1333,8 +1367,14 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     hipLaunchKernelGGL(k_coherence, dim3(1), dim3(kBlock), 0, sb, xyz_new, np_new, (int *)c->oflag.p, force,
                        c->bin_bits);
   }
-  hipLaunchKernelGGL(k_reset, dim3(blocks_for(ng > nsg ? ng : nsg, 2048)), dim3(kBlock), 0, s, fr, st, grid, ng,
-                     sgrid, nsg, (int *)c->oflag.p, force, c->bin_bits);
+  // seed grids: cleared here unless the previous call left them clean (a
+  // large grid is refilled at the end of the call that used it, beside the
+  // other stream's tail: r05, cfg4 k_reset 32 us -> the stats only)
+  const long long ng_clr = (c->grid.p == c->grid_clean_p && ng <= c->grid_clean_n) ? 0 : ng;
+  const long long nsg_clr = (c->sgrid.p == c->sgrid_clean_p && nsg <= c->sgrid_clean_n) ? 0 : nsg;
+  c->grid_clean_n = c->sgrid_clean_n = 0; // dirty until this call's refill is enqueued
+  hipLaunchKernelGGL(k_reset, dim3(blocks_for(ng_clr > nsg_clr ? ng_clr : nsg_clr, 2048)), dim3(kBlock), 0, s, fr, st,
+                     grid, ng_clr, sgrid, nsg_clr, (int *)c->oflag.p, force, c->bin_bits);
   // bbox (its last block finalises the frame), the seed grid's axis maps
   hipLaunchKernelGGL(k_bbox, dim3(blocks_for(bg.np / c->bbox_stride + 1, 256)), dim3(kBlock), 0, s, bg.xyz, bg.np, fr,
                      c->bbox_stride, g, gs, gb);
@@ -1359,7 +1399,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   {
     const long long nsamp = ng < bg.ne ? ng : bg.ne;
     hipLaunchKernelGGL(k_seed_vol, dim3((blocks_for(nsamp, 8192) + 7) & ~7), dim3(kBlock), 0, s, bg, fr, grid, g,
-                       nsamp, c->seed_lanes);
+                       nsamp, c->seed_lanes, c->seed_v0);
   }
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[EV_PREP], s));
@@ -1431,6 +1471,11 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
                        FbInit{(int *)c->bbest.p});
     launch_bdy_fallbacks(c, sb, S, xyz_new, elem_out, hit_out);
     HIPCK(c, hipGetLastError());
+    if (nsg >= kRefillCells) { // the surface grid refilled for the next call (see k_reset above)
+      hipLaunchKernelGGL(k_fill32, dim3(blocks_for(nsg, 2048)), dim3(kBlock), 0, sb, sgrid, nsg, INT_MAX);
+      c->sgrid_clean_p = c->sgrid.p;
+      c->sgrid_clean_n = nsg;
+    }
   }
   HIPCK(c, hipEventRecord(c->ev[EV_BDY1], sb));
 
@@ -1458,6 +1503,12 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   launch_vol_fallbacks(c, S, xyz_new, elem_out, hit_out);
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[EV_JOIN], s));
+  if (ng >= kRefillCells) { // the volume seed grid refilled for the next call, beside the surface stream's tail
+    hipLaunchKernelGGL(k_fill64, dim3(blocks_for(ng, 2048)), dim3(kBlock), 0, s, grid, ng, ~0ULL);
+    HIPCK(c, hipGetLastError());
+    c->grid_clean_p = c->grid.p;
+    c->grid_clean_n = ng;
+  }
   HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_BDY1], 0));
   HIPCK(c, hipEventRecord(c->ev[EV_END], s));
   c->pending = true;
@@ -1972,6 +2023,140 @@ int pmmg_hip_memcpy_h2d(pmmg_hip_ctx *c, void *dst, const void *src, int64_t byt
   if (!snap_join(c)) return 0;
   if (!h2d(c, dst, src, (size_t)bytes, c->stream)) return 0;
   HIPCK(c, hipStreamSynchronize(c->stream));
+  return 1;
+}
+
+// ---- the split of a group over the node's GPUs (pmmg_comm.hpp)
+
+int pmmg_hip_comm_unique_id(void *id) {
+  if (!id) return 0;
+  Rccl &R = rccl();
+  if (!R.ok) {
+    fprintf(stderr, "[parmmg_hip] comm_unique_id: %s\n", R.why);
+    return 0;
+  }
+  ncclUniqueId u;
+  const ncclResult_t e = R.getUniqueId(&u);
+  if (e != ncclSuccess) {
+    fprintf(stderr, "[parmmg_hip] ncclGetUniqueId: %s\n", R.errorString(e));
+    return 0;
+  }
+  memcpy(id, &u, sizeof(u));
+  return 1;
+}
+
+static void comm_release(pmmg_hip_ctx *c) {
+  if (c->comm && c->comm_owned && rccl().ok) (void)rccl().commDestroy(c->comm);
+  c->comm = nullptr;
+  c->comm_owned = false;
+  c->comm_rank = c->comm_size = 0;
+}
+
+int pmmg_hip_comm_init(pmmg_hip_ctx *c, int nranks, int rank, const void *id) {
+  if (!c) return 0;
+  HIPCK(c, hipSetDevice(c->device));
+  if (!snap_join(c)) return 0;
+  if (nranks < 1 || rank < 0 || rank >= nranks || !id) {
+    set_err(c, "comm_init: invalid arguments (nranks=%d rank=%d)", nranks, rank);
+    return 0;
+  }
+  Rccl &R = rccl();
+  if (!R.ok) {
+    set_err(c, "comm_init: %s", R.why);
+    return 0;
+  }
+  comm_release(c);
+  ncclUniqueId u;
+  memcpy(&u, id, sizeof(u));
+  ncclComm_t comm = nullptr;
+  const ncclResult_t e = R.commInitRank(&comm, nranks, u, rank);
+  if (e != ncclSuccess) {
+    set_err(c, "ncclCommInitRank(%d of %d): %s", rank, nranks, R.errorString(e));
+    return 0;
+  }
+  c->comm = comm;
+  c->comm_owned = true;
+  c->comm_rank = rank;
+  c->comm_size = nranks;
+  return 1;
+}
+
+int pmmg_hip_comm_attach(pmmg_hip_ctx *c, void *comm, int nranks, int rank) {
+  if (!c) return 0;
+  if (nranks < 1 || rank < 0 || rank >= nranks || !comm) {
+    set_err(c, "comm_attach: invalid arguments (nranks=%d rank=%d)", nranks, rank);
+    return 0;
+  }
+  if (!rccl().ok) {
+    set_err(c, "comm_attach: %s", rccl().why);
+    return 0;
+  }
+  comm_release(c);
+  c->comm = (ncclComm_t)comm;
+  c->comm_owned = false;
+  c->comm_rank = rank;
+  c->comm_size = nranks;
+  return 1;
+}
+
+int pmmg_hip_allgather_points(pmmg_hip_ctx *c, const int64_t *counts, int nslot, const int *slot_size,
+                              const double *const *rows, double *const *rows_all, const int *elem, int *elem_all,
+                              const int8_t *hit, int8_t *hit_all) {
+  if (!c) return 0;
+  HIPCK(c, hipSetDevice(c->device));
+  if (!snap_join(c)) return 0;
+  if (!c->comm) {
+    set_err(c, "allgather_points: no communicator (pmmg_hip_comm_init / pmmg_hip_comm_attach)");
+    return 0;
+  }
+  const int N = c->comm_size;
+  if (!counts || nslot < 0 || nslot > kMaxSlot || (nslot > 0 && (!slot_size || !rows || !rows_all)) ||
+      (!elem) != (!elem_all) || (!hit) != (!hit_all)) {
+    set_err(c, "allgather_points: invalid arguments (nslot=%d)", nslot);
+    return 0;
+  }
+  AgSlots S{};
+  S.n = nslot;
+  for (int j = 0; j < nslot; j++) {
+    if (slot_size[j] < 1 || slot_size[j] > 6 || !rows_all[j] || (counts[c->comm_rank] > 0 && !rows[j])) {
+      set_err(c, "allgather_points: slot %d (size %d) invalid", j, slot_size[j]);
+      return 0;
+    }
+    S.in[j] = rows[j];
+    S.out[j] = rows_all[j];
+    S.size[j] = slot_size[j];
+    S.K += slot_size[j];
+  }
+  std::vector<long long> off((size_t)N + 1, 0);
+  long long maxn = 0;
+  for (int r = 0; r < N; r++) {
+    if (counts[r] < 0) {
+      set_err(c, "allgather_points: counts[%d] = %lld", r, (long long)counts[r]);
+      return 0;
+    }
+    off[r + 1] = off[r] + counts[r];
+    maxn = std::max(maxn, (long long)counts[r]);
+  }
+  const long long R = 8LL * S.K + 8, n = counts[c->comm_rank];
+  if (maxn == 0) return 1;
+  if (!ensure(c, c->ag_send, (size_t)(R * maxn)) || !ensure(c, c->ag_recv, (size_t)(R * maxn * N)) ||
+      !ensure(c, c->ag_off, sizeof(long long) * off.size()))
+    return 0;
+  hipStream_t s = c->stream;
+  HIPCK(c, hipMemcpyAsync(c->ag_off.p, off.data(), sizeof(long long) * off.size(), hipMemcpyHostToDevice, s));
+  if (n > 0)
+    hipLaunchKernelGGL(k_ag_pack, dim3(blocks_for(n, 4096)), dim3(kBlock), 0, s, S, elem, hit, n, (char *)c->ag_send.p);
+  HIPCK(c, hipGetLastError());
+  const ncclResult_t e =
+      rccl().allGather(c->ag_send.p, c->ag_recv.p, (size_t)(R * maxn), ncclInt8, c->comm, s);
+  if (e != ncclSuccess) {
+    set_err(c, "ncclAllGather: %s", rccl().errorString(e));
+    return 0;
+  }
+  hipLaunchKernelGGL(k_ag_unpack, dim3(blocks_for(off[N], 8192)), dim3(kBlock), 0, s, S, (const char *)c->ag_recv.p,
+                     maxn, N, (const long long *)c->ag_off.p, elem_all, hit_all);
+  HIPCK(c, hipGetLastError());
+  HIPCK(c, hipStreamSynchronize(s));
   return 1;
 }
 

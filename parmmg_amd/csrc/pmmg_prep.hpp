@@ -168,24 +168,47 @@ __device__ __forceinline__ int quant(double x, const Frame *fr, int d) {
   return __double2int_rn(t);
 }
 
-// Two vertices per thread when xyz is 16-byte aligned: three 16-byte loads
-// and three 8-byte stores (the lanes of a wave stream 3 KiB in, 1.5 KiB out)
-// instead of six single-double loads and six int stores
+// The fixed-point copy is an elementwise map of the coordinate stream: with
+// 3 ints per row, xq[e] = quant(xyz[e], axis e % 3) for every double e, so
+// the kernel streams pairs of doubles in (one 16-byte load per lane, every
+// wave-instruction one contiguous KiB) and pairs of ints out (8 bytes per
+// lane, 512 contiguous bytes), kQuantU pairs in flight per lane.  (r04: two
+// whole vertices per lane, 48-byte strided pieces: 175 us at cfg4, 3.5 TB/s.)
+constexpr int kQuantU = 4;
 __global__ __launch_bounds__(kBlock) void k_quantize(const double *xyz, long long np, const Frame *fr, int *xq) {
   const long long nth = (long long)gridDim.x * blockDim.x;
   if (kXqStride == 3 && ((uintptr_t)xyz & 15) == 0 && ((uintptr_t)xq & 7) == 0) {
-    const long long npair = np / 2;
-    for (long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x; j < npair; j += nth) {
-      const ntd2 *src = reinterpret_cast<const ntd2 *>(xyz) + 3 * j;
-      const ntd2 a = __builtin_nontemporal_load(src), b = __builtin_nontemporal_load(src + 1),
-                 c = __builtin_nontemporal_load(src + 2);
-      int2 *dst = reinterpret_cast<int2 *>(xq) + 3 * j;
-      dst[0] = make_int2(quant(a.x, fr, 0), quant(a.y, fr, 1));
-      dst[1] = make_int2(quant(b.x, fr, 2), quant(b.y, fr, 0));
-      dst[2] = make_int2(quant(c.x, fr, 1), quant(c.y, fr, 2));
+    const double qs = fr->qs, qc0 = fr->qc[0], qc1 = fr->qc[1], qc2 = fr->qc[2];
+    const double lim = 2.0 * kQuantHalf;
+    auto q = [&](double x, unsigned d) {
+      double t = (x - (d == 0 ? qc0 : (d == 1 ? qc1 : qc2))) * qs;
+      t = t > lim ? lim : (t < -lim ? -lim : t);
+      return __double2int_rn(t);
+    };
+    const long long n = 3 * np, npair = n / 2;
+    const ntd2 *src = reinterpret_cast<const ntd2 *>(xyz);
+    nti2 *dst = reinterpret_cast<nti2 *>(xq);
+    for (long long p0 = blockIdx.x * (long long)blockDim.x * kQuantU + threadIdx.x; p0 < npair;
+         p0 += nth * kQuantU) {
+      ntd2 v[kQuantU];
+#pragma unroll
+      for (int u = 0; u < kQuantU; u++) {
+        const long long p = p0 + (long long)u * blockDim.x;
+        if (p < npair) v[u] = __builtin_nontemporal_load(src + p);
+      }
+#pragma unroll
+      for (int u = 0; u < kQuantU; u++) {
+        const long long p = p0 + (long long)u * blockDim.x;
+        if (p < npair) {
+          const unsigned d0 = (unsigned)((2 * p) % 3); // 64-bit: 3 * np doubles may pass 2^31
+          const unsigned d1 = d0 == 2u ? 0u : d0 + 1u;
+          const nti2 w = {q(v[u].x, d0), q(v[u].y, d1)};
+          __builtin_nontemporal_store(w, dst + p);
+        }
+      }
     }
-    if (blockIdx.x == 0 && threadIdx.x < 3 && (np & 1))
-      xq[3 * (np - 1) + threadIdx.x] = quant(xyz[3 * (np - 1) + threadIdx.x], fr, (int)threadIdx.x);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && (n & 1))
+      xq[n - 1] = q(xyz[n - 1], (unsigned)((n - 1) % 3));
     return;
   }
   for (long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x; j < 3 * np; j += nth)
@@ -325,7 +348,7 @@ constexpr unsigned long long kSeedIdMask = (1ULL << 29) - 1; // ids below 2^29 (
 // quantile map (Frame::adaptive) goes through seed_pos.
 constexpr int kSeedBatch = 3;
 __global__ __launch_bounds__(kBlock) void k_seed_vol(Bg bg, Frame *fr, unsigned long long *cell, int g,
-                                                     long long nsamp, int lanes) {
+                                                     long long nsamp, int lanes, int v0only) {
   constexpr int R = kSeedRun, B = kSeedBatch;
   __shared__ int smin;
   if (threadIdx.x == 0) smin = INT_MAX;
@@ -372,7 +395,11 @@ __global__ __launch_bounds__(kBlock) void k_seed_vol(Bg bg, Frame *fr, unsigned 
       ok[b] = ok[b] && tv[b].x > 0;
 #pragma unroll
       for (int d = 0; d < 3; d++) sq[b][d] = 0;
-      if (ok[b]) {
+      if (ok[b] && v0only) { // measurement build (PMMG_HIP_SEEDV0=1): the first vertex stands for the centroid
+        const int *q0 = bg.xq + kXqStride * (size_t)(tv[b].x - 1);
+#pragma unroll
+        for (int d = 0; d < 3; d++) sq[b][d] = 4LL * q0[d];
+      } else if (ok[b]) {
         const int *q0 = bg.xq + kXqStride * (size_t)(tv[b].x - 1), *q1 = bg.xq + kXqStride * (size_t)(tv[b].y - 1);
         const int *q2 = bg.xq + kXqStride * (size_t)(tv[b].z - 1), *q3 = bg.xq + kXqStride * (size_t)(tv[b].w - 1);
         int a0[3], a1[3], a2[3], a3[3];

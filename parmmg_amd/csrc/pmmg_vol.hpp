@@ -586,7 +586,7 @@ struct VolShared {
   BlockStats bs;
   union {
     float slots[12 * 64]; // walk: the vertex slots [slot*3 + dim][lane]
-    double img[8 * 64]; // interpolation: 64 rows of up to 6 doubles, or 64 x 8 doubles of packed records
+    double img[16 * 64]; // interpolation: 64 rows of up to 6 doubles, or 64 packed records of up to 16 doubles
   } u;
 };
 
@@ -702,25 +702,37 @@ __device__ __forceinline__ void vol_slot(const Slot &sl, bool act, const int4 &v
 //
 // With packed per-vertex records (pmmg_hip_set_solutions_packed: the slots'
 // rows back to back, [slot 0 | slot 1 | ...], RS doubles per vertex) a
-// vertex's whole solution is one 128-byte line for K <= 16 doubles: the
-// interpolation gathers, per vertex of the wave's 64 queries, 64 records in
-// one or two passes of 8 doubles (64 B) per record — the 64 lanes of a load
-// instruction cover 16 records — into a 4 KiB LDS image; each lane then takes
-// its doubles of that pass and accumulates every slot component living in it
-// (an iso slot component by component, a tensor slot whole: it must not
-// straddle the 8-double pass boundary).  One slot-independent gather per
-// vertex instead of one per slot.
+// vertex's whole solution is one record — one 128-byte line for K <= 16
+// doubles (cfg3 / cfg4: 16) — so the interpolation gathers, per vertex of the
+// wave's 64 queries, the 64 records in RS / 2 load instructions of 16 bytes
+// per lane, each instruction covering whole records (one line access per
+// record and vertex, against ~4.6 for the four separate arrays' rows), into
+// an LDS image; each lane reads its own record's doubles back from it and
+// accumulates every slot in the reference's order.
+//
+// NP passes over the record (NP = 1: the whole record per gather, every
+// slot's accumulator live over the four vertices; NP = 2: the record's two
+// halves in turn, a slot's accumulator live only over the passes holding its
+// components, a tensor never across the halves).  r04h ran NP = 2 with 8-byte
+// image reads at a 64-byte lane stride (16-way bank conflicts); r05 swizzles
+// the image so that the cooperative writes and each lane's reads of its own
+// record are conflict-free: piece k of record r sits at
+// PP r + (k ^ ((r >> SH) & (PP - 1))) (PP pieces of 16 bytes per record and
+// pass, a power of two; SH chosen so that 16 consecutive lanes reading piece
+// k of their records hit 16 distinct 16-byte bank groups).
 template <int C0, int C1, int C2, int C3, int C4, int C5>
 struct PackedLayout {
   static constexpr int c[6] = {C0 > 0 ? C0 : 0, C1, C2, C3, C4, C5};
   static constexpr int K = c[0] + c[1] + c[2] + c[3] + c[4] + c[5];
-  static constexpr int RS = (K + 1) & ~1;              // record stride (doubles)
-  static constexpr int NPASS = RS <= 8 ? 1 : 2;        // passes of at most 8 doubles per record
+  static constexpr int RS = (K + 1) & ~1; // record stride (doubles)
   static constexpr int off(int s) { return s == 0 ? 0 : off(s - 1) + c[s - 1]; }
-  static constexpr bool valid() {                      // tensors inside one pass, K <= 16
-    if (C0 < 0 || K == 0 || RS > 16) return false;
+  static constexpr bool valid() { return C0 >= 0 && K > 0 && RS <= 16; }
+  // NP passes possible: RS / 2 pieces split evenly, no tensor across a pass boundary
+  static constexpr bool passes_ok(int np) {
+    if ((RS / 2) % np) return false;
+    const int pw = RS / np; // doubles per pass
     for (int s = 0; s < 6; s++)
-      if (c[s] == 6 && NPASS == 2 && off(s) < 8 && off(s) + 6 > 8) return false;
+      if (c[s] == 6 && off(s) / pw != (off(s) + 5) / pw) return false;
     return true;
   }
 };
@@ -742,23 +754,38 @@ struct SlotAcc {
   }
 };
 
-// slot s's components that live in pass `pass` (record doubles [8 pass, 8 pass + 8))
-template <class L, int S, int C>
-__device__ __forceinline__ void packed_take(SlotAcc<C> &a, int pass, int i, double ph, const double *mine) {
+template <int PP>
+__device__ __forceinline__ constexpr int packed_swizzle_shift() {
+  return PP >= 8 ? 1 : (PP == 4 ? 2 : (PP == 2 ? 3 : 0));
+}
+template <int PP>
+__device__ __forceinline__ int packed_pos(int r, int k) {
+  if constexpr ((PP & (PP - 1)) == 0 && PP > 1) return PP * r + (k ^ ((r >> packed_swizzle_shift<PP>()) & (PP - 1)));
+  else return PP * r + k;
+}
+// double j (of this pass's PW = 2 PP doubles) of this lane's record in the image
+template <int PP>
+__device__ __forceinline__ double packed_dbl(const double *img, int lane, int j) {
+  return img[2 * packed_pos<PP>(lane, j >> 1) + (j & 1)];
+}
+
+// slot S's components of vertex i that live in pass `pass`, read from the
+// image as they are needed (only one slot's pieces in registers at a time)
+template <class L, int NP, int S, int C>
+__device__ __forceinline__ void packed_take(SlotAcc<C> &a, int pass, int i, double ph, const double *img, int lane) {
   if constexpr (C > 0) {
-    constexpr int o = L::off(S);
-    const int lo = 8 * pass;
+    constexpr int o = L::off(S), PW = L::RS / NP, PP = PW / 2;
     if constexpr (C == 6) {
-      if (o / 8 == pass || L::NPASS == 1) {
+      if (o / PW == pass) {
         double m[6];
 #pragma unroll
-        for (int q = 0; q < 6; q++) m[q] = mine[o - lo + q];
+        for (int q = 0; q < 6; q++) m[q] = packed_dbl<PP>(img, lane, o + q - PW * pass);
         a.ani(i, ph, m);
       }
     } else {
 #pragma unroll
       for (int q = 0; q < C; q++)
-        if ((o + q) / 8 == pass || L::NPASS == 1) a.iso(i, ph, q, mine[o + q - lo]);
+        if ((o + q) / PW == pass) a.iso(i, ph, q, packed_dbl<PP>(img, lane, o + q - PW * pass));
     }
   }
 }
@@ -776,36 +803,21 @@ __device__ __forceinline__ void packed_store(const Slot &sl, SlotAcc<C> &a, doub
   }
 }
 
-// slot S's components in pass `pass` are accumulated there; the slot is
-// finished (stored) after the pass holding its last component
-template <class L, int S, int C>
-__device__ __forceinline__ constexpr int last_pass() {
-  return L::NPASS == 1 ? 0 : (L::off(S) + C - 1) / 8;
-}
-template <class L, int S, int C>
-__device__ __forceinline__ constexpr int first_pass() {
-  return L::NPASS == 1 ? 0 : L::off(S) / 8;
-}
-
-template <class L, int S, int C>
-__device__ __forceinline__ void packed_pass_slot(const Slots &Sl, SlotAcc<C> &a, int pass, int i, double ph,
-                                                 const double *mine, double *img, const Sink &k, bool store) {
+// slot S is finished (stored) after the pass holding its last component
+template <class L, int NP, int S, int C>
+__device__ __forceinline__ void packed_finish(const Slots &Sl, SlotAcc<C> &a, int pass, double *img, const Sink &k) {
   if constexpr (C > 0) {
-    if (pass < first_pass<L, S, C>() || pass > last_pass<L, S, C>()) return;
-    if (!store) packed_take<L, S>(a, pass, i, ph, mine);
-    else if (pass == last_pass<L, S, C>()) packed_store<C>(Sl.s[S], a, img, k);
+    constexpr int PW = L::RS / NP;
+    if (pass == (L::off(S) + C - 1) / PW) packed_store<C>(Sl.s[S], a, img, k);
   }
 }
 
-template <int C0, int C1, int C2, int C3, int C4, int C5>
+template <int NP, int C0, int C1, int C2, int C3, int C4, int C5>
 __device__ __forceinline__ void vol_interp_packed(const Slots &S, bool acc, const VolLoc &loc, double *img,
                                                   const Sink &k) {
   using L = PackedLayout<C0, C1, C2, C3, C4, C5>;
-  constexpr int PW = L::NPASS == 1 ? L::RS : 8; // doubles per record and pass
-  constexpr int PR = PW / 2;                     // 16-byte pieces per record and pass
+  constexpr int PW = L::RS / NP, PP = PW / 2; // doubles / 16-byte pieces per record and pass
   const int lane = __lane_id();
-  // pass-major: only the slots living in the current pass hold accumulators
-  // (fewer live registers than vertex-major over the whole record)
   SlotAcc<C0> a0;
   SlotAcc<C1> a1;
   SlotAcc<C2> a2;
@@ -816,45 +828,53 @@ __device__ __forceinline__ void vol_interp_packed(const Slots &S, bool acc, cons
     a0.ok = a1.ok = a2.ok = a3.ok = a4.ok = a5.ok = false;
   }
   const double2 *rec = reinterpret_cast<const double2 *>(S.rec);
+  double2 *img2 = reinterpret_cast<double2 *>(img);
 #pragma unroll
-  for (int pass = 0; pass < L::NPASS; pass++) {
-#pragma unroll
+  for (int pass = 0; pass < NP; pass++) {
+    // the vertex loop is not unrolled: unrolled, the four vertices' copies of
+    // a tensor slot's MMG5_invmat temporaries pushed the kernel past 128 VGPRs
+#pragma unroll 1
     for (int i = 0; i < 4; i++) {
       const int myv = sel4(loc.v, i);
-      const double ph = loc.phi[i];
-      // piece p = 64t + lane of the image: record p / PR, piece p % PR
-      double2 b[PR];
+      const double ph = i == 0 ? loc.phi[0] : (i == 1 ? loc.phi[1] : (i == 2 ? loc.phi[2] : loc.phi[3]));
+      // piece p = 64t + lane of the wave's records: record p / PP, piece p % PP
+      double2 b[PP];
 #pragma unroll
-      for (int t = 0; t < PR; t++) {
-        const int p = 64 * t + lane, r = p / PR, k = p - PR * r;
+      for (int t = 0; t < PP; t++) {
+        const int p = 64 * t + lane, r = p / PP, kk = p - PP * r;
         const int v = __shfl(myv, r);
-        b[t] = rec[(size_t)(L::RS / 2) * (v - 1) + 4 * pass + k];
+        b[t] = rec[(size_t)(L::RS / 2) * (v - 1) + PP * pass + kk];
       }
 #pragma unroll
-      for (int t = 0; t < PR; t++) reinterpret_cast<double2 *>(img)[64 * t + lane] = b[t];
+      for (int t = 0; t < PP; t++) {
+        const int p = 64 * t + lane, r = p / PP, kk = p - PP * r;
+        img2[packed_pos<PP>(r, kk)] = b[t];
+      }
       wait_lgkm();
       __builtin_amdgcn_wave_barrier();
-      const double *mine = img + PW * lane;
-      packed_pass_slot<L, 0>(S, a0, pass, i, ph, mine, img, k, false);
-      packed_pass_slot<L, 1>(S, a1, pass, i, ph, mine, img, k, false);
-      packed_pass_slot<L, 2>(S, a2, pass, i, ph, mine, img, k, false);
-      packed_pass_slot<L, 3>(S, a3, pass, i, ph, mine, img, k, false);
-      packed_pass_slot<L, 4>(S, a4, pass, i, ph, mine, img, k, false);
-      packed_pass_slot<L, 5>(S, a5, pass, i, ph, mine, img, k, false);
+      packed_take<L, NP, 0>(a0, pass, i, ph, img, lane);
+      packed_take<L, NP, 1>(a1, pass, i, ph, img, lane);
+      packed_take<L, NP, 2>(a2, pass, i, ph, img, lane);
+      packed_take<L, NP, 3>(a3, pass, i, ph, img, lane);
+      packed_take<L, NP, 4>(a4, pass, i, ph, img, lane);
+      packed_take<L, NP, 5>(a5, pass, i, ph, img, lane);
       wait_lgkm();
       __builtin_amdgcn_wave_barrier(); // every lane has read its record: the image is free again
+      // one vertex's pieces in registers at a time (left alone, the scheduler
+      // hoists the four vertices' gathers together)
+      __builtin_amdgcn_sched_barrier(0);
     }
-    // slots whose last component lives in this pass: finished and stored
-    packed_pass_slot<L, 0>(S, a0, pass, 0, 0.0, nullptr, img, k, true);
-    packed_pass_slot<L, 1>(S, a1, pass, 0, 0.0, nullptr, img, k, true);
-    packed_pass_slot<L, 2>(S, a2, pass, 0, 0.0, nullptr, img, k, true);
-    packed_pass_slot<L, 3>(S, a3, pass, 0, 0.0, nullptr, img, k, true);
-    packed_pass_slot<L, 4>(S, a4, pass, 0, 0.0, nullptr, img, k, true);
-    packed_pass_slot<L, 5>(S, a5, pass, 0, 0.0, nullptr, img, k, true);
+    packed_finish<L, NP, 0>(S, a0, pass, img, k);
+    packed_finish<L, NP, 1>(S, a1, pass, img, k);
+    packed_finish<L, NP, 2>(S, a2, pass, img, k);
+    packed_finish<L, NP, 3>(S, a3, pass, img, k);
+    packed_finish<L, NP, 4>(S, a4, pass, img, k);
+    packed_finish<L, NP, 5>(S, a5, pass, img, k);
   }
 }
 
-template <bool PK, int C0, int C1, int C2, int C3, int C4, int C5>
+// PK: 0 = one array per solution, 1 / 2 = packed records in 1 / 2 passes
+template <int PK, int C0, int C1, int C2, int C3, int C4, int C5>
 __global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsigned long long *grid, int g,
                                             const double *qxyz, const uint8_t *pclass, const int *order,
                                             const double *qs, int np, ContEntry *cont, DevStats *st, Slots S,
@@ -995,8 +1015,8 @@ __global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsign
     }
     double *img = sh.u.img;
     __builtin_amdgcn_wave_barrier(); // the walk's slots are dead: the buffer becomes the gather image
-    if constexpr (PK) {
-      vol_interp_packed<C0, C1, C2, C3, C4, C5>(S, acc, loc, img, snk);
+    if constexpr (PK > 0) {
+      vol_interp_packed<PK, C0, C1, C2, C3, C4, C5>(S, acc, loc, img, snk);
     } else if constexpr (C0 < 0) {
       if (acc) {
         const int vv[4] = {loc.v.x, loc.v.y, loc.v.z, loc.v.w};

@@ -68,6 +68,15 @@ def _reduce(ri: RankInfo, value: float, op_name: str) -> float:
     return float(t.item())
 
 
+def broadcast_object(ri: RankInfo, objs: list, src: int = 0) -> None:
+    """objs (a list) replaced in place by rank src's (e.g. the RCCL unique id
+    of pmmg_hip_comm_init, as a shim would MPI_Bcast it)."""
+    if ri.distributed:
+        import torch.distributed as dist
+
+        dist.broadcast_object_list(objs, src=src)
+
+
 def max_over_ranks(ri: RankInfo, value: float) -> float:
     return _reduce(ri, value, "MAX")
 

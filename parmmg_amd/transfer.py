@@ -317,6 +317,32 @@ class TransferContext:
                  "compute_wgt_faces")
         return wgt
 
+    # ------------------------------------------------------------------ split over GPUs (RCCL)
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        """pmmg_hip_comm_unique_id: the RCCL id one rank makes and broadcasts."""
+        buf = ctypes.create_string_buffer(128)
+        if not hip_lib().pmmg_hip_comm_unique_id(buf):
+            raise RuntimeError("pmmg_hip_comm_unique_id failed (RCCL unavailable?)")
+        return buf.raw
+
+    def comm_init(self, nranks: int, rank: int, uid: bytes) -> None:
+        """pmmg_hip_comm_init (collective over the nranks processes)."""
+        buf = ctypes.create_string_buffer(bytes(uid), 128)
+        self._ck(self.lib.pmmg_hip_comm_init(self.h, int(nranks), int(rank), buf), "comm_init")
+
+    def allgather_points(self, counts, rows, rows_all, elem=None, elem_all=None, hit=None, hit_all=None) -> None:
+        """pmmg_hip_allgather_points: this rank's rows (device arrays / tensors,
+        one per slot) and optional elem / hit gathered in rank order into
+        rows_all / elem_all / hit_all on every rank."""
+        cnt = np.ascontiguousarray(counts, np.int64)
+        rows, rows_all = list(rows), list(rows_all)
+        sizes = (ctypes.c_int * max(1, len(rows)))(*[int(r.shape[1]) for r in rows])
+        rin = (ctypes.c_void_p * max(1, len(rows)))(*[_p(r) for r in rows])
+        rout = (ctypes.c_void_p * max(1, len(rows_all)))(*[_p(r) for r in rows_all])
+        self._ck(self.lib.pmmg_hip_allgather_points(self.h, _p(cnt), len(rows), sizes, rin, rout, _p(elem),
+                                                    _p(elem_all), _p(hit), _p(hit_all)), "allgather_points")
+
     def sync(self) -> HipStats:
         st = HipStats()
         self._ck(self.lib.pmmg_hip_sync(self.h, ctypes.byref(st)), "sync")

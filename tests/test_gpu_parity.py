@@ -38,7 +38,10 @@ MODES = {"auto": {}, "morton": dict(sort=True), "nosort": dict(sort=False), "tet
          "tet8-morton": dict(tet8=True, sort=True), "packed": dict(tet8=True, packed=True),
          "packed-morton": dict(tet8=True, packed=True, sort=True),
          "morton-fine": dict(sort=True, env=FINE), "packed-morton-fine": dict(tet8=True, packed=True, sort=True,
-                                                                              env=FINE)}
+                                                                              env=FINE),
+         # packed records gathered in two passes over the record halves (PMMG_HIP_PACKPASS=2)
+         "packed2": dict(tet8=True, packed=True, env={"PMMG_HIP_PACKPASS": "2"}),
+         "packed2-morton": dict(tet8=True, packed=True, sort=True, env={"PMMG_HIP_PACKPASS": "2"})}
 
 
 @pytest.mark.gpu
@@ -188,9 +191,10 @@ def test_packed_records_bit_identical(name):
                      if CASES[name].get("metric", synth.F_ANI) == synth.F_ANI else CASES[name], with_ref=False)
     assert _packable(case)
     a = run_gpu(case, tet8=True)
-    b = run_gpu(case, tet8=True, packed=True)
-    np.testing.assert_array_equal(a["elem"], b["elem"])
-    np.testing.assert_array_equal(a["hit"], b["hit"])
-    for x, y in zip(([a["met"]] if a["met"] is not None else []) + a["fields"],
-                    ([b["met"]] if b["met"] is not None else []) + b["fields"]):
-        assert np.array_equal(x, y, equal_nan=True)
+    for env in ({}, {"PMMG_HIP_PACKPASS": "2"}):  # one gather per record, or one per record half
+        b = run_gpu(case, tet8=True, packed=True, env=env)
+        np.testing.assert_array_equal(a["elem"], b["elem"])
+        np.testing.assert_array_equal(a["hit"], b["hit"])
+        for x, y in zip(([a["met"]] if a["met"] is not None else []) + a["fields"],
+                        ([b["met"]] if b["met"] is not None else []) + b["fields"]):
+            assert np.array_equal(x, y, equal_nan=True)
