@@ -692,6 +692,9 @@ def main():
     ap.add_argument("--split", default="rcb", choices=["rcb", "morton"],
                     help="split modes: the new points cut by recursive coordinate bisection (compact boxes of equal "
                          "cost) or into contiguous Morton ranges")
+    ap.add_argument("--shard-build", default="parts", choices=["parts", "group"],
+                    help="halo mode: each rank's shard assembled from every rank's part of the group (all-to-all), "
+                         "or cut from the whole group")
     ap.add_argument("--halo", type=float, default=-1.0,
                     help="halo mode: growth of the range box (< 0: in largest-tetra extents, at least hausd)")
     ap.add_argument("--no-host-mode", action="store_true",
@@ -738,11 +741,35 @@ def main():
         if shard_mode == "halo":
             from parmmg_amd import shard
             t_sh = time.time()
-            sh = shard.halo_shard_cells(bg, q_xyz, args.halo, hausd=w.hausd)
-            bg, met, fields = sh.mesh, sh.rows(met), [sh.rows(f) for f in fields]
+            built = "whole group (halo_shard_cells)"
+            if args.shard_build == "parts":
+                # every rank keeps only its part of the group (pmmg_shard_part_pack), the parts are exchanged
+                # all-to-all and assembled (pmmg_shard_assemble): the shard the whole-group builder makes
+                try:
+                    h = -args.halo * shard.max_tet_extent(bg) if args.halo < 0 else float(args.halo)
+                    h = max(h, 1.01 * w.hausd)
+                    grid = shard.grid_for(bg.xyz.min(axis=0), bg.xyz.max(axis=0), h)
+                    sol = np.concatenate([met] + list(fields), axis=1)
+                    part = shard.part_of(bg, sol, rank, world)
+                    sh = shard.shard_from_parts(ri, part, q_xyz, h, *grid, bg.kind, bg.n)
+                    del part
+                    c0 = met.shape[1]
+                    met, fields = sh.sol[:, :c0].copy(), []
+                    for f in fields_group:
+                        fields.append(np.ascontiguousarray(sh.sol[:, c0:c0 + f.shape[1]]))
+                        c0 += f.shape[1]
+                    bg = sh.mesh
+                    built = "the ranks' parts (pmmg_shard_part_pack, all-to-all, pmmg_shard_assemble)"
+                except Exception as e:  # reported; the whole-group builder stands in
+                    log(f"[bench r{rank}] shard from parts failed: {e}")
+                    built = f"whole group (the parts' build failed: {e})"
+                    sh = None
+            if sh is None or args.shard_build != "parts":
+                sh = shard.halo_shard_cells(bg, q_xyz, args.halo, hausd=w.hausd)
+                bg, met, fields = sh.mesh, sh.rows(met), [sh.rows(f) for f in fields]
             halo_info = {"what": "halo shard of the background around this rank's Morton range (rank 0): the tetra "
                                  "meeting, grown by the halo, the range's box and a halo-sized grid cell holding "
-                                 "one of its points",
+                                 "one of its points", "built_from": built,
                          "tets": bg.ne, "verts": bg.np, "trias": bg.nt, "halo": sh.halo,
                          "tet_fraction_of_group": round(bg.ne / ne_group, 4),
                          "build_s": round(time.time() - t_sh, 2)}

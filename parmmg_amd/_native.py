@@ -139,6 +139,13 @@ HOST_API = {
     "pmmg_shard_fill": (c_int64, [c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_void_p, c_void_p, c_void_p]),
+    "pmmg_shard_mark_trias": (c_int64, [c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    "pmmg_shard_fill_region": (c_int64, [c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
+                                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                         c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pmmg_shard_part_pack": (c_int64, [c_void_p, c_void_p, c_void_p, c_int64]),
+    "pmmg_shard_assemble": (c_int, [c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pmmg_medit_read_mesh": (c_int, [ctypes.c_char_p, c_void_p, ctypes.c_char_p, c_int]),
     "pmmg_medit_read_sol": (c_int, [ctypes.c_char_p, c_void_p, ctypes.c_char_p, c_int]),
     "pmmg_medit_free_mesh": (None, [c_void_p]),

@@ -140,6 +140,70 @@ int64_t pmmg_shard_fill(int np, const double *xyz, int ne, const int *tetv, cons
                         double *s_xyz, int *s_tetv, int *s_adja, int *s_triv, int *s_adjt, int *tet_gid,
                         int *vert_gid, int *tria_gid);
 
+/* ---- halo shards built from the ranks' parts of a group (r05) --------------
+ * The builders above read the whole group; a rank of a distributed group
+ * holds only its part.  Each rank packs, for every destination rank, the
+ * tetra, trias and vertex rows of its part that the destination's region
+ * needs (pmmg_shard_part_pack), the ranks exchange the buffers (MPI /
+ * RCCL all-to-all; bench and tests: torch.distributed), and each rank
+ * assembles its shard from what it received (pmmg_shard_assemble).  The
+ * shard is the one pmmg_shard_mark_cells + pmmg_shard_fill_region build
+ * from the whole group: local ids ascend with the global ids, cut faces and
+ * edges are walls. */
+
+/* A destination's region: the tetra / trias whose bounding box grown by
+ * `halo` meets the box (when box_lo) and a grid cell with occ != 0 (the
+ * cells holding the destination's points, as pmmg_shard_mark_cells). */
+typedef struct {
+  const double *box_lo, *box_hi; /* 3 each, or NULL */
+  double g_lo[3];
+  double cell;
+  int g_n[3];
+  const uint8_t *occ;
+  double halo; /* absolute, >= 0 */
+} pmmg_shard_region;
+
+/* A rank's part of a background group, global ids (1-based) ascending:
+ * every vertex a part tetra or tria uses is a part vertex; tetv / triv hold
+ * GLOBAL vertex ids, adja / adjt the group's codes (4 gk + i, 3 gt + i). */
+typedef struct {
+  int np, ne, nt, K;
+  const int *vert_gid;  /* np */
+  const double *xyz;    /* 3 np */
+  const double *sol;    /* K np (solution rows: metric | fields), NULL when K == 0 */
+  const int *tet_gid;   /* ne */
+  const int *tetv;      /* 4 ne */
+  const int *adja;      /* 4 ne */
+  const int *tria_gid;  /* nt */
+  const int *triv;      /* 3 nt */
+  const int *adjt;      /* 3 nt (may be NULL) */
+} pmmg_shard_part;
+
+/* Trias of the whole group meeting the region: tria_map[nt] = 1-based local
+ * id (ascending) or 0; returns their count, -1 on invalid input. */
+int64_t pmmg_shard_mark_trias(int np, const double *xyz, int nt, const int *triv, const pmmg_shard_region *reg,
+                              int *tria_map);
+
+/* pmmg_shard_fill with the trias of tria_map (pmmg_shard_mark_trias) instead
+ * of "all three vertices in the shard": the rule the part builders share. */
+int64_t pmmg_shard_fill_region(int np, const double *xyz, int ne, const int *tetv, const int *adja, int nt,
+                               const int *triv, const int *adjt, const int *tet_map, const int *vert_map,
+                               const int *tria_map, double *s_xyz, int *s_tetv, int *s_adja, int *s_triv,
+                               int *s_adjt, int *tet_gid, int *vert_gid, int *tria_gid);
+
+/* The records of `part` the region needs, into buf (bytes; NULL or too small:
+ * only sized).  Returns the bytes needed, or -1 on invalid input. */
+int64_t pmmg_shard_part_pack(const pmmg_shard_part *part, const pmmg_shard_region *reg, void *buf, int64_t cap);
+
+/* A shard from the buffers received from every rank (nbuf of them, lens
+ * bytes each; K solution doubles per vertex, the same in every buffer).
+ * counts[3] = {vertices, tetra, trias}; with xyz == NULL only counts are
+ * computed.  Outputs as pmmg_shard_fill_region, plus the vertex rows
+ * s_sol[K nv].  Returns 1, or 0 on inconsistent buffers. */
+int pmmg_shard_assemble(int nbuf, const void *const *bufs, const int64_t *lens, int K, int64_t counts[3],
+                        double *s_xyz, double *s_sol, int *s_tetv, int *s_adja, int *s_triv, int *s_adjt,
+                        int *tet_gid, int *vert_gid, int *tria_gid);
+
 #ifdef __cplusplus
 }
 #endif
