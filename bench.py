@@ -40,7 +40,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from parmmg_amd import configs, ranks, synth  # noqa: E402
-from parmmg_amd.transfer import TransferContext, pack_tet8  # noqa: E402
+from parmmg_amd.transfer import TransferContext, pack_solutions, pack_tet8  # noqa: E402
 
 METRIC = "new-mesh points located+interpolated/sec (Mpts/s) and HBM GB/s, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
@@ -459,22 +459,36 @@ def host_mode_iteration2(ctx, w, bg, mo, fo, rank: int) -> dict:
     return res
 
 
-def renumbered_timing(ctx, args, w, step_bg, q_xyz, q_pc, d_mo, d_fo, d_elem, d_hit, rank: int, perm, what: str):
+def renumbered_timing(ctx, args, w, step_bg, q_xyz, q_pc, d_mo, d_fo, d_elem, d_hit, rank: int, perm, what: str,
+                      records=None):
     """The same step on a renumbering of the new points (perm[new id] = old
     id); the module decides on the device whether the numbering is
     spatially coherent (input order) or Morton-bins the queries.  Reported
     beside the bench value, which is measured on the generator's lattice
     numbering.  Checked against the input-order step: a point located in
-    the same element gets bit-identical rows."""
+    the same element gets bit-identical rows.
+
+    records = the packed solution records in HBM (pack_solutions): the step
+    then reads them (pmmg_hip_set_solutions_packed) and writes its rows as
+    records of the same layout (pmmg_hip_locate_interp_rec), one 128-byte
+    line per point where the reference's layout scatters four arrays' rows."""
     nq = q_xyz.shape[0]
     s_xyz, s_pc = ctx.upload(np.ascontiguousarray(q_xyz[perm])), ctx.upload(np.ascontiguousarray(q_pc[perm]))
-    s_mo = ctx.empty((nq, w.met_size), np.float64)
-    s_fo = [ctx.empty(f.shape, np.float64) for f in d_fo]
+    sizes = [w.met_size] + [f.shape[1] for f in d_fo]
+    if records is None:
+        s_mo = ctx.empty((nq, w.met_size), np.float64)
+        s_fo = [ctx.empty(f.shape, np.float64) for f in d_fo]
+    else:
+        s_rec = ctx.empty((nq, records.shape[1]), np.float64)
     s_elem, s_hit = ctx.empty((nq,), np.int32), ctx.empty((nq,), np.int8)
 
     def step():
         step_bg()
-        ctx.locate_interp(s_xyz, s_pc, s_mo, s_fo, s_elem, s_hit, sync=False)
+        if records is None:
+            ctx.locate_interp(s_xyz, s_pc, s_mo, s_fo, s_elem, s_hit, sync=False)
+        else:
+            ctx.set_solutions_packed(records, w.met_size, sizes[1:])
+            ctx.locate_interp_rec(s_xyz, s_pc, s_rec, s_elem, s_hit, sync=False)
 
     for _ in range(args.warmup):
         step()
@@ -494,9 +508,16 @@ def renumbered_timing(ctx, args, w, step_bg, q_xyz, q_pc, d_mo, d_fo, d_elem, d_
     located = (h0 != 0) & (h1 != 0)
     same = located & (e0 == e1) & (h0 == h1)
     ident = same.copy()
-    for a, b in [(d_mo, s_mo)] + list(zip(d_fo, s_fo)):
-        x0, x1 = a.download(), b.download()[inv]
-        ident &= np.all(x0.view(np.uint64) == x1.view(np.uint64), axis=1)
+    if records is None:
+        got = [b.download()[inv] for b in [s_mo] + s_fo]
+    else:
+        r = s_rec.download()[inv]
+        offs = np.cumsum([0] + sizes)
+        got = [r[:, offs[j]:offs[j + 1]] for j in range(len(sizes))]
+        s_rec.free()
+    for a, x1 in zip([d_mo] + list(d_fo), got):
+        x0 = a.download()
+        ident &= np.all(x0.view(np.uint64) == np.ascontiguousarray(x1).view(np.uint64), axis=1)
     npts = int(st.nvol + st.nbdy)
     res = {"what": what,
            "morton_binned": bool(st.sorted), "ms_per_step": round(1e3 * wall, 4),
@@ -506,7 +527,7 @@ def renumbered_timing(ctx, args, w, step_bg, q_xyz, q_pc, d_mo, d_fo, d_elem, d_
            "same_element_rows_bit_identical": int((same & ident).sum()),
            "ok": bool(np.all(ident[same])) and int(located.sum()) == npts}
     log(f"[bench r{rank}] renumbered ({what}): {res}")
-    for b in [s_xyz, s_pc, s_mo, s_elem, s_hit] + s_fo:
+    for b in [s_xyz, s_pc, s_elem, s_hit] + ([s_mo] + s_fo if records is None else []):
         b.free()
     return res
 
@@ -946,6 +967,18 @@ def main():
                                               perm, what)
             except Exception as e:  # reported, never fatal to the bench line
                 out[name] = {"error": str(e)}
+        # the shuffled numbering again with the solutions as packed records in and out (the layout a
+        # device-resident pipeline keeps across iterations, pmmg_hip_locate_interp_rec)
+        try:
+            d_rec = ctx.upload(pack_solutions(met, fields))
+            out["shuffled_order_records"] = renumbered_timing(
+                ctx, args, w, step_bg, q_xyz, q_pc, d_mo, d_fo, d_elem, d_hit, rank, legs["shuffled_order"][0],
+                "the shuffled numbering's step with packed solution records in (pmmg_hip_set_solutions_packed) "
+                "and out (pmmg_hip_locate_interp_rec): one record line per point written; rows checked "
+                "against the input-order step's arrays; not the bench value", records=d_rec)
+            d_rec.free()
+        except Exception as e:  # reported, never fatal to the bench line (e.g. a layout without packed records)
+            out["shuffled_order_records"] = {"error": str(e)}
     gpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not split:
         # outputs of the last timed step (the host-mode call used its own buffers)

@@ -323,6 +323,20 @@ int pmmg_hip_tetra_qual(pmmg_hip_ctx *ctx, int np, const double *xyz, int ne,
 int pmmg_hip_set_solutions_packed(pmmg_hip_ctx *ctx, int met_size, int nfield,
                                   const int *field_size, const double *rec, int where);
 
+/* pmmg_hip_locate_interp with the new points' values written as records of
+ * the same layout as the packed input (rec_out[RS*np_new], point ip's record
+ * at rec_out + RS*(ip-1): [metric | field 0 | ...]): after
+ * pmmg_hip_set_solutions_packed, device pointers only (rec_out 16-byte
+ * aligned; 128-byte aligned puts each 16-double record on one line).  What a
+ * record is not written for keeps its previous content, per solution as in
+ * the reference (skipped points, MMG5_invmat failures).  The records a step
+ * writes are the next iteration's background records as they are (the
+ * adapted group becomes the old group, src/libparmmg1.c:653): a resident
+ * pipeline never repacks.  Same results, bit for bit, as
+ * pmmg_hip_locate_interp.  Returns 1/0. */
+int pmmg_hip_locate_interp_rec(pmmg_hip_ctx *ctx, int np_new, const double *xyz_new, const uint8_t *pclass,
+                               double *rec_out, int *elem_out, int8_t *hit_out, pmmg_hip_stats *stats, int where);
+
 /* Load-balancing weights from the interpolated metric (SURVEY.md §8(f)
  * rank 2, the second consumer after PMMG_tetraQual), device arrays, 1-based
  * vertex ids, synchronous.

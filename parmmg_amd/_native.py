@@ -76,6 +76,8 @@ HIP_API = {
                                     P(c_double)]),
     "pmmg_hip_memcpy_h2d": (c_int, [c_void_p, c_void_p, c_void_p, c_int64]),
     "pmmg_hip_memcpy_d2h": (c_int, [c_void_p, c_void_p, c_void_p, c_int64]),
+    "pmmg_hip_locate_interp_rec": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                           c_void_p, c_int]),
     "pmmg_hip_comm_unique_id": (c_int, [c_void_p]),
     "pmmg_hip_comm_init": (c_int, [c_void_p, c_int, c_int, c_void_p]),
     "pmmg_hip_comm_attach": (c_int, [c_void_p, c_void_p, c_int, c_int]),

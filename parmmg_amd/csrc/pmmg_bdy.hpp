@@ -112,7 +112,7 @@ __device__ __forceinline__ int bdy_query(const Bg &bg, const Frame *fr, const in
 // slowed the volume kernel beside them (profiles/r03y).
 __global__ __launch_bounds__(kBlock) void k_bdy(Bg bg, const Frame *fr, const int *sgrid, int gs, const double *qxyz,
                                                 const int *order, Slots S, int *elem_out, int8_t *hit_out, int *fb,
-                                                DevStats *st, int maxstep, int dyn, FbInit fi) {
+                                                DevStats *st, int maxstep, int dyn, FbInit fi, FbGridBufs gb) {
   __shared__ BlockStats bs;
   bstats_init(&bs);
   __syncthreads();
@@ -147,6 +147,10 @@ __global__ __launch_bounds__(kBlock) void k_bdy(Bg bg, const Frame *fr, const in
   }
   __syncthreads();
   bstats_flush(&bs, st);
+  // the surface fallback list is complete: its query grid (fb_grid_build)
+  if (!last_block(&st->bdy_done)) return;
+  const int nfb = load_agent(&st->nfb_bdy);
+  if (nfb > 0) fb_grid_build(qxyz, fb, nfb, st, 1, gb.cells, gb.cur, gb.items);
 }
 
 } // namespace pmmg

@@ -53,9 +53,10 @@ __device__ __forceinline__ int4 adja_row(const Bg &bg, int k) { return bg.adja[(
 // 6 = symmetric tensor (inverse-tensor interpolation)
 struct Slot {
   const double *in; // row of vertex v at in + istride*(v-1)
-  double *out;      // row of point ip at out + code*(ip-1)
+  double *out;      // row of point ip at out + ostride*(ip-1)
   int code;
   int istride; // doubles between input rows: code (one array per solution) or the record stride (packed)
+  int ostride; // doubles between output rows: code, or the output record stride (pmmg_hip_locate_interp_rec)
 };
 
 struct Slots {
@@ -63,6 +64,7 @@ struct Slots {
   int n;
   int has_met;        // slot 0 is the metric (boundary points treat it differently)
   const double *rec;  // packed per-vertex records (pmmg_hip_set_solutions_packed), else null
+  double *rec_out;    // output records of the new points (same layout as rec), else null
 };
 
 // ------------------------------------------------------------ small helpers
@@ -354,9 +356,14 @@ __device__ __forceinline__ void nt_store2(double *p, double a, double b) {
 // continuation, the fallbacks): non-temporal pieces (r03ab: plain stores
 // here made the surface branch alone 0.40 -> 0.67 ms)
 __device__ __forceinline__ void store6(double *p, const double *m) {
-  nt_store2(p, m[0], m[1]);
-  nt_store2(p + 2, m[2], m[3]);
-  nt_store2(p + 4, m[4], m[5]);
+  if (((uintptr_t)p & 15) == 0) {
+    nt_store2(p, m[0], m[1]);
+    nt_store2(p + 2, m[2], m[3]);
+    nt_store2(p + 4, m[4], m[5]);
+  } else { // a tensor at an odd offset of an output record
+#pragma unroll
+    for (int j = 0; j < 6; j++) nt_store(p + j, m[j]);
+  }
 }
 
 // ------------------------------------------------------------ interpolators
@@ -415,7 +422,7 @@ template <int NV, int CODE>
 __device__ __forceinline__ void interp_code(const Slot &sl, int ip, const int *v, const double *phi) {
   double r[CODE];
   if (!interp_row<NV, CODE>(sl, v, phi, r)) return;
-  double *out = sl.out + (size_t)CODE * (ip - 1);
+  double *out = sl.out + (size_t)sl.ostride * (ip - 1);
   if constexpr (CODE == 6) store6(out, r);
   else {
 #pragma unroll
@@ -444,18 +451,18 @@ __device__ __forceinline__ void interp_edge(const Slot &sl, int ip, const int *v
     ok = invmat(m, mi1) && ok;
 #pragma unroll
     for (int s = 0; s < 6; s++) mint[s] = f0 * mi0[s] + f1 * mi1[s];
-    if (invmat(mint, r) && ok) store6(sl.out + 6 * (size_t)(ip - 1), r);
+    if (invmat(mint, r) && ok) store6(sl.out + (size_t)sl.ostride * (ip - 1), r);
   } else {
     // sizes 1 and 3 (a vertex / edge hit of the metric is size 1 or 6; the
     // fields always go through interp3bar)
     for (int j = 0; j < sl.code; j++)
-      sl.out[(size_t)sl.code * (ip - 1) + j] =
+      sl.out[(size_t)sl.ostride * (ip - 1) + j] =
           f0 * sl.in[(size_t)sl.istride * (v0 - 1) + j] + f1 * sl.in[(size_t)sl.istride * (v1 - 1) + j];
   }
 }
 
 __device__ __forceinline__ void copy_row(const Slot &sl, int ip, int vsrc) {
-  double *out = sl.out + (size_t)sl.code * (ip - 1);
+  double *out = sl.out + (size_t)sl.ostride * (ip - 1);
   const double *in = sl.in + (size_t)sl.istride * (vsrc - 1);
   if (sl.code == 6) {
     double m[6];

@@ -16,10 +16,11 @@
 // from 0.24 to 6.7 s):
 //   accept   element-major: each thread holds one element and its bounding
 //            box inflated past what the acceptance test can pass, and tests
-//            every query of the list against the box; only the few pairs
-//            inside it run the reference's test (one atomicMin per accepting
-//            pair).  The last block interpolates the accepted queries and
-//            lists the others.
+//            the queries of the list in the grid cells the box covers (a
+//            grid over the list built when the list is complete); only the
+//            few pairs inside the box run the reference's test (one atomicMin
+//            per accepting pair).  The last block interpolates the accepted
+//            queries and lists the others.
 //   closest  query-major, only for the queries nothing accepted (points
 //            outside the domain): elements staged in LDS tiles, every lane
 //            keeps its query's running (key, index) minimum over a range of
@@ -32,7 +33,6 @@
 
 namespace pmmg {
 
-constexpr int kFbQ = 256;        // fallback queries staged in LDS per pass of an accept scan
 constexpr int kFbGridVol = 1024; // blocks of the volume exhaustive kernels (fixed: the counts are on the device)
 constexpr int kFbGridBdy = 256;  // blocks of the surface ones (trias: ~1-2 % of the tetra)
 
@@ -55,64 +55,6 @@ __device__ __forceinline__ double centroid_dist3(const double *x, const double (
   return sqrt(nrm);
 }
 
-// the last block of a grid to pass this point (after its device-scope
-// atomics) gets true: the other blocks' results are then visible to it.  The
-// barrier before the ticket: every wave of the block has issued its atomics
-// (r04l: without it a block's later waves could still be scanning when the
-// last block read the results — 4 surface points left unprocessed, once)
-__device__ __forceinline__ bool last_block(unsigned *done) {
-  __threadfence();
-  __syncthreads();
-  __shared__ bool last;
-  if (threadIdx.x == 0) last = atomicAdd(done, 1u) == gridDim.x - 1;
-  __syncthreads();
-  if (last) __threadfence();
-  return last;
-}
-
-__device__ __forceinline__ int load_agent(const int *p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// ---------------------------------------------------------------- accept scans
-
-// The bounding box of an element inflated so that every point its
-// acceptance test can pass lies inside.  Volume: every barycentric
-// coordinate > -EPS puts x within 3 EPS of the extent outside the vertices'
-// box (x_c = sum_i b_i p_ic, sum_i b_i = 1); the pad is 1e-4 of the extent
-// (33x that, room for the coordinates' rounding on any element with an
-// aspect ratio below ~1e10) plus 1e-12 of the coordinates' magnitude.
-// Surface: the projection is inside the tria within the same margin and
-// |dist| <= hausd along the unit normal.  A degenerate element (zero or
-// non-finite volume / area) gets an infinite box: every query takes the
-// reference's test there, as in the oracle.
-constexpr double kBoxRel = 1e-4, kBoxAbs = 1e-12;
-struct Box {
-  double lo[3], hi[3];
-};
-__device__ __forceinline__ bool in_box(const Box &b, const double *x) {
-  // NaN coordinates compare false everywhere and fall through to the test
-  return !(x[0] < b.lo[0] || x[0] > b.hi[0] || x[1] < b.lo[1] || x[1] > b.hi[1] || x[2] < b.lo[2] ||
-           x[2] > b.hi[2]);
-}
-template <int NV>
-__device__ __forceinline__ Box elem_box(const double (*p)[3], double extra, bool degenerate) {
-  Box b;
-#pragma unroll
-  for (int c = 0; c < 3; c++) {
-    double lo = p[0][c], hi = p[0][c];
-#pragma unroll
-    for (int v = 1; v < NV; v++) {
-      lo = fmin(lo, p[v][c]);
-      hi = fmax(hi, p[v][c]);
-    }
-    const double pad = kBoxRel * (hi - lo) + kBoxAbs * fmax(fabs(lo), fabs(hi)) + extra + 1e-300;
-    b.lo[c] = degenerate ? -INFINITY : lo - pad;
-    b.hi[c] = degenerate ? INFINITY : hi + pad;
-  }
-  return b;
-}
-
 // per-block hit counters of a finishing last block, flushed once
 __device__ __forceinline__ void count_hits_flush(unsigned *cnt, DevStats *st, int h0, int h1) {
   __syncthreads();
@@ -122,54 +64,38 @@ __device__ __forceinline__ void count_hits_flush(unsigned *cnt, DevStats *st, in
   }
 }
 
-// lowest-index tetra accepting each fallback query (locate_pmmg.c:743-762);
-// the last block interpolates the accepted ones and lists the others (nac)
+// lowest-index tetra accepting each fallback query (locate_pmmg.c:743-762),
+// each tetra tested against the queries of the grid cells its inflated box
+// covers; the last block interpolates the accepted ones and lists the others
+// (nac)
 __global__ __launch_bounds__(kBlock) void k_vol_exhaust_accept(Bg bg, const double *qxyz, const int *fb, DevStats *st,
-                                                               int *best, int *nac, Slots S, int *elem_out,
+                                                               int *best, int *nac, const int *gcells,
+                                                               const int *gitems, Slots S, int *elem_out,
                                                                int8_t *hit_out) {
-  __shared__ double sq[kFbQ][3];
   const int nfb = st->nfb_vol;
   if (nfb == 0) return;
-  const bool once = nfb <= kFbQ; // the usual case: the whole list stays in LDS
-  if (once) {
-    for (int j = threadIdx.x; j < nfb; j += blockDim.x) load_pt(qxyz, fb[j], sq[j]);
-    __syncthreads();
-  }
   const XcdChunk ch = xcd_chunk(bg.ne); // each XCD a contiguous eighth of the tetra (shared vertex rows in its L2)
   for (int it = 0; it < ch.iters; it++) {
     const long long j0 = ch.start + it * ch.stride;
+    if (j0 >= ch.hi) break;
     const int k = (int)(j0 + 1);
+    const int4 tv = tetv_row(bg, k);
+    if (tv.x <= 0) continue;
     double p[4][3];
-    Box box;
-    bool live = false;
-    if (j0 < ch.hi) {
-      const int4 tv = tetv_row(bg, k);
-      if (tv.x > 0) {
-        live = true;
-        load_pt(bg.xyz, tv.x, p[0]);
-        load_pt(bg.xyz, tv.y, p[1]);
-        load_pt(bg.xyz, tv.z, p[2]);
-        load_pt(bg.xyz, tv.w, p[3]);
-        const double vol = orvol4(p[0], p[1], p[2], p[3]);
-        box = elem_box<4>(p, 0.0, !(fabs(vol) > 0.0) || !isfinite(vol));
-      }
-    }
-    for (int q0 = 0; q0 < nfb; q0 += kFbQ) {
-      const int nq = min(kFbQ, nfb - q0);
-      if (!once) {
-        __syncthreads();
-        for (int j = threadIdx.x; j < nq; j += blockDim.x) load_pt(qxyz, fb[q0 + j], sq[j]);
-        __syncthreads();
-      }
-      if (!live) continue;
-      for (int j = 0; j < nq; j++) {
-        const double *x = sq[j];
-        if (!in_box(box, x) || best[q0 + j] <= k) continue; // (a stale read only costs a test)
-        double b[4];
-        tet_bary(x, p[0], p[1], p[2], p[3], b);
-        if (min4(b) > -kEps) atomicMin(&best[q0 + j], k);
-      }
-    }
+    load_pt(bg.xyz, tv.x, p[0]);
+    load_pt(bg.xyz, tv.y, p[1]);
+    load_pt(bg.xyz, tv.z, p[2]);
+    load_pt(bg.xyz, tv.w, p[3]);
+    const double vol = orvol4(p[0], p[1], p[2], p[3]);
+    const Box box = elem_box<4>(p, 0.0, !(fabs(vol) > 0.0) || !isfinite(vol));
+    fb_grid_visit(st, 0, gcells, gitems, box, [&](int j) {
+      double x[3];
+      load_pt(qxyz, fb[j], x);
+      if (!in_box(box, x) || best[j] <= k) return; // (a stale read only costs a test)
+      double b4[4];
+      tet_bary(x, p[0], p[1], p[2], p[3], b4);
+      if (min4(b4) > -kEps) atomicMin(&best[j], k);
+    });
   }
   if (!last_block(&st->fb_done[0])) return;
   __shared__ int s_nac;
@@ -205,48 +131,33 @@ __global__ __launch_bounds__(kBlock) void k_vol_exhaust_accept(Bg bg, const doub
   count_hits_flush(s_cnt, st, PMMG_HIT_VOL_EXHAUST, PMMG_HIT_VOL_EXHAUST);
 }
 
-// surface: the lowest-index accepting tria (locate_pmmg.c:483-503); the last
+// surface: the lowest-index accepting tria (locate_pmmg.c:483-503), each tria
+// against the queries of the grid cells its inflated box covers; the last
 // block interpolates the accepted queries and lists the others
 __global__ __launch_bounds__(kBlock) void k_bdy_exhaust_accept(Bg bg, const double *qxyz, const int *fb, DevStats *st,
-                                                               int *best, int *nac, Slots S, int *elem_out,
+                                                               int *best, int *nac, const int *gcells,
+                                                               const int *gitems, Slots S, int *elem_out,
                                                                int8_t *hit_out) {
-  __shared__ double sq[kFbQ][3];
   const int nfb = st->nfb_bdy;
   if (nfb == 0) return;
-  const bool once = nfb <= kFbQ;
-  if (once) {
-    for (int j = threadIdx.x; j < nfb; j += blockDim.x) load_pt(qxyz, fb[j], sq[j]);
-    __syncthreads();
-  }
   const XcdChunk ch = xcd_chunk(bg.nt);
   for (int it = 0; it < ch.iters; it++) {
     const long long j0 = ch.start + it * ch.stride;
+    if (j0 >= ch.hi) break;
     const int k = (int)(j0 + 1);
+    if (bg.triv[3 * (size_t)(k - 1)] <= 0) continue;
     TriGeom t;
-    Box box;
-    bool live = false;
-    if (j0 < ch.hi && bg.triv[3 * (size_t)(k - 1)] > 0) {
-      live = true;
-      tri_load(bg, k, t);
-      box = elem_box<3>(t.p, bg.hausd, !(t.q > 0.0) || !isfinite(t.q));
-    }
-    for (int q0 = 0; q0 < nfb; q0 += kFbQ) {
-      const int nq = min(kFbQ, nfb - q0);
-      if (!once) {
-        __syncthreads();
-        for (int j = threadIdx.x; j < nq; j += blockDim.x) load_pt(qxyz, fb[q0 + j], sq[j]);
-        __syncthreads();
-      }
-      if (!live) continue;
-      for (int j = 0; j < nq; j++) {
-        const double *x = sq[j];
-        if (!in_box(box, x) || best[q0 + j] <= k) continue;
-        double b[3];
-        const double dist = tri_bary(x, t.p, t.q, t.n, b);
-        const double bmin = fmin(b[0], fmin(b[1], b[2]));
-        if (bmin > -kEps && !(fabs(dist) > bg.hausd)) atomicMin(&best[q0 + j], k);
-      }
-    }
+    tri_load(bg, k, t);
+    const Box box = elem_box<3>(t.p, bg.hausd, !(t.q > 0.0) || !isfinite(t.q));
+    fb_grid_visit(st, 1, gcells, gitems, box, [&](int j) {
+      double x[3];
+      load_pt(qxyz, fb[j], x);
+      if (!in_box(box, x) || best[j] <= k) return;
+      double b3[3];
+      const double dist = tri_bary(x, t.p, t.q, t.n, b3);
+      const double bmin = fmin(b3[0], fmin(b3[1], b3[2]));
+      if (bmin > -kEps && !(fabs(dist) > bg.hausd)) atomicMin(&best[j], k);
+    });
   }
   if (!last_block(&st->fb_done[2])) return;
   __shared__ int s_nac;

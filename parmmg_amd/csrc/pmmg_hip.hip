@@ -92,8 +92,10 @@ const LayoutEntry kLayouts[] = {
 #undef PMMG_LAYOUT
 
 // passes: packed records' gather passes (1 or 2; the other is taken when the
-// layout allows only it)
-VolFn pick_layout(const Slots &S, int passes = 1) {
+// layout allows only it; 0 = by the record's size: two above 8 doubles, where
+// one pass holds the whole record in registers — cfg4's 16 doubles: 168
+// VGPRs, 3 waves per SIMD, 4.42 ms per step against 4.18 in two passes, r05d)
+VolFn pick_layout(const Slots &S, int passes = 0) {
   for (const LayoutEntry &e : kLayouts) {
     int n = 0;
     while (n < 6 && e.c[n] > 0) n++;
@@ -102,6 +104,11 @@ VolFn pick_layout(const Slots &S, int passes = 1) {
     for (int j = 0; j < n; j++) ok = ok && (S.s[j].code == e.c[j]);
     if (!ok) continue;
     if (!S.rec) return e.fn;
+    if (passes == 0) {
+      int k = 0;
+      for (int j = 0; j < n; j++) k += e.c[j];
+      passes = k > 8 ? 2 : 1;
+    }
     VolFn a = passes == 2 ? e.fn_packed2 : e.fn_packed, b = passes == 2 ? e.fn_packed : e.fn_packed2;
     return a ? a : b;
   }
@@ -163,7 +170,7 @@ struct pmmg_hip_ctx {
   std::vector<DevBuf> o_f;
   // work buffers
   DevBuf frame, stats, grid, sgrid, order_v, order_b, cont, xq;
-  DevBuf axh;                             // per-axis histograms of the seed grid map (k_axis_hist)
+  DevBuf axh;                             // per-axis histograms of the seed grid map (k_quantize)
   DevBuf bkeys, bkeys2, bvals, bvals2;    // Morton binning: keys and ids, ping-ponged by the radix sort
   DevBuf rs_hist, rs_csum;                // the radix sort's digit table and its scan's chunk sums
   // PMMG_HIP_BRICK (measurement only, pmmg_brick.hpp): the background renumbered by bricks
@@ -183,6 +190,7 @@ struct pmmg_hip_ctx {
   DevBuf qmin;                               // tetra quality minimum (pmmg_hip_tetra_qual)
   DevBuf fb_vol, fb_bdy, best, nac, cres, bbest, bnac, bcres; // exhaustive searches: fallback lists, lowest
   DevBuf fbp_vol, fbp_bdy; // accepting element, unaccepted lists, closest results and range minima (FbPart)
+  DevBuf fbg_vol_c, fbg_vol_u, fbg_vol_i, fbg_bdy_c, fbg_bdy_u, fbg_bdy_i; // the lists' query grids
   // host-mode staging
   DevBuf h_xyz, h_cls, h_met, h_elem, h_hit;
   std::vector<DevBuf> h_f;
@@ -208,7 +216,7 @@ struct pmmg_hip_ctx {
   int tpc = 8;        // background tetra per volume seed cell (PMMG_HIP_TPC)
   int seed_lanes = 4;  // sampled tetra per seed run of 4 records (PMMG_HIP_SEEDLANES, 1..4)
   int seed_v0 = 0;     // measurement build, PMMG_HIP_SEEDV0=1: a sample's first vertex instead of its centroid
-  int pack_passes = 1; // packed records gathered in 1 or 2 passes over the record (PMMG_HIP_PACKPASS)
+  int pack_passes = 0; // packed records gathered in 1 or 2 passes over the record (PMMG_HIP_PACKPASS; 0: by size)
   int bbox_stride = 64;  // the frame's bbox samples np / n vertices (PMMG_HIP_BBOX; r03o: 64 instead of 16 and
   int hist_stride = 256; // 256 instead of 64 for the axis histograms: preparation -0.15 ms at cfg4, same walks)
   int bdy_bpx = 512;     // k_bdy blocks per XCD at most (PMMG_HIP_BDYBPX)
@@ -222,8 +230,10 @@ struct pmmg_hip_ctx {
                                     // PMMG_HIP_BINBITS; auto mode: the coherence test picks)
   int bin_qs = 0;       // the binning copies the volume queries' coordinates in processing order (PMMG_HIP_BINQS=1;
                         // r03: -0.5 ms in the walk on a shuffled numbering, +1 ms in the binning)
-  int maxstep = 4096; // longer walks go to the exact continuation / exhaustive kernels (PMMG_HIP_MAXSTEP; the
-                      // reference caps at ne)
+  int maxstep = 1024; // longer walks go to the exhaustive kernels (PMMG_HIP_MAXSTEP; the reference caps at ne).
+                      // r05: 4096 -> 1024; a walk that long cycles along a concave boundary (carried cfg4
+                      // iteration: 2644 queries at the cap, all then accepted by the exhaustive search; the
+                      // longest legitimate walk seen is 302 steps, cfgG)
   int fanmax = kFanMax;    // cone fans longer than this take the O(nt) scan (test-only PMMG_HIP_FANMAX)
   int pad = 0;           // measurement build, PMMG_HIP_PAD: extra VALU / L1 work per walk step (k_vol)
   int xcd_run = 64;      // k_vol's blocks dealt to the XCDs in runs of 64 (4096 queries) instead of contiguous
@@ -612,11 +622,11 @@ static pmmg_hip_ctx *create_ctx(int device, int options, bool srf_prio, pmmg_hip
   c->bin_bits = std::min(7, env_int("PMMG_HIP_BINBITS", c->bin_bits));
   c->verbose = env_int("PMMG_HIP_VERBOSE", 0);
   c->maxstep = env_int("PMMG_HIP_MAXSTEP", c->maxstep);
-  c->group_lanes = std::min(8, env_int("PMMG_HIP_GROUP_LANES", c->group_lanes));
+  c->group_lanes = std::min(16, env_int("PMMG_HIP_GROUP_LANES", c->group_lanes));
   // test-only path selection (tests/test_gpu_hits.py, tests/test_gpu_parity.py)
   c->fanmax = env_int("PMMG_HIP_FANMAX", c->fanmax);
   c->srf_g = std::min(1024, env_int("PMMG_HIP_SRFG", 0));
-  c->pack_passes = env_int("PMMG_HIP_PACKPASS", c->pack_passes) == 2 ? 2 : 1; // packed records: gather passes
+  c->pack_passes = std::max(0, std::min(2, env_int("PMMG_HIP_PACKPASS", c->pack_passes))); // packed: gather passes
   c->bg.fanmax = c->fanmax; // every kernel's Bg copy carries it
   c->filter_steps = c->filter_steps < c->maxstep ? c->filter_steps : c->maxstep;
   if (const char *e = getenv("PMMG_HIP_FILTER_STEPS"))
@@ -658,7 +668,8 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   DevBuf *bufs[] = {&c->o_xyz, &c->o_tetv, &c->o_adja, &c->o_triv, &c->o_adjt, &c->o_met, &c->o_rec, &c->frame,
                     &c->stats, &c->grid, &c->sgrid, &c->order_v,
                     &c->order_b, &c->cont, &c->xq, &c->qs, &c->axh, &c->bkeys, &c->bkeys2, &c->bvals, &c->bvals2, &c->rs_hist, &c->rs_csum, &c->oflag, &c->cls_cnt, &c->qmin, &c->fb_vol, &c->fb_bdy,
-                    &c->best, &c->nac, &c->cres, &c->bbest, &c->bnac, &c->bcres, &c->fbp_vol, &c->fbp_bdy, &c->h_xyz,
+                    &c->best, &c->nac, &c->cres, &c->bbest, &c->bnac, &c->bcres, &c->fbp_vol, &c->fbp_bdy, &c->fbg_vol_c,
+                    &c->fbg_vol_u, &c->fbg_vol_i, &c->fbg_bdy_c, &c->fbg_bdy_u, &c->fbg_bdy_i, &c->h_xyz,
                     &c->h_cls, &c->h_met, &c->h_elem, &c->h_hit, &c->brk_k, &c->brk_k2, &c->brk_v, &c->brk_v2,
                     &c->brk_vinv, &c->brk_tinv, &c->brk_xq, &c->brk_xyz, &c->brk_sol, &c->brk_rec, &c->brk_tmp};
   for (DevBuf *b : bufs) release(*b);
@@ -1204,9 +1215,13 @@ static void launch_vol_fallbacks(pmmg_hip_ctx *c, const Slots &S, const double *
   hipStream_t s = c->stream;
   DevStats *st = (DevStats *)c->stats.p;
   const int *fb = (const int *)c->fb_vol.p;
-  hipLaunchKernelGGL(k_vol_exhaust_accept, dim3(kFbGridVol), dim3(kBlock), 0, s, bg, xyz_new, fb, st,
-                     (int *)c->best.p, (int *)c->nac.p, S, elem_out, hit_out);
-  hipLaunchKernelGGL(k_vol_exhaust_closest, dim3(kFbGridVol), dim3(kBlock), 0, s, bg, xyz_new, fb, st,
+  // grids sized by the background (a small group's empty fallback launches cost their dispatch: r04l, cfg2,
+  // ~4 us each at 1024 blocks)
+  const int gv = (int)std::min<long long>(kFbGridVol, std::max<long long>(64, bg.ne / 16384)) & ~7;
+  hipLaunchKernelGGL(k_vol_exhaust_accept, dim3(gv), dim3(kBlock), 0, s, bg, xyz_new, fb, st,
+                     (int *)c->best.p, (int *)c->nac.p, (const int *)c->fbg_vol_c.p, (const int *)c->fbg_vol_i.p, S,
+                     elem_out, hit_out);
+  hipLaunchKernelGGL(k_vol_exhaust_closest, dim3(gv), dim3(kBlock), 0, s, bg, xyz_new, fb, st,
                      (const int *)c->nac.p, (FbPart *)c->fbp_vol.p, (int *)c->cres.p, S, elem_out, hit_out);
 }
 
@@ -1215,9 +1230,11 @@ static void launch_bdy_fallbacks(pmmg_hip_ctx *c, hipStream_t s, const Slots &S,
   const Bg &bg = c->bg;
   DevStats *st = (DevStats *)c->stats.p;
   const int *fb = (const int *)c->fb_bdy.p;
-  hipLaunchKernelGGL(k_bdy_exhaust_accept, dim3(kFbGridBdy), dim3(kBlock), 0, s, bg, xyz_new, fb, st,
-                     (int *)c->bbest.p, (int *)c->bnac.p, S, elem_out, hit_out);
-  hipLaunchKernelGGL(k_bdy_exhaust_closest, dim3(kFbGridBdy), dim3(kBlock), 0, s, bg, xyz_new, fb, st,
+  const int gb = (int)std::min<long long>(kFbGridBdy, std::max<long long>(32, bg.nt / 4096)) & ~7;
+  hipLaunchKernelGGL(k_bdy_exhaust_accept, dim3(gb), dim3(kBlock), 0, s, bg, xyz_new, fb, st,
+                     (int *)c->bbest.p, (int *)c->bnac.p, (const int *)c->fbg_bdy_c.p, (const int *)c->fbg_bdy_i.p, S,
+                     elem_out, hit_out);
+  hipLaunchKernelGGL(k_bdy_exhaust_closest, dim3(gb), dim3(kBlock), 0, s, bg, xyz_new, fb, st,
                      (const int *)c->bnac.p, (FbPart *)c->fbp_bdy.p, (int *)c->bcres.p, S, elem_out, hit_out);
 }
 
@@ -1277,7 +1294,7 @@ static int brick_renumber(pmmg_hip_ctx *c, hipStream_t s, const Bg &bg, const Sl
 // on the coherence test's flag on the device (r04), and every fallback kernel
 // reads its list's count on the device.
 static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const uint8_t *pclass, double *met_out,
-                      double *const *fields_out, int *elem_out, int8_t *hit_out) {
+                      double *const *fields_out, int *elem_out, int8_t *hit_out, double *rec_out = nullptr) {
   Bg bg = c->bg;
   hipStream_t s = c->stream, sb = c->stream2;
   // Measurement build (PMMG_HIP_SRFPRIO=1): a large call runs its second
@@ -1301,19 +1318,23 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   Slots S{};
   S.n = 0;
   S.has_met = c->met_size ? 1 : 0;
+  if (rec_out && !c->rec) {
+    set_err(c, "locate_interp_rec: output records need packed input records (pmmg_hip_set_solutions_packed)");
+    return 0;
+  }
   if (c->met_size) {
-    if (!met_out) {
+    if (!met_out && !rec_out) {
       set_err(c, "locate_interp: met_out is NULL");
       return 0;
     }
-    S.s[S.n++] = Slot{c->met, met_out, c->met_size, c->met_size};
+    S.s[S.n++] = Slot{c->met, met_out, c->met_size, c->met_size, c->met_size};
   }
   for (int j = 0; j < c->nfield; j++) {
-    if (!fields_out || !fields_out[j]) {
+    if (!rec_out && (!fields_out || !fields_out[j])) {
       set_err(c, "locate_interp: fields_out[%d] is NULL", j);
       return 0;
     }
-    S.s[S.n++] = Slot{c->fin[j], fields_out[j], c->fsize[j], c->fsize[j]};
+    S.s[S.n++] = Slot{c->fin[j], rec_out ? nullptr : fields_out[j], c->fsize[j], c->fsize[j], c->fsize[j]};
   }
   if (c->rec) { // packed records: every slot reads its columns of the record
     S.rec = c->rec;
@@ -1321,8 +1342,13 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     for (int j = 0; j < S.n; j++) {
       S.s[j].in = c->rec + off;
       S.s[j].istride = c->rstride;
+      if (rec_out) { // and writes its columns of the new point's output record
+        S.s[j].out = rec_out + off;
+        S.s[j].ostride = c->rstride;
+      }
       off += S.s[j].code;
     }
+    S.rec_out = rec_out;
   }
   const VolFn vol_fn = pick_layout(S, c->pack_passes);
   if (!vol_fn) {
@@ -1344,7 +1370,10 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
       !ensure(c, c->nac, 4 * nq) || !ensure(c, c->cres, 4 * nq) || !ensure(c, c->bbest, 4 * nq) ||
       !ensure(c, c->bnac, 4 * nq) || !ensure(c, c->bcres, 4 * nq) ||
       !ensure(c, c->fbp_vol, sizeof(FbPart) * (size_t)kFbPartCap) ||
-      !ensure(c, c->fbp_bdy, sizeof(FbPart) * 256 * (size_t)kFbGridBdy))
+      !ensure(c, c->fbp_bdy, sizeof(FbPart) * 256 * (size_t)kFbGridBdy) ||
+      !ensure(c, c->fbg_vol_c, 4 * (size_t)(kFbCells + 1)) || !ensure(c, c->fbg_vol_u, 4 * (size_t)kFbCells) ||
+      !ensure(c, c->fbg_vol_i, 4 * nq) || !ensure(c, c->fbg_bdy_c, 4 * (size_t)(kFbCells + 1)) ||
+      !ensure(c, c->fbg_bdy_u, 4 * (size_t)kFbCells) || !ensure(c, c->fbg_bdy_i, 4 * nq))
     return 0;
   if (!ensure(c, c->xq, sizeof(int) * kXqStride * (size_t)bg.np) || !ensure(c, c->oflag, 2 * sizeof(int)) ||
       !ensure(c, c->axh, sizeof(int) * 3 * kMapBins * (size_t)kHistBlocks))
@@ -1381,8 +1410,9 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   // the second stream needs the frame only (lo, inv_bin, inv_srf), not the
   // axis maps (r04: EV_FRAME moved here from after k_axis_map)
   HIPCK(c, hipEventRecord(c->ev[EV_FRAME], s));
-  hipLaunchKernelGGL(k_axis_hist, dim3(kHistBlocks), dim3(kBlock), 0, s, bg.xyz, bg.np, (const Frame *)fr,
-                     c->hist_stride, (int *)c->axh.p);
+  // fixed-point vertex copy + the axis histograms (first kHistBlocks blocks), then the axis maps
+  hipLaunchKernelGGL(k_quantize, dim3(std::max(kHistBlocks, blocks_for(3LL * bg.np, 8192))), dim3(kBlock), 0, s,
+                     bg.xyz, (long long)bg.np, (const Frame *)fr, (int *)c->xq.p, c->hist_stride, (int *)c->axh.p);
   hipLaunchKernelGGL(k_axis_map, dim3(3), dim3(kBlock), 0, s, (const int *)c->axh.p, fr, g);
   HIPCK(c, hipGetLastError());
 
@@ -1393,9 +1423,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_FRAME], 0));
   HIPCK(c, hipGetLastError());
 
-  // ---- seed grid (main stream): fixed-point vertex copy, volume seeds
-  hipLaunchKernelGGL(k_quantize, dim3(blocks_for(3LL * bg.np, 8192)), dim3(kBlock), 0, s, bg.xyz, (long long)bg.np,
-                     (const Frame *)fr, (int *)c->xq.p);
+  // ---- seed grid (main stream): volume seeds
   {
     const long long nsamp = ng < bg.ne ? ng : bg.ne;
     hipLaunchKernelGGL(k_seed_vol, dim3((blocks_for(nsamp, 8192) + 7) & ~7), dim3(kBlock), 0, s, bg, fr, grid, g,
@@ -1467,8 +1495,8 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     // second, nearly empty round doubled the surface branch alone)
     hipLaunchKernelGGL(k_bdy, dim3(8 * blocks_for((np_new + 7) / 8, c->bdy_bpx)), dim3(kBlock), 0, sb, bg,
                        (const Frame *)fr, (const int *)sgrid, gs, xyz_new, (const int *)order_b, S, elem_out, hit_out,
-                       (int *)c->fb_bdy.p, st, c->maxstep, c->bdy_dyn,
-                       FbInit{(int *)c->bbest.p});
+                       (int *)c->fb_bdy.p, st, c->maxstep, c->bdy_dyn, FbInit{(int *)c->bbest.p},
+                       FbGridBufs{(int *)c->fbg_bdy_c.p, (int *)c->fbg_bdy_u.p, (int *)c->fbg_bdy_i.p});
     launch_bdy_fallbacks(c, sb, S, xyz_new, elem_out, hit_out);
     HIPCK(c, hipGetLastError());
     if (nsg >= kRefillCells) { // the surface grid refilled for the next call (see k_reset above)
@@ -1493,9 +1521,11 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
                      (ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->filter_steps, flag, c->xcd_run,
                      c->pad);
   HIPCK(c, hipEventRecord(c->ev[EV_WALK], s));
-  hipLaunchKernelGGL(k_vol_walk_exact, dim3(8 * 64), dim3(64), 0, s, bg, xyz_new, (int *)c->fb_vol.p,
-                     (const ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->maxstep,
-                     FbInit{(int *)c->best.p});
+  // (8 x 64 one-wave blocks for a large call; fewer for a small group, whose continuations are a few hundred)
+  const int wx = (int)std::min<long long>(64, std::max<long long>(2, (long long)np_new / 65536));
+  hipLaunchKernelGGL(k_vol_walk_exact, dim3(8 * wx), dim3(64), 0, s, bg, xyz_new, (int *)c->fb_vol.p,
+                     (const ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->maxstep, FbInit{(int *)c->best.p},
+                     FbGridBufs{(int *)c->fbg_vol_c.p, (int *)c->fbg_vol_u.p, (int *)c->fbg_vol_i.p});
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[EV_VOL], s));
   // ---- exhaustive fallbacks of the volume queries (lists and counts on the
@@ -1679,6 +1709,36 @@ int pmmg_hip_locate_interp(pmmg_hip_ctx *c, int np_new, const double *xyz_new, c
   c->last_host_met = c->met_size;
   c->last_host_fsize = c->fsize;
   if (stats) return collect_stats(c, stats);
+  return 1;
+}
+
+int pmmg_hip_locate_interp_rec(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const uint8_t *pclass,
+                               double *rec_out, int *elem_out, int8_t *hit_out, pmmg_hip_stats *stats, int where) {
+  if (!c) return 0;
+  HIPCK(c, hipSetDevice(c->device));
+  if (!snap_join(c)) return 0;
+  if (where != PMMG_HIP_DEVICE) {
+    set_err(c, "locate_interp_rec: device pointers only (PMMG_HIP_DEVICE)");
+    return 0;
+  }
+  if (c->bg.ne <= 0) {
+    set_err(c, "locate_interp_rec: no background set");
+    return 0;
+  }
+  if (!c->rec) {
+    set_err(c, "locate_interp_rec: output records need packed input records (pmmg_hip_set_solutions_packed)");
+    return 0;
+  }
+  if (np_new <= 0) {
+    if (stats) memset(stats, 0, sizeof(*stats));
+    return 1;
+  }
+  if (!xyz_new || !pclass || !rec_out || ((uintptr_t)rec_out & 15)) {
+    set_err(c, "locate_interp_rec: xyz_new / pclass / rec_out NULL or rec_out not 16-byte aligned");
+    return 0;
+  }
+  if (!run_device(c, np_new, xyz_new, pclass, nullptr, nullptr, elem_out, hit_out, rec_out)) return 0;
+  if (stats) return pmmg_hip_sync(c, stats);
   return 1;
 }
 

@@ -26,6 +26,12 @@ struct DevStats {
   int pad;
   int bdy_next[8];      // k_bdy: per-XCD work counters (the next unclaimed surface query of each eighth)
   int nac_vol, nac_bdy; // fallback queries no element accepted (the closest searches' lists)
+  // uniform grids over each fallback list's queries (fb_grid_build): origin,
+  // inverse cell size, cells per axis (0: not built)
+  double fbg_lo[2][3], fbg_inv[2][3];
+  int fbg_n[2];
+  unsigned walk_done;   // k_vol_walk_exact blocks done (its last block builds the volume list's grid)
+  unsigned bdy_done;    // k_bdy blocks done (the surface list's grid)
   unsigned fb_done[4];  // blocks done with an exhaustive kernel (volume accept / closest, surface accept /
                         // closest): the last one finishes
 };
@@ -168,14 +174,50 @@ __device__ __forceinline__ int quant(double x, const Frame *fr, int d) {
   return __double2int_rn(t);
 }
 
+// the seed grid axis maps' input: the per-axis histogram of np / stride
+// background vertices at pseudo-random positions (splitmix64 of the sample
+// index: a strided sample aliases with a lattice numbering's row length —
+// cfg5's halo shard put 14 % of an every-256th sample on its x = 0 plane and
+// mapped a uniform axis); vertices outside the (sampled) frame are left out,
+// not clamped into the edge bins.  Block b < kHistBlocks's share, counted in
+// its LDS histogram h and flushed to H[b][d][bin] (no atomics outside LDS)
+__device__ __forceinline__ void axis_hist_block(int (*h)[kMapBins], const double *xyz, long long np, const Frame *fr,
+                                                int stride, int *H) {
+  for (int j = threadIdx.x; j < 3 * kMapBins; j += kBlock) (&h[0][0])[j] = 0;
+  __syncthreads();
+  const long long ns = (np + stride - 1) / stride;
+  for (long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x; j < ns; j += (long long)kHistBlocks * blockDim.x) {
+    unsigned long long z = (unsigned long long)j * 0x9E3779B97F4A7C15ULL + 0x5EED2025ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    z ^= z >> 31;
+    const long long i = (long long)(z % (unsigned long long)np);
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+      const double e = fr->ext[d];
+      const double b = e > 0.0 ? (xyz[3 * i + d] - fr->lo[d]) * ((double)kMapBins / e) : 0.0;
+      if (b >= 0.0 && b < (double)kMapBins) atomicAdd(&h[d][(int)b], 1);
+    }
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < 3 * kMapBins; j += kBlock) H[(size_t)blockIdx.x * 3 * kMapBins + j] = (&h[0][0])[j];
+}
+
 // The fixed-point copy is an elementwise map of the coordinate stream: with
 // 3 ints per row, xq[e] = quant(xyz[e], axis e % 3) for every double e, so
 // the kernel streams pairs of doubles in (one 16-byte load per lane, every
 // wave-instruction one contiguous KiB) and pairs of ints out (8 bytes per
 // lane, 512 contiguous bytes), kQuantU pairs in flight per lane.  (r04: two
 // whole vertices per lane, 48-byte strided pieces: 175 us at cfg4, 3.5 TB/s.)
+// The seed grid's axis histograms (one sample of np / hstride vertices, see
+// axis_hist_block) are taken by the first kHistBlocks blocks of the same
+// launch: both need only the frame (r05: one launch and its gap less per call;
+// the grid is at least kHistBlocks blocks).
 constexpr int kQuantU = 4;
-__global__ __launch_bounds__(kBlock) void k_quantize(const double *xyz, long long np, const Frame *fr, int *xq) {
+__global__ __launch_bounds__(kBlock) void k_quantize(const double *xyz, long long np, const Frame *fr, int *xq,
+                                                     int hstride, int *H) {
+  __shared__ int h[3][kMapBins];
+  if (blockIdx.x < kHistBlocks) axis_hist_block(h, xyz, np, fr, hstride, H); // (block-uniform)
   const long long nth = (long long)gridDim.x * blockDim.x;
   if (kXqStride == 3 && ((uintptr_t)xyz & 15) == 0 && ((uintptr_t)xq & 7) == 0) {
     const double qs = fr->qs, qc0 = fr->qc[0], qc1 = fr->qc[1], qc2 = fr->qc[2];
@@ -632,34 +674,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_top(int *bsum, int nb, int *tot
 
 // ---------------------------------------------------------------- seed grid axis maps
 
-// the per-axis histogram of np / stride background vertices at
-// pseudo-random positions (splitmix64 of the sample index: a strided sample
-// aliases with a lattice numbering's row length — cfg5's halo shard put 14 %
-// of an every-256th sample on its x = 0 plane and mapped a uniform axis);
-// vertices outside the (sampled) frame are left out, not clamped into the
-// edge bins.  H[block][d][bin] (kHistBlocks blocks, no atomics outside LDS)
-__global__ __launch_bounds__(kBlock) void k_axis_hist(const double *xyz, int np, const Frame *fr, int stride, int *H) {
-  __shared__ int h[3][kMapBins];
-  for (int j = threadIdx.x; j < 3 * kMapBins; j += kBlock) (&h[0][0])[j] = 0;
-  __syncthreads();
-  const long long ns = ((long long)np + stride - 1) / stride;
-  for (long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x; j < ns; j += (long long)gridDim.x * blockDim.x) {
-    unsigned long long z = (unsigned long long)j * 0x9E3779B97F4A7C15ULL + 0x5EED2025ULL;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
-    z ^= z >> 31;
-    const long long i = (long long)(z % (unsigned long long)np);
-#pragma unroll
-    for (int d = 0; d < 3; d++) {
-      const double e = fr->ext[d];
-      const double b = e > 0.0 ? (xyz[3 * i + d] - fr->lo[d]) * ((double)kMapBins / e) : 0.0;
-      if (b >= 0.0 && b < (double)kMapBins) atomicAdd(&h[d][(int)b], 1);
-    }
-  }
-  __syncthreads();
-  for (int j = threadIdx.x; j < 3 * kMapBins; j += kBlock) H[(size_t)blockIdx.x * 3 * kMapBins + j] = (&h[0][0])[j];
-}
-
+// (the histograms: axis_hist_block, inside k_quantize)
 // one block per axis: counts -> quantile map, adaptive bit.  The test is on
 // the scale of the grid's cells: the heaviest window of kMapBins / g bins
 // (one uniform cell's slab) against the mean slab, g * max / total.  Bins
@@ -961,5 +976,195 @@ __global__ __launch_bounds__(kBlock) void k_cls_scatter(const uint8_t *pclass, l
     out[pos++] = (int)(i0 + j + 1);
   }
 }
+
+// ---------------------------------------------------------------- exhaustive-search helpers
+// (pmmg_fallback.hpp; the grids are built by the last blocks of k_vol_walk_exact and k_bdy)
+
+// the last block of a grid to pass this point (after its device-scope
+// atomics) gets true: the other blocks' results are then visible to it.  The
+// barrier before the ticket: every wave of the block has issued its atomics
+// (r04l: without it a block's later waves could still be scanning when the
+// last block read the results — 4 surface points left unprocessed, once)
+__device__ __forceinline__ bool last_block(unsigned *done) {
+  __threadfence();
+  __syncthreads();
+  __shared__ bool last;
+  if (threadIdx.x == 0) last = atomicAdd(done, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (last) __threadfence();
+  return last;
+}
+
+__device__ __forceinline__ int load_agent(const int *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The bounding box of an element inflated so that every point its
+// acceptance test can pass lies inside.  Volume: every barycentric
+// coordinate > -EPS puts x within 3 EPS of the extent outside the vertices'
+// box (x_c = sum_i b_i p_ic, sum_i b_i = 1); the pad is 1e-4 of the extent
+// (33x that, room for the coordinates' rounding on any element with an
+// aspect ratio below ~1e10) plus 1e-12 of the coordinates' magnitude.
+// Surface: the projection is inside the tria within the same margin and
+// |dist| <= hausd along the unit normal.  A degenerate element (zero or
+// non-finite volume / area) gets an infinite box: every query takes the
+// reference's test there, as in the oracle.
+constexpr double kBoxRel = 1e-4, kBoxAbs = 1e-12;
+struct Box {
+  double lo[3], hi[3];
+};
+__device__ __forceinline__ bool in_box(const Box &b, const double *x) {
+  // NaN coordinates compare false everywhere and fall through to the test
+  return !(x[0] < b.lo[0] || x[0] > b.hi[0] || x[1] < b.lo[1] || x[1] > b.hi[1] || x[2] < b.lo[2] ||
+           x[2] > b.hi[2]);
+}
+template <int NV>
+__device__ __forceinline__ Box elem_box(const double (*p)[3], double extra, bool degenerate) {
+  Box b;
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    double lo = p[0][c], hi = p[0][c];
+#pragma unroll
+    for (int v = 1; v < NV; v++) {
+      lo = fmin(lo, p[v][c]);
+      hi = fmax(hi, p[v][c]);
+    }
+    const double pad = kBoxRel * (hi - lo) + kBoxAbs * fmax(fabs(lo), fabs(hi)) + extra + 1e-300;
+    b.lo[c] = degenerate ? -INFINITY : lo - pad;
+    b.hi[c] = degenerate ? INFINITY : hi + pad;
+  }
+  return b;
+}
+
+// ---------------------------------------------------------------- query grids
+//
+// The accept scans test an element only against the fallback queries in the
+// grid cells its inflated box covers (r05: against every query of the list,
+// the scan cost ne x nfb box tests — 92 ms for 2644 queries over 120M tetra
+// in a carried iteration).  The grid is built by the last block of the kernel
+// that finishes the list (k_vol_walk_exact, k_bdy): G^3 cells over the
+// queries' box, G = cbrt(nfb / 4) + 1 <= kFbGridMax; cells[c] .. cells[c + 1]
+// index items[], the list positions of cell c's queries.  A query inside an
+// element's box is in a cell of the box's (clamped) cell range, so the pairs
+// tested are a superset of the accepting pairs: the same results as the full
+// scan.
+constexpr int kFbGridMax = 16;
+constexpr int kFbCells = kFbGridMax * kFbGridMax * kFbGridMax;
+struct FbGridBufs {
+  int *cells; // kFbCells + 1 starts
+  int *cur;   // kFbCells scratch
+  int *items; // one per list entry
+};
+
+__device__ __forceinline__ int fb_cell1(double x, double lo, double inv, int G) {
+  const double t = (x - lo) * inv;
+  return t > 0.0 ? (t < (double)G ? (int)t : G - 1) : 0; // NaN -> 0, +inf -> G - 1
+}
+
+// one block: the grid of the list fb[0, nfb) (cls 0 volume, 1 surface);
+// cells[kFbCells + 1] starts, cur[kFbCells] scratch, items[nfb]
+__device__ __noinline__ void fb_grid_build(const double *qxyz, const int *fb, int nfb, DevStats *st, int cls,
+                                           int *cells, int *cur, int *items) {
+  __shared__ double rlo[3][kBlock / 64], rhi[3][kBlock / 64]; // per-wave partial boxes
+  __shared__ int sG;
+  const int t = threadIdx.x, nt = blockDim.x, w = t >> 6, nw = (nt + 63) >> 6;
+  double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int j = t; j < nfb; j += nt) {
+    double x[3];
+    load_pt(qxyz, fb[j], x);
+    for (int d = 0; d < 3; d++) {
+      lo[d] = fmin(lo[d], x[d]);
+      hi[d] = fmax(hi[d], x[d]);
+    }
+  }
+  for (int d = 0; d < 3; d++)
+    for (int o = 32; o > 0; o >>= 1) {
+      lo[d] = fmin(lo[d], __shfl_xor(lo[d], o));
+      hi[d] = fmax(hi[d], __shfl_xor(hi[d], o));
+    }
+  if (__lane_id() == 0)
+    for (int d = 0; d < 3; d++) {
+      rlo[d][w] = lo[d];
+      rhi[d][w] = hi[d];
+    }
+  __syncthreads();
+  if (t == 0) {
+    for (int d = 0; d < 3; d++) {
+      double a = INFINITY, b = -INFINITY;
+      for (int i = 0; i < nw; i++) {
+        a = fmin(a, rlo[d][i]);
+        b = fmax(b, rhi[d][i]);
+      }
+      rlo[d][0] = a;
+      rhi[d][0] = b;
+    }
+    int G = (int)cbrt((double)nfb / 4.0) + 1;
+    G = G < 1 ? 1 : (G > kFbGridMax ? kFbGridMax : G);
+    for (int d = 0; d < 3; d++) {
+      const double e = rhi[d][0] - rlo[d][0];
+      st->fbg_lo[cls][d] = rlo[d][0];
+      st->fbg_inv[cls][d] = e > 0.0 ? (double)G / e : 0.0;
+    }
+    st->fbg_n[cls] = G;
+    sG = G;
+  }
+  __syncthreads();
+  const int G = sG, nc = G * G * G;
+  const double l0 = st->fbg_lo[cls][0], l1 = st->fbg_lo[cls][1], l2 = st->fbg_lo[cls][2];
+  const double i0 = st->fbg_inv[cls][0], i1 = st->fbg_inv[cls][1], i2 = st->fbg_inv[cls][2];
+  for (int c = t; c < nc; c += nt) cur[c] = 0;
+  __syncthreads();
+  for (int j = t; j < nfb; j += nt) {
+    double x[3];
+    load_pt(qxyz, fb[j], x);
+    const int c = fb_cell1(x[0], l0, i0, G) + G * (fb_cell1(x[1], l1, i1, G) + G * fb_cell1(x[2], l2, i2, G));
+    atomicAdd(&cur[c], 1);
+  }
+  __threadfence_block();
+  __syncthreads();
+  if (t == 0) { // exclusive scan (at most kFbCells entries, once per call with fallbacks)
+    int acc = 0;
+    for (int c = 0; c < nc; c++) {
+      const int v = cur[c];
+      cells[c] = acc;
+      cur[c] = acc;
+      acc += v;
+    }
+    cells[nc] = acc;
+  }
+  __threadfence_block();
+  __syncthreads();
+  for (int j = t; j < nfb; j += nt) {
+    double x[3];
+    load_pt(qxyz, fb[j], x);
+    const int c = fb_cell1(x[0], l0, i0, G) + G * (fb_cell1(x[1], l1, i1, G) + G * fb_cell1(x[2], l2, i2, G));
+    items[atomicAdd(&cur[c], 1)] = j;
+  }
+}
+
+// the queries of the cells an element's (inflated) box covers: visit(j) for
+// each list position j (the accept test itself); nothing when the box misses
+// the grid's box
+template <class F>
+__device__ __forceinline__ void fb_grid_visit(const DevStats *st, int cls, const int *cells, const int *items,
+                                              const Box &b, F &&visit) {
+  const int G = st->fbg_n[cls];
+  int a[3], e[3];
+  for (int d = 0; d < 3; d++) {
+    const double lo = st->fbg_lo[cls][d], inv = st->fbg_inv[cls][d];
+    const double hi = inv > 0.0 ? lo + (double)G / inv : lo;
+    if (b.hi[d] < lo || b.lo[d] > hi) return; // (NaN boxes: degenerate elements have infinite ones)
+    a[d] = fb_cell1(b.lo[d], lo, inv, G);
+    e[d] = fb_cell1(b.hi[d], lo, inv, G);
+  }
+  for (int z = a[2]; z <= e[2]; z++)
+    for (int y = a[1]; y <= e[1]; y++)
+      for (int x = a[0]; x <= e[0]; x++) {
+        const int c = x + G * (y + G * z);
+        for (int q = cells[c]; q < cells[c + 1]; q++) visit(items[q]);
+      }
+}
+
+// ---------------------------------------------------------------- accept scans
 
 } // namespace pmmg

@@ -421,7 +421,7 @@ __device__ __forceinline__ int walk_exact(const Bg &bg, const double *x, int ip,
 // count is read on the device.
 __global__ __launch_bounds__(64) void k_vol_walk_exact(Bg bg, const double *qxyz, int *fb, const ContEntry *cont,
                                                        DevStats *st, Slots S, int *elem_out, int8_t *hit_out,
-                                                       int maxstep, FbInit fi) {
+                                                       int maxstep, FbInit fi, FbGridBufs gb) {
   __shared__ BlockStats bs;
   __shared__ double slot_img[12 * 64];
   const LaneSlotsD L{&slot_img[__lane_id()]};
@@ -461,6 +461,10 @@ __global__ __launch_bounds__(64) void k_vol_walk_exact(Bg bg, const double *qxyz
   }
   __syncthreads();
   bstats_flush(&bs, st);
+  // the volume fallback list is complete: its query grid (fb_grid_build)
+  if (!last_block(&st->walk_done)) return;
+  const int nfb = load_agent(&st->nfb_vol);
+  if (nfb > 0) fb_grid_build(qxyz, fb, nfb, st, 0, gb.cells, gb.cur, gb.items);
 }
 
 // ---------------------------------------------------------------- interpolation
@@ -582,11 +586,16 @@ __device__ __forceinline__ void sink_rows(const Slot &sl, const double *r, bool 
 // an image of the wave's distinct vertices, sorted, for the exact test and the
 // interpolation: 20 % fewer L1 accesses, +23 % VALU for the sort, +10 % time;
 // profiles/r04b/unique_vertex_rows.patch.txt.)
+// (the image of the array layout holds 8 doubles per lane: 4.3 KB per block
+// where the packed records' 16 take 8.4 KB, which would hold a 6-wave layout
+// (80 VGPRs) to 19 blocks per CU)
+template <int PK>
 struct VolShared {
   BlockStats bs;
+  unsigned short okm[PK > 0 ? 64 : 1]; // output records: the doubles of each lane's record that are written (bit j)
   union {
     float slots[12 * 64]; // walk: the vertex slots [slot*3 + dim][lane]
-    double img[16 * 64]; // interpolation: 64 rows of up to 6 doubles, or 64 packed records of up to 16 doubles
+    double img[(PK > 0 ? 16 : 8) * 64]; // interpolation: 64 rows of up to 6 doubles, or 64 records of up to 16
   } u;
 };
 
@@ -803,18 +812,78 @@ __device__ __forceinline__ void packed_store(const Slot &sl, SlotAcc<C> &a, doub
   }
 }
 
+// Output records (pmmg_hip_locate_interp_rec): each finished slot's row goes
+// into an LDS image of the wave's 64 output records, in two halves of 8
+// doubles (half 0 = record doubles 0-7 at img + 512 doubles, half 1 = 8-15 at
+// img), each 4 swizzled 16-byte pieces per record; half 1 is written only
+// after the last gather pass, so that with two passes the first pass's slots
+// are staged while the second pass gathers into img[0, 512).  Then the wave
+// stores whole records (kOutRecPieces pieces of 16 bytes each), one line per
+// 16-double record and instruction-covered records whole, in input order or
+// to each query's own record (Morton order).  okm: the doubles each lane
+// writes (a failed MMG5_invmat leaves its slot's doubles untouched).
+__device__ __forceinline__ double *rec_half(double *img, int h) { return h == 0 ? img + 512 : img; }
+__device__ __forceinline__ void rec_put(double *img, int lane, int j, double x) {
+  double *reg = rec_half(img, j >> 3);
+  const int jj = j & 7;
+  reg[2 * packed_pos<4>(lane, jj >> 1) + (jj & 1)] = x;
+}
+
+template <class L, int S, int C>
+__device__ __forceinline__ void packed_stage(SlotAcc<C> &a, bool act, double *img, unsigned short *okm) {
+  if constexpr (C > 0) {
+    constexpr int o = L::off(S);
+    const int lane = __lane_id();
+    double r[C];
+    bool ok = a.ok && act;
+    if constexpr (C == 6) ok = invmat(a.v, r) && ok;
+    else
+#pragma unroll
+      for (int q = 0; q < C; q++) r[q] = a.v[q];
+#pragma unroll
+    for (int q = 0; q < C; q++) rec_put(img, lane, o + q, r[q]);
+    if (ok) okm[lane] |= (unsigned short)(((1u << C) - 1u) << o);
+  }
+}
+
 // slot S is finished (stored) after the pass holding its last component
 template <class L, int NP, int S, int C>
-__device__ __forceinline__ void packed_finish(const Slots &Sl, SlotAcc<C> &a, int pass, double *img, const Sink &k) {
+__device__ __forceinline__ void packed_finish(const Slots &Sl, SlotAcc<C> &a, int pass, double *img, const Sink &k,
+                                              bool act, unsigned short *okm) {
   if constexpr (C > 0) {
     constexpr int PW = L::RS / NP;
-    if (pass == (L::off(S) + C - 1) / PW) packed_store<C>(Sl.s[S], a, img, k);
+    if (pass != (L::off(S) + C - 1) / PW) return;
+    if (Sl.rec_out) packed_stage<L, S, C>(a, act, img, okm);
+    else packed_store<C>(Sl.s[S], a, img, k);
+  }
+}
+
+// the wave's staged output records to memory (see rec_half)
+template <int RS>
+__device__ __forceinline__ void rec_flush(double *out, const double *img, const unsigned short *okm, const Sink &k) {
+  constexpr int PR = RS / 2; // 16-byte pieces per record
+  const int lane = __lane_id();
+#pragma unroll
+  for (int t = 0; t < PR; t++) {
+    const int p = 64 * t + lane, r = p / PR, kk = p - PR * r;
+    const int dst = __shfl(k.ip, r);
+    const unsigned m = (okm[r] >> (2 * kk)) & 3u;
+    const double *reg = rec_half(const_cast<double *>(img), kk >> 2);
+    const double2 v = reinterpret_cast<const double2 *>(reg)[packed_pos<4>(r, kk & 3)];
+    double *q = out + (size_t)RS * (k.coalesced ? k.w0 + (size_t)r : (size_t)(dst - 1)) + 2 * kk;
+    if (m == 3u) {
+      if (k.coalesced) nt_store2(q, v.x, v.y);
+      else *reinterpret_cast<double2 *>(q) = v;
+    } else {
+      if (m & 1u) q[0] = v.x;
+      if (m & 2u) q[1] = v.y;
+    }
   }
 }
 
 template <int NP, int C0, int C1, int C2, int C3, int C4, int C5>
 __device__ __forceinline__ void vol_interp_packed(const Slots &S, bool acc, const VolLoc &loc, double *img,
-                                                  const Sink &k) {
+                                                  const Sink &k, unsigned short *okm) {
   using L = PackedLayout<C0, C1, C2, C3, C4, C5>;
   constexpr int PW = L::RS / NP, PP = PW / 2; // doubles / 16-byte pieces per record and pass
   const int lane = __lane_id();
@@ -829,6 +898,7 @@ __device__ __forceinline__ void vol_interp_packed(const Slots &S, bool acc, cons
   }
   const double2 *rec = reinterpret_cast<const double2 *>(S.rec);
   double2 *img2 = reinterpret_cast<double2 *>(img);
+  if (S.rec_out) okm[lane] = 0;
 #pragma unroll
   for (int pass = 0; pass < NP; pass++) {
     // the vertex loop is not unrolled: unrolled, the four vertices' copies of
@@ -838,17 +908,25 @@ __device__ __forceinline__ void vol_interp_packed(const Slots &S, bool acc, cons
       const int myv = sel4(loc.v, i);
       const double ph = i == 0 ? loc.phi[0] : (i == 1 ? loc.phi[1] : (i == 2 ? loc.phi[2] : loc.phi[3]));
       // piece p = 64t + lane of the wave's records: record p / PP, piece p % PP
-      double2 b[PP];
+      // (every load instruction covers whole records: one line access per
+      // record).  In batches of at most 4 instructions, each landed in LDS
+      // before the next is issued: 16 VGPRs of loads in flight instead of 32
+      constexpr int TB = PP < 4 ? PP : 4;
 #pragma unroll
-      for (int t = 0; t < PP; t++) {
-        const int p = 64 * t + lane, r = p / PP, kk = p - PP * r;
-        const int v = __shfl(myv, r);
-        b[t] = rec[(size_t)(L::RS / 2) * (v - 1) + PP * pass + kk];
-      }
+      for (int t0 = 0; t0 < PP; t0 += TB) {
+        double2 b[TB];
 #pragma unroll
-      for (int t = 0; t < PP; t++) {
-        const int p = 64 * t + lane, r = p / PP, kk = p - PP * r;
-        img2[packed_pos<PP>(r, kk)] = b[t];
+        for (int t = 0; t < TB; t++) {
+          const int p = 64 * (t0 + t) + lane, r = p / PP, kk = p - PP * r;
+          const int v = __shfl(myv, r);
+          b[t] = rec[(size_t)(L::RS / 2) * (v - 1) + PP * pass + kk];
+        }
+#pragma unroll
+        for (int t = 0; t < TB; t++) {
+          const int p = 64 * (t0 + t) + lane, r = p / PP, kk = p - PP * r;
+          img2[packed_pos<PP>(r, kk)] = b[t];
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
       wait_lgkm();
       __builtin_amdgcn_wave_barrier();
@@ -864,12 +942,19 @@ __device__ __forceinline__ void vol_interp_packed(const Slots &S, bool acc, cons
       // hoists the four vertices' gathers together)
       __builtin_amdgcn_sched_barrier(0);
     }
-    packed_finish<L, NP, 0>(S, a0, pass, img, k);
-    packed_finish<L, NP, 1>(S, a1, pass, img, k);
-    packed_finish<L, NP, 2>(S, a2, pass, img, k);
-    packed_finish<L, NP, 3>(S, a3, pass, img, k);
-    packed_finish<L, NP, 4>(S, a4, pass, img, k);
-    packed_finish<L, NP, 5>(S, a5, pass, img, k);
+    packed_finish<L, NP, 0>(S, a0, pass, img, k, acc, okm);
+    packed_finish<L, NP, 1>(S, a1, pass, img, k, acc, okm);
+    packed_finish<L, NP, 2>(S, a2, pass, img, k, acc, okm);
+    packed_finish<L, NP, 3>(S, a3, pass, img, k, acc, okm);
+    packed_finish<L, NP, 4>(S, a4, pass, img, k, acc, okm);
+    packed_finish<L, NP, 5>(S, a5, pass, img, k, acc, okm);
+  }
+  if (S.rec_out) {
+    wait_lgkm();
+    __builtin_amdgcn_wave_barrier(); // every lane's record staged
+    rec_flush<L::RS>(S.rec_out, img, okm, k);
+    wait_lgkm();
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -880,7 +965,7 @@ __global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsign
                                             const double *qs, int np, ContEntry *cont, DevStats *st, Slots S,
                                             int *elem_out, int8_t *hit_out, int filter_steps,
                                             const int *order_flag, int xcd_run, int pad) {
-  __shared__ VolShared sh;
+  __shared__ VolShared<PK> sh;
   bstats_init(&sh.bs);
   __syncthreads();
   const LaneSlotsF L{(lds_float *)&sh.u.slots[__lane_id()]};
@@ -1016,7 +1101,7 @@ __global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsign
     double *img = sh.u.img;
     __builtin_amdgcn_wave_barrier(); // the walk's slots are dead: the buffer becomes the gather image
     if constexpr (PK > 0) {
-      vol_interp_packed<PK, C0, C1, C2, C3, C4, C5>(S, acc, loc, img, snk);
+      vol_interp_packed<PK, C0, C1, C2, C3, C4, C5>(S, acc, loc, img, snk, sh.okm);
     } else if constexpr (C0 < 0) {
       if (acc) {
         const int vv[4] = {loc.v.x, loc.v.y, loc.v.z, loc.v.w};

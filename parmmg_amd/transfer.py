@@ -232,6 +232,17 @@ class TransferContext:
                  "locate_interp")
         return st if (sync or where == HOST) else None
 
+    def locate_interp_rec(self, xyz_new, pclass, rec_out, elem_out=None, hit_out=None,
+                          sync: bool = True) -> HipStats | None:
+        """pmmg_hip_locate_interp_rec: device arrays; after set_solutions_packed,
+        the new points' values as records of the packed layout (rec_out
+        [np_new, RS])."""
+        st = HipStats()
+        self._ck(self.lib.pmmg_hip_locate_interp_rec(self.h, xyz_new.shape[0], _p(xyz_new), _p(pclass), _p(rec_out),
+                                                     _p(elem_out), _p(hit_out), ctypes.byref(st) if sync else None,
+                                                     DEVICE), "locate_interp_rec")
+        return st if sync else None
+
     def locate_interp_groups(self, groups, sync: bool = True) -> HipStats | None:
         """pmmg_hip_locate_interp_groups: many groups in one call, device
         arrays only.  Each group is a dict {xyz, tet8 | (tetv, adja), triv,

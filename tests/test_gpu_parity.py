@@ -34,11 +34,12 @@ def _packable(case):
 # (morton-fine: the fine binning cells auto mode picks for a numbering
 # without coherence)
 FINE = {"PMMG_HIP_BINBITS": "7"}
+ONEPASS = {"PMMG_HIP_PACKPASS": "1"}  # packed records in one gather pass (the default picks by record size)
 MODES = {"auto": {}, "morton": dict(sort=True), "nosort": dict(sort=False), "tet8": dict(tet8=True),
-         "tet8-morton": dict(tet8=True, sort=True), "packed": dict(tet8=True, packed=True),
-         "packed-morton": dict(tet8=True, packed=True, sort=True),
+         "tet8-morton": dict(tet8=True, sort=True), "packed": dict(tet8=True, packed=True, env=ONEPASS),
+         "packed-morton": dict(tet8=True, packed=True, sort=True, env=ONEPASS),
          "morton-fine": dict(sort=True, env=FINE), "packed-morton-fine": dict(tet8=True, packed=True, sort=True,
-                                                                              env=FINE),
+                                                                              env={**FINE, **ONEPASS}),
          # packed records gathered in two passes over the record halves (PMMG_HIP_PACKPASS=2)
          "packed2": dict(tet8=True, packed=True, env={"PMMG_HIP_PACKPASS": "2"}),
          "packed2-morton": dict(tet8=True, packed=True, sort=True, env={"PMMG_HIP_PACKPASS": "2"})}
@@ -191,7 +192,7 @@ def test_packed_records_bit_identical(name):
                      if CASES[name].get("metric", synth.F_ANI) == synth.F_ANI else CASES[name], with_ref=False)
     assert _packable(case)
     a = run_gpu(case, tet8=True)
-    for env in ({}, {"PMMG_HIP_PACKPASS": "2"}):  # one gather per record, or one per record half
+    for env in (ONEPASS, {"PMMG_HIP_PACKPASS": "2"}, {}):  # one gather per record, one per half, by size
         b = run_gpu(case, tet8=True, packed=True, env=env)
         np.testing.assert_array_equal(a["elem"], b["elem"])
         np.testing.assert_array_equal(a["hit"], b["hit"])

@@ -16,7 +16,10 @@ Steps:
                          within one pass's limits); table -> <tag>/pmc_*.txt
   trace ARGS             rocprofv3 --kernel-trace --stats of bench.py ARGS
                          (kernel_stats.csv copied to <tag>/)
+  tracepy ARGS           the same of python3 -u ARGS (a tools/ script); the
+                         kernel_trace.csv is copied too
   py ARGS                python3 -u ARGS (a tools/ script)
+A step may start with NAME=VALUE tokens: environment variables of that step.
 """
 from __future__ import annotations
 
@@ -30,7 +33,7 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIMITS = {"pytest": 900, "sweep": 900, "bench": 900, "pmc": 120, "trace": 900, "py": 600}
+LIMITS = {"pytest": 900, "sweep": 900, "bench": 900, "pmc": 120, "trace": 900, "tracepy": 600, "py": 600}
 
 
 def run(cmd: list[str], log: str, limit: int, kill_signal: str = "TERM") -> int:
@@ -66,6 +69,13 @@ def main() -> int:
     for step in a.steps:
         kind, _, rest = step.partition(" ")
         args = shlex.split(rest)
+        # leading NAME=VALUE tokens: environment of this step only
+        env = {}
+        while args and "=" in args[0] and args[0].split("=")[0].isidentifier() and args[0].split("=")[0].isupper():
+            k, v = args.pop(0).split("=", 1)
+            env[k] = v
+        saved = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
         i = counts.get(kind, 0)
         counts[kind] = i + 1
         name = f"{kind}{i if i else ''}"
@@ -97,15 +107,24 @@ def main() -> int:
                     f.write(f"# variant {variant!r}, counters {ctrs}\n")
                     f.flush()
                     subprocess.call([sys.executable, "tools/pmc_table.py", d, "k_"], stdout=f, cwd=ROOT)
-        elif kind == "trace":
+        elif kind in ("trace", "tracepy"):
             d = os.path.join(out, name)
+            prog = ["bench.py"] if kind == "trace" else []
             rc = run(["rocprofv3", "--kernel-trace", "--stats", "-d", d, "-o", "run", "--output-format", "csv", "--",
-                      sys.executable, "-u", "bench.py"] + args, log, LIMITS[kind])
+                      sys.executable, "-u"] + prog + args, log, LIMITS[kind])
             for p in glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True):
                 shutil.copy(p, os.path.join(out, f"{name}_kernel_stats.csv"))
+            if kind == "tracepy":
+                for p in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+                    shutil.copy(p, os.path.join(out, f"{name}_kernel_trace.csv"))
         else:
             print(f"[gpu_job] unknown step kind {kind!r}", flush=True)
             return 2
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
         tail(log)
         if rc != 0:
             print(f"[gpu_job] step {name} failed (rc={rc}); stopping", flush=True)

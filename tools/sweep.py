@@ -82,7 +82,8 @@ def main():
             k, v = item.split("=")
             if k.lower() == "sort":  # context option: 1 Morton bins, 0 input order
                 sort = v == "1"
-            elif k.lower() in ("sol", "perm", "packed", "so"):  # measurement only: slots / renumbering / packed records / build
+            elif k.lower() in ("sol", "perm", "packed", "so", "recout"):  # measurement only: slots / renumbering / packed
+                # records / build / output records (pmmg_hip_locate_interp_rec, with packed=1)
                 pass
             else:
                 os.environ["PMMG_HIP_" + k.upper()] = v
@@ -123,7 +124,12 @@ def main():
                 else:
                     ctx.set_solutions(*sols(spec))
                 q, qpc = qperm.get(spec, (d["q"], d["pc"]))
-                ctx.locate_interp(q, qpc, d["mo"], d["fo"], d["el"], d["hit"], sync=False)
+                if dict(item.split("=") for item in spec.split(",") if item).get("recout") == "1":
+                    if "ro" not in d:
+                        d["ro"] = base.empty((new.np, d["rec"].shape[1]), np.float64)
+                    ctx.locate_interp_rec(q, qpc, d["ro"], d["el"], d["hit"], sync=False)
+                else:
+                    ctx.locate_interp(q, qpc, d["mo"], d["fo"], d["el"], d["hit"], sync=False)
                 st = ctx.sync()
                 if s == 0:
                     continue  # first call of a round: warm-up
