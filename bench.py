@@ -442,9 +442,7 @@ def host_mode_iteration2(ctx, w, bg, mo, fo, rank: int) -> dict:
         res[mode] = {"ms": round(1e3 * t, 2), "bytes_up": ctx.bytes_up(reset=True),
                      "located_points": int(st.nvol + st.nbdy),
                      # the walks' hand-overs and the exhaustive searches they needed
-                     "locate_stats": {k: sd[k] for k in ("nvol", "nbdy", "nvol_exact", "nvol_stuck", "nvol_limit",
-                                                         "nvol_noseed", "nvol_exhaust", "nvol_closest",
-                                                         "nbdy_exhaust", "nbdy_stale", "nbdy_closest", "stepmax")},
+                     "locate_stats": locate_stats(st),
                      "device_ms": {"step_total": round(float(st.ms_total), 3),
                                    "volume_fallback": round(float(st.ms_fallback), 3),
                                    "surface_branch": round(float(st.ms_bdy), 3)}}
@@ -457,6 +455,17 @@ def host_mode_iteration2(ctx, w, bg, mo, fo, rank: int) -> dict:
                 "bit_identical": bool(same)})
     log(f"[bench r{rank}] host-mode iteration 2: {res}")
     return res
+
+
+LOCATE_KEYS = ("nvol", "nbdy", "nvol_exact", "nvol_stuck", "nvol_limit", "nvol_noseed", "nvol_exhaust",
+               "nvol_closest", "nbdy_exhaust", "nbdy_stale", "nbdy_closest", "stepmax")
+
+
+def locate_stats(st) -> dict:
+    """the walks' hand-overs and the exhaustive searches a leg's call needed
+    (every leg that can reach a fallback reports them)"""
+    d = st.as_dict()
+    return {k: int(d[k]) for k in LOCATE_KEYS}
 
 
 def renumbered_timing(ctx, args, w, step_bg, q_xyz, q_pc, d_mo, d_fo, d_elem, d_hit, rank: int, perm, what: str,
@@ -523,6 +532,7 @@ def renumbered_timing(ctx, args, w, step_bg, q_xyz, q_pc, d_mo, d_fo, d_elem, d_
            "morton_binned": bool(st.sorted), "ms_per_step": round(1e3 * wall, 4),
            "mpts_per_s": round(npts / wall / 1e6, 1), "device_ms_total": round(float(np.mean(ms)), 4),
            "volume_stage_ms": round(float(np.mean(vol)), 4),
+           "locate_stats": locate_stats(st),
            "located_points": int(located.sum()), "same_element_as_input_order": int(same.sum()),
            "same_element_rows_bit_identical": int((same & ident).sum()),
            "ok": bool(np.all(ident[same])) and int(located.sum()) == npts}
@@ -551,7 +561,8 @@ def surface_solo(ctx, step_bg, q_xyz, q_pc, d_mo, d_fo, d_elem, d_hit, device: i
     d_pc.free()
     return {"what": "surface branch alone (volume points skipped): HIP events of the surface stream, "
                     "starting after the seed grid as in a large call's step",
-            "surface_points": int(st.nbdy), "ms_branch": round(float(np.median(ms_bdy)), 4),
+            "surface_points": int(st.nbdy), "locate_stats": locate_stats(st),
+            "ms_branch": round(float(np.median(ms_bdy)), 4),
             "ms_call": round(float(np.median(ms_tot)), 4)}
 
 
@@ -602,7 +613,7 @@ def graded_leg(args, rank: int, budget_s: float = 60.0) -> dict:
            "size_grading": round(stats["size_grading"], 1), "max_aspect_ratio": round(stats["max_aspect"], 1),
            "ms_per_step": round(1e3 * wall, 4), "mpts_per_s": round(npts / wall / 1e6, 1),
            "volume_stage_ms": round(float(st.ms_vol), 4), "nvol": int(st.nvol), "nvol_exact": int(st.nvol_exact),
-           "nvol_exhaust": int(st.nvol_exhaust), "stepmax": int(st.stepmax),
+           "nvol_exhaust": int(st.nvol_exhaust), "stepmax": int(st.stepmax), "locate_stats": locate_stats(st),
            "walk_steps_per_point": round(st.steps_total / max(1, npts), 3)}
     if not args.no_cpu_baseline:
         from oracle import oracle as O
@@ -676,7 +687,7 @@ def groups_leg(args, ngroup: int = 10, reps: int = 5, budget_s: float = 30.0) ->
            "ms_per_group_groups_call": round(1e3 * t_groups, 4), "ms_per_group_single_calls": round(1e3 * t_single, 4),
            "host_enqueue_ms_per_group": {"groups_call": round(1e3 * e_groups, 4), "single_calls": round(1e3 * e_single, 4)},
            "mpts_per_s_groups_call": round(npts / ngroup / t_groups / 1e6, 1),
-           "bit_identical_to_single_calls": bool(same)}
+           "bit_identical_to_single_calls": bool(same), "locate_stats": locate_stats(st)}
     ctx.close()
     if not args.no_cpu_baseline:
         from oracle import oracle as O

@@ -120,6 +120,7 @@ __global__ __launch_bounds__(kBlock) void k_bdy(Bg bg, const Frame *fr, const in
   const int x = blockIdx.x & 7;
   const long long lo = n * x / 8, hi = n * (x + 1) / 8;
   const XcdChunk ch = xcd_chunk(n); // static split (dyn == 0)
+  bool wrote = false;               // fallback entries written (read by the last block)
   for (int it = 0;; it++) {
     long long i;
     if (dyn) {
@@ -142,13 +143,14 @@ __global__ __launch_bounds__(kBlock) void k_bdy(Bg bg, const Frame *fr, const in
     if (active && hit == 0) {
       fb[slot] = ip;
       fi.at(slot);
+      wrote = true;
     }
     wave_stats(&bs, active, hit, steps);
   }
   __syncthreads();
   bstats_flush(&bs, st);
   // the surface fallback list is complete: its query grid (fb_grid_build)
-  if (!last_block(&st->bdy_done)) return;
+  if (!last_block(&st->bdy_done, wrote)) return;
   const int nfb = load_agent(&st->nfb_bdy);
   if (nfb > 0) fb_grid_build(qxyz, fb, nfb, st, 1, gb.cells, gb.cur, gb.items);
 }

@@ -97,7 +97,7 @@ __global__ __launch_bounds__(kBlock) void k_vol_exhaust_accept(Bg bg, const doub
       if (min4(b4) > -kEps) atomicMin(&best[j], k);
     });
   }
-  if (!last_block(&st->fb_done[0])) return;
+  if (!last_block(&st->fb_done[0], true)) return; // (only when there are fallbacks)
   __shared__ int s_nac;
   __shared__ unsigned s_cnt[2];
   if (threadIdx.x == 0) {
@@ -159,7 +159,7 @@ __global__ __launch_bounds__(kBlock) void k_bdy_exhaust_accept(Bg bg, const doub
       if (bmin > -kEps && !(fabs(dist) > bg.hausd)) atomicMin(&best[j], k);
     });
   }
-  if (!last_block(&st->fb_done[2])) return;
+  if (!last_block(&st->fb_done[2], true)) return; // (only when there are fallbacks)
   __shared__ int s_nac;
   __shared__ unsigned s_cnt[2];
   if (threadIdx.x == 0) {
@@ -354,7 +354,7 @@ __global__ __launch_bounds__(kBlock) void k_vol_exhaust_closest(Bg bg, const dou
   const int n = st->nac_vol;
   if (n == 0) return;
   closest_scan<4>(bg, qxyz, fb, nac, n, bg.ne, part, res);
-  if (!last_block(&st->fb_done[1])) return;
+  if (!last_block(&st->fb_done[1], true)) return; // (only when there are fallbacks)
   __shared__ unsigned s_cnt[2];
   if (threadIdx.x == 0) s_cnt[0] = s_cnt[1] = 0u;
   __syncthreads();
@@ -389,7 +389,7 @@ __global__ __launch_bounds__(kBlock) void k_bdy_exhaust_closest(Bg bg, const dou
   const int n = st->nac_bdy;
   if (n == 0) return;
   closest_scan<3>(bg, qxyz, fb, nac, n, bg.nt, part, res);
-  if (!last_block(&st->fb_done[3])) return;
+  if (!last_block(&st->fb_done[3], true)) return; // (only when there are fallbacks)
   __shared__ unsigned s_cnt[2];
   if (threadIdx.x == 0) s_cnt[0] = s_cnt[1] = 0u;
   __syncthreads();

@@ -985,9 +985,15 @@ __global__ __launch_bounds__(kBlock) void k_cls_scatter(const uint8_t *pclass, l
 // barrier before the ticket: every wave of the block has issued its atomics
 // (r04l: without it a block's later waves could still be scanning when the
 // last block read the results — 4 surface points left unprocessed, once)
-__device__ __forceinline__ bool last_block(unsigned *done) {
-  __threadfence();
-  __syncthreads();
+// The last block of a grid to get here returns true.  wrote: this thread
+// stored data the last block reads; a block any of whose threads did
+// releases it first (__threadfence).  The release is an L2 write-back on
+// gfx950 (the XCDs' L2s are not coherent with each other): taken in every
+// block of k_bdy (808 blocks for a 205k-point group) it took the kernel 17 ->
+// 87 us and slowed the volume kernel beside it (r05h trace) — only the blocks
+// that appended to a fallback list pay it.
+__device__ __forceinline__ bool last_block(unsigned *done, bool wrote) {
+  if (__syncthreads_or(wrote)) __threadfence();
   __shared__ bool last;
   if (threadIdx.x == 0) last = atomicAdd(done, 1u) == gridDim.x - 1;
   __syncthreads();
