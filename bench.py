@@ -680,7 +680,9 @@ def groups_leg(args, ngroup: int = 10, reps: int = 5, budget_s: float = 30.0) ->
                for k in ("elem", "hit", "met")) and all(
         np.array_equal(x, y, equal_nan=True) for a, b in zip(out_g, ref_out) for x, y in zip(a["fields"], b["fields"]))
     npts = int(st.nvol + st.nbdy)
-    lanes = int(os.environ.get("PMMG_HIP_GROUP_LANES", "4"))
+    lmax = max(1, int(os.environ.get("PMMG_HIP_GROUP_LANES", "5")))
+    rounds = -(-ngroup // lmax)
+    lanes = min(ngroup, -(-ngroup // rounds))  # as pmmg_hip_locate_interp_groups deals them
     res = {"what": f"{ngroup} cfg2-size groups (own copies in HBM) in one pmmg_hip_locate_interp_groups call vs one "
                    "pmmg_hip_locate_interp per group; not the bench value",
            "groups": ngroup, "lanes": lanes, "points_per_group": npts // ngroup,

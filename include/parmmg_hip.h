@@ -103,6 +103,8 @@ typedef struct {
   int64_t nvol_stuck;    /* exact volume walks stuck (no eligible neighbour) -> exhaustive */
   int64_t nvol_limit;    /* exact volume walks stopped at maxstep -> exhaustive */
   int64_t seed_map_axes; /* bit d: axis d of the volume seed grid followed the vertex quantiles */
+  int64_t nbdy_fanscan;  /* surface queries whose cone test scanned every tria for a vertex's ball (its fan
+                            open, non-manifold or longer than 64: e.g. at a halo shard's cut) */
 } pmmg_hip_stats;
 
 /* Options (bit flags) for pmmg_hip_create.  Default: Morton-bin the queries
@@ -248,7 +250,9 @@ typedef struct {
 } pmmg_hip_group;
 
 /* Enqueue the transfer of ngroup groups: group i runs on lane i % L of the
- * context (L = min(ngroup, PMMG_HIP_GROUP_LANES, default 4); a lane is a
+ * context (L = ceil(ngroup / rounds), rounds = ceil(ngroup / Lmax), Lmax =
+ * PMMG_HIP_GROUP_LANES, default 5: every lane gets the same number of groups
+ * give or take one, in the fewest rounds; a lane is a
  * pair of streams with its own work buffers, so the groups of different lanes
  * overlap on the device).  stats == NULL: the call only enqueues (nothing is
  * read back; use pmmg_hip_sync before reading outputs).  stats != NULL: the

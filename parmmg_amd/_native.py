@@ -28,6 +28,7 @@ class HipStats(ctypes.Structure):
         ("ms_bdy", ctypes.c_float), ("ms_fallback", ctypes.c_float), ("ms_total", ctypes.c_float),
         ("ms_vol_locate", ctypes.c_float),
         ("nvol_noseed", c_int64), ("nvol_stuck", c_int64), ("nvol_limit", c_int64), ("seed_map_axes", c_int64),
+        ("nbdy_fanscan", c_int64),
     ]
 
     def as_dict(self) -> dict:

@@ -10,7 +10,7 @@ namespace pmmg {
 // one surface query; returns the hit code (0 = not located: exhaustive list)
 __device__ __forceinline__ int bdy_query(const Bg &bg, const Frame *fr, const int *sgrid, int gs, const double *qxyz,
                                          int ip, const Slots &S, int *elem_out, int8_t *hit_out, int maxstep,
-                                         int &steps) {
+                                         int &steps, int &scans) {
   int hit = 0;
   double x[3];
   load_pt(qxyz, ip, x);
@@ -79,7 +79,7 @@ __device__ __forceinline__ int bdy_query(const Bg &bg, const Frame *fr, const in
           edge = f;
           hit = PMMG_HIT_BDY_WEDGE;
           done = true;
-        } else if (tri_cone(bg, k, il, t, x)) {
+        } else if (tri_cone(bg, k, il, t, x, scans)) {
           vertex = il;
           hit = PMMG_HIT_BDY_CONE;
           done = true;
@@ -134,11 +134,12 @@ __global__ __launch_bounds__(kBlock) void k_bdy(Bg bg, const Frame *fr, const in
       i = ch.start + it * ch.stride;
     }
     const bool active = i < (dyn ? hi : ch.hi);
-    int steps = 0, hit = 0, ip = 0;
+    int steps = 0, hit = 0, ip = 0, scans = 0;
     if (active) {
       ip = order[i];
-      hit = bdy_query(bg, fr, sgrid, gs, qxyz, ip, S, elem_out, hit_out, maxstep, steps);
+      hit = bdy_query(bg, fr, sgrid, gs, qxyz, ip, S, elem_out, hit_out, maxstep, steps, scans);
     }
+    wave_count(&bs, kCntFanScan, active && scans > 0);
     int slot = wave_append(&st->nfb_bdy, active && hit == 0);
     if (active && hit == 0) {
       fb[slot] = ip;

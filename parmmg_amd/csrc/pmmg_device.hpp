@@ -635,7 +635,8 @@ __device__ __noinline__ bool tri_cone_scan(const int *triv, const double *xyz, i
   return true;
 }
 
-__device__ __forceinline__ bool tri_cone(const Bg &bg, int k, int iloc, const TriGeom &t, const double *x) {
+__device__ __forceinline__ bool tri_cone(const Bg &bg, int k, int iloc, const TriGeom &t, const double *x,
+                                         int &scans) {
   const int ip = sel3i(t.v[0], t.v[1], t.v[2], iloc);
   double p0[3], p[3], dist = 0.0;
   tri_pick(t, iloc, p0);
@@ -647,12 +648,16 @@ __device__ __forceinline__ bool tri_cone(const Bg &bg, int k, int iloc, const Tr
     int tcur = k;
     int e = dir == 0 ? (iloc + 1) % 3 : (iloc + 2) % 3; // an edge of tcur incident to ip
     for (int it = 0;; it++) {
-      if (it == bg.fanmax)
+      if (it == bg.fanmax) {
+        ++scans;
         return tri_cone_scan(bg.triv, bg.xyz, bg.nt, bg.hausd, ip, p0[0], p0[1], p0[2], p[0], p[1], p[2], dist);
+      }
       const int code = bg.adjt[3 * (size_t)(tcur - 1) + e];
       const int tn = code / 3, en = code % 3;
-      if (tn == 0) // open or non-manifold fan
+      if (tn == 0) { // open or non-manifold fan
+        ++scans;
         return tri_cone_scan(bg.triv, bg.xyz, bg.nt, bg.hausd, ip, p0[0], p0[1], p0[2], p[0], p[1], p[2], dist);
+      }
       if (tn == k) return true;                                // the fan closed: every tria tested
       if (!cone_tria(bg, tn, ip, p0, p, dist)) return false;
       const int *tvn = bg.triv + 3 * (size_t)(tn - 1);

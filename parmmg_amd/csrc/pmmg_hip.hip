@@ -146,7 +146,8 @@ struct DevBuf {
 };
 
 enum {
-  EV_START, EV_FRAME, EV_PREP, EV_ORDER, EV_VOL0, EV_WALK, EV_VOL, EV_JOIN, EV_END, EV_BDY0, EV_BDY1, EV_COUNT
+  EV_START, EV_FRAME, EV_PREP, EV_ORDER, EV_VOL0, EV_WALK, EV_VOL, EV_JOIN, EV_END, EV_BDY0, EV_BDY1, EV_RESET,
+  EV_SB0, EV_COUNT
 };
 
 struct pmmg_hip_ctx {
@@ -177,6 +178,7 @@ struct pmmg_hip_ctx {
   DevBuf brk_k, brk_k2, brk_v, brk_v2, brk_vinv, brk_tinv, brk_xq, brk_xyz, brk_sol, brk_rec, brk_tmp;
   int brick = 0;
   int set_order = 0; // test-only PMMG_HIP_SETORDER=1 (see k_set_order)
+  int no_fb = 0;     // measurement build: PMMG_HIP_NOFB
   int srf_solo = -1; // the surface branch waits for the seed grid: -1 in calls of >= kSmallGroup queries (r04zo,
                      // cfg4: the seed grid ran at 455 instead of 261 us beside k_bdy; step 4.24 -> 4.13 ms,
                      // Mmg-like 5.01 -> 4.93, shuffled =), 1 always, 0 never (PMMG_HIP_SRFSOLO)
@@ -269,7 +271,10 @@ struct pmmg_hip_ctx {
   bool comm_owned = false;
   int comm_rank = 0, comm_size = 0;
   DevBuf ag_send, ag_recv, ag_off;
-  int group_lanes = 4; // PMMG_HIP_GROUP_LANES (r04i, 10 cfg2-size groups: 1 / 2 / 4 lanes 0.165 / 0.125 / 0.108 ms per group)
+  // PMMG_HIP_GROUP_LANES: most lanes of a groups call (r05k, 10 cfg2-size groups, 4 hardware queues: 4 / 5 /
+  // 8 / 10 lanes 0.096 / 0.083 / 0.092 / 0.095 ms per group — 5 lanes take 2 groups each, 4 take 3, 3, 2, 2;
+  // more hardware queues made it slower: 8 queues, 5 lanes 0.127; r04i: 1 / 2 lanes 0.165 / 0.125)
+  int group_lanes = 5;
   struct Pool *lane_pool = nullptr; // host threads enqueueing the other lanes' groups
   int lane_streams = 2; // a group lane's streams: 2 = its own surface stream, 1 = the surface branch on the
                         // main stream (measurement build: PMMG_HIP_LANE_STREAMS)
@@ -649,6 +654,8 @@ static pmmg_hip_ctx *create_ctx(int device, int options, bool srf_prio, pmmg_hip
   c->lane_streams = std::max(1, std::min(3, env_int("PMMG_HIP_LANE_STREAMS", c->lane_streams)));
   c->lane0 = env_int("PMMG_HIP_LANE0", 1) ? 1 : 0;
   c->bdy_first = env_int("PMMG_HIP_BDYFIRST", 0);
+  c->no_fb = env_int("PMMG_HIP_NOFB", 0); // the exhaustive kernels not launched (a launch's price; wrong results
+                                           // wherever a query needs them)
 #endif
   return c;
 }
@@ -1404,6 +1411,8 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   c->grid_clean_n = c->sgrid_clean_n = 0; // dirty until this call's refill is enqueued
   hipLaunchKernelGGL(k_reset, dim3(blocks_for(ng_clr > nsg_clr ? ng_clr : nsg_clr, 2048)), dim3(kBlock), 0, s, fr, st,
                      grid, ng_clr, sgrid, nsg_clr, (int *)c->oflag.p, force, c->bin_bits);
+  // input order forced (a small group): the surface list needs only the zeroed counters, not the frame
+  if (force == 0) HIPCK(c, hipEventRecord(c->ev[EV_RESET], s));
   // bbox (its last block finalises the frame), the seed grid's axis maps
   hipLaunchKernelGGL(k_bbox, dim3(blocks_for(bg.np / c->bbox_stride + 1, 256)), dim3(kBlock), 0, s, bg.xyz, bg.np, fr,
                      c->bbox_stride, g, gs, gb);
@@ -1420,7 +1429,8 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   // the frame.  (r04: the axis maps moved here beside the fixed-point copy
   // cost 10 groups 0.11 -> 0.25 ms per group and the 8-way rank +0.02 ms for
   // -0.0 at cfg4, `profiles/r04s`: not kept)
-  HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_FRAME], 0));
+  HIPCK(c, hipStreamWaitEvent(sb, c->ev[force == 0 ? EV_RESET : EV_FRAME], 0));
+  HIPCK(c, hipEventRecord(c->ev[EV_SB0], sb));
   HIPCK(c, hipGetLastError());
 
   // ---- seed grid (main stream): volume seeds
@@ -1489,6 +1499,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_PREP], 0));
   HIPCK(c, hipEventRecord(c->ev[EV_BDY0], sb));
   if (bg.nt > 0) {
+    if (force == 0) HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_FRAME], 0)); // (the surface seeds need the frame)
     hipLaunchKernelGGL(k_seed_srf, dim3(blocks_for(bg.nt, 4096)), dim3(kBlock), 0, sb, bg, (const Frame *)fr, sgrid,
                        gs);
     // one round of the grid for up to 1M surface points (static split: a
@@ -1497,7 +1508,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
                        (const Frame *)fr, (const int *)sgrid, gs, xyz_new, (const int *)order_b, S, elem_out, hit_out,
                        (int *)c->fb_bdy.p, st, c->maxstep, c->bdy_dyn, FbInit{(int *)c->bbest.p},
                        FbGridBufs{(int *)c->fbg_bdy_c.p, (int *)c->fbg_bdy_u.p, (int *)c->fbg_bdy_i.p});
-    launch_bdy_fallbacks(c, sb, S, xyz_new, elem_out, hit_out);
+    if (!c->no_fb) launch_bdy_fallbacks(c, sb, S, xyz_new, elem_out, hit_out);
     HIPCK(c, hipGetLastError());
     if (nsg >= kRefillCells) { // the surface grid refilled for the next call (see k_reset above)
       hipLaunchKernelGGL(k_fill32, dim3(blocks_for(nsg, 2048)), dim3(kBlock), 0, sb, sgrid, nsg, INT_MAX);
@@ -1510,7 +1521,10 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
 #ifdef PMMG_HIP_MEASURE
   if (c->brick > 0 && !brick_renumber(c, s, bg, S, fr, g)) return 0;
 #endif
-  HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_ORDER], 0));
+  // the volume kernel reads the order branch's lists only in Morton order (or when it may be chosen); in
+  // forced input order its queries are the input's volume points and the wait is dropped (r05: the
+  // cross-stream wait was ~20 us of a small group's main chain)
+  if (force != 0) HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_ORDER], 0));
   if (c->bdy_first) HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_BDY1], 0));
   HIPCK(c, hipEventRecord(c->ev[EV_VOL0], s));
   // ---- volume (main stream): walk + exact test + interpolation in one
@@ -1530,7 +1544,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   HIPCK(c, hipEventRecord(c->ev[EV_VOL], s));
   // ---- exhaustive fallbacks of the volume queries (lists and counts on the
   // device; the surface ones ran on the surface stream after k_bdy)
-  launch_vol_fallbacks(c, S, xyz_new, elem_out, hit_out);
+  if (!c->no_fb) launch_vol_fallbacks(c, S, xyz_new, elem_out, hit_out);
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[EV_JOIN], s));
   if (ng >= kRefillCells) { // the volume seed grid refilled for the next call, beside the surface stream's tail
@@ -1585,11 +1599,12 @@ static int collect_stats(pmmg_hip_ctx *c, pmmg_hip_stats *out) {
     int ad = 0;
     HIPCK(c, hipMemcpy(&ad, &((const Frame *)c->frame.p)->adaptive, sizeof(int), hipMemcpyDeviceToHost));
     out->seed_map_axes = ad;
+    out->nbdy_fanscan = (int64_t)cnt[kCntFanScan];
   }
   float ms = 0.f;
   HIPCK(c, hipEventElapsedTime(&ms, c->ev[EV_START], c->ev[EV_PREP]));
   out->ms_prepare = ms;
-  HIPCK(c, hipEventElapsedTime(&ms, c->ev[EV_FRAME], c->ev[EV_ORDER]));
+  HIPCK(c, hipEventElapsedTime(&ms, c->ev[EV_SB0], c->ev[EV_ORDER]));
   out->ms_sort = ms; // on the second stream, concurrent with the seed grid
   HIPCK(c, hipEventElapsedTime(&ms, c->ev[EV_VOL0], c->ev[EV_VOL]));
   out->ms_vol = ms;
@@ -1836,6 +1851,7 @@ static void stats_sum(pmmg_hip_stats *a, const pmmg_hip_stats &b) {
   a->ms_fallback += b.ms_fallback; a->ms_total += b.ms_total; a->ms_vol_locate += b.ms_vol_locate;
   a->nvol_noseed += b.nvol_noseed; a->nvol_stuck += b.nvol_stuck; a->nvol_limit += b.nvol_limit;
   a->seed_map_axes |= b.seed_map_axes;
+  a->nbdy_fanscan += b.nbdy_fanscan;
 }
 
 static pmmg_hip_ctx *group_lane(pmmg_hip_ctx *c, int j) {
@@ -1909,7 +1925,10 @@ int pmmg_hip_locate_interp_groups(pmmg_hip_ctx *c, int ngroup, const pmmg_hip_gr
     HIPCK(c, hipStreamDestroy(c->stream2_hi));
     c->stream2_hi = nullptr;
   }
-  const int L = std::max(1, std::min(ngroup, c->group_lanes));
+  // lanes dealt an equal number of groups: ceil(n / rounds) lanes for the rounds the most lanes need
+  // (10 groups, 5 lanes: 2 each; 7 groups: 4 lanes of 2, 2, 2, 1 rather than 5 of 2, 2, 1, 1, 1)
+  const int Lmax = std::max(1, c->group_lanes), rounds = (ngroup + Lmax - 1) / Lmax;
+  const int L = std::max(1, std::min(ngroup, (ngroup + rounds - 1) / rounds));
   std::vector<pmmg_hip_ctx *> lane(L);
   for (int j = 0; j < L; j++)
     if (!(lane[j] = group_lane(c, j))) return 0;

@@ -164,6 +164,7 @@ static void stats_add(pmmg_hip_stats *a, const pmmg_hip_stats *b) {
   a->ms_fallback += b->ms_fallback; a->ms_total += b->ms_total; a->ms_vol_locate += b->ms_vol_locate;
   a->nvol_noseed += b->nvol_noseed; a->nvol_stuck += b->nvol_stuck; a->nvol_limit += b->nvol_limit;
   a->seed_map_axes |= b->seed_map_axes;
+  a->nbdy_fanscan += b->nbdy_fanscan;
 }
 
 static int interp_groups(pmmg_hip_ctx *ctx, int ngrp, const pmmg_old_group *old, pmmg_new_group *grp, int input_met,

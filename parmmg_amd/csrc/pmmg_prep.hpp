@@ -52,6 +52,7 @@ constexpr int kCntExact = 14;      // queries handed to the exact continuation (
 constexpr int kCntNoSeed = 15;     // volume queries without a seed (empty seed neighbourhood)
 constexpr int kCntStuck = 16;      // exact walks stuck (no eligible neighbour)
 constexpr int kCntLimit = 17;      // exact walks stopped at maxstep
+constexpr int kCntFanScan = 18;    // surface queries whose cone test scanned every tria (tri_cone_scan)
 constexpr int kNumCnt = 20;
 struct StatPart {
   unsigned long long cnt[kNumCnt];

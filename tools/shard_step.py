@@ -94,6 +94,7 @@ def run_rank(a, w, r, var, bg, bg0, met, fields, q_xyz, q_pc):
                 ms[k].append(getattr(st, k))
         res = {"rank": r, "variant": var, "world": a.world, "mode": a.mode, "nvol_exhaust": int(st.nvol_exhaust),
                "nvol_closest": int(st.nvol_closest), "nbdy_exhaust": int(st.nbdy_exhaust),
+               "nbdy_cone": int(st.nbdy_cone), "nbdy_wedge": int(st.nbdy_wedge), "nbdy_fanscan": int(st.nbdy_fanscan),
                "points": int(st.nvol + st.nbdy), "nbdy": int(st.nbdy), "sorted": int(st.sorted),
                "steps_pp": round(st.steps_total / max(1, st.nvol + st.nbdy), 3), "shard_tets": bg.ne,
                "shard_tet_fraction": round(bg.ne / bg0.ne, 4), "ms_per_step_wall": round(1e3 * wall, 4)}
