@@ -216,6 +216,14 @@ int pmmg_hip_carry_over(pmmg_hip_ctx *ctx, int slot, int np, const int *src);
 /* Host -> device bytes moved by host-mode calls since the last reset. */
 int64_t pmmg_hip_bytes_up(pmmg_hip_ctx *ctx, int reset);
 
+/* Free the context's reusable scratch: the snapshot builders' buckets (12 B x
+ * 4 x ne for the adjacency: ~4.8 GB at 101M tetra), the Morton binning's
+ * second key / value arrays and digit tables, and the group lanes (contexts
+ * of their own, re-created by the next groups call).  The next call that
+ * needs any of them allocates it again.  Waits for the context's work first.
+ * The background, solutions, kept slots and seed grids stay.  Returns 1/0. */
+int pmmg_hip_release_scratch(pmmg_hip_ctx *ctx);
+
 /* ---- Many groups in one call ------------------------------------------------
  * ParMmg transfers group by group (the loop of src/interpmesh_pmmg.c:690 over
  * up to PMMG_REMESHER_NGRPS_MAX = 100 groups per rank, src/parmmg.h:212);

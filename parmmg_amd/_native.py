@@ -63,6 +63,7 @@ HIP_API = {
     "pmmg_hip_keep": (c_int, [c_void_p, c_int]),
     "pmmg_hip_carry_over": (c_int, [c_void_p, c_int, c_int, c_void_p]),
     "pmmg_hip_bytes_up": (c_int64, [c_void_p, c_int]),
+    "pmmg_hip_release_scratch": (c_int, [c_void_p]),
     "pmmg_hip_malloc": (c_void_p, [c_void_p, c_int64]),
     "pmmg_hip_free": (c_int, [c_void_p, c_void_p]),
     "pmmg_hip_build_adjacency": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),

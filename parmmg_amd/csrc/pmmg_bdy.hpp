@@ -112,7 +112,9 @@ __device__ __forceinline__ int bdy_query(const Bg &bg, const Frame *fr, const in
 // slowed the volume kernel beside them (profiles/r03y).
 __global__ __launch_bounds__(kBlock) void k_bdy(Bg bg, const Frame *fr, const int *sgrid, int gs, const double *qxyz,
                                                 const int *order, Slots S, int *elem_out, int8_t *hit_out, int *fb,
-                                                DevStats *st, int maxstep, int dyn, FbInit fi, FbGridBufs gb) {
+                                                DevStats *st, int maxstep, int dyn, FbInit fi, FbGridBufs gb,
+                                                const int *gate, int want) {
+  if (want >= 0 && gate[0] != want) return; // (one of the two orders' launches, as k_vol)
   __shared__ BlockStats bs;
   bstats_init(&bs);
   __syncthreads();

@@ -61,7 +61,7 @@ namespace {
 
 typedef void (*VolFn)(Bg, const Frame *, const unsigned long long *, int, const double *, const uint8_t *,
                       const int *, const double *, int, ContEntry *, DevStats *, Slots, int *, int8_t *, int,
-                      const int *, int, int);
+                      const int *, int, int, int);
 
 struct LayoutEntry {
   int c[6];
@@ -147,7 +147,7 @@ struct DevBuf {
 
 enum {
   EV_START, EV_FRAME, EV_PREP, EV_ORDER, EV_VOL0, EV_WALK, EV_VOL, EV_JOIN, EV_END, EV_BDY0, EV_BDY1, EV_RESET,
-  EV_SB0, EV_COUNT
+  EV_SB0, EV_COH, EV_ORDER2, EV_COUNT
 };
 
 struct pmmg_hip_ctx {
@@ -155,6 +155,8 @@ struct pmmg_hip_ctx {
   int options = 0;
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr; // surface branch, concurrent with the volume walk
+  hipStream_t stream3 = nullptr; // Morton binning of a call whose order is decided on the device (created at the
+                                 // first such call), beside the input order's surface list on stream2
   hipStream_t stream2_hi = nullptr; // measurement build, PMMG_HIP_SRFPRIO=1: the same at the highest priority,
   bool srf_prio = false;            // for calls of >= kSmallGroup queries (see run_device)
   char err[512] = {0};
@@ -671,6 +673,7 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   (void)hipStreamSynchronize(c->stream);
   (void)hipStreamSynchronize(c->stream2);
   if (c->stream2_hi) (void)hipStreamSynchronize(c->stream2_hi);
+  if (c->stream3) (void)hipStreamSynchronize(c->stream3);
   if (c->cstream) (void)hipStreamSynchronize(c->cstream);
   DevBuf *bufs[] = {&c->o_xyz, &c->o_tetv, &c->o_adja, &c->o_triv, &c->o_adjt, &c->o_met, &c->o_rec, &c->frame,
                     &c->stats, &c->grid, &c->sgrid, &c->order_v,
@@ -705,6 +708,7 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
     if (c->stream) (void)hipStreamDestroy(c->stream);
   }
   if (c->stream2_hi) (void)hipStreamDestroy(c->stream2_hi);
+  if (c->stream3) (void)hipStreamDestroy(c->stream3);
   if (c->cstream) (void)hipStreamDestroy(c->cstream);
   delete c;
 }
@@ -1402,6 +1406,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_START], 0));
     hipLaunchKernelGGL(k_coherence, dim3(1), dim3(kBlock), 0, sb, xyz_new, np_new, (int *)c->oflag.p, force,
                        c->bin_bits);
+    HIPCK(c, hipEventRecord(c->ev[EV_COH], sb));
   }
   // seed grids: cleared here unless the previous call left them clean (a
   // large grid is refilled at the end of the call that used it, beside the
@@ -1411,8 +1416,8 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   c->grid_clean_n = c->sgrid_clean_n = 0; // dirty until this call's refill is enqueued
   hipLaunchKernelGGL(k_reset, dim3(blocks_for(ng_clr > nsg_clr ? ng_clr : nsg_clr, 2048)), dim3(kBlock), 0, s, fr, st,
                      grid, ng_clr, sgrid, nsg_clr, (int *)c->oflag.p, force, c->bin_bits);
-  // input order forced (a small group): the surface list needs only the zeroed counters, not the frame
-  if (force == 0) HIPCK(c, hipEventRecord(c->ev[EV_RESET], s));
+  // the input order's surface list needs only the zeroed counters (and the coherence flag), not the frame
+  HIPCK(c, hipEventRecord(c->ev[EV_RESET], s));
   // bbox (its last block finalises the frame), the seed grid's axis maps
   hipLaunchKernelGGL(k_bbox, dim3(blocks_for(bg.np / c->bbox_stride + 1, 256)), dim3(kBlock), 0, s, bg.xyz, bg.np, fr,
                      c->bbox_stride, g, gs, gb);
@@ -1429,15 +1434,27 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   // the frame.  (r04: the axis maps moved here beside the fixed-point copy
   // cost 10 groups 0.11 -> 0.25 ms per group and the 8-way rank +0.02 ms for
   // -0.0 at cfg4, `profiles/r04s`: not kept)
-  HIPCK(c, hipStreamWaitEvent(sb, c->ev[force == 0 ? EV_RESET : EV_FRAME], 0));
+  HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_RESET], 0));
   HIPCK(c, hipEventRecord(c->ev[EV_SB0], sb));
+  // the Morton binning on a third stream (r05, `profiles/r05m`: on the second stream its ~19 launches, each
+  // returning at once when the coherence test picks input order, held the 8-way rank's volume kernel 86 us
+  // behind the seed grid)
+  hipStream_t sc = sb;
+  if (force != 0) {
+    if (!c->stream3 && hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess) c->stream3 = nullptr;
+    if (c->stream3) sc = c->stream3;
+    HIPCK(c, hipStreamWaitEvent(sc, c->ev[EV_FRAME], 0));
+    if (force < 0 && sc != sb) HIPCK(c, hipStreamWaitEvent(sc, c->ev[EV_COH], 0));
+  }
   HIPCK(c, hipGetLastError());
 
   // ---- seed grid (main stream): volume seeds
   {
     const long long nsamp = ng < bg.ne ? ng : bg.ne;
-    hipLaunchKernelGGL(k_seed_vol, dim3((blocks_for(nsamp, 8192) + 7) & ~7), dim3(kBlock), 0, s, bg, fr, grid, g,
-                       nsamp, c->seed_lanes, c->seed_v0);
+    // kSeedBatch samples per thread in flight together (r05m: one per thread, the 8-way rank's 1.65M samples
+    // took 107 us — the grid's latency in rounds of waves — where cfg4's 12.6M take 262 us)
+    hipLaunchKernelGGL(k_seed_vol, dim3((blocks_for((nsamp + kSeedBatch - 1) / kSeedBatch, 8192) + 7) & ~7),
+                       dim3(kBlock), 0, s, bg, fr, grid, g, nsamp, c->seed_lanes, c->seed_v0);
   }
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[EV_PREP], s));
@@ -1451,35 +1468,6 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
 #ifdef PMMG_HIP_MEASURE
   if (c->set_order) hipLaunchKernelGGL(k_set_order, dim3(1), dim3(1), 0, s, st, force > 0 ? 1 : 0, c->bin_bits);
 #endif
-  if (force != 0 && np_new > 0) {
-    // stable LSD radix sort of the keys (<= 3 * 7 + 2 bits) in 3 passes of 8 bits (pmmg_sort.hpp); the key
-    // kernel writes the first pass's digit table
-    const int ntile = (int)((np_new + kRsTile - 1) / kRsTile);
-    const long long nh = 256LL * ntile;
-    const int nch = (int)((nh + kScanChunk - 1) / kScanChunk);
-    if (!ensure(c, c->bvals2, 4 * nq) || !ensure(c, c->rs_hist, 4 * (size_t)nh) || !ensure(c, c->rs_csum, 4 * (size_t)nch))
-      return 0;
-    unsigned *k0 = (unsigned *)c->bkeys.p, *k1 = (unsigned *)c->bkeys2.p;
-    int *v0 = (int *)c->bvals.p, *v1 = (int *)c->bvals2.p, *hist = (int *)c->rs_hist.p, *csum = (int *)c->rs_csum.p;
-    const int tgrid = std::min(ntile, kRsGrid);
-    hipLaunchKernelGGL(k_bin_keys, dim3(tgrid), dim3(kBlock), 0, sb, xyz_new, pclass, np_new, (const Frame *)fr, flag,
-                       k0, v0, st, kRsTile, ntile, hist);
-    for (int pass = 0; pass < 3; pass++) {
-      const unsigned *kin = pass == 1 ? k1 : k0;
-      const int *vin = pass == 1 ? v1 : v0;
-      unsigned *kout = pass == 1 ? k0 : k1;
-      int *vout = pass == 1 ? v0 : (pass == 0 ? v1 : order_v);
-      if (pass > 0)
-        hipLaunchKernelGGL(k_rs_hist, dim3(tgrid), dim3(kBlock), 0, sb, kin, np_new, 8 * pass, ntile, hist, flag, 1);
-      hipLaunchKernelGGL(k_rs_scan_local, dim3(nch), dim3(kBlock), 0, sb, hist, (int)nh, csum, flag, 1);
-      hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, sb, csum, nch, (int *)nullptr, flag, 1);
-      hipLaunchKernelGGL(k_rs_scan_add, dim3(nch), dim3(kBlock), 0, sb, hist, (int)nh, (const int *)csum, flag, 1);
-      hipLaunchKernelGGL(k_rs_scatter, dim3(tgrid), dim3(kBlock), 0, sb, kin, vin, np_new, 8 * pass, ntile,
-                         (const int *)hist, kout, vout, flag, 1);
-    }
-    hipLaunchKernelGGL(k_bin_split, dim3(blocks_for(np_new, 4096)), dim3(kBlock), 0, sb, (const int *)order_v, xyz_new,
-                       np_new, order_b, c->bin_qs ? (double *)c->qs.p : nullptr, (const DevStats *)st, flag);
-  }
   if (force != 1 && bg.nt > 0) {
     // input order: the surface points in input order (stable compaction:
     // per-block counts, their scan, the scatter; rocPRIM's select took 0.2 ms
@@ -1491,8 +1479,46 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     hipLaunchKernelGGL(k_cls_scatter, dim3((unsigned)ncls), dim3(kBlock), 0, sb, pclass, (long long)np_new,
                        (int)PMMG_PT_BDY, (const int *)bc, order_b, flag, 0);
   }
+  if (force != 0 && np_new > 0) {
+    // stable LSD radix sort of the keys (<= 3 * 7 + 2 bits) in 3 passes of 8 bits (pmmg_sort.hpp); the key
+    // kernel writes the first pass's digit table
+    const int ntile = (int)((np_new + kRsTile - 1) / kRsTile);
+    const long long nh = 256LL * ntile;
+    const int nch = (int)((nh + kScanChunk - 1) / kScanChunk);
+    if (!ensure(c, c->bvals2, 4 * nq) || !ensure(c, c->rs_hist, 4 * (size_t)nh) || !ensure(c, c->rs_csum, 4 * (size_t)nch))
+      return 0;
+    unsigned *k0 = (unsigned *)c->bkeys.p, *k1 = (unsigned *)c->bkeys2.p;
+    int *v0 = (int *)c->bvals.p, *v1 = (int *)c->bvals2.p, *hist = (int *)c->rs_hist.p, *csum = (int *)c->rs_csum.p;
+    const int tgrid = std::min(ntile, kRsGrid);
+    hipLaunchKernelGGL(k_bin_keys, dim3(tgrid), dim3(kBlock), 0, sc, xyz_new, pclass, np_new, (const Frame *)fr, flag,
+                       k0, v0, st, kRsTile, ntile, hist);
+    for (int pass = 0; pass < 3; pass++) {
+      const unsigned *kin = pass == 1 ? k1 : k0;
+      const int *vin = pass == 1 ? v1 : v0;
+      unsigned *kout = pass == 1 ? k0 : k1;
+      int *vout = pass == 1 ? v0 : (pass == 0 ? v1 : order_v);
+      if (pass > 0)
+        hipLaunchKernelGGL(k_rs_hist, dim3(tgrid), dim3(kBlock), 0, sc, kin, np_new, 8 * pass, ntile, hist, flag, 1);
+      hipLaunchKernelGGL(k_rs_scan_local, dim3(nch), dim3(kBlock), 0, sc, hist, (int)nh, csum, flag, 1);
+      hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, sc, csum, nch, (int *)nullptr, flag, 1);
+      hipLaunchKernelGGL(k_rs_scan_add, dim3(nch), dim3(kBlock), 0, sc, hist, (int)nh, (const int *)csum, flag, 1);
+      hipLaunchKernelGGL(k_rs_scatter, dim3(tgrid), dim3(kBlock), 0, sc, kin, vin, np_new, 8 * pass, ntile,
+                         (const int *)hist, kout, vout, flag, 1);
+    }
+    hipLaunchKernelGGL(k_bin_split, dim3(blocks_for(np_new, 4096)), dim3(kBlock), 0, sc, (const int *)order_v, xyz_new,
+                       np_new, order_b, c->bin_qs ? (double *)c->qs.p : nullptr, (const DevStats *)st, flag);
+  }
   HIPCK(c, hipGetLastError());
+  // auto mode with the binning on its own stream (split): the input order's lists (EV_ORDER, second stream)
+  // and the Morton order's (EV_ORDER2, third stream) are waited for separately, each by the launch of the
+  // volume / surface kernel for its order (the other launch returns at once): a call in input order no longer
+  // waits for the ~19 binning launches, which return at once but take ~130 us in a row (r05n, 8-way rank)
+  // (below 2^23 queries: a larger call's seed grid outlasts the binning chain anyway — cfg4's preparation
+  // 0.41 ms — and keeps one volume launch per call)
+  const bool split = force < 0 && sc != sb && np_new < (1 << 23);
   HIPCK(c, hipEventRecord(c->ev[EV_ORDER], sb));
+  HIPCK(c, hipEventRecord(c->ev[EV_ORDER2], sc)); // (sc == sb: the same point)
+  if (!split && sc != sb) HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_ORDER2], 0)); // the Morton surface list
 
   // ---- surface branch (second stream, after the order): seeds, k_bdy
   if (c->srf_solo > 0 || (c->srf_solo < 0 && np_new >= kSmallGroup))
@@ -1504,10 +1530,19 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
                        gs);
     // one round of the grid for up to 1M surface points (static split: a
     // second, nearly empty round doubled the surface branch alone)
-    hipLaunchKernelGGL(k_bdy, dim3(8 * blocks_for((np_new + 7) / 8, c->bdy_bpx)), dim3(kBlock), 0, sb, bg,
-                       (const Frame *)fr, (const int *)sgrid, gs, xyz_new, (const int *)order_b, S, elem_out, hit_out,
-                       (int *)c->fb_bdy.p, st, c->maxstep, c->bdy_dyn, FbInit{(int *)c->bbest.p},
-                       FbGridBufs{(int *)c->fbg_bdy_c.p, (int *)c->fbg_bdy_u.p, (int *)c->fbg_bdy_i.p});
+    auto bdy = [&](int want) {
+      hipLaunchKernelGGL(k_bdy, dim3(8 * blocks_for((np_new + 7) / 8, c->bdy_bpx)), dim3(kBlock), 0, sb, bg,
+                         (const Frame *)fr, (const int *)sgrid, gs, xyz_new, (const int *)order_b, S, elem_out,
+                         hit_out, (int *)c->fb_bdy.p, st, c->maxstep, c->bdy_dyn, FbInit{(int *)c->bbest.p},
+                         FbGridBufs{(int *)c->fbg_bdy_c.p, (int *)c->fbg_bdy_u.p, (int *)c->fbg_bdy_i.p}, flag, want);
+    };
+    if (split) { // input order's surface list first; the Morton one after the binning stream's join
+      bdy(0);
+      HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_ORDER2], 0));
+      bdy(1);
+    } else {
+      bdy(-1);
+    }
     if (!c->no_fb) launch_bdy_fallbacks(c, sb, S, xyz_new, elem_out, hit_out);
     HIPCK(c, hipGetLastError());
     if (nsg >= kRefillCells) { // the surface grid refilled for the next call (see k_reset above)
@@ -1524,16 +1559,26 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   // the volume kernel reads the order branch's lists only in Morton order (or when it may be chosen); in
   // forced input order its queries are the input's volume points and the wait is dropped (r05: the
   // cross-stream wait was ~20 us of a small group's main chain)
-  if (force != 0) HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_ORDER], 0));
+  if (force < 0) HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_ORDER], 0));
+  else if (force > 0) HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_ORDER2], 0));
   if (c->bdy_first) HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_BDY1], 0));
   HIPCK(c, hipEventRecord(c->ev[EV_VOL0], s));
   // ---- volume (main stream): walk + exact test + interpolation in one
   // kernel, then the exact continuation of the few queries it did not settle
-  hipLaunchKernelGGL(vol_fn, dim3((np_new + 63) / 64), dim3(64), 0, s, bg, (const Frame *)fr,
-                     (const unsigned long long *)grid, g, xyz_new, pclass, (const int *)order_v,
-                     c->bin_qs ? (const double *)c->qs.p : nullptr, np_new,
-                     (ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->filter_steps, flag, c->xcd_run,
-                     c->pad);
+  auto vol = [&](int want) {
+    hipLaunchKernelGGL(vol_fn, dim3((np_new + 63) / 64), dim3(64), 0, s, bg, (const Frame *)fr,
+                       (const unsigned long long *)grid, g, xyz_new, pclass, (const int *)order_v,
+                       c->bin_qs ? (const double *)c->qs.p : nullptr, np_new, (ContEntry *)c->cont.p, st, S,
+                       elem_out, hit_out, c->filter_steps, flag, c->xcd_run, c->pad, want);
+  };
+  if (split) {
+    vol(0);
+    HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_ORDER2], 0));
+    vol(1);
+  } else {
+    if (force < 0) HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_ORDER2], 0)); // (sc == sb: the same point)
+    vol(-1);
+  }
   HIPCK(c, hipEventRecord(c->ev[EV_WALK], s));
   // (8 x 64 one-wave blocks for a large call; fewer for a small group, whose continuations are a few hundred)
   const int wx = (int)std::min<long long>(64, std::max<long long>(2, (long long)np_new / 65536));
@@ -1605,7 +1650,7 @@ static int collect_stats(pmmg_hip_ctx *c, pmmg_hip_stats *out) {
   HIPCK(c, hipEventElapsedTime(&ms, c->ev[EV_START], c->ev[EV_PREP]));
   out->ms_prepare = ms;
   HIPCK(c, hipEventElapsedTime(&ms, c->ev[EV_SB0], c->ev[EV_ORDER]));
-  out->ms_sort = ms; // on the second stream, concurrent with the seed grid
+  out->ms_sort = ms; // on the second (and third) stream, concurrent with the seed grid
   HIPCK(c, hipEventElapsedTime(&ms, c->ev[EV_VOL0], c->ev[EV_VOL]));
   out->ms_vol = ms;
   HIPCK(c, hipEventElapsedTime(&ms, c->ev[EV_VOL0], c->ev[EV_WALK]));
@@ -1825,6 +1870,20 @@ int pmmg_hip_carry_over(pmmg_hip_ctx *c, int slot, int np, const int *src) {
   c->carry_slot = slot;
   c->carry_np = np;
   c->carry_bg = false;
+  return 1;
+}
+
+int pmmg_hip_release_scratch(pmmg_hip_ctx *c) {
+  if (!c) return 0;
+  HIPCK(c, hipSetDevice(c->device));
+  if (!snap_join(c)) return 0;
+  HIPCK(c, hipStreamSynchronize(c->stream));
+  HIPCK(c, hipStreamSynchronize(c->stream2));
+  if (c->stream3) HIPCK(c, hipStreamSynchronize(c->stream3));
+  pmmg_snap_cache_free(&c->snap_cache);
+  for (DevBuf *b : {&c->bvals2, &c->rs_hist, &c->rs_csum}) release(*b);
+  for (pmmg_hip_ctx *l : c->lanes) pmmg_hip_destroy(l);
+  c->lanes.clear();
   return 1;
 }
 

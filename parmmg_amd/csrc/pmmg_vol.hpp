@@ -966,7 +966,10 @@ __global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsign
                                             const double *qxyz, const uint8_t *pclass, const int *order,
                                             const double *qs, int np, ContEntry *cont, DevStats *st, Slots S,
                                             int *elem_out, int8_t *hit_out, int filter_steps,
-                                            const int *order_flag, int xcd_run, int pad) {
+                                            const int *order_flag, int xcd_run, int pad, int want) {
+  // want >= 0: the launch for one of the two orders (auto mode launches both, each after its own lists;
+  // the other returns at once)
+  if (want >= 0 && order_flag[0] != want) return;
   __shared__ VolShared<PK> sh;
   bstats_init(&sh.bs);
   __syncthreads();

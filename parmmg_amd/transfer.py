@@ -289,6 +289,11 @@ class TransferContext:
         s = None if src is None else np.ascontiguousarray(src, np.int32)
         self._ck(self.lib.pmmg_hip_carry_over(self.h, int(slot), int(npt), _p(s)), "carry_over")
 
+    def release_scratch(self) -> None:
+        """pmmg_hip_release_scratch: free the snapshot buckets, the binning's
+        scratch and the group lanes (re-allocated on demand)."""
+        self._ck(self.lib.pmmg_hip_release_scratch(self.h), "release_scratch")
+
     def bytes_up(self, reset: bool = False) -> int:
         """host -> device bytes of host-mode calls (pmmg_hip_bytes_up)"""
         return int(self.lib.pmmg_hip_bytes_up(self.h, int(reset)))

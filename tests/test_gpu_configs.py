@@ -157,3 +157,31 @@ def test_cfgG_graded_full_size_visit_range():
     print("cfgG nvol_exact", st.nvol_exact, "stepmax", st.stepmax, "steps/pt",
           st.steps_total / max(1, st.nvol + st.nbdy))
     assert st.nvol_exact < 0.01 * st.nvol
+
+
+@pytest.mark.gpu
+def test_cfg3_shuffled_numbering_auto_order():
+    """cfg3's new points shuffled: the coherence test picks the Morton order,
+    which (below 2^23 queries) runs beside the input order's lists on a
+    stream of its own, each order with its own volume / surface launch.  Every
+    point is located, and a point located in the same element as in the
+    input-order call gets bit-identical rows."""
+    w = configs.CFG3
+    bg, new = configs.build_meshes(w, seed=synth.SEED, with_new_tetra=False)
+    pc = synth.classes(new)
+    met = synth.solution(w.metric, bg.xyz)
+    fields = [synth.solution(f, bg.xyz) for f in w.fields]
+    perm = np.random.default_rng(7).permutation(new.np)
+    with TransferContext(0) as ctx:
+        a = run_dev(ctx, bg, new.xyz, met, fields, pc, w.hausd)
+        b = run_dev(ctx, bg, np.ascontiguousarray(new.xyz[perm]), met, fields, np.ascontiguousarray(pc[perm]),
+                    w.hausd)
+    assert a[4].sorted == 0 and b[4].sorted == 1
+    inv = np.argsort(perm)
+    el_b, hit_b = b[2][inv], b[3][inv]
+    act = pc != 0
+    assert ((hit_b & 15) != 0).sum() == act.sum()
+    same = act & (a[2] == el_b) & (a[3] == hit_b)
+    assert same.sum() > 0.99 * act.sum()
+    for x, y in zip([a[0]] + a[1], [b[0]] + b[1]):
+        assert np.array_equal(x[same].view(np.uint64), y[inv][same].view(np.uint64))

@@ -120,3 +120,31 @@ def test_groups_call_leaves_the_context_background(cases):
         _same(out, run_gpu(case, tet8=False))
         rep = check(case, out)
         assert rep["class_i"] == rep["class_i_same"]
+
+
+@pytest.mark.gpu
+def test_groups_after_release_scratch(cases, singles):
+    """pmmg_hip_release_scratch between calls: the lanes and the binning /
+    snapshot scratch are re-created on demand, the outputs unchanged; a
+    Morton-binned single call and a device adjacency build after it too."""
+    with TransferContext(0) as ctx:
+        gs = [_device_group(ctx, c) for c in cases]
+        for rep in range(2):
+            ctx.locate_interp_groups(gs, sync=True)
+            for g, one in zip(gs, singles):
+                _same(_download(g), one)
+            ctx.release_scratch()
+    case = cases[1]
+    with TransferContext(0, sort=True) as ctx:
+        a = run_gpu(case, ctx=ctx)
+        ctx.release_scratch()
+        b = run_gpu(case, ctx=ctx)
+        _same(a, b)
+        assert a["stats"]["sorted"] == 1 and b["stats"]["sorted"] == 1
+        bg = case["bg"]
+        tetv = ctx.upload(bg.tetv)
+        adja, _ = ctx.build_adjacency(bg.np, tetv, adja=True, tet8=False)
+        ctx.release_scratch()
+        adja2, _ = ctx.build_adjacency(bg.np, tetv, adja=True, tet8=False)
+        np.testing.assert_array_equal(adja.download(), bg.adja)
+        np.testing.assert_array_equal(adja2.download(), bg.adja)
