@@ -24,7 +24,13 @@ __device__ __forceinline__ int bdy_query(const Bg &bg, const Frame *fr, const in
   double phi[3];
   for (;;) {
     ++steps;
-    tri_load(bg, k, t);
+    int ad[3];
+    if (bg.trec) {
+      tri_load_rec(bg.trec, k, t, ad);
+    } else {
+      tri_load(bg, k, t);
+      for (int j = 0; j < 3; j++) ad[j] = bg.adjt[3 * (size_t)(k - 1) + j];
+    }
     double b[3];
     double dist = tri_bary(x, t.p, t.q, t.n, b);
     int r[3];
@@ -57,7 +63,6 @@ __device__ __forceinline__ int bdy_query(const Bg &bg, const Frame *fr, const in
     // step through the first edge (sorted order) whose neighbour exists; a
     // visited neighbour triggers the wedge test of that edge and, outside
     // it, the cone test of the wedge's end vertex (locate_pmmg.c:629-668)
-    const int *ad = bg.adjt + 3 * (size_t)(k - 1);
     const int a0 = ad[0], a1 = ad[1], a2 = ad[2];
     int next = 0;
     bool done = false;

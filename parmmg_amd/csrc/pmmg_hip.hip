@@ -147,7 +147,7 @@ struct DevBuf {
 
 enum {
   EV_START, EV_FRAME, EV_PREP, EV_ORDER, EV_VOL0, EV_WALK, EV_VOL, EV_JOIN, EV_END, EV_BDY0, EV_BDY1, EV_RESET,
-  EV_SB0, EV_COH, EV_ORDER2, EV_COUNT
+  EV_SB0, EV_ORDER2, EV_COUNT
 };
 
 struct pmmg_hip_ctx {
@@ -173,6 +173,7 @@ struct pmmg_hip_ctx {
   std::vector<DevBuf> o_f;
   // work buffers
   DevBuf frame, stats, grid, sgrid, order_v, order_b, cont, xq;
+  DevBuf trec;                            // boundary trias' walk records (TriRec, per call)
   DevBuf axh;                             // per-axis histograms of the seed grid map (k_quantize)
   DevBuf bkeys, bkeys2, bvals, bvals2;    // Morton binning: keys and ids, ping-ponged by the radix sort
   DevBuf rs_hist, rs_csum;                // the radix sort's digit table and its scan's chunk sums
@@ -676,7 +677,7 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   if (c->stream3) (void)hipStreamSynchronize(c->stream3);
   if (c->cstream) (void)hipStreamSynchronize(c->cstream);
   DevBuf *bufs[] = {&c->o_xyz, &c->o_tetv, &c->o_adja, &c->o_triv, &c->o_adjt, &c->o_met, &c->o_rec, &c->frame,
-                    &c->stats, &c->grid, &c->sgrid, &c->order_v,
+                    &c->stats, &c->grid, &c->sgrid, &c->order_v, &c->trec,
                     &c->order_b, &c->cont, &c->xq, &c->qs, &c->axh, &c->bkeys, &c->bkeys2, &c->bvals, &c->bvals2, &c->rs_hist, &c->rs_csum, &c->oflag, &c->cls_cnt, &c->qmin, &c->fb_vol, &c->fb_bdy,
                     &c->best, &c->nac, &c->cres, &c->bbest, &c->bnac, &c->bcres, &c->fbp_vol, &c->fbp_bdy, &c->fbg_vol_c,
                     &c->fbg_vol_u, &c->fbg_vol_i, &c->fbg_bdy_c, &c->fbg_bdy_u, &c->fbg_bdy_i, &c->h_xyz,
@@ -1390,6 +1391,14 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
       !ensure(c, c->axh, sizeof(int) * 3 * kMapBins * (size_t)kHistBlocks))
     return 0;
   bg.xq = (const int *)c->xq.p;
+  // the boundary trias' walk records (written by k_seed_srf, read by k_bdy's walk only)
+  TriRec *trec = nullptr;
+  if (bg.nt > 0) {
+    if (!ensure(c, c->trec, sizeof(TriRec) * (size_t)bg.nt)) return 0;
+    trec = (TriRec *)c->trec.p;
+  }
+  Bg bgw = bg; // the surface walk's view
+  bgw.trec = trec;
   Frame *fr = (Frame *)c->frame.p;
   DevStats *st = (DevStats *)c->stats.p;
   unsigned long long *grid = (unsigned long long *)c->grid.p;
@@ -1400,14 +1409,6 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
 
   // ---- frame (main stream)
   HIPCK(c, hipEventRecord(c->ev[EV_START], s));
-  // the coherence test first, on the second stream beside the frame kernels
-  // (it reads only the queries); a forced order's flag is written by k_reset
-  if (force < 0) {
-    HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_START], 0));
-    hipLaunchKernelGGL(k_coherence, dim3(1), dim3(kBlock), 0, sb, xyz_new, np_new, (int *)c->oflag.p, force,
-                       c->bin_bits);
-    HIPCK(c, hipEventRecord(c->ev[EV_COH], sb));
-  }
   // seed grids: cleared here unless the previous call left them clean (a
   // large grid is refilled at the end of the call that used it, beside the
   // other stream's tail: r05, cfg4 k_reset 32 us -> the stats only)
@@ -1419,8 +1420,10 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   // the input order's surface list needs only the zeroed counters (and the coherence flag), not the frame
   HIPCK(c, hipEventRecord(c->ev[EV_RESET], s));
   // bbox (its last block finalises the frame), the seed grid's axis maps
-  hipLaunchKernelGGL(k_bbox, dim3(blocks_for(bg.np / c->bbox_stride + 1, 256)), dim3(kBlock), 0, s, bg.xyz, bg.np, fr,
-                     c->bbox_stride, g, gs, gb);
+  // (auto order: one more block, the queries' coherence test, whose flag the order and volume kernels read)
+  hipLaunchKernelGGL(k_bbox, dim3(blocks_for(bg.np / c->bbox_stride + 1, 256) + (force < 0 ? 1 : 0)), dim3(kBlock), 0,
+                     s, bg.xyz, bg.np, fr, c->bbox_stride, g, gs, gb, xyz_new, np_new,
+                     force < 0 ? (int *)c->oflag.p : nullptr);
   // the second stream needs the frame only (lo, inv_bin, inv_srf), not the
   // axis maps (r04: EV_FRAME moved here from after k_axis_map)
   HIPCK(c, hipEventRecord(c->ev[EV_FRAME], s));
@@ -1434,7 +1437,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   // the frame.  (r04: the axis maps moved here beside the fixed-point copy
   // cost 10 groups 0.11 -> 0.25 ms per group and the 8-way rank +0.02 ms for
   // -0.0 at cfg4, `profiles/r04s`: not kept)
-  HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_RESET], 0));
+  HIPCK(c, hipStreamWaitEvent(sb, c->ev[force < 0 ? EV_FRAME : EV_RESET], 0)); // (the order flag)
   HIPCK(c, hipEventRecord(c->ev[EV_SB0], sb));
   // the Morton binning on a third stream (r05, `profiles/r05m`: on the second stream its ~19 launches, each
   // returning at once when the coherence test picks input order, held the 8-way rank's volume kernel 86 us
@@ -1443,9 +1446,15 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   if (force != 0) {
     if (!c->stream3 && hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess) c->stream3 = nullptr;
     if (c->stream3) sc = c->stream3;
-    HIPCK(c, hipStreamWaitEvent(sc, c->ev[EV_FRAME], 0));
-    if (force < 0 && sc != sb) HIPCK(c, hipStreamWaitEvent(sc, c->ev[EV_COH], 0));
+    HIPCK(c, hipStreamWaitEvent(sc, c->ev[EV_FRAME], 0)); // (the frame and the order flag)
   }
+  // auto mode with the binning on its own stream (split): the input order's lists (EV_ORDER, second stream)
+  // and the Morton order's (EV_ORDER2, third stream) are waited for separately, each by the launch of the
+  // volume / surface kernel for its order (the other launch returns at once): a call in input order no longer
+  // waits for the ~19 binning launches, which return at once but take ~130 us in a row (r05n, 8-way rank).
+  // Below 2^23 queries: a larger call's seed grid outlasts the binning chain anyway (cfg4's preparation
+  // 0.41 ms) and keeps one volume launch per call.
+  const bool split = force < 0 && sc != sb && np_new < (1 << 23);
   HIPCK(c, hipGetLastError());
 
   // ---- seed grid (main stream): volume seeds
@@ -1460,7 +1469,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   HIPCK(c, hipEventRecord(c->ev[EV_PREP], s));
 
   // ---- query order (second stream, after the frame): the kernels of both
-  // orders, each gated on k_coherence's flag on the device — no host read.
+  // orders, each gated on the coherence test's flag (k_bbox's extra block) on the device — no host read.
   // Forced orders enqueue only theirs; a small group (below kSmallGroup
   // queries: its background and solutions stay in the Infinity Cache, where
   // a numbering's locality matters little) takes the input order untested.
@@ -1468,20 +1477,22 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
 #ifdef PMMG_HIP_MEASURE
   if (c->set_order) hipLaunchKernelGGL(k_set_order, dim3(1), dim3(1), 0, s, st, force > 0 ? 1 : 0, c->bin_bits);
 #endif
-  if (force != 1 && bg.nt > 0) {
-    // input order: the surface points in input order (stable compaction:
-    // per-block counts, their scan, the scatter; rocPRIM's select took 0.2 ms
-    // longer here, r03o)
+  // input order: the surface points in input order (stable compaction:
+  // per-block counts, their scan, the scatter; rocPRIM's select took 0.2 ms
+  // longer here, r03o)
+  auto launch_cls = [&]() {
+    if (force == 1 || bg.nt <= 0) return;
     int *bc = (int *)c->cls_cnt.p;
     hipLaunchKernelGGL(k_cls_count, dim3((unsigned)ncls), dim3(kBlock), 0, sb, pclass, (long long)np_new,
                        (int)PMMG_PT_BDY, bc, flag, 0);
     hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, sb, bc, (int)ncls, &st->nbdy, flag, 0);
     hipLaunchKernelGGL(k_cls_scatter, dim3((unsigned)ncls), dim3(kBlock), 0, sb, pclass, (long long)np_new,
                        (int)PMMG_PT_BDY, (const int *)bc, order_b, flag, 0);
-  }
-  if (force != 0 && np_new > 0) {
-    // stable LSD radix sort of the keys (<= 3 * 7 + 2 bits) in 3 passes of 8 bits (pmmg_sort.hpp); the key
-    // kernel writes the first pass's digit table
+  };
+  // Morton order: stable LSD radix sort of the keys (<= 3 * 7 + 2 bits) in 3 passes of 8 bits
+  // (pmmg_sort.hpp); the key kernel writes the first pass's digit table
+  auto launch_morton = [&]() -> int {
+    if (force == 0 || np_new <= 0) return 1;
     const int ntile = (int)((np_new + kRsTile - 1) / kRsTile);
     const long long nh = 256LL * ntile;
     const int nch = (int)((nh + kScanChunk - 1) / kScanChunk);
@@ -1507,62 +1518,41 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     }
     hipLaunchKernelGGL(k_bin_split, dim3(blocks_for(np_new, 4096)), dim3(kBlock), 0, sc, (const int *)order_v, xyz_new,
                        np_new, order_b, c->bin_qs ? (double *)c->qs.p : nullptr, (const DevStats *)st, flag);
-  }
-  HIPCK(c, hipGetLastError());
-  // auto mode with the binning on its own stream (split): the input order's lists (EV_ORDER, second stream)
-  // and the Morton order's (EV_ORDER2, third stream) are waited for separately, each by the launch of the
-  // volume / surface kernel for its order (the other launch returns at once): a call in input order no longer
-  // waits for the ~19 binning launches, which return at once but take ~130 us in a row (r05n, 8-way rank)
-  // (below 2^23 queries: a larger call's seed grid outlasts the binning chain anyway — cfg4's preparation
-  // 0.41 ms — and keeps one volume launch per call)
-  const bool split = force < 0 && sc != sb && np_new < (1 << 23);
-  HIPCK(c, hipEventRecord(c->ev[EV_ORDER], sb));
-  HIPCK(c, hipEventRecord(c->ev[EV_ORDER2], sc)); // (sc == sb: the same point)
-  if (!split && sc != sb) HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_ORDER2], 0)); // the Morton surface list
-
+    return 1;
+  };
+  // one round of the grid for up to 1M surface points (static split: a
+  // second, nearly empty round doubled the surface branch alone)
+  auto bdy = [&](int want) {
+    hipLaunchKernelGGL(k_bdy, dim3(8 * blocks_for((np_new + 7) / 8, c->bdy_bpx)), dim3(kBlock), 0, sb, bgw,
+                       (const Frame *)fr, (const int *)sgrid, gs, xyz_new, (const int *)order_b, S, elem_out,
+                       hit_out, (int *)c->fb_bdy.p, st, c->maxstep, c->bdy_dyn, FbInit{(int *)c->bbest.p},
+                       FbGridBufs{(int *)c->fbg_bdy_c.p, (int *)c->fbg_bdy_u.p, (int *)c->fbg_bdy_i.p}, flag, want);
+  };
   // ---- surface branch (second stream, after the order): seeds, k_bdy
-  if (c->srf_solo > 0 || (c->srf_solo < 0 && np_new >= kSmallGroup))
-    HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_PREP], 0));
-  HIPCK(c, hipEventRecord(c->ev[EV_BDY0], sb));
-  if (bg.nt > 0) {
-    if (force == 0) HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_FRAME], 0)); // (the surface seeds need the frame)
-    hipLaunchKernelGGL(k_seed_srf, dim3(blocks_for(bg.nt, 4096)), dim3(kBlock), 0, sb, bg, (const Frame *)fr, sgrid,
-                       gs);
-    // one round of the grid for up to 1M surface points (static split: a
-    // second, nearly empty round doubled the surface branch alone)
-    auto bdy = [&](int want) {
-      hipLaunchKernelGGL(k_bdy, dim3(8 * blocks_for((np_new + 7) / 8, c->bdy_bpx)), dim3(kBlock), 0, sb, bg,
-                         (const Frame *)fr, (const int *)sgrid, gs, xyz_new, (const int *)order_b, S, elem_out,
-                         hit_out, (int *)c->fb_bdy.p, st, c->maxstep, c->bdy_dyn, FbInit{(int *)c->bbest.p},
-                         FbGridBufs{(int *)c->fbg_bdy_c.p, (int *)c->fbg_bdy_u.p, (int *)c->fbg_bdy_i.p}, flag, want);
-    };
-    if (split) { // input order's surface list first; the Morton one after the binning stream's join
-      bdy(0);
-      HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_ORDER2], 0));
-      bdy(1);
-    } else {
-      bdy(-1);
+  auto srf_head = [&]() {
+    if (c->srf_solo > 0 || (c->srf_solo < 0 && np_new >= kSmallGroup))
+      HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_PREP], 0));
+    HIPCK(c, hipEventRecord(c->ev[EV_BDY0], sb));
+    if (bg.nt > 0) {
+      if (force == 0) HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_FRAME], 0)); // (the surface seeds need the frame)
+      hipLaunchKernelGGL(k_seed_srf, dim3(blocks_for(bg.nt, 4096)), dim3(kBlock), 0, sb, bg, (const Frame *)fr,
+                         sgrid, gs, trec);
     }
-    if (!c->no_fb) launch_bdy_fallbacks(c, sb, S, xyz_new, elem_out, hit_out);
-    HIPCK(c, hipGetLastError());
-    if (nsg >= kRefillCells) { // the surface grid refilled for the next call (see k_reset above)
-      hipLaunchKernelGGL(k_fill32, dim3(blocks_for(nsg, 2048)), dim3(kBlock), 0, sb, sgrid, nsg, INT_MAX);
-      c->sgrid_clean_p = c->sgrid.p;
-      c->sgrid_clean_n = nsg;
+    return 1;
+  };
+  auto srf_tail = [&]() {
+    if (bg.nt > 0) {
+      if (!c->no_fb) launch_bdy_fallbacks(c, sb, S, xyz_new, elem_out, hit_out);
+      HIPCK(c, hipGetLastError());
+      if (nsg >= kRefillCells) { // the surface grid refilled for the next call (see k_reset above)
+        hipLaunchKernelGGL(k_fill32, dim3(blocks_for(nsg, 2048)), dim3(kBlock), 0, sb, sgrid, nsg, INT_MAX);
+        c->sgrid_clean_p = c->sgrid.p;
+        c->sgrid_clean_n = nsg;
+      }
     }
-  }
-  HIPCK(c, hipEventRecord(c->ev[EV_BDY1], sb));
-
-#ifdef PMMG_HIP_MEASURE
-  if (c->brick > 0 && !brick_renumber(c, s, bg, S, fr, g)) return 0;
-#endif
-  // the volume kernel reads the order branch's lists only in Morton order (or when it may be chosen); in
-  // forced input order its queries are the input's volume points and the wait is dropped (r05: the
-  // cross-stream wait was ~20 us of a small group's main chain)
-  if (force < 0) HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_ORDER], 0));
-  else if (force > 0) HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_ORDER2], 0));
-  if (c->bdy_first) HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_BDY1], 0));
-  HIPCK(c, hipEventRecord(c->ev[EV_VOL0], s));
+    HIPCK(c, hipEventRecord(c->ev[EV_BDY1], sb));
+    return 1;
+  };
   // ---- volume (main stream): walk + exact test + interpolation in one
   // kernel, then the exact continuation of the few queries it did not settle
   auto vol = [&](int want) {
@@ -1572,11 +1562,46 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
                        elem_out, hit_out, c->filter_steps, flag, c->xcd_run, c->pad, want);
   };
   if (split) {
+    // Host enqueue order (r05q trace): the input order's kernels first — the surface list, the surface
+    // seeds and walk, the volume kernel — then the ~19 binning launches and the Morton order's launches.
+    // Enqueued after the binning chain, the input order's volume kernel started ~200 us after the seed grid
+    // had finished: the host was still enqueueing (~8 us per launch), the device idle.
+    launch_cls();
+    HIPCK(c, hipEventRecord(c->ev[EV_ORDER], sb));
+    if (!srf_head()) return 0;
+    if (bg.nt > 0) bdy(0);
+    HIPCK(c, hipEventRecord(c->ev[EV_VOL0], s));
     vol(0);
+    if (!launch_morton()) return 0;
+    HIPCK(c, hipGetLastError());
+    HIPCK(c, hipEventRecord(c->ev[EV_ORDER2], sc));
+    if (bg.nt > 0) {
+      HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_ORDER2], 0));
+      bdy(1);
+    }
+    if (!srf_tail()) return 0;
     HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_ORDER2], 0));
     vol(1);
   } else {
-    if (force < 0) HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_ORDER2], 0)); // (sc == sb: the same point)
+    launch_cls();
+    if (!launch_morton()) return 0;
+    HIPCK(c, hipGetLastError());
+    HIPCK(c, hipEventRecord(c->ev[EV_ORDER], sb));
+    HIPCK(c, hipEventRecord(c->ev[EV_ORDER2], sc)); // (sc == sb: the same point)
+    if (sc != sb) HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_ORDER2], 0)); // the Morton surface list
+    if (!srf_head()) return 0;
+    if (bg.nt > 0) bdy(-1);
+    if (!srf_tail()) return 0;
+#ifdef PMMG_HIP_MEASURE
+    if (c->brick > 0 && !brick_renumber(c, s, bg, S, fr, g)) return 0;
+#endif
+    // the volume kernel reads the order branch's lists only in Morton order (or when it may be chosen); in
+    // forced input order its queries are the input's volume points and the wait is dropped (r05: the
+    // cross-stream wait was ~20 us of a small group's main chain)
+    if (force < 0) HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_ORDER], 0));
+    if (force != 0 && sc != sb) HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_ORDER2], 0));
+    if (c->bdy_first) HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_BDY1], 0));
+    HIPCK(c, hipEventRecord(c->ev[EV_VOL0], s));
     vol(-1);
   }
   HIPCK(c, hipEventRecord(c->ev[EV_WALK], s));

@@ -2,7 +2,7 @@
 // (included by pmmg_hip.hip only): state reset, background frame, volume and
 // surface seed grids, and the query order.
 //
-// The input-order coherence test runs on the device (k_coherence's flag); in
+// The input-order coherence test runs on the device (coherence_block, run by k_bbox's extra block); in
 // auto mode both the Morton binning (pmmg_sort.hpp) and the class compaction
 // of the surface list are enqueued, each gated on that flag, and the volume
 // kernel reads it: nothing is read back inside a call.
@@ -260,7 +260,7 @@ __global__ __launch_bounds__(kBlock) void k_quantize(const double *xyz, long lon
 
 // one launch initialises the per-call state: frame accumulators, counters,
 // seed grids
-// (and writes the order flag of a forced order, when k_coherence is not
+// (and writes the order flag of a forced order, when the coherence test is not
 // launched: force >= 0)
 __global__ __launch_bounds__(kBlock) void k_reset(Frame *fr, DevStats *st, unsigned long long *grid, long long ng,
                                                   int *sgrid, long long nsg, int *flag, int force, int force_bits) {
@@ -297,12 +297,21 @@ __device__ void frame_final(Frame *fr, int g, int gs, int gb);
 
 // the last block to finish also finalises the frame (one launch less per
 // call; the other blocks' atomics are read back atomically)
+// flag != null (auto order): the grid's last block runs the queries' coherence
+// test (coherence_block) instead of sampling vertices — the other blocks take
+// the same samples as without it — so the order flag is on the main stream
+// after k_bbox (r05: as a one-block kernel on the second stream, every kernel
+// of the other streams that reads the flag waited on it across queues, and
+// the runtime released the volume kernel only after the binning chain)
+__device__ void coherence_block(const double *xyz, int np, int *flag);
 __global__ __launch_bounds__(kBlock) void k_bbox(const double *xyz, int np, Frame *fr, int stride, int g, int gs,
-                                                 int gb) {
+                                                 int gb, const double *qxyz, int nq, int *flag) {
   __shared__ unsigned long long slo[3][kBlock / 64], shi[3][kBlock / 64];
   unsigned long long lo[3] = {~0ULL, ~0ULL, ~0ULL}, hi[3] = {0ULL, 0ULL, 0ULL};
   const long long ns = ((long long)np + stride - 1) / stride + 2;
-  for (long long j = blockIdx.x * blockDim.x + threadIdx.x; j < ns; j += gridDim.x * blockDim.x) {
+  const int nb = flag ? gridDim.x - 1 : gridDim.x; // blocks sampling the vertices
+  if (flag && blockIdx.x == nb) coherence_block(qxyz, nq, flag); // (block-uniform)
+  for (long long j = blockIdx.x * blockDim.x + threadIdx.x; blockIdx.x < nb && j < ns; j += (long long)nb * blockDim.x) {
     unsigned long long z = (unsigned long long)j * 0x9E3779B97F4A7C15ULL + 0xB0B0B0B0ULL;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
@@ -583,10 +592,12 @@ __device__ __forceinline__ int seed_vol(const unsigned long long *cell, int g, c
 // ---------------------------------------------------------------- surface seeds and node -> tria CSR
 
 // surface seeds: cell of each tria centroid -> min id
-__global__ __launch_bounds__(kBlock) void k_seed_srf(Bg bg, const Frame *fr, int *cell, int g) {
+// (and the trias' walk records, rec: TriRec, when not null)
+__global__ __launch_bounds__(kBlock) void k_seed_srf(Bg bg, const Frame *fr, int *cell, int g, TriRec *rec) {
   for (int k = 1 + blockIdx.x * blockDim.x + threadIdx.x; k <= bg.nt; k += gridDim.x * blockDim.x) {
     const int *tv = bg.triv + 3 * (size_t)(k - 1);
     if (tv[0] <= 0) continue;
+    if (rec) tri_rec_build(bg, k, rec);
     double p0[3], p1[3], p2[3];
     load_pt(bg.xyz, tv[0], p0);
     load_pt(bg.xyz, tv[1], p1);
@@ -747,22 +758,16 @@ constexpr int kBinBitsCoherent = 5; // 32^3 cells for a mostly coherent numberin
 // points in the bbox of the sample: coherent when at least half of them are
 // below 4h (a median test: the jumps at the ends of lattice rows or of Mmg's
 // local numbering runs do not count; a shuffled numbering has almost every
-// distance at the scale of the bbox).  force: 1 always Morton-bin, 0 never,
-// -1 test.  Writes flag[0] (1: Morton bins) and flag[1] (their bits per
-// axis), which the host reads back and passes to the volume kernel.
-__global__ __launch_bounds__(kBlock) void k_coherence(const double *xyz, int np, int *flag, int force,
-                                                      int force_bits) {
-  if (force >= 0) {
-    if (threadIdx.x == 0) {
-      flag[0] = force;
-      flag[1] = force_bits;
-    }
-    return;
-  }
-  constexpr int nsamp = 4096, per = nsamp / kBlock;
-  __shared__ double slo[3][kBlock], shi[3][kBlock];
+// distance at the scale of the bbox).  One block of k_quantize runs it (r05:
+// on a stream of its own, as a one-block kernel, every other stream's kernels
+// that read the flag waited on it across queues); writes flag[0] (1: Morton
+// bins) and flag[1] (their bits per axis), read on the device by the order
+// kernels and the volume / surface kernels.
+__device__ __noinline__ void coherence_block(const double *xyz, int np, int *flag) {
+  constexpr int nsamp = 4096, per = nsamp / kBlock, nw = kBlock / 64;
+  __shared__ double s_lo[3][nw], s_hi[3][nw];
+  __shared__ int s_near[nw];
   __shared__ double s_h;
-  __shared__ int s_near[kBlock];
   double dist[per], lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
 #pragma unroll
   for (int q = 0; q < per; q++) {
@@ -786,17 +791,24 @@ __global__ __launch_bounds__(kBlock) void k_coherence(const double *xyz, int np,
     }
     dist[q] = sqrt(d2);
   }
-  for (int d = 0; d < 3; d++) {
-    slo[d][threadIdx.x] = lo[d];
-    shi[d][threadIdx.x] = hi[d];
-  }
+  const int w = threadIdx.x >> 6;
+  for (int d = 0; d < 3; d++)
+    for (int o = 32; o > 0; o >>= 1) {
+      lo[d] = fmin(lo[d], __shfl_xor(lo[d], o));
+      hi[d] = fmax(hi[d], __shfl_xor(hi[d], o));
+    }
+  if (__lane_id() == 0)
+    for (int d = 0; d < 3; d++) {
+      s_lo[d][w] = lo[d];
+      s_hi[d][w] = hi[d];
+    }
   __syncthreads();
   if (threadIdx.x == 0) {
     double L[3] = {1e300, 1e300, 1e300}, H[3] = {-1e300, -1e300, -1e300};
-    for (int j = 0; j < kBlock; j++)
+    for (int j = 0; j < nw; j++)
       for (int d = 0; d < 3; d++) {
-        L[d] = fmin(L[d], slo[d][j]);
-        H[d] = fmax(H[d], shi[d][j]);
+        L[d] = fmin(L[d], s_lo[d][j]);
+        H[d] = fmax(H[d], s_hi[d][j]);
       }
     double vol = fmax(H[0] - L[0], 1e-300) * fmax(H[1] - L[1], 1e-300) * fmax(H[2] - L[2], 1e-300);
     s_h = cbrt(vol / (double)(np > 1 ? np : 1));
@@ -805,11 +817,12 @@ __global__ __launch_bounds__(kBlock) void k_coherence(const double *xyz, int np,
   int near = 0;
 #pragma unroll
   for (int q = 0; q < per; q++) near += dist[q] < 4.0 * s_h ? 1 : 0;
-  s_near[threadIdx.x] = near;
+  for (int o = 32; o > 0; o >>= 1) near += __shfl_xor(near, o);
+  if (__lane_id() == 0) s_near[w] = near;
   __syncthreads();
   if (threadIdx.x == 0) {
     int tot = 0;
-    for (int j = 0; j < kBlock; j++) tot += s_near[j];
+    for (int j = 0; j < nw; j++) tot += s_near[j];
     // input order when 3 in 4 steps are short; else Morton bins, with
     // coarse cells (kBinBitsCoherent bits per axis: the input order inside a
     // cell is kept and mostly coherent) when at least half are short, fine
@@ -837,7 +850,7 @@ __global__ __launch_bounds__(kBlock) void k_coherence(const double *xyz, int np,
 // them coalesced) and the surface list.  The radix sort is stable: the order
 // is a deterministic function of the input.
 
-// flag: the order decision {sorted, bits per axis} (k_coherence); the kernel
+// flag: the order decision {sorted, bits per axis} (coherence_block); the kernel
 // runs only when flag[0] == 1.  Blocks loop over the radix sort's tiles
 // (tile_keys keys, pmmg_sort.hpp): besides the keys it writes each tile's
 // histogram of the first 8-bit digit (hist[digit * ntile + tile]), the first

@@ -975,7 +975,7 @@ __global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsign
   __syncthreads();
   const LaneSlotsF L{(lds_float *)&sh.u.slots[__lane_id()]};
   const int i = xcd_block_runs(xcd_run) * 64 + threadIdx.x;
-  const bool sorted = order_flag[0] == 1; // the call's query order, decided on the device (k_coherence)
+  const bool sorted = order_flag[0] == 1; // the call's query order, decided on the device (the coherence test in k_bbox)
   bool active;
   int ip = 0;
   if (sorted) {
