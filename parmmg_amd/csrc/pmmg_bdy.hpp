@@ -24,13 +24,13 @@ __device__ __forceinline__ int bdy_query(const Bg &bg, const Frame *fr, const in
   double phi[3];
   for (;;) {
     ++steps;
+    // (r05: 128-byte walk records per tria — coordinates, normal, ids,
+    // adjacency, one line per step — built by k_seed_srf made the surface
+    // branch 0.44 -> 0.50 ms at cfg4 and the volume stage +3 %: not kept,
+    // profiles/r05u)
+    tri_load(bg, k, t);
     int ad[3];
-    if (bg.trec) {
-      tri_load_rec(bg.trec, k, t, ad);
-    } else {
-      tri_load(bg, k, t);
-      for (int j = 0; j < 3; j++) ad[j] = bg.adjt[3 * (size_t)(k - 1) + j];
-    }
+    for (int j = 0; j < 3; j++) ad[j] = bg.adjt[3 * (size_t)(k - 1) + j];
     double b[3];
     double dist = tri_bary(x, t.p, t.q, t.n, b);
     int r[3];

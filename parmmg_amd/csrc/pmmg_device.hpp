@@ -32,22 +32,6 @@ constexpr int kXqStride = PMMG_XQ_STRIDE; // ints per row of the fixed-point ver
 // tstride 1) or one packed 32-byte record per tetra {v[4], adja[4]}
 // (tetv = rec, adja = rec + 1, tstride 2), whose two halves share a cache
 // line, so a walk step costs one line request for the tetra instead of two.
-// A boundary tria's walk record, one 128-byte line (built per call by
-// k_seed_srf, which reads the same rows for the surface seeds): vertex
-// coordinates, unit normal and |nonunit normal| as tri_load computes them (the
-// same operations, so the same bits), vertex ids and tria adjacency — a
-// surface walk step is one line load instead of the tria row, then its three
-// vertex rows (r05: the surface branch is a chain of dependent loads, its
-// time the longest walk's, not the points')
-struct TriRec {
-  double p[3][3];
-  double n[3];
-  double q;
-  int v[3];
-  int a[3];
-};
-static_assert(sizeof(TriRec) == 128, "one line per tria");
-
 struct Bg {
   const double *xyz;
   const int *xq; // fixed-point copy of xyz (kXqStride int32 per vertex, Frame::quant), built per call
@@ -59,7 +43,6 @@ struct Bg {
   int tstride;
   double hausd;
   int fanmax; // cone test: fans longer than this take the full tria scan (kFanMax; test-only PMMG_HIP_FANMAX)
-  const TriRec *trec; // walk records of the boundary trias (run_device; null outside the surface walk)
 };
 
 __device__ __forceinline__ int4 tetv_row(const Bg &bg, int k) { return bg.tetv[(size_t)(k - 1) * bg.tstride]; }
@@ -532,43 +515,6 @@ __device__ __forceinline__ void tri_load(const Bg &bg, int k, TriGeom &t) {
   t.n[0] *= dd;
   t.n[1] *= dd;
   t.n[2] *= dd;
-}
-
-// tri_load from the tria's walk record, with its adjacency row
-__device__ __forceinline__ void tri_load_rec(const TriRec *rec, int k, TriGeom &t, int *a) {
-  const double2 *r = reinterpret_cast<const double2 *>(rec + (k - 1));
-  double2 w[8];
-#pragma unroll
-  for (int j = 0; j < 8; j++) w[j] = r[j]; // one line, eight 16-byte loads in flight together
-  t.p[0][0] = w[0].x; t.p[0][1] = w[0].y; t.p[0][2] = w[1].x;
-  t.p[1][0] = w[1].y; t.p[1][1] = w[2].x; t.p[1][2] = w[2].y;
-  t.p[2][0] = w[3].x; t.p[2][1] = w[3].y; t.p[2][2] = w[4].x;
-  t.n[0] = w[4].y; t.n[1] = w[5].x; t.n[2] = w[5].y;
-  t.q = w[6].x;
-  int iv[6];
-  __builtin_memcpy(iv, &w[6].y, 8);
-  __builtin_memcpy(iv + 2, &w[7], 16);
-  t.v[0] = iv[0]; t.v[1] = iv[1]; t.v[2] = iv[2];
-  a[0] = iv[3]; a[1] = iv[4]; a[2] = iv[5];
-}
-
-// the record of tria k (its vertices valid), as tri_load computes the geometry
-__device__ __forceinline__ void tri_rec_build(const Bg &bg, int k, TriRec *rec) {
-  TriGeom t;
-  tri_load(bg, k, t);
-  TriRec r;
-  for (int i = 0; i < 3; i++)
-    for (int d = 0; d < 3; d++) r.p[i][d] = t.p[i][d];
-  for (int d = 0; d < 3; d++) r.n[d] = t.n[d];
-  r.q = t.q;
-  for (int i = 0; i < 3; i++) {
-    r.v[i] = t.v[i];
-    r.a[i] = bg.adjt[3 * (size_t)(k - 1) + i];
-  }
-  const double2 *src = reinterpret_cast<const double2 *>(&r);
-  double2 *dst = reinterpret_cast<double2 *>(rec + (k - 1));
-#pragma unroll
-  for (int j = 0; j < 8; j++) dst[j] = src[j];
 }
 
 // PMMG_quickarea (barycoord_pmmg.c:44-61)

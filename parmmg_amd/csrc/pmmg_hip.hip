@@ -173,7 +173,6 @@ struct pmmg_hip_ctx {
   std::vector<DevBuf> o_f;
   // work buffers
   DevBuf frame, stats, grid, sgrid, order_v, order_b, cont, xq;
-  DevBuf trec;                            // boundary trias' walk records (TriRec, per call)
   DevBuf axh;                             // per-axis histograms of the seed grid map (k_quantize)
   DevBuf bkeys, bkeys2, bvals, bvals2;    // Morton binning: keys and ids, ping-ponged by the radix sort
   DevBuf rs_hist, rs_csum;                // the radix sort's digit table and its scan's chunk sums
@@ -677,7 +676,7 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   if (c->stream3) (void)hipStreamSynchronize(c->stream3);
   if (c->cstream) (void)hipStreamSynchronize(c->cstream);
   DevBuf *bufs[] = {&c->o_xyz, &c->o_tetv, &c->o_adja, &c->o_triv, &c->o_adjt, &c->o_met, &c->o_rec, &c->frame,
-                    &c->stats, &c->grid, &c->sgrid, &c->order_v, &c->trec,
+                    &c->stats, &c->grid, &c->sgrid, &c->order_v,
                     &c->order_b, &c->cont, &c->xq, &c->qs, &c->axh, &c->bkeys, &c->bkeys2, &c->bvals, &c->bvals2, &c->rs_hist, &c->rs_csum, &c->oflag, &c->cls_cnt, &c->qmin, &c->fb_vol, &c->fb_bdy,
                     &c->best, &c->nac, &c->cres, &c->bbest, &c->bnac, &c->bcres, &c->fbp_vol, &c->fbp_bdy, &c->fbg_vol_c,
                     &c->fbg_vol_u, &c->fbg_vol_i, &c->fbg_bdy_c, &c->fbg_bdy_u, &c->fbg_bdy_i, &c->h_xyz,
@@ -1391,14 +1390,6 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
       !ensure(c, c->axh, sizeof(int) * 3 * kMapBins * (size_t)kHistBlocks))
     return 0;
   bg.xq = (const int *)c->xq.p;
-  // the boundary trias' walk records (written by k_seed_srf, read by k_bdy's walk only)
-  TriRec *trec = nullptr;
-  if (bg.nt > 0) {
-    if (!ensure(c, c->trec, sizeof(TriRec) * (size_t)bg.nt)) return 0;
-    trec = (TriRec *)c->trec.p;
-  }
-  Bg bgw = bg; // the surface walk's view
-  bgw.trec = trec;
   Frame *fr = (Frame *)c->frame.p;
   DevStats *st = (DevStats *)c->stats.p;
   unsigned long long *grid = (unsigned long long *)c->grid.p;
@@ -1523,7 +1514,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   // one round of the grid for up to 1M surface points (static split: a
   // second, nearly empty round doubled the surface branch alone)
   auto bdy = [&](int want) {
-    hipLaunchKernelGGL(k_bdy, dim3(8 * blocks_for((np_new + 7) / 8, c->bdy_bpx)), dim3(kBlock), 0, sb, bgw,
+    hipLaunchKernelGGL(k_bdy, dim3(8 * blocks_for((np_new + 7) / 8, c->bdy_bpx)), dim3(kBlock), 0, sb, bg,
                        (const Frame *)fr, (const int *)sgrid, gs, xyz_new, (const int *)order_b, S, elem_out,
                        hit_out, (int *)c->fb_bdy.p, st, c->maxstep, c->bdy_dyn, FbInit{(int *)c->bbest.p},
                        FbGridBufs{(int *)c->fbg_bdy_c.p, (int *)c->fbg_bdy_u.p, (int *)c->fbg_bdy_i.p}, flag, want);
@@ -1536,7 +1527,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     if (bg.nt > 0) {
       if (force == 0) HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_FRAME], 0)); // (the surface seeds need the frame)
       hipLaunchKernelGGL(k_seed_srf, dim3(blocks_for(bg.nt, 4096)), dim3(kBlock), 0, sb, bg, (const Frame *)fr,
-                         sgrid, gs, trec);
+                         sgrid, gs);
     }
     return 1;
   };

@@ -592,12 +592,10 @@ __device__ __forceinline__ int seed_vol(const unsigned long long *cell, int g, c
 // ---------------------------------------------------------------- surface seeds and node -> tria CSR
 
 // surface seeds: cell of each tria centroid -> min id
-// (and the trias' walk records, rec: TriRec, when not null)
-__global__ __launch_bounds__(kBlock) void k_seed_srf(Bg bg, const Frame *fr, int *cell, int g, TriRec *rec) {
+__global__ __launch_bounds__(kBlock) void k_seed_srf(Bg bg, const Frame *fr, int *cell, int g) {
   for (int k = 1 + blockIdx.x * blockDim.x + threadIdx.x; k <= bg.nt; k += gridDim.x * blockDim.x) {
     const int *tv = bg.triv + 3 * (size_t)(k - 1);
     if (tv[0] <= 0) continue;
-    if (rec) tri_rec_build(bg, k, rec);
     double p0[3], p1[3], p2[3];
     load_pt(bg.xyz, tv[0], p0);
     load_pt(bg.xyz, tv[1], p1);
