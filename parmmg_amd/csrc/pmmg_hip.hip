@@ -181,6 +181,8 @@ struct pmmg_hip_ctx {
   int brick = 0;
   int set_order = 0; // test-only PMMG_HIP_SETORDER=1 (see k_set_order)
   int no_fb = 0;     // measurement build: PMMG_HIP_NOFB
+  int stream3_mode = 1; // the binning's own stream: 1 created at the first auto-order call, 2 with the context,
+                        // 0 none (measurement build: PMMG_HIP_STREAM3)
   int srf_solo = -1; // the surface branch waits for the seed grid: -1 in calls of >= kSmallGroup queries (r04zo,
                      // cfg4: the seed grid ran at 455 instead of 261 us beside k_bdy; step 4.24 -> 4.13 ms,
                      // Mmg-like 5.01 -> 4.93, shuffled =), 1 always, 0 never (PMMG_HIP_SRFSOLO)
@@ -656,7 +658,10 @@ static pmmg_hip_ctx *create_ctx(int device, int options, bool srf_prio, pmmg_hip
   c->lane_streams = std::max(1, std::min(3, env_int("PMMG_HIP_LANE_STREAMS", c->lane_streams)));
   c->lane0 = env_int("PMMG_HIP_LANE0", 1) ? 1 : 0;
   c->bdy_first = env_int("PMMG_HIP_BDYFIRST", 0);
-  c->no_fb = env_int("PMMG_HIP_NOFB", 0); // the exhaustive kernels not launched (a launch's price; wrong results
+  c->no_fb = env_int("PMMG_HIP_NOFB", 0);
+  c->stream3_mode = env_int("PMMG_HIP_STREAM3", c->stream3_mode);
+  if (c->stream3_mode == 2 && hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess)
+    c->stream3 = nullptr; // the exhaustive kernels not launched (a launch's price; wrong results
                                            // wherever a query needs them)
 #endif
   return c;
@@ -1435,7 +1440,9 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   // behind the seed grid)
   hipStream_t sc = sb;
   if (force != 0) {
-    if (!c->stream3 && hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess) c->stream3 = nullptr;
+    if (c->stream3_mode == 1 && !c->stream3 &&
+        hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess)
+      c->stream3 = nullptr;
     if (c->stream3) sc = c->stream3;
     HIPCK(c, hipStreamWaitEvent(sc, c->ev[EV_FRAME], 0)); // (the frame and the order flag)
   }

@@ -1,0 +1,7 @@
+B="--steps 5 --warmup 2 --no-cpu-baseline --no-host-mode --no-snapshot --no-quality --no-graded --no-shuffled --no-surface-solo"
+python3 tools/gpu_job.py --tag r05y \
+ "bench $B" \
+ "py tools/groups_only.py --no-parity" \
+ "bench $B" \
+ "py tools/groups_only.py --no-parity" \
+ "bench $B --sort off"
