@@ -297,9 +297,10 @@ __device__ void frame_final(Frame *fr, int g, int gs, int gb);
 
 // the last block to finish also finalises the frame (one launch less per
 // call; the other blocks' atomics are read back atomically)
-// flag != null (auto order): the grid's last block runs the queries' coherence
+// flag != null (auto order): the grid's first block runs the queries' coherence
 // test (coherence_block) instead of sampling vertices — the other blocks take
-// the same samples as without it — so the order flag is on the main stream
+// the same samples as without it; the first block is dispatched first, so the
+// longer test overlaps the sampling — so the order flag is on the main stream
 // after k_bbox (r05: as a one-block kernel on the second stream, every kernel
 // of the other streams that reads the flag waited on it across queues, and
 // the runtime released the volume kernel only after the binning chain)
@@ -309,9 +310,10 @@ __global__ __launch_bounds__(kBlock) void k_bbox(const double *xyz, int np, Fram
   __shared__ unsigned long long slo[3][kBlock / 64], shi[3][kBlock / 64];
   unsigned long long lo[3] = {~0ULL, ~0ULL, ~0ULL}, hi[3] = {0ULL, 0ULL, 0ULL};
   const long long ns = ((long long)np + stride - 1) / stride + 2;
-  const int nb = flag ? gridDim.x - 1 : gridDim.x; // blocks sampling the vertices
-  if (flag && blockIdx.x == nb) coherence_block(qxyz, nq, flag); // (block-uniform)
-  for (long long j = blockIdx.x * blockDim.x + threadIdx.x; blockIdx.x < nb && j < ns; j += (long long)nb * blockDim.x) {
+  const int nb = flag ? gridDim.x - 1 : gridDim.x;       // blocks sampling the vertices
+  const int bb = flag ? (int)blockIdx.x - 1 : (int)blockIdx.x; // this block's index among them (-1: the test)
+  if (bb < 0) coherence_block(qxyz, nq, flag);                 // (block-uniform)
+  for (long long j = (long long)bb * blockDim.x + threadIdx.x; bb >= 0 && j < ns; j += (long long)nb * blockDim.x) {
     unsigned long long z = (unsigned long long)j * 0x9E3779B97F4A7C15ULL + 0xB0B0B0B0ULL;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
