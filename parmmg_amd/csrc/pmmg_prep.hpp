@@ -246,7 +246,7 @@ __global__ __launch_bounds__(kBlock) void k_quantize(const double *xyz, long lon
           const unsigned d0 = (unsigned)((2 * p) % 3); // 64-bit: 3 * np doubles may pass 2^31
           const unsigned d1 = d0 == 2u ? 0u : d0 + 1u;
           const nti2 w = {q(v[u].x, d0), q(v[u].y, d1)};
-          __builtin_nontemporal_store(w, dst + p);
+          __builtin_nontemporal_store(w, dst + p); // (cached stores: ±0 for the seed grid and the walk, r05ac)
         }
       }
     }
