@@ -62,3 +62,34 @@ def test_no_cpu_fallback_without_gpu():
         pytest.skip("a GPU is visible")
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         transfer.TransferContext(0)
+
+
+def test_ctypes_structs_match_the_header(tmp_path):
+    """The Python mirrors of the header's structs (pmmg_hip_stats,
+    pmmg_hip_group) have the C compiler's size and field offsets: a field
+    added to include/parmmg_hip.h without its mirror would shift every later
+    field the bench and the tests read."""
+    import ctypes
+    import subprocess
+
+    from parmmg_amd._native import HipGroup, HipStats
+
+    checks = []
+    for cname, py in (("pmmg_hip_stats", HipStats), ("pmmg_hip_group", HipGroup)):
+        checks.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
+        for fname, _ in py._fields_:
+            checks.append(f'printf("{cname} {fname} %zu\\n", offsetof({cname}, {fname}));')
+    src = tmp_path / "layout.c"
+    src.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "parmmg_hip.h"\nint main(void) {\n'
+                   + "\n".join(checks) + "\nreturn 0;\n}\n")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    want = {}
+    for line in filter(None, out):
+        cname, fname, v = line.split()
+        want[(cname, fname)] = int(v)
+    for cname, py in (("pmmg_hip_stats", HipStats), ("pmmg_hip_group", HipGroup)):
+        assert ctypes.sizeof(py) == want[(cname, "size")], cname
+        for fname, _ in py._fields_:
+            assert getattr(py, fname).offset == want[(cname, fname)], (cname, fname)
