@@ -173,6 +173,7 @@ struct pmmg_hip_ctx {
   std::vector<DevBuf> o_f;
   // work buffers
   DevBuf frame, stats, grid, sgrid, order_v, order_b, cont, xq;
+  DevBuf cohd;                            // the coherence test's sampled distances (k_bbox)
   DevBuf axh;                             // per-axis histograms of the seed grid map (k_quantize)
   DevBuf bkeys, bkeys2, bvals, bvals2;    // Morton binning: keys and ids, ping-ponged by the radix sort
   DevBuf rs_hist, rs_csum;                // the radix sort's digit table and its scan's chunk sums
@@ -681,7 +682,7 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   if (c->stream3) (void)hipStreamSynchronize(c->stream3);
   if (c->cstream) (void)hipStreamSynchronize(c->cstream);
   DevBuf *bufs[] = {&c->o_xyz, &c->o_tetv, &c->o_adja, &c->o_triv, &c->o_adjt, &c->o_met, &c->o_rec, &c->frame,
-                    &c->stats, &c->grid, &c->sgrid, &c->order_v,
+                    &c->stats, &c->grid, &c->sgrid, &c->order_v, &c->cohd,
                     &c->order_b, &c->cont, &c->xq, &c->qs, &c->axh, &c->bkeys, &c->bkeys2, &c->bvals, &c->bvals2, &c->rs_hist, &c->rs_csum, &c->oflag, &c->cls_cnt, &c->qmin, &c->fb_vol, &c->fb_bdy,
                     &c->best, &c->nac, &c->cres, &c->bbest, &c->bnac, &c->bcres, &c->fbp_vol, &c->fbp_bdy, &c->fbg_vol_c,
                     &c->fbg_vol_u, &c->fbg_vol_i, &c->fbg_bdy_c, &c->fbg_bdy_u, &c->fbg_bdy_i, &c->h_xyz,
@@ -1392,6 +1393,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
       !ensure(c, c->fbg_bdy_u, 4 * (size_t)kFbCells) || !ensure(c, c->fbg_bdy_i, 4 * nq))
     return 0;
   if (!ensure(c, c->xq, sizeof(int) * kXqStride * (size_t)bg.np) || !ensure(c, c->oflag, 2 * sizeof(int)) ||
+      !ensure(c, c->cohd, sizeof(double) * kCohSamples) ||
       !ensure(c, c->axh, sizeof(int) * 3 * kMapBins * (size_t)kHistBlocks))
     return 0;
   bg.xq = (const int *)c->xq.p;
@@ -1416,10 +1418,10 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   // the input order's surface list needs only the zeroed counters (and the coherence flag), not the frame
   HIPCK(c, hipEventRecord(c->ev[EV_RESET], s));
   // bbox (its last block finalises the frame), the seed grid's axis maps
-  // (auto order: one more block, the queries' coherence test, whose flag the order and volume kernels read)
-  hipLaunchKernelGGL(k_bbox, dim3(blocks_for(bg.np / c->bbox_stride + 1, 256) + (force < 0 ? 1 : 0)), dim3(kBlock), 0,
-                     s, bg.xyz, bg.np, fr, c->bbox_stride, g, gs, gb, xyz_new, np_new,
-                     force < 0 ? (int *)c->oflag.p : nullptr);
+  // (auto order: the queries' coherence test rides along, its flag read by the order and volume kernels)
+  hipLaunchKernelGGL(k_bbox, dim3(std::max(force < 0 ? kCohBlocks : 1, blocks_for(bg.np / c->bbox_stride + 1, 256))),
+                     dim3(kBlock), 0, s, bg.xyz, bg.np, fr, c->bbox_stride, g, gs, gb, xyz_new, np_new,
+                     force < 0 ? (int *)c->oflag.p : nullptr, (double *)c->cohd.p);
   // the second stream needs the frame only (lo, inv_bin, inv_srf), not the
   // axis maps (r04: EV_FRAME moved here from after k_axis_map)
   HIPCK(c, hipEventRecord(c->ev[EV_FRAME], s));

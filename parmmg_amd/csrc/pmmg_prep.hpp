@@ -2,7 +2,7 @@
 // (included by pmmg_hip.hip only): state reset, background frame, volume and
 // surface seed grids, and the query order.
 //
-// The input-order coherence test runs on the device (coherence_block, run by k_bbox's extra block); in
+// The input-order coherence test runs on the device (in k_bbox: coherence_final's flag); in
 // auto mode both the Morton binning (pmmg_sort.hpp) and the class compaction
 // of the surface list are enqueued, each gated on that flag, and the volume
 // kernel reads it: nothing is read back inside a call.
@@ -297,23 +297,44 @@ __device__ void frame_final(Frame *fr, int g, int gs, int gb);
 
 // the last block to finish also finalises the frame (one launch less per
 // call; the other blocks' atomics are read back atomically)
-// flag != null (auto order): the grid's first block runs the queries' coherence
-// test (coherence_block) instead of sampling vertices — the other blocks take
-// the same samples as without it; the first block is dispatched first, so the
-// longer test overlaps the sampling — so the order flag is on the main stream
-// after k_bbox (r05: as a one-block kernel on the second stream, every kernel
-// of the other streams that reads the flag waited on it across queues, and
-// the runtime released the volume kernel only after the binning chain)
-__device__ void coherence_block(const double *xyz, int np, int *flag);
+// flag != null (auto order): the queries' coherence test rides along — the
+// first kCohBlocks blocks each also measure 512 of its 4096 consecutive-point
+// distances (2 per thread) into cohd, and the last block, after finalising
+// the frame, counts them (coherence_final) — so the order flag is on the main
+// stream after k_bbox.  (r05: a one-block kernel on the second stream, every
+// kernel of the other streams that reads the flag waited on it across
+// queues; then one block of k_bbox running the whole test, ~30 us on the
+// main stream's critical path, r05ag)
+constexpr int kCohBlocks = 8, kCohSamples = 4096; // 2 samples per thread of each test block
+__device__ void coherence_final(const Frame *fr, const double *cohd, int nq, int *flag);
+__device__ __forceinline__ double coh_sample(const double *xyz, int np, int smp) {
+  // pseudo-random positions (splitmix64 of the sample index): an evenly
+  // strided sample can alias with the row length of a lattice numbering
+  unsigned long long z = (unsigned long long)smp * 0x9E3779B97F4A7C15ULL + 0x5EED2025ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  z ^= z >> 31;
+  const long long i = (long long)(z % (unsigned long long)(np - 1));
+  double d2 = 0.0;
+  for (int d = 0; d < 3; d++) {
+    const double t = xyz[3 * (size_t)(i + 1) + d] - xyz[3 * (size_t)i + d];
+    d2 += t * t;
+  }
+  return sqrt(d2);
+}
 __global__ __launch_bounds__(kBlock) void k_bbox(const double *xyz, int np, Frame *fr, int stride, int g, int gs,
-                                                 int gb, const double *qxyz, int nq, int *flag) {
+                                                 int gb, const double *qxyz, int nq, int *flag, double *cohd) {
   __shared__ unsigned long long slo[3][kBlock / 64], shi[3][kBlock / 64];
   unsigned long long lo[3] = {~0ULL, ~0ULL, ~0ULL}, hi[3] = {0ULL, 0ULL, 0ULL};
   const long long ns = ((long long)np + stride - 1) / stride + 2;
-  const int nb = flag ? gridDim.x - 1 : gridDim.x;       // blocks sampling the vertices
-  const int bb = flag ? (int)blockIdx.x - 1 : (int)blockIdx.x; // this block's index among them (-1: the test)
-  if (bb < 0) coherence_block(qxyz, nq, flag);                 // (block-uniform)
-  for (long long j = (long long)bb * blockDim.x + threadIdx.x; bb >= 0 && j < ns; j += (long long)nb * blockDim.x) {
+  if (flag && blockIdx.x < kCohBlocks && nq >= 2) {
+#pragma unroll
+    for (int s = 0; s < kCohSamples / (kCohBlocks * kBlock); s++) {
+      const int smp = (blockIdx.x * (kCohSamples / (kCohBlocks * kBlock)) + s) * kBlock + threadIdx.x;
+      cohd[smp] = coh_sample(qxyz, nq, smp);
+    }
+  }
+  for (long long j = blockIdx.x * blockDim.x + threadIdx.x; j < ns; j += gridDim.x * blockDim.x) {
     unsigned long long z = (unsigned long long)j * 0x9E3779B97F4A7C15ULL + 0xB0B0B0B0ULL;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
@@ -356,10 +377,13 @@ __global__ __launch_bounds__(kBlock) void k_bbox(const double *xyz, int np, Fram
   __shared__ bool last;
   if (threadIdx.x == 0) last = atomicAdd(&fr->bbox_done, 1u) == gridDim.x - 1;
   __syncthreads();
-  if (last && threadIdx.x == 0) {
+  if (!last) return; // (block-uniform)
+  if (threadIdx.x == 0) {
     __threadfence();
     frame_final(fr, g, gs, gb);
   }
+  __syncthreads();
+  if (flag) coherence_final(fr, cohd, nq, flag);
 }
 
 __device__ void frame_final(Frame *fr, int g, int gs, int gb) {
@@ -763,62 +787,17 @@ constexpr int kBinBitsCoherent = 5; // 32^3 cells for a mostly coherent numberin
 // that read the flag waited on it across queues); writes flag[0] (1: Morton
 // bins) and flag[1] (their bits per axis), read on the device by the order
 // kernels and the volume / surface kernels.
-__device__ __noinline__ void coherence_block(const double *xyz, int np, int *flag) {
-  constexpr int nsamp = 4096, per = nsamp / kBlock, nw = kBlock / 64;
-  __shared__ double s_lo[3][nw], s_hi[3][nw];
+__device__ __noinline__ void coherence_final(const Frame *fr, const double *cohd, int nq, int *flag) {
+  constexpr int nw = kBlock / 64;
   __shared__ int s_near[nw];
-  __shared__ double s_h;
-  double dist[per], lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
-#pragma unroll
-  for (int q = 0; q < per; q++) {
-    const int smp = threadIdx.x + q * kBlock;
-    dist[q] = 0.0;
-    if (np < 2) continue;
-    // pseudo-random positions (splitmix64 of the sample index): an evenly
-    // strided sample can alias with the row length of a lattice numbering
-    unsigned long long z = (unsigned long long)smp * 0x9E3779B97F4A7C15ULL + 0x5EED2025ULL;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
-    z ^= z >> 31;
-    const long long i = (long long)(z % (unsigned long long)(np - 1));
-    double d2 = 0.0;
-    for (int d = 0; d < 3; d++) {
-      double a = xyz[3 * (size_t)i + d], b = xyz[3 * (size_t)(i + 1) + d];
-      double t = b - a;
-      d2 += t * t;
-      lo[d] = fmin(lo[d], a);
-      hi[d] = fmax(hi[d], a);
-    }
-    dist[q] = sqrt(d2);
-  }
-  const int w = threadIdx.x >> 6;
-  for (int d = 0; d < 3; d++)
-    for (int o = 32; o > 0; o >>= 1) {
-      lo[d] = fmin(lo[d], __shfl_xor(lo[d], o));
-      hi[d] = fmax(hi[d], __shfl_xor(hi[d], o));
-    }
-  if (__lane_id() == 0)
-    for (int d = 0; d < 3; d++) {
-      s_lo[d][w] = lo[d];
-      s_hi[d][w] = hi[d];
-    }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double L[3] = {1e300, 1e300, 1e300}, H[3] = {-1e300, -1e300, -1e300};
-    for (int j = 0; j < nw; j++)
-      for (int d = 0; d < 3; d++) {
-        L[d] = fmin(L[d], s_lo[d][j]);
-        H[d] = fmax(H[d], s_hi[d][j]);
-      }
-    double vol = fmax(H[0] - L[0], 1e-300) * fmax(H[1] - L[1], 1e-300) * fmax(H[2] - L[2], 1e-300);
-    s_h = cbrt(vol / (double)(np > 1 ? np : 1));
-  }
-  __syncthreads();
+  // the mean spacing of nq points in the (sampled) background box
+  __threadfence(); // (the test blocks' distances, released before their tickets)
+  const double vol = fmax(fr->ext[0], 1e-300) * fmax(fr->ext[1], 1e-300) * fmax(fr->ext[2], 1e-300);
+  const double h = cbrt(vol / (double)(nq > 1 ? nq : 1));
   int near = 0;
-#pragma unroll
-  for (int q = 0; q < per; q++) near += dist[q] < 4.0 * s_h ? 1 : 0;
+  for (int j = threadIdx.x; nq >= 2 && j < kCohSamples; j += kBlock) near += cohd[j] < 4.0 * h ? 1 : 0;
   for (int o = 32; o > 0; o >>= 1) near += __shfl_xor(near, o);
-  if (__lane_id() == 0) s_near[w] = near;
+  if (__lane_id() == 0) s_near[threadIdx.x >> 6] = near;
   __syncthreads();
   if (threadIdx.x == 0) {
     int tot = 0;
@@ -830,9 +809,9 @@ __device__ __noinline__ void coherence_block(const double *xyz, int np, int *fla
     // Mmg-like numbering — 83 % short steps, the inserted sixth appended —
     // takes 4.96 ms per cfg4 call in input order, 5.96 binned; r03's 95 %
     // threshold binned it.)
-    const bool coherent = np > 1 && 4 * tot >= 3 * nsamp;
+    const bool coherent = nq > 1 && 4 * tot >= 3 * kCohSamples;
     flag[0] = coherent ? 0 : 1;
-    flag[1] = 2 * tot >= nsamp ? kBinBitsCoherent : kBinBitsAxis;
+    flag[1] = 2 * tot >= kCohSamples ? kBinBitsCoherent : kBinBitsAxis;
   }
 }
 
@@ -850,7 +829,7 @@ __device__ __noinline__ void coherence_block(const double *xyz, int np, int *fla
 // them coalesced) and the surface list.  The radix sort is stable: the order
 // is a deterministic function of the input.
 
-// flag: the order decision {sorted, bits per axis} (coherence_block); the kernel
+// flag: the order decision {sorted, bits per axis} (coherence_final); the kernel
 // runs only when flag[0] == 1.  Blocks loop over the radix sort's tiles
 // (tile_keys keys, pmmg_sort.hpp): besides the keys it writes each tile's
 // histogram of the first 8-bit digit (hist[digit * ntile + tile]), the first

@@ -3,7 +3,7 @@
 //
 // A stable LSD radix sort of (32-bit key, 32-bit value) pairs, 8 bits per
 // pass, whose every kernel returns at once unless *gate == want: the query
-// order of a call is chosen on the device (coherence_block, in k_bbox) and both orders'
+// order of a call is chosen on the device (the coherence test in k_bbox) and both orders'
 // kernels are enqueued, so the call never waits for the flag on the host
 // (rocPRIM's sort, used up to r03, takes its work from host arguments and
 // cannot be skipped from the device).
