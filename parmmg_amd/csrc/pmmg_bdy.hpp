@@ -115,6 +115,8 @@ __device__ __forceinline__ int bdy_query(const Bg &bg, const Frame *fr, const in
 // (default), or (dyn, PMMG_HIP_BDYDYN=1) every wave claiming the next 64
 // queries of its XCD's eighth from a counter: measured, the claiming waves
 // slowed the volume kernel beside them (profiles/r03y).
+// (r05: a register budget for 5 or 6 waves per SIMD instead of the compiler's
+// 4: the step +-0 / +2 %, the 8-way rank's surface branch +-0, profiles/r05ak)
 __global__ __launch_bounds__(kBlock) void k_bdy(Bg bg, const Frame *fr, const int *sgrid, int gs, const double *qxyz,
                                                 const int *order, Slots S, int *elem_out, int8_t *hit_out, int *fb,
                                                 DevStats *st, int maxstep, int dyn, FbInit fi, FbGridBufs gb,
