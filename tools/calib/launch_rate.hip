@@ -1,7 +1,10 @@
 // Host cost of a kernel launch on this image (ROCm 7.2, MI355X): N launches
 // of an empty kernel with a small / a ~400-byte argument block, on one
 // stream, and with an event record between launches.  Prints us per launch
-// (host enqueue time) and the device time of the whole sequence.
+// (host enqueue time) and the device time of the whole sequence.  Modes 7-8:
+// the same kernels as a hipGraph of 16 dependent launches, replayed N / 16
+// times (one host call per 16 kernels: what graph replay of a group's chain
+// would leave of the launch cost).
 //   hipcc --offload-arch=gfx950 -O2 -o /tmp/launch_rate tools/calib/launch_rate.hip
 #include <hip/hip_runtime.h>
 #include <chrono>
@@ -32,8 +35,17 @@ int main() {
   int *p = nullptr;
   (void)hipMalloc(&p, 16);
   Big b{};
-  const int N = 2000;
-  for (int mode = 0; mode < 7; mode++) {
+  const int N = 2000, G = 16;
+  hipGraphExec_t gx[2] = {nullptr, nullptr};
+  for (int v = 0; v < 2; v++) {
+    hipGraph_t gr;
+    (void)hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal);
+    for (int i = 0; i < G; i++) hipLaunchKernelGGL(k_small, dim3(v ? 4096 : 1), dim3(v ? 256 : 64), 0, s, p);
+    (void)hipStreamEndCapture(s, &gr);
+    (void)hipGraphInstantiate(&gx[v], gr, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(gr);
+  }
+  for (int mode = 0; mode < 9; mode++) {
     for (int rep = 0; rep < 2; rep++) {
       (void)hipDeviceSynchronize();
       (void)hipEventRecord(e0, s);
@@ -60,6 +72,7 @@ int main() {
           (void)hipStreamWaitEvent(s2, evn, 0);
           hipLaunchKernelGGL(k_small, dim3(1), dim3(64), 0, s2, p);
         }
+        if (mode >= 7 && i % G == 0) (void)hipGraphLaunch(gx[mode - 7], s);
       }
       auto t1 = std::chrono::steady_clock::now();
       (void)hipEventRecord(e1, s);
@@ -75,7 +88,9 @@ int main() {
                : mode == 3 ? "4096 blocks"
                : mode == 4 ? "small + no-timing event record"
                : mode == 5 ? "small + wait on a completed event"
-                           : "launch, record, other stream waits and launches",
+               : mode == 6 ? "launch, record, other stream waits and launches"
+               : mode == 7 ? "graph of 16 small launches, per kernel"
+                           : "graph of 16 launches of 4096 blocks, per kernel",
                us / N, 1e3 * ms / N);
     }
   }
