@@ -172,6 +172,9 @@ def parent(args):
         row += f"{np.median(res[spec]['steps_pp']):10.3f}{np.median(res[spec]['iters']):10.0f}"
         row += f"{np.median(res[spec]['exact']):8.0f}"
         print(row, flush=True)
+    print("ms_total per call, min / max over all rounds (one process per variant and round):")
+    for spec in variants:
+        print(f"{spec:28s}{np.min(res[spec]['ms_total']):11.3f}{np.max(res[spec]['ms_total']):11.3f}", flush=True)
 
 
 if __name__ == "__main__":
