@@ -70,7 +70,9 @@ def build_hip(force: bool = False, measure: bool = False) -> str:
         # max-memory-clause scheduling: the gathers of a step issued as clauses
         # (volume kernel -4.6 % at cfg4, same registers; profiles/r02e/sweep_sched_strategy.txt)
         _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-mllvm", "-amdgpu-sched-strategy=max-memory-clause",
-              "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared"] + (["-DPMMG_HIP_MEASURE"] if measure else []) +
+              "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
+              # (r05: flowing off a lambda that a `return 0` made non-void is undefined: a host segfault)
+              "-Werror=return-type"] + (["-DPMMG_HIP_MEASURE"] if measure else []) +
              [f"-I{INC}", "-o", out, src, snap, qual])
     return out
 

@@ -147,7 +147,7 @@ struct DevBuf {
 
 enum {
   EV_START, EV_FRAME, EV_PREP, EV_ORDER, EV_VOL0, EV_WALK, EV_VOL, EV_JOIN, EV_END, EV_BDY0, EV_BDY1, EV_RESET,
-  EV_SB0, EV_ORDER2, EV_COUNT
+  EV_SB0, EV_ORDER2, EV_SRFSEED, EV_COUNT
 };
 
 struct pmmg_hip_ctx {
@@ -284,6 +284,7 @@ struct pmmg_hip_ctx {
   int lane_streams = 2; // a group lane's streams: 2 = its own surface stream, 1 = the surface branch on the
                         // main stream (measurement build: PMMG_HIP_LANE_STREAMS)
   int bdy_first = 0; // measurement build, PMMG_HIP_BDYFIRST=1: the volume kernel waits for the surface branch
+  int vol_wait_seed = 0; // measurement build, PMMG_HIP_VOLWAIT=1: the volume kernel waits for the surface seeds
   int lane0 = 1; // lane 0 enqueues on this context's streams (measurement build: PMMG_HIP_LANE0=0 gives it
                  // streams of its own)
   int filter_steps = 64; // step cap of the fp32 filter walk (then the exact fp64 walk continues from where it
@@ -569,9 +570,16 @@ static int snap_join(pmmg_hip_ctx *c) {
   return 1;
 }
 
+// 16-byte streaming stores (a from hipMalloc: 16-byte aligned); the odd last
+// element by the first thread.  (r05: 8-byte stores refilled cfg4's 101 MB
+// seed grid in 43 us, ~2.3 TB/s)
+typedef unsigned long long ntu2 __attribute__((ext_vector_type(2)));
 __global__ void k_fill64(unsigned long long *a, long long n, unsigned long long v) {
-  for (long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x; j < n; j += (long long)gridDim.x * blockDim.x)
-    a[j] = v;
+  const ntu2 vv = {v, v};
+  const long long n2 = n >> 1;
+  for (long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x; j < n2; j += (long long)gridDim.x * blockDim.x)
+    __builtin_nontemporal_store(vv, reinterpret_cast<ntu2 *>(a) + j);
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) a[n - 1] = v;
 }
 __global__ void k_fill32(int *a, long long n, int v) {
   for (long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x; j < n; j += (long long)gridDim.x * blockDim.x)
@@ -659,6 +667,7 @@ static pmmg_hip_ctx *create_ctx(int device, int options, bool srf_prio, pmmg_hip
   c->lane_streams = std::max(1, std::min(3, env_int("PMMG_HIP_LANE_STREAMS", c->lane_streams)));
   c->lane0 = env_int("PMMG_HIP_LANE0", 1) ? 1 : 0;
   c->bdy_first = env_int("PMMG_HIP_BDYFIRST", 0);
+  c->vol_wait_seed = env_int("PMMG_HIP_VOLWAIT", 0);
   c->no_fb = env_int("PMMG_HIP_NOFB", 0);
   c->stream3_mode = env_int("PMMG_HIP_STREAM3", c->stream3_mode);
   if (c->stream3_mode == 2 && hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess)
@@ -1539,6 +1548,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
       if (force == 0) HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_FRAME], 0)); // (the surface seeds need the frame)
       hipLaunchKernelGGL(k_seed_srf, dim3(blocks_for(bg.nt, 4096)), dim3(kBlock), 0, sb, bg, (const Frame *)fr,
                          sgrid, gs);
+      if (c->vol_wait_seed) HIPCK(c, hipEventRecord(c->ev[EV_SRFSEED], sb));
     }
     return 1;
   };
@@ -1558,6 +1568,8 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   // ---- volume (main stream): walk + exact test + interpolation in one
   // kernel, then the exact continuation of the few queries it did not settle
   auto vol = [&](int want) {
+    // (measurement build; a plain call: HIPCK's `return 0` would give this void lambda a return type)
+    if (c->vol_wait_seed && bg.nt > 0 && want <= 0) (void)hipStreamWaitEvent(s, c->ev[EV_SRFSEED], 0);
     hipLaunchKernelGGL(vol_fn, dim3((np_new + 63) / 64), dim3(64), 0, s, bg, (const Frame *)fr,
                        (const unsigned long long *)grid, g, xyz_new, pclass, (const int *)order_v,
                        c->bin_qs ? (const double *)c->qs.p : nullptr, np_new, (ContEntry *)c->cont.p, st, S,
@@ -1620,7 +1632,9 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[EV_JOIN], s));
   if (ng >= kRefillCells) { // the volume seed grid refilled for the next call, beside the surface stream's tail
-    hipLaunchKernelGGL(k_fill64, dim3(blocks_for(ng, 2048)), dim3(kBlock), 0, s, grid, ng, ~0ULL);
+    // (r05ao: on the surface stream right after the volume kernel it ran behind k_bdy's tail instead — the
+    // surface branch ends last at cfg4)
+    hipLaunchKernelGGL(k_fill64, dim3(blocks_for((ng + 1) / 2, 2048)), dim3(kBlock), 0, s, grid, ng, ~0ULL);
     HIPCK(c, hipGetLastError());
     c->grid_clean_p = c->grid.p;
     c->grid_clean_n = ng;

@@ -157,7 +157,7 @@ def parent(args):
             if so:  # another build of the module for this variant (e.g. the previous commit's, for an A/B)
                 env["PMMG_HIP_SO"] = os.path.join(ROOT, so)
             p = subprocess.run([sys.executable, "-u", os.path.abspath(__file__), "--config", args.config, "--steps",
-                                str(args.steps), "--child", spec], stdout=subprocess.PIPE, text=True, env=env)
+                                str(args.steps), "--child", spec], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env)
             line = [x for x in p.stdout.splitlines() if x.startswith("RESULT ")]
             if p.returncode != 0 or not line:
                 print(p.stdout[-2000:])
