@@ -407,13 +407,13 @@ def host_mode_timing(ctx, w, bg, met, fields, q_xyz, q_pc, rank: int, reps: int 
            "ms_locate_interp": round(1e3 * l_, 2), "mpts_per_s": round(npts / t / 1e6, 1),
            "bytes_up": int(up), "bytes_down": int(down), "pcie_gbps_effective": round((up + down) / t / 1e9, 1)}
     try:
-        out["iteration2"] = host_mode_iteration2(ctx, w, bg, mo, fo, rank)
+        out["iteration2"] = host_mode_iteration2(ctx, w, bg, met, fields, rank)
     except Exception as e:  # reported, never fatal to the bench line
         out["iteration2"] = {"error": str(e)}
     return out
 
 
-def host_mode_iteration2(ctx, w, bg, mo, fo, rank: int) -> dict:
+def host_mode_iteration2(ctx, w, bg, met, fields, rank: int) -> dict:
     """The next iteration through host buffers (src/libparmmg1.c:653: the
     adapted group becomes the old group): its background is the new mesh just
     transferred into (the new points, with the rows the step wrote) and the
@@ -421,22 +421,38 @@ def host_mode_iteration2(ctx, w, bg, mo, fo, rank: int) -> dict:
     Timed twice: cold (everything uploaded) and carried (pmmg_hip_keep after
     the first iteration, pmmg_hip_carry_over: only the connectivity and the
     next queries go up), outputs compared bit for bit; bytes_up counted by
-    the module."""
-    ctx.keep(0)  # the first iteration's last call (host_mode_timing) stays on the device
-    new_t = synth.lattice(w.kind, w.n_new, jitter=w.jitter_new, seed=synth.SEED, with_trias=False)
+    the module.
+
+    The adapted mesh must be a valid mesh, as Mmg's output is: its points are
+    jittered with the cap of synth_vertices_valid (r06).  Up to r05 this leg
+    used the plainly jittered shell, whose lattice connectivity has 0.23 % of
+    its tetra inverted along the radial map's crease planes (|y_i| = |y_j|):
+    2655 walks cycled through them to the step cap and the exhaustive search
+    (tools/walk_emu.py reproduces it on the CPU: 164 of 258k walks at n = 68 /
+    72, none once the mesh is valid).  So this leg runs its own first
+    iteration, on those points, and keeps that call."""
+    new_t = synth.lattice(w.kind, w.n_new, jitter=w.jitter_new, seed=synth.SEED, with_trias=False, valid=True)
+    pc1 = synth.classes(new_t)
+    mo = np.empty((new_t.np, w.met_size), np.float64)
+    fo = [np.empty((new_t.np, f.shape[1]), np.float64) for f in fields]
+    ctx.set_background(bg.xyz, bg.tetv, None, None, None, w.hausd)
+    ctx.set_solutions(met, fields)
+    ctx.locate_interp(new_t.xyz, pc1, mo, fo)
+    ctx.keep(0)  # this first iteration's call stays on the device
     q2, pc2 = bg.xyz, synth.classes(bg)
     res = {}
     outs = {}
     for mode in ("cold", "carried"):
         m2 = np.full((q2.shape[0], mo.shape[1]), np.nan)
         f2 = [np.full((q2.shape[0], f.shape[1]), np.nan) for f in fo]
+        el2, hit2 = np.zeros(q2.shape[0], np.int32), np.zeros(q2.shape[0], np.int8)
         if mode == "carried":
             ctx.carry_over(0, new_t.np)
         ctx.bytes_up(reset=True)
         t0 = time.perf_counter()
         ctx.set_background(new_t.xyz, new_t.tetv, None, None, None, w.hausd)
         ctx.set_solutions(mo, fo)
-        st = ctx.locate_interp(q2, pc2, m2, f2)
+        st = ctx.locate_interp(q2, pc2, m2, f2, el2, hit2)
         t = time.perf_counter() - t0
         sd = st.as_dict()
         res[mode] = {"ms": round(1e3 * t, 2), "bytes_up": ctx.bytes_up(reset=True),
@@ -446,8 +462,12 @@ def host_mode_iteration2(ctx, w, bg, mo, fo, rank: int) -> dict:
                      "device_ms": {"step_total": round(float(st.ms_total), 3),
                                    "volume_fallback": round(float(st.ms_fallback), 3),
                                    "surface_branch": round(float(st.ms_bdy), 3)}}
-        outs[mode] = [m2] + f2
+        outs[mode] = [m2] + f2 + [el2, hit2]
     same = all(np.array_equal(a, b, equal_nan=True) for a, b in zip(outs["cold"], outs["carried"]))
+    try:
+        res["oracle_check"] = iteration2_oracle_check(new_t, mo, fo, w, q2, pc2, outs["cold"])
+    except Exception as e:  # reported, never fatal to the bench line
+        res["oracle_check"] = {"error": str(e)}
     res.update({"what": "second iteration through host buffers: background = the new mesh of the first "
                         f"({new_t.ne} tets, {new_t.np} verts), queries = the first background's points; cold vs "
                         "carried over from the device (pmmg_hip_keep / pmmg_hip_carry_over)",
@@ -455,6 +475,35 @@ def host_mode_iteration2(ctx, w, bg, mo, fo, rank: int) -> dict:
                 "bit_identical": bool(same)})
     log(f"[bench r{rank}] host-mode iteration 2: {res}")
     return res
+
+
+def iteration2_oracle_check(new_t, mo, fo, w, q2, pc2, out, nsample: int = 20000) -> dict:
+    """The second iteration's rows against the oracle on its background (the
+    first iteration's valid new mesh with the rows written into it): every
+    volume point the exhaustive search settled — its element must be the
+    reference's lowest accepting index (src/locate_pmmg.c:737-770) or, when
+    none accepts, the closest — and a seeded sample of the other volume
+    points, with the parity contract of tests/parity.py (orc_check_batch).
+    Surface points are not checked here (the background's trias are built on
+    the device in this leg)."""
+    from oracle import oracle as orc
+
+    m2, f2, el2, hit2 = out[0], out[1:-2], out[-2], out[-1]
+    bgo = orc.Background(new_t, mo, fo, w.hausd)
+    code = hit2 & 15
+    fb = np.nonzero((pc2 == 1) & ((code == 2) | (code == 3)))[0]
+    rng = np.random.default_rng(20260)
+    vol = np.nonzero(pc2 == 1)[0]
+    samp = np.unique(np.concatenate([fb, rng.choice(vol, size=min(nsample, vol.size), replace=False)]))
+    rep = orc.check_batch(bgo, q2, pc2, el2, hit2, m2, f2, idx=samp)
+    fbc = fb[:200]  # each an O(ne) scan on the CPU
+    lowest = sum(int(orc.first_accepting_tetra(bgo, q2[i]) == el2[i]) for i in fbc if code[i] == 2)
+    closest = sum(int(orc.first_accepting_tetra(bgo, q2[i]) == 0 and orc.closest_tetra(bgo, q2[i]) == el2[i])
+                  for i in fbc if code[i] == 3)
+    ok = rep["accept_fail"] == 0 and rep["value_fail"] == 0 and rep["unprocessed"] == 0
+    return {"points_checked": int(samp.size), "fallback_points": int(fb.size), "fallback_checked": int(fbc.size),
+            "fallback_lowest_accepting_same": lowest, "fallback_closest_same": closest,
+            "contract": rep, "ok": bool(ok and lowest + closest == fbc.size)}
 
 
 LOCATE_KEYS = ("nvol", "nbdy", "nvol_exact", "nvol_stuck", "nvol_limit", "nvol_noseed", "nvol_exhaust",

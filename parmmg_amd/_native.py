@@ -92,6 +92,7 @@ HIP_API = {
 SYNTH_API = {
     "synth_counts": (c_int, [c_int, c_int, P(c_int64)]),
     "synth_vertices": (c_int, [c_int, c_int, c_double, ctypes.c_uint64, c_void_p, c_void_p]),
+    "synth_vertices_valid": (c_int, [c_int, c_int, c_double, ctypes.c_uint64, c_void_p, c_void_p]),
     "synth_tetra": (c_int, [c_int, c_int, c_void_p, c_void_p]),
     "synth_trias": (c_int64, [c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "synth_field": (c_int, [c_int, c_int64, c_void_p, c_void_p]),

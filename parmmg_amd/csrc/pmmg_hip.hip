@@ -61,13 +61,18 @@ namespace {
 
 typedef void (*VolFn)(Bg, const Frame *, const unsigned long long *, int, const double *, const uint8_t *,
                       const int *, const double *, int, ContEntry *, DevStats *, Slots, int *, int8_t *, int,
-                      const int *, int, int, int);
+                      const int *, int, int, int, LocBuf, int);
+typedef void (*InterpFn)(LocBuf, const int *, const DevStats *, int, Slots, const int *, int, int, int);
+
+// the split stage's walk kernel: the locate-only layout, writing located records
+constexpr VolFn kVolWalk = k_vol<0, 0, 0, 0, 0, 0, 0>;
 
 struct LayoutEntry {
   int c[6];
   VolFn fn;         // one array per solution (the reference's layout)
   VolFn fn_packed;  // packed per-vertex records, one pass (null: layout not packable)
   VolFn fn_packed2; // the same in two passes over the record halves (null: not splittable)
+  InterpFn ifn, ifn_packed, ifn_packed2; // the split stage's interpolation kernels, same three forms
 };
 
 template <int NP, int A, int B, int C, int D, int E, int F>
@@ -76,10 +81,17 @@ constexpr VolFn packed_fn() {
   if constexpr (L::valid() && L::passes_ok(NP)) return k_vol<NP, A, B, C, D, E, F>;
   else return nullptr;
 }
+template <int NP, int A, int B, int C, int D, int E, int F>
+constexpr InterpFn packed_ifn() {
+  using L = PackedLayout<A, B, C, D, E, F>;
+  if constexpr (L::valid() && L::passes_ok(NP)) return k_vol_interp<NP, A, B, C, D, E, F>;
+  else return nullptr;
+}
 
 #define PMMG_LAYOUT(a, b, c, d, e, f)                                                                    \
   {{a, b, c, d, e, f}, k_vol<0, a, b, c, d, e, f>, packed_fn<1, a, b, c, d, e, f>(),                    \
-   packed_fn<2, a, b, c, d, e, f>()}
+   packed_fn<2, a, b, c, d, e, f>(), k_vol_interp<0, a, b, c, d, e, f>, packed_ifn<1, a, b, c, d, e, f>(), \
+   packed_ifn<2, a, b, c, d, e, f>()}
 // common slot layouts (metric first): aniso metric + scalar/vector/tensor
 // (BASELINE cfg3/cfg4, libexamples cube-solphys.sol), iso metric + scalars
 // (cfg2, cfg5), metric only; anything else runs the runtime-layout variant
@@ -95,7 +107,11 @@ const LayoutEntry kLayouts[] = {
 // layout allows only it; 0 = by the record's size: two above 8 doubles, where
 // one pass holds the whole record in registers — cfg4's 16 doubles: 168
 // VGPRs, 3 waves per SIMD, 4.42 ms per step against 4.18 in two passes, r05d)
-VolFn pick_layout(const Slots &S, int passes = 0) {
+struct VolPick {
+  VolFn fn;     // the fused kernel (walk + exact test + interpolation)
+  InterpFn ifn; // the split stage's interpolation kernel (after kVolWalk)
+};
+VolPick pick_layout(const Slots &S, int passes = 0) {
   for (const LayoutEntry &e : kLayouts) {
     int n = 0;
     while (n < 6 && e.c[n] > 0) n++;
@@ -103,16 +119,18 @@ VolFn pick_layout(const Slots &S, int passes = 0) {
     bool ok = true;
     for (int j = 0; j < n; j++) ok = ok && (S.s[j].code == e.c[j]);
     if (!ok) continue;
-    if (!S.rec) return e.fn;
+    if (!S.rec) return {e.fn, e.ifn};
     if (passes == 0) {
       int k = 0;
       for (int j = 0; j < n; j++) k += e.c[j];
       passes = k > 8 ? 2 : 1;
     }
     VolFn a = passes == 2 ? e.fn_packed2 : e.fn_packed, b = passes == 2 ? e.fn_packed : e.fn_packed2;
-    return a ? a : b;
+    InterpFn ia = passes == 2 ? e.ifn_packed2 : e.ifn_packed, ib = passes == 2 ? e.ifn_packed : e.ifn_packed2;
+    return {a ? a : b, ia ? ia : ib};
   }
-  return S.rec ? nullptr : k_vol<0, -1, 0, 0, 0, 0, 0>;
+  if (S.rec) return {nullptr, nullptr};
+  return {k_vol<0, -1, 0, 0, 0, 0, 0>, k_vol_interp<0, -1, 0, 0, 0, 0, 0>};
 }
 
 
@@ -122,7 +140,7 @@ bool packed_supported(int met_size, int nfield, const int *fsize) {
   S.rec = reinterpret_cast<const double *>(16);
   if (met_size) S.s[S.n++].code = met_size;
   for (int j = 0; j < nfield && S.n < kMaxSlot; j++) S.s[S.n++].code = fsize[j];
-  return pick_layout(S) != nullptr;
+  return pick_layout(S).fn != nullptr;
 }
 
 #ifdef PMMG_HIP_MEASURE
@@ -287,6 +305,23 @@ struct pmmg_hip_ctx {
   int vol_wait_seed = 0; // measurement build, PMMG_HIP_VOLWAIT=1: the volume kernel waits for the surface seeds
   int lane0 = 1; // lane 0 enqueues on this context's streams (measurement build: PMMG_HIP_LANE0=0 gives it
                  // streams of its own)
+  // the volume stage split into a walk kernel that writes located records and an interpolation kernel
+  // (r06), measured and not the default: at cfg4 the fused kernel's volume stage 3.30-3.35 ms,
+  // split 3.60-3.66 (arrays) / 3.52 (packed records, one pass), chunked with the interpolation on its own stream
+  // beside the next walk chunk 3.62-3.77 (profiles/r06a-r06c): the walk alone takes 1.91 ms and the
+  // interpolation alone 1.90-1.99, whose sum the fused kernel beats by overlapping them across its waves, and
+  // the located records add 1.9 GB of traffic.  PMMG_HIP_VOLSPLIT: 1 split (every call), 0 fused (default);
+  // -1 split for calls of >= kSmallGroup queries
+  int vol_split = 0;
+  DevBuf locv, locp; // the split stage's located records (LocBuf): vertex ids, coordinates
+  // the split stage in chunks: walk chunk j on the main stream, its interpolation on stream_i after the
+  // chunk's event, so that interpolation j runs beside walk j + 1 (PMMG_HIP_VOLCHUNKS, 1..kMaxVolChunks)
+  static constexpr int kMaxVolChunks = 16;
+  int vol_chunks = 4;
+  hipStream_t stream_i = nullptr;
+  hipEvent_t ev_chunk[2][kMaxVolChunks] = {};
+  hipEvent_t ev_interp = nullptr;
+  int ixcd_run = -1; // measurement build, PMMG_HIP_IXCDRUN: the interpolation kernel's XCD run (-1: xcd_run)
   int filter_steps = 64; // step cap of the fp32 filter walk (then the exact fp64 walk continues from where it
                          // stopped: a query the filter misjudges hands over early instead of cycling through a
                          // 4-entry history for up to maxstep steps); test-only PMMG_HIP_FILTER_STEPS=0 sends every
@@ -645,6 +680,9 @@ static pmmg_hip_ctx *create_ctx(int device, int options, bool srf_prio, pmmg_hip
   c->fanmax = env_int("PMMG_HIP_FANMAX", c->fanmax);
   c->srf_g = std::min(1024, env_int("PMMG_HIP_SRFG", 0));
   c->pack_passes = std::max(0, std::min(2, env_int("PMMG_HIP_PACKPASS", c->pack_passes))); // packed: gather passes
+  if (const char *e = getenv("PMMG_HIP_VOLSPLIT"))
+    if (*e == '0' || *e == '1') c->vol_split = *e - '0';
+  c->vol_chunks = std::max(1, std::min((int)pmmg_hip_ctx::kMaxVolChunks, env_int("PMMG_HIP_VOLCHUNKS", c->vol_chunks)));
   c->bg.fanmax = c->fanmax; // every kernel's Bg copy carries it
   c->filter_steps = c->filter_steps < c->maxstep ? c->filter_steps : c->maxstep;
   if (const char *e = getenv("PMMG_HIP_FILTER_STEPS"))
@@ -664,6 +702,7 @@ static pmmg_hip_ctx *create_ctx(int device, int options, bool srf_prio, pmmg_hip
   if (const char *e = getenv("PMMG_HIP_XCDRUN"))
     if (*e && atoi(e) >= 0) c->xcd_run = atoi(e);
   c->pad = env_int("PMMG_HIP_PAD", 0);
+  c->ixcd_run = env_int("PMMG_HIP_IXCDRUN", -1);
   c->lane_streams = std::max(1, std::min(3, env_int("PMMG_HIP_LANE_STREAMS", c->lane_streams)));
   c->lane0 = env_int("PMMG_HIP_LANE0", 1) ? 1 : 0;
   c->bdy_first = env_int("PMMG_HIP_BDYFIRST", 0);
@@ -690,13 +729,22 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   if (c->stream2_hi) (void)hipStreamSynchronize(c->stream2_hi);
   if (c->stream3) (void)hipStreamSynchronize(c->stream3);
   if (c->cstream) (void)hipStreamSynchronize(c->cstream);
+  if (c->stream_i) {
+    (void)hipStreamSynchronize(c->stream_i);
+    (void)hipStreamDestroy(c->stream_i);
+  }
+  for (auto &row : c->ev_chunk)
+    for (hipEvent_t &e : row)
+      if (e) (void)hipEventDestroy(e);
+  if (c->ev_interp) (void)hipEventDestroy(c->ev_interp);
   DevBuf *bufs[] = {&c->o_xyz, &c->o_tetv, &c->o_adja, &c->o_triv, &c->o_adjt, &c->o_met, &c->o_rec, &c->frame,
                     &c->stats, &c->grid, &c->sgrid, &c->order_v, &c->cohd,
                     &c->order_b, &c->cont, &c->xq, &c->qs, &c->axh, &c->bkeys, &c->bkeys2, &c->bvals, &c->bvals2, &c->rs_hist, &c->rs_csum, &c->oflag, &c->cls_cnt, &c->qmin, &c->fb_vol, &c->fb_bdy,
                     &c->best, &c->nac, &c->cres, &c->bbest, &c->bnac, &c->bcres, &c->fbp_vol, &c->fbp_bdy, &c->fbg_vol_c,
                     &c->fbg_vol_u, &c->fbg_vol_i, &c->fbg_bdy_c, &c->fbg_bdy_u, &c->fbg_bdy_i, &c->h_xyz,
                     &c->h_cls, &c->h_met, &c->h_elem, &c->h_hit, &c->brk_k, &c->brk_k2, &c->brk_v, &c->brk_v2,
-                    &c->brk_vinv, &c->brk_tinv, &c->brk_xq, &c->brk_xyz, &c->brk_sol, &c->brk_rec, &c->brk_tmp};
+                    &c->brk_vinv, &c->brk_tinv, &c->brk_xq, &c->brk_xyz, &c->brk_sol, &c->brk_rec, &c->brk_tmp,
+                    &c->locv, &c->locp};
   for (DevBuf *b : bufs) release(*b);
   for (auto &b : c->o_f) release(b);
   for (auto &b : c->h_f) release(b);
@@ -1376,11 +1424,23 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     }
     S.rec_out = rec_out;
   }
-  const VolFn vol_fn = pick_layout(S, c->pack_passes);
-  if (!vol_fn) {
+  const VolPick vpick = pick_layout(S, c->pack_passes);
+  if (!vpick.fn) {
     set_err(c, "locate_interp: no packed-record kernel for this slot layout");
     return 0;
   }
+  const bool vsplit = S.n > 0 && vpick.ifn && (c->vol_split < 0 ? np_new >= kSmallGroup : c->vol_split == 1);
+  LocBuf lb{nullptr, nullptr, nullptr};
+  if (vsplit) {
+    if (!ensure(c, c->locv, 16 * (size_t)np_new) || !ensure(c, c->locp, 32 * (size_t)np_new)) return 0;
+    lb = LocBuf{(nti4 *)c->locv.p, (ntd2 *)c->locp.p, (ntd2 *)c->locp.p + np_new};
+    if (!c->stream_i) HIPCK(c, hipStreamCreateWithFlags(&c->stream_i, hipStreamNonBlocking));
+    for (auto &row : c->ev_chunk)
+      for (hipEvent_t &e : row)
+        if (!e) HIPCK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    if (!c->ev_interp) HIPCK(c, hipEventCreateWithFlags(&c->ev_interp, hipEventDisableTiming));
+  }
+  const VolFn vol_fn = vsplit ? kVolWalk : vpick.fn;
   const int g = grid_dim(bg.ne, c->tpc, 1024);
   const int gs = bg.nt <= 0 ? 1 : (c->srf_g > 0 ? c->srf_g : grid_dim((long long)bg.nt * c->srf_mult, 2, 1024));
   const int gb = 1 << kBinBitsAxis;
@@ -1570,10 +1630,32 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   auto vol = [&](int want) {
     // (measurement build; a plain call: HIPCK's `return 0` would give this void lambda a return type)
     if (c->vol_wait_seed && bg.nt > 0 && want <= 0) (void)hipStreamWaitEvent(s, c->ev[EV_SRFSEED], 0);
-    hipLaunchKernelGGL(vol_fn, dim3((np_new + 63) / 64), dim3(64), 0, s, bg, (const Frame *)fr,
-                       (const unsigned long long *)grid, g, xyz_new, pclass, (const int *)order_v,
-                       c->bin_qs ? (const double *)c->qs.p : nullptr, np_new, (ContEntry *)c->cont.p, st, S,
-                       elem_out, hit_out, c->filter_steps, flag, c->xcd_run, c->pad, want);
+    const int nb = (np_new + 63) / 64;
+    if (!vsplit) {
+      hipLaunchKernelGGL(vol_fn, dim3(nb), dim3(64), 0, s, bg, (const Frame *)fr, (const unsigned long long *)grid,
+                         g, xyz_new, pclass, (const int *)order_v, c->bin_qs ? (const double *)c->qs.p : nullptr,
+                         np_new, (ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->filter_steps, flag,
+                         c->xcd_run, c->pad, want, lb, 0);
+      return;
+    }
+    // split stage: walk chunk j (main stream), then its interpolation on stream_i, beside walk chunk j + 1
+    // (chunks of whole XCD runs)
+    const int run = 8 * std::max(1, c->xcd_run);
+    const int per = std::max(run, (nb + c->vol_chunks - 1) / c->vol_chunks / run * run);
+    const int ixr = c->ixcd_run >= 0 ? c->ixcd_run : c->xcd_run;
+    const int w = want > 0 ? 1 : 0;
+    for (int j = 0, b0 = 0; b0 < nb; j++, b0 += per) {
+      const int nbj = std::min(per, nb - b0);
+      hipLaunchKernelGGL(vol_fn, dim3(nbj), dim3(64), 0, s, bg, (const Frame *)fr, (const unsigned long long *)grid,
+                         g, xyz_new, pclass, (const int *)order_v, c->bin_qs ? (const double *)c->qs.p : nullptr,
+                         np_new, (ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->filter_steps, flag,
+                         c->xcd_run, c->pad, want, lb, b0);
+      hipEvent_t ej = c->ev_chunk[w][std::min(j, (int)pmmg_hip_ctx::kMaxVolChunks - 1)];
+      (void)hipEventRecord(ej, s);
+      (void)hipStreamWaitEvent(c->stream_i, ej, 0);
+      hipLaunchKernelGGL(vpick.ifn, dim3(nbj), dim3(64), 0, c->stream_i, lb, (const int *)order_v,
+                         (const DevStats *)st, np_new, S, flag, ixr, want, b0);
+    }
   };
   if (split) {
     // Host enqueue order (r05q trace): the input order's kernels first — the surface list, the surface
@@ -1625,6 +1707,10 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
                      (const ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->maxstep, FbInit{(int *)c->best.p},
                      FbGridBufs{(int *)c->fbg_vol_c.p, (int *)c->fbg_vol_u.p, (int *)c->fbg_vol_i.p});
   HIPCK(c, hipGetLastError());
+  if (vsplit) { // the volume stage ends with the interpolation's last chunk
+    HIPCK(c, hipEventRecord(c->ev_interp, c->stream_i));
+    HIPCK(c, hipStreamWaitEvent(s, c->ev_interp, 0));
+  }
   HIPCK(c, hipEventRecord(c->ev[EV_VOL], s));
   // ---- exhaustive fallbacks of the volume queries (lists and counts on the
   // device; the surface ones ran on the surface stream after k_bdy)

@@ -128,7 +128,64 @@ static inline double unit_rand(uint64_t seed, int64_t id, int c) {
   return (double)(r >> 11) * (1.0 / 9007199254740992.0); /* [0,1) */
 }
 
-int synth_vertices(int kind, int n, double jitter, uint64_t seed, double *xyz, uint8_t *isbdy) {
+/* lattice point idx (jittered by jit * h per unpinned coordinate) mapped to
+ * the mesh: the cube as is, the shell radially onto spheres (|p| = ninf(y)) */
+static void place(int kind, int n, const int *idx, const int *pinned, double jit, uint64_t seed, int64_t v,
+                  double *p) {
+  double h = (kind == SYNTH_CUBE) ? 1.0 / n : 2.0 / n;
+  double y[3];
+  for (int d = 0; d < 3; d++) {
+    y[d] = (kind == SYNTH_CUBE) ? (double)idx[d] / n : -1.0 + 2.0 * idx[d] / n;
+    if (jit != 0.0 && !pinned[d]) y[d] += (2.0 * unit_rand(seed, v, d) - 1.0) * jit * h;
+  }
+  if (kind == SYNTH_CUBE) {
+    p[0] = y[0]; p[1] = y[1]; p[2] = y[2];
+  } else {
+    double ninf = fmax(fabs(y[0]), fmax(fabs(y[1]), fabs(y[2])));
+    double n2 = sqrt(y[0] * y[0] + y[1] * y[1] + y[2] * y[2]);
+    double s = ninf / n2;
+    p[0] = y[0] * s; p[1] = y[1] * s; p[2] = y[2] * s;
+  }
+}
+
+/* smallest height of lattice vertex idx over the Kuhn tetra around it
+ * (unjittered positions): the distance to the opposite face */
+static double min_height(const lattice *L, const int *idx) {
+  static const int e[3][3] = {{1,0,0},{0,1,0},{0,0,1}};
+  static const int zero[3] = {0, 0, 0};
+  const int n = L->n;
+  double hmin = HUGE_VAL;
+  for (int dk = -1; dk <= 0; dk++)
+    for (int dj = -1; dj <= 0; dj++)
+      for (int di = -1; di <= 0; di++) {
+        int cc[3] = {idx[0] + di, idx[1] + dj, idx[2] + dk};
+        if (!cell_in(L, cc[0], cc[1], cc[2])) continue;
+        for (int p = 0; p < 6; p++) {
+          int a = kPerm[p][0], b = kPerm[p][1];
+          int q[4][3], me = -1;
+          for (int x = 0; x < 3; x++) {
+            q[0][x] = cc[x];
+            q[1][x] = cc[x] + e[a][x];
+            q[2][x] = cc[x] + e[a][x] + e[b][x];
+            q[3][x] = cc[x] + 1;
+          }
+          for (int j = 0; j < 4; j++)
+            if (q[j][0] == idx[0] && q[j][1] == idx[1] && q[j][2] == idx[2]) me = j;
+          if (me < 0) continue;
+          double P[4][3];
+          for (int j = 0; j < 4; j++) place(L->kind, n, q[j], zero, 0.0, 0, 0, P[j]);
+          const double *A = P[(me + 1) & 3], *B = P[(me + 2) & 3], *C = P[(me + 3) & 3];
+          double u[3] = {B[0] - A[0], B[1] - A[1], B[2] - A[2]}, w[3] = {C[0] - A[0], C[1] - A[1], C[2] - A[2]};
+          double nn[3] = {u[1] * w[2] - u[2] * w[1], u[2] * w[0] - u[0] * w[2], u[0] * w[1] - u[1] * w[0]};
+          double len = sqrt(nn[0] * nn[0] + nn[1] * nn[1] + nn[2] * nn[2]);
+          double hh = fabs((P[me][0] - A[0]) * nn[0] + (P[me][1] - A[1]) * nn[1] + (P[me][2] - A[2]) * nn[2]) / len;
+          if (hh < hmin) hmin = hh;
+        }
+      }
+  return hmin;
+}
+
+static int vertices(int kind, int n, double jitter, uint64_t seed, int valid, double *xyz, uint8_t *isbdy) {
   lattice L;
   if (!lattice_init(&L, kind, n)) { lattice_free(&L); return 0; }
   const int lo = n / 4, hi = 3 * n / 4;
@@ -151,21 +208,21 @@ int synth_vertices(int kind, int n, double jitter, uint64_t seed, double *xyz, u
           }
         }
         int64_t v = vid(&L, i, j, k);
-        double h = (kind == SYNTH_CUBE) ? 1.0 / n : 2.0 / n;
-        double y[3];
-        for (int d = 0; d < 3; d++) {
-          y[d] = (kind == SYNTH_CUBE) ? (double)idx[d] / n : -1.0 + 2.0 * idx[d] / n;
-          if (jitter != 0.0 && !pinned[d])
-            y[d] += (2.0 * unit_rand(seed, v, d) - 1.0) * jitter * h;
-        }
         double *p = xyz + 3 * (v - 1);
-        if (kind == SYNTH_CUBE) {
-          p[0] = y[0]; p[1] = y[1]; p[2] = y[2];
-        } else {
-          double ninf = fmax(fabs(y[0]), fmax(fabs(y[1]), fabs(y[2])));
-          double n2 = sqrt(y[0] * y[0] + y[1] * y[1] + y[2] * y[2]);
-          double s = ninf / n2;
-          p[0] = y[0] * s; p[1] = y[1] * s; p[2] = y[2] * s;
+        place(kind, n, idx, pinned, jitter, seed, v, p);
+        if (valid && jitter != 0.0) {
+          /* a vertex moves by at most kValidFrac of its smallest height, so
+           * that no Kuhn tetra inverts (the shell's radial map leaves slivers
+           * along the planes |y_i| = |y_j| = ninf, volume down to 7e-5 of the
+           * median, which a jitter of 0.05 cell already inverts) */
+          const double kValidFrac = 0.2;
+          static const int zero[3] = {0, 0, 0};
+          double p0[3];
+          place(kind, n, idx, zero, 0.0, 0, 0, p0);
+          double dd = sqrt((p[0] - p0[0]) * (p[0] - p0[0]) + (p[1] - p0[1]) * (p[1] - p0[1]) +
+                           (p[2] - p0[2]) * (p[2] - p0[2]));
+          double cap = kValidFrac * min_height(&L, idx);
+          if (dd > cap) place(kind, n, idx, pinned, jitter * cap / dd, seed, v, p);
         }
         if (isbdy) isbdy[v - 1] = (uint8_t)bdy;
       }
@@ -173,6 +230,14 @@ int synth_vertices(int kind, int n, double jitter, uint64_t seed, double *xyz, u
   }
   lattice_free(&L);
   return 1;
+}
+
+int synth_vertices(int kind, int n, double jitter, uint64_t seed, double *xyz, uint8_t *isbdy) {
+  return vertices(kind, n, jitter, seed, 0, xyz, isbdy);
+}
+
+int synth_vertices_valid(int kind, int n, double jitter, uint64_t seed, double *xyz, uint8_t *isbdy) {
+  return vertices(kind, n, jitter, seed, 1, xyz, isbdy);
 }
 
 int synth_tetra(int kind, int n, int *tetv, int *adja) {

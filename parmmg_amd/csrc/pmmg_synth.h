@@ -34,6 +34,14 @@ int synth_counts(int kind, int n, int64_t *out);
 int synth_vertices(int kind, int n, double jitter, uint64_t seed,
                    double *xyz, uint8_t *isbdy);
 
+/* The same, every vertex's displacement capped at 0.2 of its smallest height
+ * over the Kuhn tetra around it (unjittered): the lattice's tetra stay
+ * positive, so the jittered points with synth_tetra's connectivity form a
+ * valid mesh (a remeshed group that becomes the next background).  Vertices
+ * whose cap is not reached move exactly as in synth_vertices. */
+int synth_vertices_valid(int kind, int n, double jitter, uint64_t seed,
+                         double *xyz, uint8_t *isbdy);
+
 /* Tetra vertices tetv[4*ne] (1-based ids, positively oriented) and adjacency
  * adja[4*ne] (may be NULL). */
 int synth_tetra(int kind, int n, int *tetv, int *adja);

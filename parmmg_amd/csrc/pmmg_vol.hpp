@@ -29,6 +29,18 @@ struct ContEntry {
   int k;  // tetra the exact walk starts from (0: no seed)
 };
 
+// Located records of the split volume stage (r06): the walk kernel writes, per
+// processing index i, the accepted tetra's vertex ids (v.x = 0: nothing to
+// interpolate — another class, a handed-over or failed walk) and its four
+// exact coordinates; k_vol_interp reads them back in the same order.  Three
+// arrays of 16-byte rows, so that each wave-instruction writes or reads 1 KiB
+// of consecutive bytes.  Null v: the fused kernel interpolates itself.
+typedef int nti4 __attribute__((ext_vector_type(4)));
+struct LocBuf {
+  nti4 *v;
+  ntd2 *p01, *p23;
+};
+
 __device__ __forceinline__ void load_tet_pts(const Bg &bg, const int4 &tv, double (*p)[3]) {
   load_pt(bg.xyz, tv.x, p[0]);
   load_pt(bg.xyz, tv.y, p[1]);
@@ -960,13 +972,44 @@ __device__ __forceinline__ void vol_interp_packed(const Slots &S, bool acc, cons
   }
 }
 
-// PK: 0 = one array per solution, 1 / 2 = packed records in 1 / 2 passes
+// The interpolation of the wave's 64 queries (lanes with acc); the walk's LDS
+// slots must be dead (img aliases them in k_vol)
+template <int PK, int C0, int C1, int C2, int C3, int C4, int C5>
+__device__ __forceinline__ void vol_interp_wave(const Slots &S, bool acc, VolLoc &loc, int ip, double *img,
+                                                const Sink &snk, unsigned short *okm) {
+  if (!acc) { // idle lanes gather a valid row, never stored
+    loc.v = make_int4(1, 1, 1, 1);
+#pragma unroll
+    for (int f = 0; f < 4; f++) loc.phi[f] = 0.0;
+  }
+  __builtin_amdgcn_wave_barrier(); // the walk's slots are dead: the buffer becomes the gather image
+  if constexpr (PK > 0) {
+    vol_interp_packed<PK, C0, C1, C2, C3, C4, C5>(S, acc, loc, img, snk, okm);
+  } else if constexpr (C0 < 0) {
+    if (acc) {
+      const int vv[4] = {loc.v.x, loc.v.y, loc.v.z, loc.v.w};
+      for (int s2 = 0; s2 < S.n; s2++) interp_dyn<4>(S.s[s2], ip, vv, loc.phi);
+    }
+  } else {
+    vol_slot<C0>(S.s[0], acc, loc.v, loc.phi, img, snk);
+    vol_slot<C1>(S.s[1], acc, loc.v, loc.phi, img, snk);
+    vol_slot<C2>(S.s[2], acc, loc.v, loc.phi, img, snk);
+    vol_slot<C3>(S.s[3], acc, loc.v, loc.phi, img, snk);
+    vol_slot<C4>(S.s[4], acc, loc.v, loc.phi, img, snk);
+    vol_slot<C5>(S.s[5], acc, loc.v, loc.phi, img, snk);
+  }
+}
+
+// PK: 0 = one array per solution, 1 / 2 = packed records in 1 / 2 passes.
+// lb.v non-null (split volume stage, r06; launched as the locate-only layout):
+// the located records go to lb and k_vol_interp interpolates them.
 template <int PK, int C0, int C1, int C2, int C3, int C4, int C5>
 __global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsigned long long *grid, int g,
                                             const double *qxyz, const uint8_t *pclass, const int *order,
                                             const double *qs, int np, ContEntry *cont, DevStats *st, Slots S,
                                             int *elem_out, int8_t *hit_out, int filter_steps,
-                                            const int *order_flag, int xcd_run, int pad, int want) {
+                                            const int *order_flag, int xcd_run, int pad, int want, LocBuf lb,
+                                            int blk0) {
   // want >= 0: the launch for one of the two orders (auto mode launches both, each after its own lists;
   // the other returns at once)
   if (want >= 0 && order_flag[0] != want) return;
@@ -974,7 +1017,7 @@ __global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsign
   bstats_init(&sh.bs);
   __syncthreads();
   const LaneSlotsF L{(lds_float *)&sh.u.slots[__lane_id()]};
-  const int i = xcd_block_runs(xcd_run) * 64 + threadIdx.x;
+  const int i = (blk0 + xcd_block_runs(xcd_run)) * 64 + threadIdx.x;
   const bool sorted = order_flag[0] == 1; // the call's query order, decided on the device (the coherence test in k_bbox)
   bool active;
   int ip = 0;
@@ -1087,6 +1130,13 @@ __global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsign
   wave_count(&sh.bs, kCntVolQueries, active);
   wave_count(&sh.bs, kCntExact, more);
   wave_count(&sh.bs, kCntNoSeed, active && noseed);
+  if (lb.v && (sorted ? i < st->nvol : i < np)) { // split stage: the located record of processing index i
+    __builtin_nontemporal_store(acc ? nti4{loc.v.x, loc.v.y, loc.v.z, loc.v.w} : nti4{0, 0, 0, 0}, lb.v + i);
+    if (acc) {
+      __builtin_nontemporal_store(ntd2{loc.phi[0], loc.phi[1]}, lb.p01 + i);
+      __builtin_nontemporal_store(ntd2{loc.phi[2], loc.phi[3]}, lb.p23 + i);
+    }
+  }
   // 3. interpolation
 #ifdef PMMG_HIP_MEASURE
   // measurement build: PMMG_HIP_PAD bit 30 — Morton order stores whole lines
@@ -1098,28 +1148,7 @@ __global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsign
   const Sink snk{!sorted, (size_t)(i - __lane_id()), ip};
 #endif
   if (__any(acc)) {
-    if (!acc) { // idle lanes gather a valid row, never stored
-      loc.v = make_int4(1, 1, 1, 1);
-#pragma unroll
-      for (int f = 0; f < 4; f++) loc.phi[f] = 0.0;
-    }
-    double *img = sh.u.img;
-    __builtin_amdgcn_wave_barrier(); // the walk's slots are dead: the buffer becomes the gather image
-    if constexpr (PK > 0) {
-      vol_interp_packed<PK, C0, C1, C2, C3, C4, C5>(S, acc, loc, img, snk, sh.okm);
-    } else if constexpr (C0 < 0) {
-      if (acc) {
-        const int vv[4] = {loc.v.x, loc.v.y, loc.v.z, loc.v.w};
-        for (int s2 = 0; s2 < S.n; s2++) interp_dyn<4>(S.s[s2], ip, vv, loc.phi);
-      }
-    } else {
-      vol_slot<C0>(S.s[0], acc, loc.v, loc.phi, img, snk);
-      vol_slot<C1>(S.s[1], acc, loc.v, loc.phi, img, snk);
-      vol_slot<C2>(S.s[2], acc, loc.v, loc.phi, img, snk);
-      vol_slot<C3>(S.s[3], acc, loc.v, loc.phi, img, snk);
-      vol_slot<C4>(S.s[4], acc, loc.v, loc.phi, img, snk);
-      vol_slot<C5>(S.s[5], acc, loc.v, loc.phi, img, snk);
-    }
+    if constexpr (PK > 0 || C0 != 0) vol_interp_wave<PK, C0, C1, C2, C3, C4, C5>(S, acc, loc, ip, sh.u.img, snk, sh.okm);
     if (acc) {
       if (sorted) { // scattered: cached stores (see wave_store_rows_scat)
         if (elem_out) elem_out[ip - 1] = k;
@@ -1132,6 +1161,50 @@ __global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsign
   }
   __syncthreads();
   bstats_flush(&sh.bs, st);
+}
+
+// ---------------------------------------------------------------- split interpolation (r06)
+//
+// The second kernel of the split volume stage: the located records of 64
+// consecutive processing indices per one-wave block (the walk kernel's block
+// order), read as whole lines, then the same wave-cooperative interpolation
+// as the fused kernel's third phase — but under its own register budget and
+// occupancy, where in the fused kernel the interpolation's gathers were issued
+// under the walk's.  Launched right after the walk kernel
+// on the same stream.
+template <int PK>
+struct InterpShared {
+  unsigned short okm[PK > 0 ? 64 : 1];
+  double img[(PK > 0 ? 16 : 8) * 64];
+};
+
+template <int PK, int C0, int C1, int C2, int C3, int C4, int C5>
+__global__ __launch_bounds__(64) void k_vol_interp(LocBuf lb, const int *order, const DevStats *st, int np, Slots S,
+                                                   const int *order_flag, int xcd_run, int want, int blk0) {
+  if (want >= 0 && order_flag[0] != want) return;
+  __shared__ InterpShared<PK> sh;
+  const int i = (blk0 + xcd_block_runs(xcd_run)) * 64 + threadIdx.x;
+  const bool sorted = order_flag[0] == 1;
+  const int bound = sorted ? st->nvol : np;
+  VolLoc loc;
+  bool acc = false;
+  int ip = 0;
+  if (i < bound) {
+    const nti4 v = __builtin_nontemporal_load(lb.v + i);
+    acc = v.x != 0;
+    loc.v = make_int4(v.x, v.y, v.z, v.w);
+    if (acc) {
+      const ntd2 a = __builtin_nontemporal_load(lb.p01 + i), b = __builtin_nontemporal_load(lb.p23 + i);
+      loc.phi[0] = a.x;
+      loc.phi[1] = a.y;
+      loc.phi[2] = b.x;
+      loc.phi[3] = b.y;
+    }
+    ip = sorted ? order[i] : i + 1;
+  }
+  if (!__any(acc)) return;
+  const Sink snk{!sorted, (size_t)(i - __lane_id()), ip};
+  vol_interp_wave<PK, C0, C1, C2, C3, C4, C5>(S, acc, loc, ip, sh.img, snk, sh.okm);
 }
 
 } // namespace pmmg

@@ -185,3 +185,35 @@ def test_cfg3_shuffled_numbering_auto_order():
     assert same.sum() > 0.99 * act.sum()
     for x, y in zip([a[0]] + a[1], [b[0]] + b[1]):
         assert np.array_equal(x[same].view(np.uint64), y[inv][same].view(np.uint64))
+
+
+@pytest.mark.gpu
+def test_split_volume_stage_bit_identical_to_fused(monkeypatch):
+    """The split volume stage (PMMG_HIP_VOLSPLIT=1: a walk kernel writing
+    located records, an interpolation kernel per chunk on its own stream —
+    measured slower than the fused kernel and not the default)
+    gives the fused kernel's outputs bit for bit, in input order and in the
+    Morton order of a shuffled numbering, with the reference's arrays and
+    with packed records."""
+    w = configs.CFG3
+    bg, new = configs.build_meshes(w, seed=synth.SEED, with_new_tetra=False)
+    pc = synth.classes(new)
+    met = synth.solution(w.metric, bg.xyz)
+    fields = [synth.solution(f, bg.xyz) for f in w.fields]
+    perm = np.random.default_rng(11).permutation(new.np)
+    orders = [(new.xyz, pc), (np.ascontiguousarray(new.xyz[perm]), np.ascontiguousarray(pc[perm]))]
+    res = {}
+    for split in ("0", "1"):
+        monkeypatch.setenv("PMMG_HIP_VOLSPLIT", split)
+        monkeypatch.setenv("PMMG_HIP_VOLCHUNKS", "3")
+        with TransferContext(0) as ctx:
+            res[split] = [run_dev(ctx, bg, q, met, fields, c, w.hausd) for q, c in orders]
+            res[split].append(run_dev(ctx, bg, new.xyz, met, fields, pc, w.hausd, packed=True))
+    for a, b in zip(res["0"], res["1"]):
+        assert a[4].sorted == b[4].sorted
+        assert np.array_equal(a[2], b[2]) and np.array_equal(a[3], b[3])
+        wr = (a[3] & 15) != 0
+        assert wr.sum() == (pc != 0).sum()
+        for x, y in zip([a[0]] + a[1], [b[0]] + b[1]):
+            assert np.array_equal(x[wr].view(np.uint64), y[wr].view(np.uint64))
+    assert res["0"][1][4].sorted == 1

@@ -91,3 +91,28 @@ def test_mmg_like_numbering_is_a_permutation():
     head, tail = perm[:cut], perm[cut:]
     assert np.all(np.diff(head) > 0) and np.all(np.diff(tail) > 0)
     assert 0.14 < tail.size / n < 0.19
+
+
+def _volumes(m):
+    tv = m.tetv.astype(np.int64) - 1
+    x = m.xyz
+    return np.einsum("ij,ij->i", x[tv[:, 1]] - x[tv[:, 0]], np.cross(x[tv[:, 2]] - x[tv[:, 0]], x[tv[:, 3]] - x[tv[:, 0]]))
+
+
+def test_valid_jitter_keeps_every_tetra_positive():
+    """The shell's radial map leaves slivers along the planes |y_i| = |y_j|
+    that the plain jitter inverts (the r05 iteration-2 background: 0.23 % of
+    its tetra, 2655 walks cycling to the step cap); synth_vertices_valid caps
+    each vertex's displacement so that the jittered lattice stays a valid
+    mesh, with boundary vertices still on their spheres."""
+    plain = synth.lattice(synth.SHELL, 24, jitter=0.2, seed=7, with_trias=False)
+    assert (_volumes(plain) <= 0).sum() > 0
+    for kind, n in ((synth.SHELL, 24), (synth.SHELL, 40), (synth.CUBE, 20)):
+        m = synth.lattice(kind, n, jitter=0.2, seed=7, with_trias=False, valid=True)
+        assert (_volumes(m) > 0).all()
+        ref = synth.lattice(kind, n, jitter=0.0, with_tetra=False)
+        assert not np.array_equal(m.xyz, ref.xyz)  # still jittered
+        b = m.isbdy.astype(bool)
+        if kind == synth.SHELL:
+            r = np.abs(np.linalg.norm(m.xyz[b], axis=1))
+            assert np.all(np.isclose(r, 1.0) | np.isclose(r, 0.5))
