@@ -837,12 +837,10 @@ def main():
                 # every rank keeps only its part of the group (pmmg_shard_part_pack), the parts are exchanged
                 # all-to-all and assembled (pmmg_shard_assemble): the shard the whole-group builder makes
                 try:
-                    h = -args.halo * shard.max_tet_extent(bg) if args.halo < 0 else float(args.halo)
-                    h = max(h, 1.01 * w.hausd)
-                    grid = shard.grid_for(bg.xyz.min(axis=0), bg.xyz.max(axis=0), h)
                     sol = np.concatenate([met] + list(fields), axis=1)
                     part = shard.part_of(bg, sol, rank, world)
-                    sh = shard.shard_from_parts(ri, part, q_xyz, h, *grid, bg.kind, bg.n)
+                    # the halo and the grid from the parts too (shard.parts_frame: all-reduced extent and box)
+                    sh = shard.shard_from_parts(ri, part, q_xyz, args.halo, kind=bg.kind, n=bg.n, hausd=w.hausd)
                     del part
                     c0 = met.shape[1]
                     met, fields = sh.sol[:, :c0].copy(), []

@@ -105,7 +105,18 @@ typedef struct {
   int64_t seed_map_axes; /* bit d: axis d of the volume seed grid followed the vertex quantiles */
   int64_t nbdy_fanscan;  /* surface queries whose cone test scanned every tria for a vertex's ball (its fan
                             open, non-manifold or longer than 64: e.g. at a halo shard's cut) */
+  int64_t reserved[6];   /* zero; room for later counters without changing the struct's size */
 } pmmg_hip_stats;
+
+/* ABI of this header (r06): a shim built against it checks, once at load,
+ *     pmmg_hip_abi_version() == PMMG_HIP_ABI_VERSION
+ *     pmmg_hip_stats_size()  == sizeof(pmmg_hip_stats)
+ * and refuses a library that differs: the library writes a whole
+ * pmmg_hip_stats into the caller's struct (round 5 appended nbdy_fanscan, so a
+ * shim built against the round-4 header would have been overrun by 8 bytes). */
+#define PMMG_HIP_ABI_VERSION 6
+int pmmg_hip_abi_version(void);
+int64_t pmmg_hip_stats_size(void);
 
 /* Options (bit flags) for pmmg_hip_create.  Default: Morton-bin the queries
  * unless a sampled test on the device finds the input numbering already
@@ -397,7 +408,10 @@ int pmmg_hip_comm_unique_id(void *id);
 int pmmg_hip_comm_init(pmmg_hip_ctx *ctx, int nranks, int rank, const void *id);
 int pmmg_hip_comm_attach(pmmg_hip_ctx *ctx, void *nccl_comm, int nranks, int rank);
 
-/* All-gather of the parts' results (collective over the communicator):
+/* All-gather of the parts' results (collective over the communicator; every
+ * rank passes the same counts[], nslot, slot_size[] and the same choice of
+ * elem / hit given or NULL — the ranks first agree on that and on their
+ * arguments' validity, and all return 0 together when one differs or fails):
  * counts[nranks] points per rank (rank order), this rank's part in
  * rows[s] (slot_size[s] doubles per point: the metric / field rows
  * pmmg_hip_locate_interp wrote), elem, hit (both optional, NULL on every

@@ -15,6 +15,9 @@ c_int, c_int64, c_double, c_void_p, c_char_p = ctypes.c_int, ctypes.c_int64, cty
 P = ctypes.POINTER
 
 
+ABI_VERSION = 6  # PMMG_HIP_ABI_VERSION of include/parmmg_hip.h
+
+
 class HipStats(ctypes.Structure):
     """``pmmg_hip_stats`` of include/parmmg_hip.h."""
 
@@ -28,11 +31,11 @@ class HipStats(ctypes.Structure):
         ("ms_bdy", ctypes.c_float), ("ms_fallback", ctypes.c_float), ("ms_total", ctypes.c_float),
         ("ms_vol_locate", ctypes.c_float),
         ("nvol_noseed", c_int64), ("nvol_stuck", c_int64), ("nvol_limit", c_int64), ("seed_map_axes", c_int64),
-        ("nbdy_fanscan", c_int64),
+        ("nbdy_fanscan", c_int64), ("reserved", c_int64 * 6),
     ]
 
     def as_dict(self) -> dict:
-        return {name: getattr(self, name) for name, _ in self._fields_}
+        return {name: getattr(self, name) for name, _ in self._fields_ if name != "reserved"}
 
 
 class HipGroup(ctypes.Structure):
@@ -49,6 +52,8 @@ class HipGroup(ctypes.Structure):
 
 # C-ABI of include/parmmg_hip.h: name -> (restype, argtypes)
 HIP_API = {
+    "pmmg_hip_abi_version": (c_int, []),
+    "pmmg_hip_stats_size": (c_int64, []),
     "pmmg_hip_create": (c_void_p, [c_int, c_int]),
     "pmmg_hip_destroy": (None, [c_void_p]),
     "pmmg_hip_set_background": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p,
@@ -122,7 +127,12 @@ def _load(path: str, api: dict, what: str) -> ctypes.CDLL:
 def hip_lib() -> ctypes.CDLL:
     """The product HIP module (include/parmmg_hip.h)."""
     # PMMG_HIP_SO: an alternative build of the same module (A/B measurements)
-    return _load(os.environ.get("PMMG_HIP_SO", _build.HIP_SO), HIP_API, "libpmmg_hip.so")
+    lib = _load(os.environ.get("PMMG_HIP_SO", _build.HIP_SO), HIP_API, "libpmmg_hip.so")
+    # the load-time ABI check a shim makes (include/parmmg_hip.h, PMMG_HIP_ABI_VERSION)
+    if lib.pmmg_hip_abi_version() != ABI_VERSION or lib.pmmg_hip_stats_size() != ctypes.sizeof(HipStats):
+        raise RuntimeError(f"libpmmg_hip.so ABI {lib.pmmg_hip_abi_version()} / stats {lib.pmmg_hip_stats_size()} B, "
+                           f"expected {ABI_VERSION} / {ctypes.sizeof(HipStats)} B: rebuild (python -m parmmg_amd.build)")
+    return lib
 
 
 def synth_lib() -> ctypes.CDLL:

@@ -216,10 +216,16 @@ __device__ __forceinline__ ClosestSplit closest_split(int n, int G) {
   return s;
 }
 
-// (key, index) order of the closest searches: the reference keeps the first
-// element strictly closer than the best so far (from 1e10, index 0) while it
-// scans in index order, i.e. the lowest index at the minimum; a NaN key never
-// wins
+// (key, index) order of the closest searches: the lowest index at the minimum
+// key, starting from (1e10, index 0); a NaN key never wins.  This is the
+// reference's exhaustive scan on its own (it keeps the first element strictly
+// closer while scanning in index order, src/locate_pmmg.c:753-765) but not its
+// whole rule: the reference seeds closestDist / closestTet with what its walk
+// met (:800-815, :864) and skips the walk's visited tetra (:753), so on an
+// exact key tie between a walked element and a lower-index one it returns the
+// walked one.  Listed as a known divergence (ties of the closest
+// metric are broken by lowest index); only exact ties of |min bary| * vol
+// for points outside every element can differ.
 __device__ __forceinline__ bool key_before(double ka, int ia, double kb, int ib) {
   return ka < kb || (ka == kb && ia < ib);
 }

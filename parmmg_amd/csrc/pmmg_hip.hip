@@ -293,7 +293,7 @@ struct pmmg_hip_ctx {
   ncclComm_t comm = nullptr;
   bool comm_owned = false;
   int comm_rank = 0, comm_size = 0;
-  DevBuf ag_send, ag_recv, ag_off;
+  DevBuf ag_send, ag_recv, ag_off, ag_chk; // (ag_chk: the all-gather's agreement, ag_agree)
   // PMMG_HIP_GROUP_LANES: most lanes of a groups call (r05k, 10 cfg2-size groups, 4 hardware queues: 4 / 5 /
   // 8 / 10 lanes 0.096 / 0.083 / 0.092 / 0.095 ms per group — 5 lanes take 2 groups each, 4 take 3, 3, 2, 2;
   // more hardware queues made it slower: 8 queues, 5 lanes 0.127; r04i: 1 / 2 lanes 0.165 / 0.125)
@@ -633,6 +633,9 @@ static int env_int(const char *name, int def) { // positive values only
 
 extern "C" {
 
+int pmmg_hip_abi_version(void) { return PMMG_HIP_ABI_VERSION; }
+int64_t pmmg_hip_stats_size(void) { return (int64_t)sizeof(pmmg_hip_stats); }
+
 int pmmg_hip_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -763,7 +766,7 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
     for (auto &b : k.f) release(b);
   }
   DevBuf *cb[] = {&c->carry_dsrc, &c->carry_need, &c->carry_ids, &c->carry_cnt, &c->carry_rows, &c->carry_bc,
-                  &c->ag_send, &c->ag_recv, &c->ag_off};
+                  &c->ag_send, &c->ag_recv, &c->ag_off, &c->ag_chk};
   for (DevBuf *b : cb) release(*b);
   if (c->comm && c->comm_owned && rccl().ok) (void)rccl().commDestroy(c->comm);
   if (!c->borrowed_streams) {
@@ -2317,6 +2320,8 @@ static void comm_release(pmmg_hip_ctx *c) {
   c->comm_rank = c->comm_size = 0;
 }
 
+static constexpr int kAgView = 8; // int64 per rank in the all-gather's agreement (ag_agree)
+
 int pmmg_hip_comm_init(pmmg_hip_ctx *c, int nranks, int rank, const void *id) {
   if (!c) return 0;
   HIPCK(c, hipSetDevice(c->device));
@@ -2343,7 +2348,9 @@ int pmmg_hip_comm_init(pmmg_hip_ctx *c, int nranks, int rank, const void *id) {
   c->comm_owned = true;
   c->comm_rank = rank;
   c->comm_size = nranks;
-  return 1;
+  // the all-gather's agreement buffer, allocated here so that pmmg_hip_allgather_points allocates nothing
+  // before every rank has agreed (ag_agree)
+  return ensure(c, c->ag_chk, sizeof(long long) * kAgView * (nranks + 1));
 }
 
 int pmmg_hip_comm_attach(pmmg_hip_ctx *c, void *comm, int nranks, int rank) {
@@ -2361,6 +2368,30 @@ int pmmg_hip_comm_attach(pmmg_hip_ctx *c, void *comm, int nranks, int rank) {
   c->comm_owned = false;
   c->comm_rank = rank;
   c->comm_size = nranks;
+  return ensure(c, c->ag_chk, sizeof(long long) * kAgView * (nranks + 1)); // (see pmmg_hip_comm_init)
+}
+
+// The all-gather's agreement: every rank that holds a
+// communicator takes part in one small all-gather of its view of the call —
+// {local arguments valid and buffers allocated, K, nslot, the slot sizes, elem
+// / hit given, a hash of counts[]} — before the data collective, and every
+// rank then takes the same decision: either all gather, or all return 0 (a
+// rank that returned early used to leave the others inside ncclAllGather, and
+// records of different sizes R = 8 K + 8 were undefined behaviour).
+static int ag_agree(pmmg_hip_ctx *c, const long long *mine, std::vector<long long> &all) {
+  const int N = c->comm_size;
+  all.assign((size_t)kAgView * N, 0);
+  if (!ensure(c, c->ag_chk, sizeof(long long) * kAgView * (N + 1))) return 0;
+  long long *d = (long long *)c->ag_chk.p;
+  hipStream_t s = c->stream;
+  HIPCK(c, hipMemcpyAsync(d, mine, sizeof(long long) * kAgView, hipMemcpyHostToDevice, s));
+  const ncclResult_t e = rccl().allGather(d, d + kAgView, kAgView, ncclInt64, c->comm, s);
+  if (e != ncclSuccess) {
+    set_err(c, "ncclAllGather (agreement): %s", rccl().errorString(e));
+    return 0;
+  }
+  HIPCK(c, hipMemcpyAsync(all.data(), d + kAgView, sizeof(long long) * kAgView * N, hipMemcpyDeviceToHost, s));
+  HIPCK(c, hipStreamSynchronize(s));
   return 1;
 }
 
@@ -2375,38 +2406,77 @@ int pmmg_hip_allgather_points(pmmg_hip_ctx *c, const int64_t *counts, int nslot,
     return 0;
   }
   const int N = c->comm_size;
+  // local checks: a failure is recorded (ok = 0), not returned, so that this
+  // rank still takes part in the agreement below
+  bool ok = true;
+  char why[256] = {0};
   if (!counts || nslot < 0 || nslot > kMaxSlot || (nslot > 0 && (!slot_size || !rows || !rows_all)) ||
       (!elem) != (!elem_all) || (!hit) != (!hit_all)) {
-    set_err(c, "allgather_points: invalid arguments (nslot=%d)", nslot);
-    return 0;
+    snprintf(why, sizeof(why), "allgather_points: invalid arguments (nslot=%d)", nslot);
+    ok = false;
   }
   AgSlots S{};
-  S.n = nslot;
-  for (int j = 0; j < nslot; j++) {
-    if (slot_size[j] < 1 || slot_size[j] > 6 || !rows_all[j] || (counts[c->comm_rank] > 0 && !rows[j])) {
-      set_err(c, "allgather_points: slot %d (size %d) invalid", j, slot_size[j]);
-      return 0;
+  long long sizes_code = 0;
+  if (ok) {
+    S.n = nslot;
+    for (int j = 0; j < nslot && ok; j++) {
+      if (slot_size[j] < 1 || slot_size[j] > 6 || !rows_all[j] || (counts[c->comm_rank] > 0 && !rows[j])) {
+        snprintf(why, sizeof(why), "allgather_points: slot %d (size %d) invalid", j, slot_size[j]);
+        ok = false;
+        break;
+      }
+      S.in[j] = rows[j];
+      S.out[j] = rows_all[j];
+      S.size[j] = slot_size[j];
+      S.K += slot_size[j];
+      sizes_code = sizes_code * 8 + slot_size[j];
     }
-    S.in[j] = rows[j];
-    S.out[j] = rows_all[j];
-    S.size[j] = slot_size[j];
-    S.K += slot_size[j];
   }
   std::vector<long long> off((size_t)N + 1, 0);
   long long maxn = 0;
-  for (int r = 0; r < N; r++) {
+  unsigned long long chash = 0x9E3779B97F4A7C15ULL;
+  for (int r = 0; r < N && ok; r++) {
     if (counts[r] < 0) {
-      set_err(c, "allgather_points: counts[%d] = %lld", r, (long long)counts[r]);
-      return 0;
+      snprintf(why, sizeof(why), "allgather_points: counts[%d] = %lld", r, (long long)counts[r]);
+      ok = false;
+      break;
     }
     off[r + 1] = off[r] + counts[r];
     maxn = std::max(maxn, (long long)counts[r]);
+    chash = (chash ^ (unsigned long long)counts[r]) * 0x100000001B3ULL;
   }
-  const long long R = 8LL * S.K + 8, n = counts[c->comm_rank];
-  if (maxn == 0) return 1;
-  if (!ensure(c, c->ag_send, (size_t)(R * maxn)) || !ensure(c, c->ag_recv, (size_t)(R * maxn * N)) ||
-      !ensure(c, c->ag_off, sizeof(long long) * off.size()))
+  const long long R = 8LL * S.K + 8;
+  if (ok && maxn > 0 &&
+      (!ensure(c, c->ag_send, (size_t)(R * maxn)) || !ensure(c, c->ag_recv, (size_t)(R * maxn * N)) ||
+       !ensure(c, c->ag_off, sizeof(long long) * off.size()))) {
+    snprintf(why, sizeof(why), "allgather_points: buffers: %s", c->err);
+    ok = false;
+  }
+  // the arguments that must be identical on every rank: nslot, slot_size[],
+  // whether elem / hit are given, counts[] (hence K, R and maxn)
+  const long long mine[kAgView] = {ok ? 1 : 0, S.K, nslot, sizes_code, elem ? 1 : 0, hit ? 1 : 0,
+                                   (long long)(chash >> 1), maxn};
+  std::vector<long long> all;
+  if (!ag_agree(c, mine, all)) return 0;
+  if (!ok) {
+    set_err(c, "%s", why);
     return 0;
+  }
+  for (int r = 0; r < N; r++) {
+    const long long *v = &all[(size_t)kAgView * r];
+    if (!v[0]) {
+      set_err(c, "allgather_points: rank %d's arguments are invalid", r);
+      return 0;
+    }
+    for (int j = 1; j < kAgView; j++)
+      if (v[j] != all[j]) {
+        set_err(c, "allgather_points: rank %d disagrees with rank 0 on %s", r,
+                j <= 3 ? "the slot layout" : (j <= 5 ? "elem / hit" : "counts[]"));
+        return 0;
+      }
+  }
+  const long long n = counts[c->comm_rank];
+  if (maxn == 0) return 1;
   hipStream_t s = c->stream;
   HIPCK(c, hipMemcpyAsync(c->ag_off.p, off.data(), sizeof(long long) * off.size(), hipMemcpyHostToDevice, s));
   if (n > 0)

@@ -278,17 +278,54 @@ def assemble(bufs, K: int, kind: int = 0, n: int = 0, halo: float = 0.0) -> Halo
     return HaloShard(mesh, tg, vg, rg, halo, sol)
 
 
-def shard_from_parts(ri, part: Part, q_xyz: np.ndarray, halo: float, g_lo, cell: float, g_n, kind: int = 0,
-                     n: int = 0) -> HaloShard:
+def parts_frame(ri, part: Part, halo: float = DEFAULT_HALO, hausd: float = 0.0, cell_factor: float = 1.0):
+    """The halo and the occupancy grid every rank's shard needs, from the
+    ranks' parts alone (collective over ri's process group): the largest tetra
+    extent and the bounding box of every part's vertices, reduced over the
+    ranks (max / min / max), then halo_shard_cells's rules — halo < 0 in units
+    of that extent, never less than 1.01 * hausd, grid_for over the box.
+    Returns (h, g_lo, cell, g_n), identical on every rank and equal to what
+    halo_shard_cells derives from the whole group (whose vertices are all
+    used by some part's tetra or trias)."""
+    import torch
+    import torch.distributed as dist
+
+    ext = 0.0
+    if part.tetv.shape[0]:
+        loc = (np.searchsorted(part.vert_gid, part.tetv) + 1).astype(np.int32)
+        ext = float(host_lib().pmmg_max_tet_extent(int(part.xyz.shape[0]), _p(np.ascontiguousarray(part.xyz)),
+                                                   int(loc.shape[0]), _p(np.ascontiguousarray(loc))))
+    lo, hi = range_box(part.xyz)
+    if part.xyz.shape[0] == 0:
+        lo, hi = np.full(3, np.inf), np.full(3, -np.inf)
+    dev = torch.device("cuda", torch.cuda.current_device()) if ri.backend == "nccl" else torch.device("cpu")
+    v = torch.tensor(np.concatenate([[ext], -np.asarray(lo, np.float64), np.asarray(hi, np.float64)]),
+                     dtype=torch.float64, device=dev)
+    dist.all_reduce(v, op=dist.ReduceOp.MAX)
+    v = v.cpu().numpy()
+    h = -halo * float(v[0]) if halo < 0 else float(halo)
+    h = max(h, 1.01 * float(hausd))
+    g_lo, cell, g_n = grid_for(-v[1:4], v[4:7], h, cell_factor)
+    return h, g_lo, cell, g_n
+
+
+def shard_from_parts(ri, part: Part, q_xyz: np.ndarray, halo: float, g_lo=None, cell: float = 0.0, g_n=None,
+                     kind: int = 0, n: int = 0, hausd: float = 0.0) -> HaloShard:
     """This rank's halo shard built from the ranks' parts (collective over
     ri's process group): every rank's region all-gathered, this rank's part
     packed for every rank, one all-to-all of the buffers (torch.distributed:
     gloo on the CPU, RCCL with device buffers), the received buffers
-    assembled.  `halo` (absolute) and the grid (grid_for over the group's
-    box) must be the same on every rank."""
+    assembled.  g_lo None: the halo (halo < 0: in units of the largest tetra
+    extent) and the grid are derived from the parts (parts_frame), so that no
+    rank needs the whole group; else `halo` (absolute) and the grid must be the
+    same on every rank.  The halo is never less than 1.01 * hausd (see
+    halo_shard)."""
     import torch
     import torch.distributed as dist
 
+    if g_lo is None:
+        halo, g_lo, cell, g_n = parts_frame(ri, part, halo, hausd)
+    halo = max(float(halo), 1.01 * float(hausd))
     reg = region_of(q_xyz, g_lo, cell, g_n, halo)
     world = dist.get_world_size()
     regs = [None] * world

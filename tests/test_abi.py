@@ -93,3 +93,19 @@ def test_ctypes_structs_match_the_header(tmp_path):
         assert ctypes.sizeof(py) == want[(cname, "size")], cname
         for fname, _ in py._fields_:
             assert getattr(py, fname).offset == want[(cname, fname)], (cname, fname)
+
+
+def test_abi_version_and_stats_size():
+    """The load-time check a shim makes (include/parmmg_hip.h): the library's
+    ABI version is the header's PMMG_HIP_ABI_VERSION and it writes exactly
+    sizeof(pmmg_hip_stats) bytes of stats (a counter appended
+    without a version let an older shim's struct be overrun)."""
+    import re
+
+    from parmmg_amd import _native
+
+    hdr = open(os.path.join(ROOT, "include", "parmmg_hip.h")).read()
+    v = int(re.search(r"#define PMMG_HIP_ABI_VERSION (\d+)", hdr).group(1))
+    lib = _native.hip_lib()
+    assert lib.pmmg_hip_abi_version() == v == _native.ABI_VERSION
+    assert lib.pmmg_hip_stats_size() == ctypes.sizeof(_native.HipStats)

@@ -37,6 +37,14 @@ def test_allgather_points_world1(n):
         ctx.allgather_points([n], d_rows[:2], d_all[:2])
         with pytest.raises(RuntimeError, match="invalid"):
             ctx.allgather_points([n], d_rows, d_all, d_e, None)  # elem without elem_all
+        # a rank's invalid arguments are found before the data collective (the
+        # ranks' agreement): the call fails on every rank, and the
+        # communicator stays usable
+        with pytest.raises(RuntimeError, match="counts"):
+            ctx.allgather_points([-1], d_rows, d_all)
+        ctx.allgather_points([n], d_rows[:1], d_all[:1])
+        if n:
+            assert np.array_equal(d_all[0].download(), rows[0])
 
 
 @pytest.mark.gpu

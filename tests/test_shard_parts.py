@@ -63,10 +63,17 @@ def _parts_worker(rank, world, port, q):
     part = shard.part_of(bg, sol, rank, world)  # all this rank holds of the group
     mine = ranks.rcb_shards(case["new"].xyz, case["pclass"], world)[rank]
     sh = shard.shard_from_parts(ri, part, case["new"].xyz[mine], h, g_lo, cell, g_n, synth.SHELL, 12)
+    # the halo and the grid from the parts alone (parts_frame's all-reduces, hausd floor)
+    frame = shard.parts_frame(ri, part, shard.DEFAULT_HALO, case["hausd"])
+    sh2 = shard.shard_from_parts(ri, part, case["new"].xyz[mine], shard.DEFAULT_HALO, kind=synth.SHELL, n=12,
+                                 hausd=case["hausd"])
     whole = shard.halo_shard_cells(bg, case["new"].xyz[mine], h, hausd=case["hausd"])
     try:
         _same_shard(sh, whole)
-        ok = bool(np.array_equal(sh.sol, sol[whole.vert_gid - 1]))
+        _same_shard(sh2, whole)
+        ok = bool(np.array_equal(sh.sol, sol[whole.vert_gid - 1])) and bool(np.array_equal(sh2.sol, sh.sol))
+        ok = ok and frame[0] == h and np.array_equal(frame[1], g_lo) and frame[2] == cell and \
+            np.array_equal(frame[3], g_n)
     except AssertionError:
         ok = False
     q.put((rank, ok, sh.mesh.ne, part.tet_gid.shape[0]))
