@@ -254,3 +254,47 @@ def check(case, gpu, max_points=None):
                 rep["srf_face"] += 1
                 rep["srf_face_same"] += int(int(ref["elem"][i]) == k)
     return rep
+
+
+def stale_case(hausd: float = 0.01):
+    """A surface fixture that reaches the reference's stale re-evaluation
+    (src/locate_pmmg.c:505-509): two boundary trias
+    without adjacency, T1 = tria 1 horizontal at z = -0.1 (normal +z), T2 =
+    tria 2 = the last tria (nt) tilted (normal (-1,-1,2)/sqrt 6), and surface
+    points above T2's foot print at |z| < hausd.  Every point is rejected by
+    both trias' own tests (T1: 0.1 below, T2: ~0.24 off its plane), the walk
+    has no neighbour to step to, so the exhaustive search accepts nothing and
+    the closest tria by centroid is T1; the reference then re-evaluates with
+    `ptr` still at T2 (the loop's last tria) but T1's normal and index — T2's
+    vertices projected along +z enclose the points, so the re-evaluation
+    accepts, and the values are T1's vertex values weighted by T2's
+    coordinates.  Returns (case, expected) with expected the values of that
+    arithmetic restated in numpy (barycoord_pmmg.c:191-223,
+    interpmesh_pmmg.c:125-149), independent of the oracle."""
+    from parmmg_amd.synth import Mesh
+
+    xyz = np.array([[5, 0, 0], [6, 0, 0.5], [5, 1, 0.5], [5.1, 0.1, -0.1], [5.6, 0.1, -0.1], [5.1, 0.6, -0.1],
+                    [5.1, 0.1, -0.6]], np.float64)
+    tetv = np.array([[4, 5, 7, 6]], np.int32)  # one positive tetra under T1 (the volume is not queried)
+    triv = np.array([[4, 5, 6], [1, 2, 3]], np.int32)
+    bg = Mesh(synth.CUBE, 0, xyz, tetv, np.zeros((1, 4), np.int32), triv, np.zeros((2, 3), np.int32), None)
+    q = np.array([[5.3, 0.3, 0.005], [5.2, 0.5, -0.004], [5.25, 0.2, 0.0]], np.float64)
+    new = Mesh(synth.CUBE, 0, q, np.zeros((0, 4), np.int32), np.zeros((0, 4), np.int32), np.zeros((0, 3), np.int32),
+               np.zeros((0, 3), np.int32), None)
+    met = np.arange(1, 8, dtype=np.float64)[:, None]
+    fs = [np.stack([np.arange(7) * 10.0 + 1, np.arange(7) ** 2 + 0.5, -np.arange(7) * 3.0], 1)]
+    pc = np.full(q.shape[0], 2, np.uint8)  # PMMG_PT_BDY
+    case = dict(bg=bg, new=new, met=met, fields=fs, pclass=pc, B=O.Background(bg, met, fs, hausd), hausd=hausd)
+    # the stale arithmetic: T2's vertices, T1's unit normal, T2's area (|non-unit normal|, locate_pmmg.c:82)
+    p1, p2 = xyz[triv[0] - 1], xyz[triv[1] - 1]
+    n1 = np.cross(p1[1] - p1[0], p1[2] - p1[0])
+    n1 /= np.linalg.norm(n1)
+    q2 = np.linalg.norm(np.cross(p2[1] - p2[0], p2[2] - p2[0]))
+    exp_met, exp_f = [], []
+    for x in q:
+        dist = np.dot(x - p2[0], n1)
+        proj = x - dist * n1
+        phi = [np.dot(np.cross(p2[(i + 1) % 3] - proj, p2[(i + 2) % 3] - proj), n1) / q2 for i in range(3)]
+        exp_met.append(sum(phi[i] * met[triv[0][i] - 1] for i in range(3)))
+        exp_f.append(sum(phi[i] * fs[0][triv[0][i] - 1] for i in range(3)))
+    return case, dict(met=np.array(exp_met), fields=[np.array(exp_f)], elem=1)

@@ -14,11 +14,10 @@ and checked against the oracle (runs on the MI355X).
  11 BDY_CLOSEST   surface point beyond hausd of every tria
  10 BDY_STALE     the reference re-evaluates the last scanned tria with the
                   closest tria's normal after a failed exhaustive search
-                  (locate_pmmg.c:505-512); restated in k_bdy_finish and the
-                  oracle, but no input found to reach it (400k random points
-                  around a flat tetra, 100k around the lattices' last trias:
-                  the closest tria's normal never accepts where the last
-                  tria's own test failed) — not asserted.
+                  (locate_pmmg.c:505-512): reached by a constructed fixture
+                  (tests/parity.py::stale_case, r06; random points around the
+                  lattices never reach it: the closest tria's normal never
+                  accepts where the last tria's own test failed).
 Each test compares with tests/parity.py::check (acceptance for the hit kind,
 values of the reference interpolator, class (i) identity against the
 oracle's run)."""
@@ -210,3 +209,26 @@ def test_unused_tetra_one_and_empty_seed_neighbourhood(mode):
     assert st["nvol_noseed"] >= 1
     assert (gpu["hit"][-1] & 15) == 3
     assert O.first_accepting_tetra(case["B"], case["new"].xyz[-1]) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tet8", [False, True])
+def test_stale_reevaluation_hits(tet8):
+    """Code 10 (BDY_STALE) on the constructed fixture of tests/parity.py::
+    stale_case: every surface point's walk and exhaustive search fail, the
+    closest tria (1) differs from the last (2), and the re-evaluation with
+    tria 2's vertices and tria 1's normal accepts.  The module's hit codes,
+    elements and values equal the oracle's faithful run bit for bit (and the
+    numpy restatement of that arithmetic within 1e-13)."""
+    from parity import stale_case
+
+    case, exp = stale_case()
+    n = case["new"].xyz.shape[0]
+    ref = O.run(case["B"], case["new"].xyz, case["pclass"], np.arange(1, n + 1, dtype=np.int32), O.MODE_FAITHFUL)
+    gpu = run_gpu(case, tet8=tet8)
+    print(gpu["hit"], gpu["elem"], gpu["stats"])
+    assert (gpu["hit"] & 15 == 10).all() and (gpu["elem"] == 1).all()
+    assert gpu["stats"]["nbdy_stale"] == n
+    assert np.array_equal(gpu["met"].view(np.uint64), ref["met"].view(np.uint64))
+    assert np.array_equal(gpu["fields"][0].view(np.uint64), ref["fields"][0].view(np.uint64))
+    assert np.allclose(gpu["met"], exp["met"], rtol=1e-13, atol=0)

@@ -230,3 +230,21 @@ def test_invmat_failure_case_on_the_oracle():
     hit = out["hit"].astype(np.int32) | (np.maximum(out["loc"], 0).astype(np.int32) << 4)
     rep = check(case, dict(met=out["met"], fields=out["fields"], elem=out["elem"], hit=hit.astype(np.int8)))
     assert rep["n"] == int((~skip).sum()) and rep["exact"] == rep["n"]
+
+
+def test_oracle_reaches_the_stale_reevaluation():
+    """The reference's stale re-evaluation after a failed exhaustive tria
+    search (src/locate_pmmg.c:505-509: `ptr` still at the last tria, the
+    closest tria's normal and index): on the constructed fixture every point
+    takes it (HIT_BDY_STALE = 10, element = the closest tria 1), in both
+    oracle modes, with the values of that arithmetic restated independently
+    in numpy (tests/parity.py::stale_case)."""
+    from parity import stale_case
+
+    case, exp = stale_case()
+    n = case["new"].xyz.shape[0]
+    for mode in (O.MODE_FAITHFUL, O.MODE_FRESH):
+        r = O.run(case["B"], case["new"].xyz, case["pclass"], np.arange(1, n + 1, dtype=np.int32), mode)
+        assert (r["hit"] == 10).all() and (r["elem"] == exp["elem"]).all(), (r["hit"], r["elem"])
+        assert np.allclose(r["met"], exp["met"], rtol=1e-13, atol=0)
+        assert np.allclose(r["fields"][0], exp["fields"][0], rtol=1e-13, atol=1e-14)
