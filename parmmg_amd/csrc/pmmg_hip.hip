@@ -322,6 +322,8 @@ struct pmmg_hip_ctx {
   hipEvent_t ev_chunk[2][kMaxVolChunks] = {};
   hipEvent_t ev_interp = nullptr;
   int ixcd_run = -1; // measurement build, PMMG_HIP_IXCDRUN: the interpolation kernel's XCD run (-1: xcd_run)
+  int null_sync = 0;   // measurement build, PMMG_HIP_NULLSYNC=1: small reads through the null stream (ctx_d2h)
+  int eager_lanes = 0; // measurement build, PMMG_HIP_EAGERLANES=1: the group lanes created with the context
   int filter_steps = 64; // step cap of the fp32 filter walk (then the exact fp64 walk continues from where it
                          // stopped: a query the filter misjudges hands over early instead of cycling through a
                          // 4-entry history for up to maxstep steps); test-only PMMG_HIP_FILTER_STEPS=0 sends every
@@ -345,6 +347,18 @@ static void set_err(pmmg_hip_ctx *c, const char *fmt, ...) {
       return 0;                                                                                      \
     }                                                                                                \
   } while (0)
+
+// Device -> host reads of a context's small state on its own stream (r06):
+// a synchronous hipMemcpy goes through the device's null stream, whose queue
+// user — created at the first such copy — shifted the hardware queues the
+// group lanes' streams were later given (the groups call
+// 25 % slower after any earlier call in the process; tools/groups_probe.py,
+// profiles/r06f).  PMMG_HIP_NULLSYNC=1 (measurement build): the null stream again.
+static hipError_t ctx_d2h(pmmg_hip_ctx *c, void *dst, const void *src, size_t n) {
+  if (c->null_sync) return hipMemcpy(dst, src, n, hipMemcpyDeviceToHost);
+  hipError_t e = hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, c->stream);
+  return e != hipSuccess ? e : hipStreamSynchronize(c->stream);
+}
 
 static int ensure(pmmg_hip_ctx *c, DevBuf &b, size_t bytes) {
   if (bytes == 0) bytes = 16;
@@ -706,6 +720,8 @@ static pmmg_hip_ctx *create_ctx(int device, int options, bool srf_prio, pmmg_hip
     if (*e && atoi(e) >= 0) c->xcd_run = atoi(e);
   c->pad = env_int("PMMG_HIP_PAD", 0);
   c->ixcd_run = env_int("PMMG_HIP_IXCDRUN", -1);
+  c->null_sync = env_int("PMMG_HIP_NULLSYNC", 0);
+  c->eager_lanes = env_int("PMMG_HIP_EAGERLANES", 0);
   c->lane_streams = std::max(1, std::min(3, env_int("PMMG_HIP_LANE_STREAMS", c->lane_streams)));
   c->lane0 = env_int("PMMG_HIP_LANE0", 1) ? 1 : 0;
   c->bdy_first = env_int("PMMG_HIP_BDYFIRST", 0);
@@ -719,7 +735,14 @@ static pmmg_hip_ctx *create_ctx(int device, int options, bool srf_prio, pmmg_hip
   return c;
 }
 
-pmmg_hip_ctx *pmmg_hip_create(int device, int options) { return create_ctx(device, options, true); }
+static pmmg_hip_ctx *group_lane(pmmg_hip_ctx *c, int j);
+
+pmmg_hip_ctx *pmmg_hip_create(int device, int options) {
+  pmmg_hip_ctx *c = create_ctx(device, options, true);
+  if (c && c->eager_lanes)
+    for (int j = 0; j < c->group_lanes; j++) (void)group_lane(c, j);
+  return c;
+}
 
 void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   if (!c) return;
@@ -958,7 +981,7 @@ static int carry_solutions_body(pmmg_hip_ctx *c, int met_size, const double *met
     HIPCK(c, hipMemcpyAsync(&n, c->carry_cnt.p, sizeof(int), hipMemcpyDeviceToHost, s));
     HIPCK(c, hipStreamSynchronize(s));
     std::vector<int> ids((size_t)n);
-    if (n > 0) HIPCK(c, hipMemcpy(ids.data(), c->carry_ids.p, sizeof(int) * (size_t)n, hipMemcpyDeviceToHost));
+    if (n > 0) HIPCK(c, ctx_d2h(c, ids.data(), c->carry_ids.p, sizeof(int) * (size_t)n));
     for (const Arr &a : carried)
       if (!carry_host_rows(c, ids, a.host, a.row, (double *)a.dst->p)) return 0;
   }
@@ -1737,11 +1760,10 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
 static int collect_stats(pmmg_hip_ctx *c, pmmg_hip_stats *out) {
   DevStats h;
   int order[2] = {0, 0}; // the call's query order, decided on the device
-  HIPCK(c, hipMemcpy(order, c->oflag.p, sizeof(order), hipMemcpyDeviceToHost));
+  HIPCK(c, ctx_d2h(c, order, c->oflag.p, sizeof(order)));
   std::vector<StatPart> parts(kStatParts);
-  HIPCK(c, hipMemcpy(&h, c->stats.p, sizeof(DevStats), hipMemcpyDeviceToHost));
-  HIPCK(c, hipMemcpy(parts.data(), (const DevStats *)c->stats.p + 1, kStatParts * sizeof(StatPart),
-                     hipMemcpyDeviceToHost));
+  HIPCK(c, ctx_d2h(c, &h, c->stats.p, sizeof(DevStats)));
+  HIPCK(c, ctx_d2h(c, parts.data(), (const DevStats *)c->stats.p + 1, kStatParts * sizeof(StatPart)));
   unsigned long long cnt[kNumCnt] = {0}, steps = 0, stepmax = 0;
   for (const StatPart &pt : parts) {
     for (int j = 0; j < kNumCnt; j++) cnt[j] += pt.cnt[j];
@@ -1772,7 +1794,7 @@ static int collect_stats(pmmg_hip_ctx *c, pmmg_hip_stats *out) {
   out->nvol_limit = (int64_t)cnt[kCntLimit];
   {
     int ad = 0;
-    HIPCK(c, hipMemcpy(&ad, &((const Frame *)c->frame.p)->adaptive, sizeof(int), hipMemcpyDeviceToHost));
+    HIPCK(c, ctx_d2h(c, &ad, &((const Frame *)c->frame.p)->adaptive, sizeof(int)));
     out->seed_map_axes = ad;
     out->nbdy_fanscan = (int64_t)cnt[kCntFanScan];
   }

@@ -8,6 +8,7 @@ prologues:
   base          nothing
   streamsN      N HIP streams created and destroyed (hipStreamCreate, ctypes)
   keepstreamsN  N HIP streams created and kept alive
+  nullcopy      one synchronous hipMemcpy (null stream)
   allocG        G GiB hipMalloc'ed in 256 MiB pieces, then freed
   big_auto      one cfg3 call in device mode, auto order (the binning's third stream is created), context closed
   big_noauto    the same with the input order forced (no third stream)
@@ -58,6 +59,14 @@ def prologue(spec: str):
                 h.hipStreamDestroy(s)
             return None
         return ss
+    if spec == "nullcopy":  # a synchronous copy on the null stream (creates the device's default queue user)
+        h = hip()
+        h.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        p, x = ctypes.c_void_p(), ctypes.c_int(1)
+        assert h.hipMalloc(ctypes.byref(p), 64) == 0
+        assert h.hipMemcpy(p, ctypes.byref(x), 4, 1) == 0
+        h.hipFree(p)
+        return None
     if spec.startswith("alloc"):
         gib = int(spec[5:])
         h = hip()
