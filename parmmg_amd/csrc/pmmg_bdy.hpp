@@ -120,8 +120,13 @@ __device__ __forceinline__ int bdy_query(const Bg &bg, const Frame *fr, const in
 __global__ __launch_bounds__(kBlock) void k_bdy(Bg bg, const Frame *fr, const int *sgrid, int gs, const double *qxyz,
                                                 const int *order, Slots S, int *elem_out, int8_t *hit_out, int *fb,
                                                 DevStats *st, int maxstep, int dyn, FbInit fi, FbGridBufs gb,
-                                                const int *gate, int want) {
+                                                const int *gate, int want, unsigned long long *wt) {
   if (want >= 0 && gate[0] != want) return; // (one of the two orders' launches, as k_vol)
+#ifdef PMMG_HIP_MEASURE
+  // measurement build, PMMG_HIP_WAVETIME=1: per wave {start, end, longest walk, active lanes} (wall clock)
+  const unsigned long long wt0 = wt ? wall_clock64() : 0ULL;
+  unsigned wt_steps = 0, wt_act = 0;
+#endif
   __shared__ BlockStats bs;
   bstats_init(&bs);
   __syncthreads();
@@ -156,7 +161,24 @@ __global__ __launch_bounds__(kBlock) void k_bdy(Bg bg, const Frame *fr, const in
       wrote = true;
     }
     wave_stats(&bs, active, hit, steps);
+#ifdef PMMG_HIP_MEASURE
+    if (wt) {
+      unsigned m = active ? (unsigned)steps : 0u;
+      for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o));
+      wt_steps = max(wt_steps, m);
+      wt_act += (unsigned)__popcll(__ballot(active));
+    }
+#endif
   }
+#ifdef PMMG_HIP_MEASURE
+  if (wt && __lane_id() == 0) {
+    unsigned long long *w = wt + 4 * (size_t)(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
+    w[0] = wt0;
+    w[1] = wall_clock64();
+    w[2] = wt_steps;
+    w[3] = wt_act;
+  }
+#endif
   __syncthreads();
   bstats_flush(&bs, st);
   // the surface fallback list is complete: its query grid (fb_grid_build)

@@ -324,6 +324,10 @@ struct pmmg_hip_ctx {
   int ixcd_run = -1; // measurement build, PMMG_HIP_IXCDRUN: the interpolation kernel's XCD run (-1: xcd_run)
   int null_sync = 0;   // measurement build, PMMG_HIP_NULLSYNC=1: small reads through the null stream (ctx_d2h)
   int eager_lanes = 0; // measurement build, PMMG_HIP_EAGERLANES=1: the group lanes created with the context
+  int wave_time = 0;   // measurement build, PMMG_HIP_WAVETIME=1: k_bdy's per-wave wall-clock records, appended
+                       // to the file PMMG_HIP_WAVETIME_OUT at each call's statistics
+  DevBuf wt;
+  size_t wt_n = 0;
   int filter_steps = 64; // step cap of the fp32 filter walk (then the exact fp64 walk continues from where it
                          // stopped: a query the filter misjudges hands over early instead of cycling through a
                          // 4-entry history for up to maxstep steps); test-only PMMG_HIP_FILTER_STEPS=0 sends every
@@ -707,7 +711,7 @@ static pmmg_hip_ctx *create_ctx(int device, int options, bool srf_prio, pmmg_hip
 #ifdef PMMG_HIP_MEASURE
   // A/B switches of the measurement build (libpmmg_hip_measure.so, tools/)
   c->seed_lanes = std::min(4, env_int("PMMG_HIP_SEEDLANES", c->seed_lanes));
-  c->seed_v0 = env_int("PMMG_HIP_SEEDV0", 0) == 1;
+  c->seed_v0 = (env_int("PMMG_HIP_SEEDV0", 0) == 1 ? 1 : 0) | (env_int("PMMG_HIP_SEEDNOATOM", 0) == 1 ? 2 : 0);
   c->bbox_stride = env_int("PMMG_HIP_BBOX", c->bbox_stride);
   c->hist_stride = env_int("PMMG_HIP_HIST", c->hist_stride);
   c->bdy_dyn = env_int("PMMG_HIP_BDYDYN", 2) == 1;
@@ -722,6 +726,7 @@ static pmmg_hip_ctx *create_ctx(int device, int options, bool srf_prio, pmmg_hip
   c->ixcd_run = env_int("PMMG_HIP_IXCDRUN", -1);
   c->null_sync = env_int("PMMG_HIP_NULLSYNC", 0);
   c->eager_lanes = env_int("PMMG_HIP_EAGERLANES", 0);
+  c->wave_time = env_int("PMMG_HIP_WAVETIME", 0);
   c->lane_streams = std::max(1, std::min(3, env_int("PMMG_HIP_LANE_STREAMS", c->lane_streams)));
   c->lane0 = env_int("PMMG_HIP_LANE0", 1) ? 1 : 0;
   c->bdy_first = env_int("PMMG_HIP_BDYFIRST", 0);
@@ -770,7 +775,7 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
                     &c->fbg_vol_u, &c->fbg_vol_i, &c->fbg_bdy_c, &c->fbg_bdy_u, &c->fbg_bdy_i, &c->h_xyz,
                     &c->h_cls, &c->h_met, &c->h_elem, &c->h_hit, &c->brk_k, &c->brk_k2, &c->brk_v, &c->brk_v2,
                     &c->brk_vinv, &c->brk_tinv, &c->brk_xq, &c->brk_xyz, &c->brk_sol, &c->brk_rec, &c->brk_tmp,
-                    &c->locv, &c->locp};
+                    &c->locv, &c->locp, &c->wt};
   for (DevBuf *b : bufs) release(*b);
   for (auto &b : c->o_f) release(b);
   for (auto &b : c->h_f) release(b);
@@ -1617,11 +1622,21 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   };
   // one round of the grid for up to 1M surface points (static split: a
   // second, nearly empty round doubled the surface branch alone)
+  unsigned long long *wt = nullptr;
+#ifdef PMMG_HIP_MEASURE
+  if (c->wave_time) {
+    const size_t nw = (size_t)8 * blocks_for((np_new + 7) / 8, c->bdy_bpx) * (kBlock / 64);
+    if (!ensure(c, c->wt, 32 * nw)) return 0;
+    HIPCK(c, hipMemsetAsync(c->wt.p, 0, 32 * nw, sb));
+    wt = (unsigned long long *)c->wt.p;
+    c->wt_n = nw;
+  }
+#endif
   auto bdy = [&](int want) {
     hipLaunchKernelGGL(k_bdy, dim3(8 * blocks_for((np_new + 7) / 8, c->bdy_bpx)), dim3(kBlock), 0, sb, bg,
                        (const Frame *)fr, (const int *)sgrid, gs, xyz_new, (const int *)order_b, S, elem_out,
                        hit_out, (int *)c->fb_bdy.p, st, c->maxstep, c->bdy_dyn, FbInit{(int *)c->bbest.p},
-                       FbGridBufs{(int *)c->fbg_bdy_c.p, (int *)c->fbg_bdy_u.p, (int *)c->fbg_bdy_i.p}, flag, want);
+                       FbGridBufs{(int *)c->fbg_bdy_c.p, (int *)c->fbg_bdy_u.p, (int *)c->fbg_bdy_i.p}, flag, want, wt);
   };
   // ---- surface branch (second stream, after the order): seeds, k_bdy
   // (r05ae: the surface seeds moved before the wait for the volume seed grid, beside it: preparation
@@ -1758,6 +1773,18 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
 }
 
 static int collect_stats(pmmg_hip_ctx *c, pmmg_hip_stats *out) {
+#ifdef PMMG_HIP_MEASURE
+  if (c->wave_time && c->wt_n) { // k_bdy's per-wave records of the call, appended to PMMG_HIP_WAVETIME_OUT
+    std::vector<unsigned long long> w(4 * c->wt_n);
+    HIPCK(c, ctx_d2h(c, w.data(), c->wt.p, 8 * w.size()));
+    const char *path = getenv("PMMG_HIP_WAVETIME_OUT");
+    if (FILE *f = path ? fopen(path, "ab") : nullptr) {
+      fwrite(w.data(), 8, w.size(), f);
+      fclose(f);
+    }
+    c->wt_n = 0;
+  }
+#endif
   DevStats h;
   int order[2] = {0, 0}; // the call's query order, decided on the device
   HIPCK(c, ctx_d2h(c, order, c->oflag.p, sizeof(order)));

@@ -334,18 +334,33 @@ __global__ __launch_bounds__(kBlock) void k_bbox(const double *xyz, int np, Fram
       cohd[smp] = coh_sample(qxyz, nq, smp);
     }
   }
-  for (long long j = blockIdx.x * blockDim.x + threadIdx.x; j < ns; j += gridDim.x * blockDim.x) {
-    unsigned long long z = (unsigned long long)j * 0x9E3779B97F4A7C15ULL + 0xB0B0B0B0ULL;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
-    z ^= z >> 31;
-    const long long i = j == 0 ? 0 : (j == 1 ? np - 1 : (long long)(z % (unsigned long long)np));
+  // kBboxBatch samples per thread and trip, their rows in flight together
+  // (r06: one sample per trip was a chain of ~4 dependent HBM round trips)
+  constexpr int kBboxBatch = 4;
+  const long long gs_ = (long long)gridDim.x * blockDim.x;
+  for (long long j0 = blockIdx.x * blockDim.x + threadIdx.x; j0 < ns; j0 += kBboxBatch * gs_) {
+    double r[kBboxBatch][3];
+    bool ok[kBboxBatch];
 #pragma unroll
-    for (int d = 0; d < 3; d++) {
-      unsigned long long k = dkey(xyz[3 * i + d]);
-      lo[d] = k < lo[d] ? k : lo[d];
-      hi[d] = k > hi[d] ? k : hi[d];
+    for (int b = 0; b < kBboxBatch; b++) {
+      const long long j = j0 + b * gs_;
+      ok[b] = j < ns;
+      unsigned long long z = (unsigned long long)j * 0x9E3779B97F4A7C15ULL + 0xB0B0B0B0ULL;
+      z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+      z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+      z ^= z >> 31;
+      const long long i = !ok[b] || j == 0 ? 0 : (j == 1 ? np - 1 : (long long)(z % (unsigned long long)np));
+#pragma unroll
+      for (int d = 0; d < 3; d++) r[b][d] = xyz[3 * i + d];
     }
+#pragma unroll
+    for (int b = 0; b < kBboxBatch; b++)
+#pragma unroll
+      for (int d = 0; d < 3; d++) {
+        const unsigned long long k = dkey(r[b][d]);
+        lo[d] = ok[b] && k < lo[d] ? k : lo[d];
+        hi[d] = ok[b] && k > hi[d] ? k : hi[d];
+      }
   }
 #pragma unroll
   for (int d = 0; d < 3; d++) {
@@ -473,7 +488,7 @@ __global__ __launch_bounds__(kBlock) void k_seed_vol(Bg bg, Frame *fr, unsigned 
       ok[b] = ok[b] && tv[b].x > 0;
 #pragma unroll
       for (int d = 0; d < 3; d++) sq[b][d] = 0;
-      if (ok[b] && v0only) { // measurement build (PMMG_HIP_SEEDV0=1): the first vertex stands for the centroid
+      if (ok[b] && (v0only & 1)) { // measurement build (PMMG_HIP_SEEDV0=1): the first vertex stands for the centroid
         const int *q0 = bg.xq + kXqStride * (size_t)(tv[b].x - 1);
 #pragma unroll
         for (int d = 0; d < 3; d++) sq[b][d] = 4LL * q0[d];
@@ -528,7 +543,10 @@ __global__ __launch_bounds__(kBlock) void k_seed_vol(Bg bg, Frame *fr, unsigned 
           if (o < r) leader = false;
         }
       }
-      if (leader) atomicMin(&cell[ci], best);
+      if (leader) {
+        if (v0only & 2) cell[ci] = best; // measurement build (PMMG_HIP_SEEDNOATOM=1): the atomics' price
+        else atomicMin(&cell[ci], best);
+      }
     }
   }
   for (int o = 32; o > 0; o >>= 1) {

@@ -11,6 +11,8 @@ Steps:
   pytest ARGS            python -m pytest ARGS -x -v --timeout 300 (thread method)
   sweep ARGS             tools/sweep.py ARGS (interleaved A/B of module settings)
   bench ARGS             bench.py ARGS; the JSON line -> <tag>/bench[_N].json
+  pmcpy FILT CTRS ARGS   one rocprofv3 --pmc pass of python3 -u ARGS (a tools/ script), table of
+                         the kernels matching FILT
   pmc CFG VARIANT CTRS   one rocprofv3 --pmc pass of tools/sweep.py (one live
                          context, one step) with counters CTRS (space separated,
                          within one pass's limits); table -> <tag>/pmc_*.txt
@@ -107,6 +109,17 @@ def main() -> int:
                     f.write(f"# variant {variant!r}, counters {ctrs}\n")
                     f.flush()
                     subprocess.call([sys.executable, "tools/pmc_table.py", d, "k_"], stdout=f, cwd=ROOT)
+        elif kind == "pmcpy":  # pmcpy KERNEL-SUBSTRING "CTRS" SCRIPT ARGS...: one --pmc pass of a tools/ script
+            filt, ctrs = args[0], args[1]
+            d = os.path.join(out, f"{name}")
+            rc = run(["rocprofv3", "--pmc"] + ctrs.split() + ["-d", os.path.join(d, "p1"), "-o", "run",
+                                                              "--output-format", "csv", "--", sys.executable, "-u"]
+                     + args[2:], log, LIMITS["pmc"], kill_signal="KILL")
+            if rc == 0:
+                with open(os.path.join(out, f"{name}.txt"), "w") as f:
+                    f.write(f"# {' '.join(args[2:])!r}, counters {ctrs}\n")
+                    f.flush()
+                    subprocess.call([sys.executable, "tools/pmc_table.py", d, filt], stdout=f, cwd=ROOT)
         elif kind in ("trace", "tracepy"):
             d = os.path.join(out, name)
             prog = ["bench.py"] if kind == "trace" else []
