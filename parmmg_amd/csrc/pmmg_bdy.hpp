@@ -134,7 +134,6 @@ __global__ __launch_bounds__(kBlock) void k_bdy(Bg bg, const Frame *fr, const in
   const int x = blockIdx.x & 7;
   const long long lo = n * x / 8, hi = n * (x + 1) / 8;
   const XcdChunk ch = xcd_chunk(n); // static split (dyn == 0)
-  bool wrote = false;               // fallback entries written (read by the last block)
   for (int it = 0;; it++) {
     long long i;
     if (dyn) {
@@ -158,7 +157,6 @@ __global__ __launch_bounds__(kBlock) void k_bdy(Bg bg, const Frame *fr, const in
     if (active && hit == 0) {
       fb[slot] = ip;
       fi.at(slot);
-      wrote = true;
     }
     wave_stats(&bs, active, hit, steps);
 #ifdef PMMG_HIP_MEASURE
@@ -181,10 +179,7 @@ __global__ __launch_bounds__(kBlock) void k_bdy(Bg bg, const Frame *fr, const in
 #endif
   __syncthreads();
   bstats_flush(&bs, st);
-  // the surface fallback list is complete: its query grid (fb_grid_build)
-  if (!last_block(&st->bdy_done, wrote)) return;
-  const int nfb = load_agent(&st->nfb_bdy);
-  if (nfb > 0) fb_grid_build(qxyz, fb, nfb, st, 1, gb.cells, gb.cur, gb.items);
+  // (the surface fallback list's query grid: k_fb_grid, launched next)
 }
 
 } // namespace pmmg

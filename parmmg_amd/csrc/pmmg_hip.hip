@@ -165,7 +165,7 @@ struct DevBuf {
 
 enum {
   EV_START, EV_FRAME, EV_PREP, EV_ORDER, EV_VOL0, EV_WALK, EV_VOL, EV_JOIN, EV_END, EV_BDY0, EV_BDY1, EV_RESET,
-  EV_SB0, EV_ORDER2, EV_SRFSEED, EV_COUNT
+  EV_SB0, EV_ORDER2, EV_SRFSEED, EV_FILL, EV_BDYFB, EV_COUNT
 };
 
 struct pmmg_hip_ctx {
@@ -175,6 +175,8 @@ struct pmmg_hip_ctx {
   hipStream_t stream2 = nullptr; // surface branch, concurrent with the volume walk
   hipStream_t stream3 = nullptr; // Morton binning of a call whose order is decided on the device (created at the
                                  // first such call), beside the input order's surface list on stream2
+  hipStream_t stream_f = nullptr; // a large call's seed-grid refill, right after the volume kernel, beside the
+                                  // main stream's tail (created at the first such call)
   hipStream_t stream2_hi = nullptr; // measurement build, PMMG_HIP_SRFPRIO=1: the same at the highest priority,
   bool srf_prio = false;            // for calls of >= kSmallGroup queries (see run_device)
   char err[512] = {0};
@@ -244,7 +246,13 @@ struct pmmg_hip_ctx {
   int pack_passes = 0; // packed records gathered in 1 or 2 passes over the record (PMMG_HIP_PACKPASS; 0: by size)
   int bbox_stride = 64;  // the frame's bbox samples np / n vertices (PMMG_HIP_BBOX; r03o: 64 instead of 16 and
   int hist_stride = 256; // 256 instead of 64 for the axis histograms: preparation -0.15 ms at cfg4, same walks)
-  int bdy_bpx = 512;     // k_bdy blocks per XCD at most (PMMG_HIP_BDYBPX)
+  int bdy_bpx = 512;     // k_bdy blocks per XCD at most (PMMG_HIP_BDYBPX), in blocks of kBlock threads
+  int bdy_wave = 0;      // k_bdy in one-wave blocks (PMMG_HIP_BDYWAVE)
+  int host_order = 1;    // a large auto-order call reads the coherence test's decision on the host after k_bbox
+                         // and enqueues that order's kernels only (PMMG_HIP_HOSTORDER=0: both, gated on the
+                         // device, as before r06)
+  int *flag_host = nullptr;     // (pinned, coherent: k_bbox's last block writes the decision here too)
+  int *flag_host_dev = nullptr; // (its device address)
   int bdy_dyn = 0;       // k_bdy: waves claim work from per-XCD counters (PMMG_HIP_BDYDYN=1; r03y: the claiming
                          // waves slowed the volume kernel beside them, 8-way rank 0.70 -> 0.64 ms static)
   int srf_g = 0;         // test-only PMMG_HIP_SRFG: the surface seed grid's cells per axis (1: one seed for all)
@@ -716,6 +724,8 @@ static pmmg_hip_ctx *create_ctx(int device, int options, bool srf_prio, pmmg_hip
   c->hist_stride = env_int("PMMG_HIP_HIST", c->hist_stride);
   c->bdy_dyn = env_int("PMMG_HIP_BDYDYN", 2) == 1;
   c->bdy_bpx = env_int("PMMG_HIP_BDYBPX", c->bdy_bpx);
+  c->bdy_wave = env_int("PMMG_HIP_BDYWAVE", c->bdy_wave);
+  c->host_order = env_int("PMMG_HIP_HOSTORDER", c->host_order);
   c->bin_qs = env_int("PMMG_HIP_BINQS", 2) == 1;
   c->brick = env_int("PMMG_HIP_BRICK", 0);
   c->srf_solo = env_int("PMMG_HIP_SRFSOLO", -1);
@@ -759,6 +769,7 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   (void)hipStreamSynchronize(c->stream2);
   if (c->stream2_hi) (void)hipStreamSynchronize(c->stream2_hi);
   if (c->stream3) (void)hipStreamSynchronize(c->stream3);
+  if (c->stream_f) (void)hipStreamSynchronize(c->stream_f);
   if (c->cstream) (void)hipStreamSynchronize(c->cstream);
   if (c->stream_i) {
     (void)hipStreamSynchronize(c->stream_i);
@@ -803,6 +814,8 @@ void pmmg_hip_destroy(pmmg_hip_ctx *c) {
   }
   if (c->stream2_hi) (void)hipStreamDestroy(c->stream2_hi);
   if (c->stream3) (void)hipStreamDestroy(c->stream3);
+  if (c->stream_f) (void)hipStreamDestroy(c->stream_f);
+  if (c->flag_host) (void)hipHostFree(c->flag_host);
   if (c->cstream) (void)hipStreamDestroy(c->cstream);
   delete c;
 }
@@ -1504,6 +1517,22 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   int *order_v = (int *)c->order_v.p, *order_b = (int *)c->order_b.p;
   int force = (c->options & PMMG_HIP_OPT_SORT) ? 1 : (c->options & PMMG_HIP_OPT_NOSORT) ? 0 : -1;
   if (force < 0 && np_new < kSmallGroup) force = 0;
+  // r06: a large auto-order call reads the decision back once k_bbox is done (the host waits while the device
+  // runs the fixed-point copy and the seed grid, ~0.4 ms at cfg4) and enqueues only the chosen order's
+  // kernels.  With both orders enqueued and gated on the device, the input order's volume kernel waited for
+  // the ~19 gated binning launches (each dispatched only when the preparation kernels left a slot free: they
+  // ended 20-55 us after the seed grid, profiles/r06i, r06k), or, below 2^23 queries, the other order's
+  // volume launch returned at once in 40-64k one-wave blocks (~35-55 us of dispatch on the main stream).
+  const bool host_order = force < 0 && c->host_order;
+  if (host_order && !c->flag_host) {
+    void *p = nullptr;
+    HIPCK(c, hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped));
+    c->flag_host = (int *)p;
+    void *d = nullptr;
+    HIPCK(c, hipHostGetDevicePointer(&d, p, 0));
+    c->flag_host_dev = (int *)d;
+  }
+  if (host_order) c->flag_host[0] = -1;
 
   // ---- frame (main stream)
   HIPCK(c, hipEventRecord(c->ev[EV_START], s));
@@ -1521,7 +1550,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   // (auto order: the queries' coherence test rides along, its flag read by the order and volume kernels)
   hipLaunchKernelGGL(k_bbox, dim3(std::max(force < 0 ? kCohBlocks : 1, blocks_for(bg.np / c->bbox_stride + 1, 256))),
                      dim3(kBlock), 0, s, bg.xyz, bg.np, fr, c->bbox_stride, g, gs, gb, xyz_new, np_new,
-                     force < 0 ? (int *)c->oflag.p : nullptr, (double *)c->cohd.p);
+                     force < 0 ? (int *)c->oflag.p : nullptr, (double *)c->cohd.p, host_order ? c->flag_host_dev : nullptr);
   // the second stream needs the frame only (lo, inv_bin, inv_srf), not the
   // axis maps (r04: EV_FRAME moved here from after k_axis_map)
   HIPCK(c, hipEventRecord(c->ev[EV_FRAME], s));
@@ -1567,6 +1596,15 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   }
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[EV_PREP], s));
+  if (host_order) { // the decision, written by k_bbox's last block (coherence_final); from here on a forced order
+    HIPCK(c, hipEventSynchronize(c->ev[EV_FRAME]));
+    const int f = __atomic_load_n(&c->flag_host[0], __ATOMIC_ACQUIRE);
+    if (f != 0 && f != 1) {
+      set_err(c, "locate_interp: the query order decision did not arrive (%d)", f);
+      return 0;
+    }
+    force = f;
+  }
 
   // ---- query order (second stream, after the frame): the kernels of both
   // orders, each gated on the coherence test's flag (k_bbox's extra block) on the device — no host read.
@@ -1632,8 +1670,12 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     c->wt_n = nw;
   }
 #endif
+  // k_bdy's blocks: kBlock threads, or one wave each (bdy_wave), so that they fit into the single-wave
+  // slots the volume kernel's one-wave blocks leave while it runs beside them
+  const int bdy_tpb = c->bdy_wave ? 64 : kBlock;
   auto bdy = [&](int want) {
-    hipLaunchKernelGGL(k_bdy, dim3(8 * blocks_for((np_new + 7) / 8, c->bdy_bpx)), dim3(kBlock), 0, sb, bg,
+    hipLaunchKernelGGL(k_bdy, dim3(8 * blocks_for((np_new + 7) / 8, c->bdy_bpx) * (kBlock / bdy_tpb)), dim3(bdy_tpb),
+                       0, sb, bg,
                        (const Frame *)fr, (const int *)sgrid, gs, xyz_new, (const int *)order_b, S, elem_out,
                        hit_out, (int *)c->fb_bdy.p, st, c->maxstep, c->bdy_dyn, FbInit{(int *)c->bbest.p},
                        FbGridBufs{(int *)c->fbg_bdy_c.p, (int *)c->fbg_bdy_u.p, (int *)c->fbg_bdy_i.p}, flag, want, wt);
@@ -1647,18 +1689,27 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     HIPCK(c, hipEventRecord(c->ev[EV_BDY0], sb));
     if (bg.nt > 0) {
       if (force == 0) HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_FRAME], 0)); // (the surface seeds need the frame)
-      hipLaunchKernelGGL(k_seed_srf, dim3(blocks_for(bg.nt, 4096)), dim3(kBlock), 0, sb, bg, (const Frame *)fr,
-                         sgrid, gs);
+      hipLaunchKernelGGL(k_seed_srf, dim3(blocks_for(bg.nt, 4096) * (kBlock / bdy_tpb)), dim3(bdy_tpb), 0, sb, bg,
+                         (const Frame *)fr, sgrid, gs);
       if (c->vol_wait_seed) HIPCK(c, hipEventRecord(c->ev[EV_SRFSEED], sb));
     }
     return 1;
   };
   auto srf_tail = [&]() {
     if (bg.nt > 0) {
-      if (!c->no_fb) launch_bdy_fallbacks(c, sb, S, xyz_new, elem_out, hit_out);
+      if (!c->no_fb) {
+        hipLaunchKernelGGL(k_fb_grid, dim3(1), dim3(bdy_tpb), 0, sb, xyz_new, (const int *)c->fb_bdy.p, st, 1,
+                           FbGridBufs{(int *)c->fbg_bdy_c.p, (int *)c->fbg_bdy_u.p, (int *)c->fbg_bdy_i.p});
+        // one-wave surface branch: its exhaustive kernels (blocks of kBlock threads, which a running volume
+        // kernel's one-wave blocks would keep waiting for four free slots) run on the main stream after the
+        // volume ones
+        if (c->bdy_wave) HIPCK(c, hipEventRecord(c->ev[EV_BDYFB], sb));
+        else launch_bdy_fallbacks(c, sb, S, xyz_new, elem_out, hit_out);
+      }
       HIPCK(c, hipGetLastError());
       if (nsg >= kRefillCells) { // the surface grid refilled for the next call (see k_reset above)
-        hipLaunchKernelGGL(k_fill32, dim3(blocks_for(nsg, 2048)), dim3(kBlock), 0, sb, sgrid, nsg, INT_MAX);
+        hipLaunchKernelGGL(k_fill32, dim3(blocks_for(nsg, 2048) * (kBlock / bdy_tpb)), dim3(bdy_tpb), 0, sb, sgrid,
+                           nsg, INT_MAX);
         c->sgrid_clean_p = c->sgrid.p;
         c->sgrid_clean_n = nsg;
       }
@@ -1742,12 +1793,30 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     vol(-1);
   }
   HIPCK(c, hipEventRecord(c->ev[EV_WALK], s));
+  // the volume seed grid refilled for the next call as soon as the volume kernel is done with it, on its own
+  // stream beside the main stream's tail (the exact continuation, the fallbacks: latency-bound) and the
+  // surface stream's; r06: at the end of the main stream it added ~36 us to a cfg4 call (r05ao: on the
+  // surface stream right after the volume kernel it ran behind k_bdy's tail instead)
+  const bool refill = ng >= kRefillCells;
+  if (refill) {
+    if (!c->stream_f) HIPCK(c, hipStreamCreateWithFlags(&c->stream_f, hipStreamNonBlocking));
+    HIPCK(c, hipStreamWaitEvent(c->stream_f, c->ev[EV_WALK], 0));
+    hipLaunchKernelGGL(k_fill64, dim3(blocks_for((ng + 1) / 2, 2048)), dim3(kBlock), 0, c->stream_f, grid, ng,
+                       ~0ULL);
+    HIPCK(c, hipGetLastError());
+    HIPCK(c, hipEventRecord(c->ev[EV_FILL], c->stream_f));
+    c->grid_clean_p = c->grid.p;
+    c->grid_clean_n = ng;
+  }
   // (8 x 64 one-wave blocks for a large call; fewer for a small group, whose continuations are a few hundred)
   const int wx = (int)std::min<long long>(64, std::max<long long>(2, (long long)np_new / 65536));
   hipLaunchKernelGGL(k_vol_walk_exact, dim3(8 * wx), dim3(64), 0, s, bg, xyz_new, (int *)c->fb_vol.p,
                      (const ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->maxstep, FbInit{(int *)c->best.p},
                      FbGridBufs{(int *)c->fbg_vol_c.p, (int *)c->fbg_vol_u.p, (int *)c->fbg_vol_i.p});
   HIPCK(c, hipGetLastError());
+  if (!c->no_fb)
+    hipLaunchKernelGGL(k_fb_grid, dim3(1), dim3(kBlock), 0, s, xyz_new, (const int *)c->fb_vol.p, st, 0,
+                       FbGridBufs{(int *)c->fbg_vol_c.p, (int *)c->fbg_vol_u.p, (int *)c->fbg_vol_i.p});
   if (vsplit) { // the volume stage ends with the interpolation's last chunk
     HIPCK(c, hipEventRecord(c->ev_interp, c->stream_i));
     HIPCK(c, hipStreamWaitEvent(s, c->ev_interp, 0));
@@ -1756,17 +1825,14 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   // ---- exhaustive fallbacks of the volume queries (lists and counts on the
   // device; the surface ones ran on the surface stream after k_bdy)
   if (!c->no_fb) launch_vol_fallbacks(c, S, xyz_new, elem_out, hit_out);
+  if (!c->no_fb && c->bdy_wave && bg.nt > 0) {
+    HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_BDYFB], 0));
+    launch_bdy_fallbacks(c, s, S, xyz_new, elem_out, hit_out);
+  }
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[EV_JOIN], s));
-  if (ng >= kRefillCells) { // the volume seed grid refilled for the next call, beside the surface stream's tail
-    // (r05ao: on the surface stream right after the volume kernel it ran behind k_bdy's tail instead — the
-    // surface branch ends last at cfg4)
-    hipLaunchKernelGGL(k_fill64, dim3(blocks_for((ng + 1) / 2, 2048)), dim3(kBlock), 0, s, grid, ng, ~0ULL);
-    HIPCK(c, hipGetLastError());
-    c->grid_clean_p = c->grid.p;
-    c->grid_clean_n = ng;
-  }
   HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_BDY1], 0));
+  if (refill) HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_FILL], 0));
   HIPCK(c, hipEventRecord(c->ev[EV_END], s));
   c->pending = true;
   return 1;

@@ -134,13 +134,18 @@ constexpr int kMapBins = 2048;
 constexpr int kMapRatio = 4;
 constexpr int kHistBlocks = 32;
 
+constexpr int kSeedAnyParts = 64;
 struct Frame {
   unsigned long long key_lo[3], key_hi[3];
   double lo[3], ext[3];
   double inv_vol[3], inv_srf[3], inv_bin[3];
   double qc[3], qs; // fixed-point frame of the walk's vertex copy
   int adaptive;     // bit d: axis d of the volume seed grid follows map[d]
-  int seed_any;     // the lowest in-use tetra the seed grid sampled (INT_MAX: none): the last-resort seed
+  // the lowest in-use tetra the seed grid sampled (INT_MAX: none), the last-resort seed: the minimum of
+  // kSeedAnyParts partial minima (block b -> part b % kSeedAnyParts).  r06: one address took every block's
+  // atomic, and atomics on one address serialise at ~11.4 ns each (tools/calib/atomic_same, profiles/r06j):
+  // k_seed_vol's 8192 blocks held ~93 us of them
+  int seed_any[kSeedAnyParts];
   unsigned bbox_done; // blocks done (the last block of k_bbox finalises the frame)
   float map[3][kMapBins + 1]; // map[d][b] = share of the vertices below bin b's lower edge
 };
@@ -265,13 +270,13 @@ __global__ __launch_bounds__(kBlock) void k_quantize(const double *xyz, long lon
 __global__ __launch_bounds__(kBlock) void k_reset(Frame *fr, DevStats *st, unsigned long long *grid, long long ng,
                                                   int *sgrid, long long nsg, int *flag, int force, int force_bits) {
   const long long tid = blockIdx.x * (long long)blockDim.x + threadIdx.x, nth = (long long)gridDim.x * blockDim.x;
+  if (tid < kSeedAnyParts) fr->seed_any[tid] = INT_MAX;
   if (tid == 0) {
     for (int d = 0; d < 3; d++) {
       fr->key_lo[d] = ~0ULL;
       fr->key_hi[d] = 0ULL;
     }
     fr->adaptive = 0;
-    fr->seed_any = INT_MAX;
     fr->bbox_done = 0u;
     if (force >= 0) {
       flag[0] = force;
@@ -306,7 +311,7 @@ __device__ void frame_final(Frame *fr, int g, int gs, int gb);
 // queues; then one block of k_bbox running the whole test, ~30 us on the
 // main stream's critical path, r05ag)
 constexpr int kCohBlocks = 8, kCohSamples = 4096; // 2 samples per thread of each test block
-__device__ void coherence_final(const Frame *fr, const double *cohd, int nq, int *flag);
+__device__ void coherence_final(const Frame *fr, const double *cohd, int nq, int *flag, int *flag_host);
 __device__ __forceinline__ double coh_sample(const double *xyz, int np, int smp) {
   // pseudo-random positions (splitmix64 of the sample index): an evenly
   // strided sample can alias with the row length of a lattice numbering
@@ -323,7 +328,8 @@ __device__ __forceinline__ double coh_sample(const double *xyz, int np, int smp)
   return sqrt(d2);
 }
 __global__ __launch_bounds__(kBlock) void k_bbox(const double *xyz, int np, Frame *fr, int stride, int g, int gs,
-                                                 int gb, const double *qxyz, int nq, int *flag, double *cohd) {
+                                                 int gb, const double *qxyz, int nq, int *flag, double *cohd,
+                                                 int *flag_host) {
   __shared__ unsigned long long slo[3][kBlock / 64], shi[3][kBlock / 64];
   unsigned long long lo[3] = {~0ULL, ~0ULL, ~0ULL}, hi[3] = {0ULL, 0ULL, 0ULL};
   const long long ns = ((long long)np + stride - 1) / stride + 2;
@@ -398,7 +404,7 @@ __global__ __launch_bounds__(kBlock) void k_bbox(const double *xyz, int np, Fram
     frame_final(fr, g, gs, gb);
   }
   __syncthreads();
-  if (flag) coherence_final(fr, cohd, nq, flag);
+  if (flag) coherence_final(fr, cohd, nq, flag, flag_host);
 }
 
 __device__ void frame_final(Frame *fr, int g, int gs, int gb) {
@@ -555,7 +561,7 @@ __global__ __launch_bounds__(kBlock) void k_seed_vol(Bg bg, Frame *fr, unsigned 
   }
   if (__lane_id() == 0 && kmin != INT_MAX) atomicMin(&smin, kmin);
   __syncthreads();
-  if (threadIdx.x == 0 && smin != INT_MAX) atomicMin(&fr->seed_any, smin);
+  if (threadIdx.x == 0 && smin != INT_MAX) atomicMin(&fr->seed_any[blockIdx.x % kSeedAnyParts], smin);
 }
 
 // rare path of seed_vol (the 8 cells are empty): lowest seed id in the shells
@@ -630,7 +636,9 @@ __device__ __forceinline__ int seed_vol(const unsigned long long *cell, int g, c
   // straight to the O(ne) search); 0 (the exhaustive search) when the grid
   // sampled no tetra in use
   noseed = true;
-  return fr->seed_any != INT_MAX ? fr->seed_any : 0;
+  int any = INT_MAX;
+  for (int j = 0; j < kSeedAnyParts; j++) any = min(any, fr->seed_any[j]);
+  return any != INT_MAX ? any : 0;
 }
 
 // ---------------------------------------------------------------- surface seeds and node -> tria CSR
@@ -805,7 +813,8 @@ constexpr int kBinBitsCoherent = 5; // 32^3 cells for a mostly coherent numberin
 // that read the flag waited on it across queues); writes flag[0] (1: Morton
 // bins) and flag[1] (their bits per axis), read on the device by the order
 // kernels and the volume / surface kernels.
-__device__ __noinline__ void coherence_final(const Frame *fr, const double *cohd, int nq, int *flag) {
+__device__ __noinline__ void coherence_final(const Frame *fr, const double *cohd, int nq, int *flag,
+                                             int *flag_host) {
   constexpr int nw = kBlock / 64;
   __shared__ int s_near[nw];
   // the mean spacing of nq points in the (sampled) background box
@@ -830,6 +839,11 @@ __device__ __noinline__ void coherence_final(const Frame *fr, const double *cohd
     const bool coherent = nq > 1 && 4 * tot >= 3 * kCohSamples;
     flag[0] = coherent ? 0 : 1;
     flag[1] = 2 * tot >= kCohSamples ? kBinBitsCoherent : kBinBitsAxis;
+    if (flag_host) { // (a large call's host reads the decision after this kernel: run_device)
+      flag_host[0] = flag[0];
+      flag_host[1] = flag[1];
+      __threadfence_system();
+    }
   }
 }
 
@@ -1157,6 +1171,17 @@ __device__ __noinline__ void fb_grid_build(const double *qxyz, const int *fb, in
     const int c = fb_cell1(x[0], l0, i0, G) + G * (fb_cell1(x[1], l1, i1, G) + G * fb_cell1(x[2], l2, i2, G));
     items[atomicAdd(&cur[c], 1)] = j;
   }
+}
+
+// The query grid of a completed fallback list (cls 0: volume, 1: surface), one
+// block, launched after the kernel that completes the list (r06: before, the
+// last block of that kernel built it after a per-block ticket on one counter
+// — k_bdy's 4096 tickets alone serialised ~47 us of atomics at the end of
+// the surface branch, profiles/r06j); returns at once for an empty list
+__global__ __launch_bounds__(kBlock) void k_fb_grid(const double *qxyz, const int *fb, DevStats *st, int cls,
+                                                   FbGridBufs gb) {
+  const int nfb = cls == 0 ? st->nfb_vol : st->nfb_bdy;
+  if (nfb > 0) fb_grid_build(qxyz, fb, nfb, st, cls, gb.cells, gb.cur, gb.items);
 }
 
 // the queries of the cells an element's (inflated) box covers: visit(j) for

@@ -440,7 +440,6 @@ __global__ __launch_bounds__(64) void k_vol_walk_exact(Bg bg, const double *qxyz
   bstats_init(&bs);
   __syncthreads();
   const XcdChunk ch = xcd_chunk(st->ncont);
-  bool wrote = false; // fallback entries written (read by the last block)
   for (int it = 0; it < ch.iters; it++) {
     const long long j = ch.start + it * ch.stride;
     const bool active = j < ch.hi;
@@ -467,7 +466,6 @@ __global__ __launch_bounds__(64) void k_vol_walk_exact(Bg bg, const double *qxyz
     if (fail) {
       fb[slot] = ip;
       fi.at(slot);
-      wrote = true;
     }
     wave_count(&bs, kCntStuck, fail && status == 2);
     wave_count(&bs, kCntLimit, fail && status == 3);
@@ -475,10 +473,7 @@ __global__ __launch_bounds__(64) void k_vol_walk_exact(Bg bg, const double *qxyz
   }
   __syncthreads();
   bstats_flush(&bs, st);
-  // the volume fallback list is complete: its query grid (fb_grid_build)
-  if (!last_block(&st->walk_done, wrote)) return;
-  const int nfb = load_agent(&st->nfb_vol);
-  if (nfb > 0) fb_grid_build(qxyz, fb, nfb, st, 0, gb.cells, gb.cur, gb.items);
+  // (the volume fallback list's query grid: k_fb_grid, launched next)
 }
 
 // ---------------------------------------------------------------- interpolation
