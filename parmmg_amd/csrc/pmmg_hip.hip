@@ -305,9 +305,16 @@ struct pmmg_hip_ctx {
   // PMMG_HIP_GROUP_LANES: most lanes of a groups call (r05k, 10 cfg2-size groups, 4 hardware queues: 4 / 5 /
   // 8 / 10 lanes 0.096 / 0.083 / 0.092 / 0.095 ms per group — 5 lanes take 2 groups each, 4 take 3, 3, 2, 2;
   // more hardware queues made it slower: 8 queues, 5 lanes 0.127; r04i: 1 / 2 lanes 0.165 / 0.125)
-  int group_lanes = 5;
+  // r06 (profiles/r06m, 3 rounds each, after a fresh start / after a large call in the process): 5 lanes of
+  // 2 streams 0.090 / 0.106 ms per group, 4 x 2 0.079 / 0.091, 4 x 1 0.096 / 0.103, 5 x 1 0.096 / 0.085,
+  // 3 x 1 0.081 / 0.082.  The hardware has 4 queues (GPU_MAX_HW_QUEUES): lane 0 on this context's two
+  // streams plus two lanes of one stream each is 4 streams, one per queue whatever queues earlier streams of
+  // the process left (a new stream takes the least used queue, ties broken in an order that changes from
+  // process to process: with 10 streams two busy lanes shared a queue in some processes and not in others —
+  // the r05 "slowdown after a large call")
+  int group_lanes = 3;
   struct Pool *lane_pool = nullptr; // host threads enqueueing the other lanes' groups
-  int lane_streams = 2; // a group lane's streams: 2 = its own surface stream, 1 = the surface branch on the
+  int lane_streams = 1; // a group lane's streams: 2 = its own surface stream, 1 = the surface branch on the
                         // main stream (measurement build: PMMG_HIP_LANE_STREAMS)
   int bdy_first = 0; // measurement build, PMMG_HIP_BDYFIRST=1: the volume kernel waits for the surface branch
   int vol_wait_seed = 0; // measurement build, PMMG_HIP_VOLWAIT=1: the volume kernel waits for the surface seeds
@@ -2229,6 +2236,14 @@ int pmmg_hip_locate_interp_groups(pmmg_hip_ctx *c, int ngroup, const pmmg_hip_gr
     HIPCK(c, hipStreamDestroy(c->stream2_hi));
     c->stream2_hi = nullptr;
   }
+  // a large call's extra streams (binning, refill) are released before the lanes take theirs, so that the
+  // lanes' streams find the queues those held (a later large call creates them again)
+  for (hipStream_t *x : {&c->stream3, &c->stream_f})
+    if (*x && c->lanes.size() < (size_t)std::min(c->group_lanes, ngroup)) {
+      HIPCK(c, hipStreamSynchronize(*x));
+      HIPCK(c, hipStreamDestroy(*x));
+      *x = nullptr;
+    }
   // lanes dealt an equal number of groups: ceil(n / rounds) lanes for the rounds the most lanes need
   // (10 groups, 5 lanes: 2 each; 7 groups: 4 lanes of 2, 2, 2, 1 rather than 5 of 2, 2, 1, 1, 1)
   const int Lmax = std::max(1, c->group_lanes), rounds = (ngroup + Lmax - 1) / Lmax;

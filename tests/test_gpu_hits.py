@@ -232,3 +232,31 @@ def test_stale_reevaluation_hits(tet8):
     assert np.array_equal(gpu["met"].view(np.uint64), ref["met"].view(np.uint64))
     assert np.array_equal(gpu["fields"][0].view(np.uint64), ref["fields"][0].view(np.uint64))
     assert np.allclose(gpu["met"], exp["met"], rtol=1e-13, atol=0)
+
+
+@pytest.mark.gpu
+def test_long_volume_walks_and_the_step_cap():
+    """walks long enough to reach the step cap.  One volume seed
+    cell (PMMG_HIP_TPC=4096 on ~10k tetra: every walk starts from the same
+    tetra and crosses the cube, tens of steps); first with the default cap
+    (nothing capped: every walk ends in an accepting tetra, class (i)
+    identical to the oracle's walk), then with the cap at a third of the
+    longest of those walks: the capped walks go to the exhaustive search,
+    whose lowest accepting index may differ from the reference's walk only
+    for points several tetra accept (class (ii)); the contract still holds."""
+    case = make_case(kind=synth.CUBE, n_old=12, n_new=13)
+    gpu = run_gpu(case, tet8=True, env={"PMMG_HIP_TPC": "4096"})
+    rep = check(case, gpu)
+    st = gpu["stats"]
+    print(rep, {k: st[k] for k in ("stepmax", "nvol_limit", "nvol_exhaust", "steps_total")})
+    assert st["stepmax"] > 12 and st["nvol_limit"] == 0 and st["nvol_exhaust"] == 0
+    assert rep["class_i"] == rep["class_i_same"]
+    # (a capped filter walk hands over to the exact walk, which has the same cap: a walk of L steps is cut
+    # only when L > 2 cap)
+    cap = max(2, int(st["stepmax"]) // 3)
+    gpu2 = run_gpu(case, tet8=True, env={"PMMG_HIP_TPC": "4096", "PMMG_HIP_MAXSTEP": str(cap)})
+    rep2 = check(case, gpu2)
+    st2 = gpu2["stats"]
+    print(cap, rep2, {k: st2[k] for k in ("stepmax", "nvol_limit", "nvol_exhaust")})
+    assert st2["nvol_limit"] > 0 and st2["nvol_exhaust"] >= st2["nvol_limit"]
+    assert rep2["class_i"] == rep2["class_i_same"]
