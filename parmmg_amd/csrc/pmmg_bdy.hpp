@@ -8,7 +8,8 @@
 namespace pmmg {
 
 // one surface query; returns the hit code (0 = not located: exhaustive list)
-__device__ __forceinline__ int bdy_query(const Bg &bg, const Frame *fr, const int *sgrid, int gs, const double *qxyz,
+__device__ __forceinline__ int bdy_query(const Bg &bg, const Frame *fr, const unsigned long long *sgrid, int gs,
+                                         const double *qxyz,
                                          int ip, const Slots &S, int *elem_out, int8_t *hit_out, int maxstep,
                                          int &steps, int &scans) {
   int hit = 0;
@@ -117,7 +118,8 @@ __device__ __forceinline__ int bdy_query(const Bg &bg, const Frame *fr, const in
 // slowed the volume kernel beside them (profiles/r03y).
 // (r05: a register budget for 5 or 6 waves per SIMD instead of the compiler's
 // 4: the step +-0 / +2 %, the 8-way rank's surface branch +-0, profiles/r05ak)
-__global__ __launch_bounds__(kBlock) void k_bdy(Bg bg, const Frame *fr, const int *sgrid, int gs, const double *qxyz,
+__global__ __launch_bounds__(kBlock) void k_bdy(Bg bg, const Frame *fr, const unsigned long long *sgrid, int gs,
+                                                const double *qxyz,
                                                 const int *order, Slots S, int *elem_out, int8_t *hit_out, int *fb,
                                                 DevStats *st, int maxstep, int dyn, FbInit fi, FbGridBufs gb,
                                                 const int *gate, int want, unsigned long long *wt) {

@@ -1499,7 +1499,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   const long long ng = (long long)g * g * g, nsg = bg.nt > 0 ? (long long)gs * gs * gs : 0;
   const long long ncls = (long long)(nq / kScanChunk + 1);
   if (!ensure(c, c->frame, sizeof(Frame)) || !ensure(c, c->stats, sizeof(DevStats) + kStatParts * sizeof(StatPart)) ||
-      !ensure(c, c->grid, 8 * (size_t)ng) || !ensure(c, c->sgrid, 4 * (size_t)nsg) || !ensure(c, c->order_v, 4 * nq) ||
+      !ensure(c, c->grid, 8 * (size_t)ng) || !ensure(c, c->sgrid, 8 * (size_t)nsg) || !ensure(c, c->order_v, 4 * nq) ||
       !ensure(c, c->order_b, 4 * nq) || !ensure(c, c->cont, sizeof(ContEntry) * nq) ||
       !ensure(c, c->bkeys, 4 * nq) || !ensure(c, c->bkeys2, 4 * nq) || !ensure(c, c->bvals, 4 * nq) ||
       !ensure(c, c->qs, 24 * nq) || !ensure(c, c->cls_cnt, 4 * (size_t)ncls) || 
@@ -1520,7 +1520,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   Frame *fr = (Frame *)c->frame.p;
   DevStats *st = (DevStats *)c->stats.p;
   unsigned long long *grid = (unsigned long long *)c->grid.p;
-  int *sgrid = (int *)c->sgrid.p;
+  unsigned long long *sgrid = (unsigned long long *)c->sgrid.p;
   int *order_v = (int *)c->order_v.p, *order_b = (int *)c->order_b.p;
   int force = (c->options & PMMG_HIP_OPT_SORT) ? 1 : (c->options & PMMG_HIP_OPT_NOSORT) ? 0 : -1;
   if (force < 0 && np_new < kSmallGroup) force = 0;
@@ -1683,7 +1683,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   auto bdy = [&](int want) {
     hipLaunchKernelGGL(k_bdy, dim3(8 * blocks_for((np_new + 7) / 8, c->bdy_bpx) * (kBlock / bdy_tpb)), dim3(bdy_tpb),
                        0, sb, bg,
-                       (const Frame *)fr, (const int *)sgrid, gs, xyz_new, (const int *)order_b, S, elem_out,
+                       (const Frame *)fr, (const unsigned long long *)sgrid, gs, xyz_new, (const int *)order_b, S, elem_out,
                        hit_out, (int *)c->fb_bdy.p, st, c->maxstep, c->bdy_dyn, FbInit{(int *)c->bbest.p},
                        FbGridBufs{(int *)c->fbg_bdy_c.p, (int *)c->fbg_bdy_u.p, (int *)c->fbg_bdy_i.p}, flag, want, wt);
   };
@@ -1715,8 +1715,8 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
       }
       HIPCK(c, hipGetLastError());
       if (nsg >= kRefillCells) { // the surface grid refilled for the next call (see k_reset above)
-        hipLaunchKernelGGL(k_fill32, dim3(blocks_for(nsg, 2048) * (kBlock / bdy_tpb)), dim3(bdy_tpb), 0, sb, sgrid,
-                           nsg, INT_MAX);
+        hipLaunchKernelGGL(k_fill64, dim3(blocks_for((nsg + 1) / 2, 2048) * (kBlock / bdy_tpb)), dim3(bdy_tpb), 0, sb,
+                           sgrid, nsg, ~0ULL);
         c->sgrid_clean_p = c->sgrid.p;
         c->sgrid_clean_n = nsg;
       }

@@ -268,7 +268,8 @@ __global__ __launch_bounds__(kBlock) void k_quantize(const double *xyz, long lon
 // (and writes the order flag of a forced order, when the coherence test is not
 // launched: force >= 0)
 __global__ __launch_bounds__(kBlock) void k_reset(Frame *fr, DevStats *st, unsigned long long *grid, long long ng,
-                                                  int *sgrid, long long nsg, int *flag, int force, int force_bits) {
+                                                  unsigned long long *sgrid, long long nsg, int *flag, int force,
+                                                  int force_bits) {
   const long long tid = blockIdx.x * (long long)blockDim.x + threadIdx.x, nth = (long long)gridDim.x * blockDim.x;
   if (tid < kSeedAnyParts) fr->seed_any[tid] = INT_MAX;
   if (tid == 0) {
@@ -290,7 +291,7 @@ __global__ __launch_bounds__(kBlock) void k_reset(Frame *fr, DevStats *st, unsig
     for (long long j = tid; j < (long long)(kStatParts * sizeof(StatPart) / 8); j += nth) pw[j] = 0ULL;
   }
   for (long long j = tid; j < ng; j += nth) grid[j] = ~0ULL;
-  for (long long j = tid; j < nsg; j += nth) sgrid[j] = INT_MAX;
+  for (long long j = tid; j < nsg; j += nth) sgrid[j] = ~0ULL;
 }
 
 // bbox of np / stride vertices at pseudo-random positions (a strided sample
@@ -643,41 +644,106 @@ __device__ __forceinline__ int seed_vol(const unsigned long long *cell, int g, c
 
 // ---------------------------------------------------------------- surface seeds and node -> tria CSR
 
-// surface seeds: cell of each tria centroid -> min id
-__global__ __launch_bounds__(kBlock) void k_seed_srf(Bg bg, const Frame *fr, int *cell, int g) {
+// surface seeds (r06): per cell the tria whose centroid is nearest the cell
+// centre, one 64-bit key {8-bit squared distance to the centre (cell units),
+// 9-bit centroid offset per axis, 29-bit id} reduced with atomicMin
+// (deterministic), the volume seed grid's scheme; a query takes the nearest
+// centroid among the 8 cells of its octant.  (Up to r05 the cell held its
+// lowest tria id and a query took its own cell's: 3.90 walk steps per
+// surface point at cfg4, the wave's longest walk 8 at the median.)
+__device__ __forceinline__ unsigned long long srf_key(const double *p, const Frame *fr, int g, long long &ci) {
+  int c[3];
+  unsigned long long off = 0;
+  float d2 = 0.f;
+#pragma unroll
+  for (int d = 0; d < 3; d++) {
+    const double t = (p[d] - fr->lo[d]) * fr->inv_srf[d];
+    c[d] = cell_coord(p[d], fr->lo[d], fr->inv_srf[d], g);
+    float f = (float)(t - c[d]);
+    f = f < 0.f ? 0.f : (f > 0.999f ? 0.999f : f);
+    off |= (unsigned long long)(unsigned)(f * 512.f) << (9 * d);
+    d2 += (f - 0.5f) * (f - 0.5f);
+  }
+  const unsigned q8 = d2 * 340.f < 255.f ? (unsigned)(d2 * 340.f) : 255u;
+  ci = c[0] + (long long)g * (c[1] + (long long)g * c[2]);
+  return ((unsigned long long)q8 << 56) | (off << 29);
+}
+
+__global__ __launch_bounds__(kBlock) void k_seed_srf(Bg bg, const Frame *fr, unsigned long long *cell, int g) {
   for (int k = 1 + blockIdx.x * blockDim.x + threadIdx.x; k <= bg.nt; k += gridDim.x * blockDim.x) {
     const int *tv = bg.triv + 3 * (size_t)(k - 1);
     if (tv[0] <= 0) continue;
-    double p0[3], p1[3], p2[3];
+    double p0[3], p1[3], p2[3], m[3];
     load_pt(bg.xyz, tv[0], p0);
     load_pt(bg.xyz, tv[1], p1);
     load_pt(bg.xyz, tv[2], p2);
-    int c[3];
-    for (int d = 0; d < 3; d++) c[d] = cell_coord((p0[d] + p1[d] + p2[d]) * (1.0 / 3.0), fr->lo[d], fr->inv_srf[d], g);
-    atomicMin(&cell[c[0] + (size_t)g * (c[1] + (size_t)g * c[2])], k);
+    for (int d = 0; d < 3; d++) m[d] = (p0[d] + p1[d] + p2[d]) * (1.0 / 3.0);
+    long long ci;
+    const unsigned long long key = srf_key(m, fr, g, ci) | (unsigned)k;
+    atomicMin(&cell[ci], key);
   }
 }
 
-// a tria's surface seed cell; empty cell -> lowest id of the shells of
-// radius 1, 2; 0 when none (-> exhaustive search)
-__device__ int seed_srf(const int *cell, int g, const Frame *fr, const double *x) {
-  int ci = cell_coord(x[0], fr->lo[0], fr->inv_srf[0], g);
-  int cj = cell_coord(x[1], fr->lo[1], fr->inv_srf[1], g);
-  int ck = cell_coord(x[2], fr->lo[2], fr->inv_srf[2], g);
-  int s = cell[ci + (size_t)g * (cj + (size_t)g * ck)];
-  if (s != INT_MAX) return s;
+// squared distance (cell units) from a query at t (cell units) to the
+// centroid a key of cell (a, b, e) records
+__device__ __forceinline__ float srf_d2(unsigned long long v, const double *t, int a, int b, int e) {
+  const unsigned q = (unsigned)((v >> 29) & 0x7FFFFFFULL);
+  const float dx = (float)(t[0] - a) - ((q & 511u) + 0.5f) * (1.0f / 512.0f);
+  const float dy = (float)(t[1] - b) - (((q >> 9) & 511u) + 0.5f) * (1.0f / 512.0f);
+  const float dz = (float)(t[2] - e) - (((q >> 18) & 511u) + 0.5f) * (1.0f / 512.0f);
+  return dx * dx + dy * dy + dz * dz;
+}
+
+// a query's surface seed: the nearest recorded centroid among the 8 cells of
+// its octant; when all 8 are empty, among the cells of the shells of radius
+// 1, 2 around its cell; 0 when none (-> exhaustive search)
+__device__ int seed_srf(const unsigned long long *cell, int g, const Frame *fr, const double *x) {
+  double t[3];
+  int c[3], o[3];
+#pragma unroll
+  for (int d = 0; d < 3; d++) {
+    t[d] = (x[d] - fr->lo[d]) * fr->inv_srf[d];
+    c[d] = cell_coord(x[d], fr->lo[d], fr->inv_srf[d], g);
+    const double f = t[d] - c[d];
+    o[d] = f < 0.5 ? (c[d] > 0 ? -1 : 0) : (c[d] < g - 1 ? 1 : 0);
+  }
+  unsigned long long v[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const int a = c[0] + ((j & 1) ? o[0] : 0), b = c[1] + ((j & 2) ? o[1] : 0), e = c[2] + ((j & 4) ? o[2] : 0);
+    v[j] = cell[a + (size_t)g * (b + (size_t)g * e)];
+  }
+  float best = 3.4e38f;
+  unsigned bid = 0xFFFFFFFFu;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    if (v[j] == ~0ULL) continue;
+    const int a = c[0] + ((j & 1) ? o[0] : 0), b = c[1] + ((j & 2) ? o[1] : 0), e = c[2] + ((j & 4) ? o[2] : 0);
+    const float d2 = srf_d2(v[j], t, a, b, e);
+    const unsigned id = (unsigned)(v[j] & kSeedIdMask);
+    if (d2 < best || (d2 == best && id < bid)) {
+      best = d2;
+      bid = id;
+    }
+  }
+  if (bid != 0xFFFFFFFFu) return (int)bid;
   for (int r = 1; r <= 2; r++) {
-    int best = INT_MAX;
     for (int dk = -r; dk <= r; dk++)
       for (int dj = -r; dj <= r; dj++)
         for (int di = -r; di <= r; di++) {
           if (max(abs(di), max(abs(dj), abs(dk))) != r) continue;
-          int a = ci + di, b = cj + dj, c = ck + dk;
-          if (a < 0 || b < 0 || c < 0 || a >= g || b >= g || c >= g) continue;
-          int v = cell[a + (size_t)g * (b + (size_t)g * c)];
-          best = v < best ? v : best;
+          const int a = c[0] + di, b = c[1] + dj, e = c[2] + dk;
+          if (a < 0 || b < 0 || e < 0 || a >= g || b >= g || e >= g) continue;
+          const unsigned long long w = cell[a + (size_t)g * (b + (size_t)g * e)];
+          if (w == ~0ULL) continue;
+          const float d2 = srf_d2(w, t, a, b, e);
+          const unsigned id = (unsigned)(w & kSeedIdMask);
+          if (d2 < best || (d2 == best && id < bid)) {
+            best = d2;
+            bid = id;
+          }
         }
-    if (best != INT_MAX) return best;
+    if (bid != 0xFFFFFFFFu) return (int)bid;
   }
   return 0;
 }
