@@ -1108,7 +1108,11 @@ __global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsign
       }
     }
   }
-  // 2. the reference's exact test at the candidate
+  // 2. the reference's exact test at the candidate.  (r06: the candidates'
+  // fp64 rows gathered by the wave cooperatively — ~1.1 line accesses per row
+  // instead of two, 16 + 8 bytes per lane — took the volume stage +50 us at
+  // cfg4, +25 at cfg3: the LDS round trip and the wave-wide wait cost more
+  // than the accesses saved, profiles/r06q)
   VolLoc loc;
   bool acc = false;
   if (status == 1) {
