@@ -61,7 +61,7 @@ namespace {
 
 typedef void (*VolFn)(Bg, const Frame *, const unsigned long long *, int, const double *, const uint8_t *,
                       const int *, const double *, int, ContEntry *, DevStats *, Slots, int *, int8_t *, int,
-                      const int *, int, int, int, LocBuf, int);
+                      const int *, int, int, int, LocBuf, int, ContArgs);
 typedef void (*InterpFn)(LocBuf, const int *, const DevStats *, int, Slots, const int *, int, int, int);
 
 // the split stage's walk kernel: the locate-only layout, writing located records
@@ -248,6 +248,8 @@ struct pmmg_hip_ctx {
   int hist_stride = 256; // 256 instead of 64 for the axis histograms: preparation -0.15 ms at cfg4, same walks)
   int bdy_bpx = 512;     // k_bdy blocks per XCD at most (PMMG_HIP_BDYBPX), in blocks of kBlock threads
   int bdy_wave = 0;      // k_bdy in one-wave blocks (PMMG_HIP_BDYWAVE)
+  int fuse_cont = 1;     // the exact continuation inside the volume kernel (PMMG_HIP_FUSECONT=0: the list and
+                         // k_vol_walk_exact, as before r06)
   int host_order = 1;    // a large auto-order call reads the coherence test's decision on the host after k_bbox
                          // and enqueues that order's kernels only (PMMG_HIP_HOSTORDER=0: both, gated on the
                          // device, as before r06)
@@ -733,6 +735,7 @@ static pmmg_hip_ctx *create_ctx(int device, int options, bool srf_prio, pmmg_hip
   c->bdy_bpx = env_int("PMMG_HIP_BDYBPX", c->bdy_bpx);
   c->bdy_wave = env_int("PMMG_HIP_BDYWAVE", c->bdy_wave);
   c->host_order = env_int("PMMG_HIP_HOSTORDER", c->host_order);
+  c->fuse_cont = env_int("PMMG_HIP_FUSECONT", c->fuse_cont);
   c->bin_qs = env_int("PMMG_HIP_BINQS", 2) == 1;
   c->brick = env_int("PMMG_HIP_BRICK", 0);
   c->srf_solo = env_int("PMMG_HIP_SRFSOLO", -1);
@@ -1726,6 +1729,8 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   };
   // ---- volume (main stream): walk + exact test + interpolation in one
   // kernel, then the exact continuation of the few queries it did not settle
+  const bool fuse_cont = c->fuse_cont && !vsplit;
+  const ContArgs ca{(int *)c->fb_vol.p, FbInit{(int *)c->best.p}, c->maxstep, fuse_cont ? 1 : 0};
   auto vol = [&](int want) {
     // (measurement build; a plain call: HIPCK's `return 0` would give this void lambda a return type)
     if (c->vol_wait_seed && bg.nt > 0 && want <= 0) (void)hipStreamWaitEvent(s, c->ev[EV_SRFSEED], 0);
@@ -1734,7 +1739,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
       hipLaunchKernelGGL(vol_fn, dim3(nb), dim3(64), 0, s, bg, (const Frame *)fr, (const unsigned long long *)grid,
                          g, xyz_new, pclass, (const int *)order_v, c->bin_qs ? (const double *)c->qs.p : nullptr,
                          np_new, (ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->filter_steps, flag,
-                         c->xcd_run, c->pad, want, lb, 0);
+                         c->xcd_run, c->pad, want, lb, 0, ca);
       return;
     }
     // split stage: walk chunk j (main stream), then its interpolation on stream_i, beside walk chunk j + 1
@@ -1748,7 +1753,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
       hipLaunchKernelGGL(vol_fn, dim3(nbj), dim3(64), 0, s, bg, (const Frame *)fr, (const unsigned long long *)grid,
                          g, xyz_new, pclass, (const int *)order_v, c->bin_qs ? (const double *)c->qs.p : nullptr,
                          np_new, (ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->filter_steps, flag,
-                         c->xcd_run, c->pad, want, lb, b0);
+                         c->xcd_run, c->pad, want, lb, b0, ca);
       hipEvent_t ej = c->ev_chunk[w][std::min(j, (int)pmmg_hip_ctx::kMaxVolChunks - 1)];
       (void)hipEventRecord(ej, s);
       (void)hipStreamWaitEvent(c->stream_i, ej, 0);
@@ -1817,9 +1822,10 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   }
   // (8 x 64 one-wave blocks for a large call; fewer for a small group, whose continuations are a few hundred)
   const int wx = (int)std::min<long long>(64, std::max<long long>(2, (long long)np_new / 65536));
-  hipLaunchKernelGGL(k_vol_walk_exact, dim3(8 * wx), dim3(64), 0, s, bg, xyz_new, (int *)c->fb_vol.p,
-                     (const ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->maxstep, FbInit{(int *)c->best.p},
-                     FbGridBufs{(int *)c->fbg_vol_c.p, (int *)c->fbg_vol_u.p, (int *)c->fbg_vol_i.p});
+  if (!fuse_cont) // (continued inside the volume kernel otherwise: ContArgs)
+    hipLaunchKernelGGL(k_vol_walk_exact, dim3(8 * wx), dim3(64), 0, s, bg, xyz_new, (int *)c->fb_vol.p,
+                       (const ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->maxstep, FbInit{(int *)c->best.p},
+                       FbGridBufs{(int *)c->fbg_vol_c.p, (int *)c->fbg_vol_u.p, (int *)c->fbg_vol_i.p});
   HIPCK(c, hipGetLastError());
   if (!c->no_fb)
     hipLaunchKernelGGL(k_fb_grid, dim3(1), dim3(kBlock), 0, s, xyz_new, (const int *)c->fb_vol.p, st, 0,

@@ -604,8 +604,23 @@ struct VolShared {
   unsigned short okm[PK > 0 ? 64 : 1]; // output records: the doubles of each lane's record that are written (bit j)
   union {
     float slots[12 * 64]; // walk: the vertex slots [slot*3 + dim][lane]
+    double dslots[12 * 64]; // the exact continuation's fp64 vertex slots (LaneSlotsD)
     double img[(PK > 0 ? 16 : 8) * 64]; // interpolation: 64 rows of up to 6 doubles, or 64 records of up to 16
   } u;
+};
+
+// The exact continuation inside k_vol (r06): a lane whose filter walk did not
+// end in an accepted tetra walks on in fp64 from where it stopped, as
+// k_vol_walk_exact does (same start, fresh history, same arithmetic: the
+// same tetra), and joins the wave's interpolation; only its failures go to
+// the exhaustive list.  Before, the continuations (~0.07 % of the queries)
+// were a list and a kernel of their own after the volume kernel, 40-80 us on
+// the volume stage's tail beside the surface kernel's blocks.
+struct ContArgs {
+  int *fb;     // the volume fallback list (ids)
+  FbInit fi;   // its best-index initialisation
+  int maxstep; // the exact walk's step cap
+  int fuse;    // 1: continue in k_vol (0: the list + k_vol_walk_exact)
 };
 
 // Rows of one vertex of the wave's 64 queries, gathered cooperatively: piece
@@ -1004,7 +1019,7 @@ __global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsign
                                             const double *qs, int np, ContEntry *cont, DevStats *st, Slots S,
                                             int *elem_out, int8_t *hit_out, int filter_steps,
                                             const int *order_flag, int xcd_run, int pad, int want, LocBuf lb,
-                                            int blk0) {
+                                            int blk0, ContArgs ca) {
   // want >= 0: the launch for one of the two orders (auto mode launches both, each after its own lists;
   // the other returns at once)
   if (want >= 0 && order_flag[0] != want) return;
@@ -1123,8 +1138,30 @@ __global__ __launch_bounds__(64) void k_vol(Bg bg, const Frame *fr, const unsign
     acc = exact_accept(x, p, tv, &loc, nullptr) && min4(loc.phi) > kEps;
   }
   const bool more = active && !acc;
-  const int slot = wave_append(&st->ncont, more);
-  if (more) cont[slot] = ContEntry{ip, k};
+  if (ca.fuse && !lb.v) {
+    if (__any(more)) {
+      const LaneSlotsD LD{&sh.u.dslots[__lane_id()]};
+      __builtin_amdgcn_wave_barrier(); // the filter walk's slots are dead
+      int st2 = 0, steps2 = 0;
+      if (more && k > 0) {
+        st2 = walk_exact(bg, x, ip, k, steps2, ca.maxstep, &loc, LD);
+        acc = st2 == 1;
+      }
+      const bool fail = more && !acc;
+      const int fslot = wave_append(&st->nfb_vol, fail);
+      if (fail) {
+        ca.fb[fslot] = ip;
+        ca.fi.at(fslot);
+      }
+      wave_count(&sh.bs, kCntStuck, fail && st2 == 2);
+      wave_count(&sh.bs, kCntLimit, fail && st2 == 3);
+      steps += steps2;
+      __builtin_amdgcn_wave_barrier(); // (the interpolation's image aliases the fp64 slots)
+    }
+  } else {
+    const int slot = wave_append(&st->ncont, more);
+    if (more) cont[slot] = ContEntry{ip, k};
+  }
   wave_stats(&sh.bs, active, acc ? PMMG_HIT_VOL_WALK : 0, steps);
   wave_count(&sh.bs, kCntVolQueries, active);
   wave_count(&sh.bs, kCntExact, more);
