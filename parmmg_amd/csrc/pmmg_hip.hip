@@ -165,7 +165,7 @@ struct DevBuf {
 
 enum {
   EV_START, EV_FRAME, EV_PREP, EV_ORDER, EV_VOL0, EV_WALK, EV_VOL, EV_JOIN, EV_END, EV_BDY0, EV_BDY1, EV_RESET,
-  EV_SB0, EV_ORDER2, EV_SRFSEED, EV_FILL, EV_BDYFB, EV_COUNT
+  EV_SB0, EV_ORDER2, EV_SRFSEED, EV_FILL, EV_BDYFB, EV_QUANT, EV_COUNT
 };
 
 struct pmmg_hip_ctx {
@@ -248,6 +248,7 @@ struct pmmg_hip_ctx {
   int hist_stride = 256; // 256 instead of 64 for the axis histograms: preparation -0.15 ms at cfg4, same walks)
   int bdy_bpx = 512;     // k_bdy blocks per XCD at most (PMMG_HIP_BDYBPX), in blocks of kBlock threads
   int bdy_wave = 0;      // k_bdy in one-wave blocks (PMMG_HIP_BDYWAVE)
+  int quant_side = 0;    // a large call's fixed-point copy beside the seed grid (PMMG_HIP_QUANTSIDE)
   int fuse_cont = 1;     // the exact continuation inside the volume kernel (PMMG_HIP_FUSECONT=0: the list and
                          // k_vol_walk_exact, as before r06)
   int host_order = 1;    // a large auto-order call reads the coherence test's decision on the host after k_bbox
@@ -736,6 +737,7 @@ static pmmg_hip_ctx *create_ctx(int device, int options, bool srf_prio, pmmg_hip
   c->bdy_wave = env_int("PMMG_HIP_BDYWAVE", c->bdy_wave);
   c->host_order = env_int("PMMG_HIP_HOSTORDER", c->host_order);
   c->fuse_cont = env_int("PMMG_HIP_FUSECONT", c->fuse_cont);
+  c->quant_side = env_int("PMMG_HIP_QUANTSIDE", c->quant_side);
   c->bin_qs = env_int("PMMG_HIP_BINQS", 2) == 1;
   c->brick = env_int("PMMG_HIP_BRICK", 0);
   c->srf_solo = env_int("PMMG_HIP_SRFSOLO", -1);
@@ -1564,9 +1566,22 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   // the second stream needs the frame only (lo, inv_bin, inv_srf), not the
   // axis maps (r04: EV_FRAME moved here from after k_axis_map)
   HIPCK(c, hipEventRecord(c->ev[EV_FRAME], s));
-  // fixed-point vertex copy + the axis histograms (first kHistBlocks blocks), then the axis maps
-  hipLaunchKernelGGL(k_quantize, dim3(std::max(kHistBlocks, blocks_for(3LL * bg.np, 8192))), dim3(kBlock), 0, s,
-                     bg.xyz, (long long)bg.np, (const Frame *)fr, (int *)c->xq.p, c->hist_stride, (int *)c->axh.p);
+  // fixed-point vertex copy + the axis histograms (first kHistBlocks blocks), then the axis maps.
+  // quant_side (r06, large calls): the histograms alone on the main stream, the copy on a stream of its own
+  // beside the seed grid, which then takes its centroids from the fp64 rows; the volume kernel waits for both
+  const bool quant_side = c->quant_side && np_new >= kSmallGroup;
+  if (quant_side) {
+    if (!c->stream_f) HIPCK(c, hipStreamCreateWithFlags(&c->stream_f, hipStreamNonBlocking));
+    HIPCK(c, hipStreamWaitEvent(c->stream_f, c->ev[EV_FRAME], 0));
+    hipLaunchKernelGGL(k_quantize, dim3(blocks_for(3LL * bg.np, 8192)), dim3(kBlock), 0, c->stream_f, bg.xyz,
+                       (long long)bg.np, (const Frame *)fr, (int *)c->xq.p, c->hist_stride, (int *)nullptr);
+    HIPCK(c, hipEventRecord(c->ev[EV_QUANT], c->stream_f));
+    hipLaunchKernelGGL(k_axis_hist, dim3(kHistBlocks), dim3(kBlock), 0, s, bg.xyz, (long long)bg.np,
+                       (const Frame *)fr, c->hist_stride, (int *)c->axh.p);
+  } else {
+    hipLaunchKernelGGL(k_quantize, dim3(std::max(kHistBlocks, blocks_for(3LL * bg.np, 8192))), dim3(kBlock), 0, s,
+                       bg.xyz, (long long)bg.np, (const Frame *)fr, (int *)c->xq.p, c->hist_stride, (int *)c->axh.p);
+  }
   hipLaunchKernelGGL(k_axis_map, dim3(3), dim3(kBlock), 0, s, (const int *)c->axh.p, fr, g);
   HIPCK(c, hipGetLastError());
 
@@ -1602,7 +1617,9 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     // kSeedBatch samples per thread in flight together (r05m: one per thread, the 8-way rank's 1.65M samples
     // took 107 us — the grid's latency in rounds of waves — where cfg4's 12.6M take 262 us)
     hipLaunchKernelGGL(k_seed_vol, dim3((blocks_for((nsamp + kSeedBatch - 1) / kSeedBatch, 8192) + 7) & ~7),
-                       dim3(kBlock), 0, s, bg, fr, grid, g, nsamp, c->seed_lanes, c->seed_v0);
+                       dim3(kBlock), 0, s, bg, fr, grid, g, nsamp, c->seed_lanes, c->seed_v0,
+                       quant_side ? bg.xyz : (const double *)nullptr);
+    if (quant_side) HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_QUANT], 0)); // (the walk reads the fixed-point copy)
   }
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[EV_PREP], s));

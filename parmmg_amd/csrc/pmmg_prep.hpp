@@ -220,10 +220,19 @@ __device__ __forceinline__ void axis_hist_block(int (*h)[kMapBins], const double
 // launch: both need only the frame (r05: one launch and its gap less per call;
 // the grid is at least kHistBlocks blocks).
 constexpr int kQuantU = 4;
+// The axis histograms alone (kHistBlocks blocks): a large call's seed grid
+// then needs only them and the frame, while the fixed-point copy runs on a
+// stream of its own beside it (r06, run_device: quant_side)
+__global__ __launch_bounds__(kBlock) void k_axis_hist(const double *xyz, long long np, const Frame *fr, int hstride,
+                                                      int *H) {
+  __shared__ int h[3][kMapBins];
+  axis_hist_block(h, xyz, np, fr, hstride, H);
+}
+
 __global__ __launch_bounds__(kBlock) void k_quantize(const double *xyz, long long np, const Frame *fr, int *xq,
                                                      int hstride, int *H) {
   __shared__ int h[3][kMapBins];
-  if (blockIdx.x < kHistBlocks) axis_hist_block(h, xyz, np, fr, hstride, H); // (block-uniform)
+  if (H && blockIdx.x < kHistBlocks) axis_hist_block(h, xyz, np, fr, hstride, H); // (block-uniform)
   const long long nth = (long long)gridDim.x * blockDim.x;
   if (kXqStride == 3 && ((uintptr_t)xyz & 15) == 0 && ((uintptr_t)xq & 7) == 0) {
     const double qs = fr->qs, qc0 = fr->qc[0], qc1 = fr->qc[1], qc2 = fr->qc[2];
@@ -448,7 +457,7 @@ constexpr unsigned long long kSeedIdMask = (1ULL << 29) - 1; // ids below 2^29 (
 // quantile map (Frame::adaptive) goes through seed_pos.
 constexpr int kSeedBatch = 3;
 __global__ __launch_bounds__(kBlock) void k_seed_vol(Bg bg, Frame *fr, unsigned long long *cell, int g,
-                                                     long long nsamp, int lanes, int v0only) {
+                                                     long long nsamp, int lanes, int v0only, const double *xyzc) {
   constexpr int R = kSeedRun, B = kSeedBatch;
   __shared__ int smin;
   if (threadIdx.x == 0) smin = INT_MAX;
@@ -490,11 +499,27 @@ __global__ __launch_bounds__(kBlock) void k_seed_vol(Bg bg, Frame *fr, unsigned 
       }
     }
     long long sq[B][3]; // 64-bit: clamped coordinates (+-2^30) of vertices outside the sampled frame
+    double cc[B][3];    // (xyzc: the centroids in fp64)
 #pragma unroll
     for (int b = 0; b < B; b++) {
       ok[b] = ok[b] && tv[b].x > 0;
 #pragma unroll
-      for (int d = 0; d < 3; d++) sq[b][d] = 0;
+      for (int d = 0; d < 3; d++) {
+        cc[b][d] = 0.0;
+        sq[b][d] = 0;
+      }
+      if (xyzc) {
+        if (ok[b]) {
+          double p0[3], p1[3], p2[3], p3[3];
+          load_pt(xyzc, tv[b].x, p0);
+          load_pt(xyzc, tv[b].y, p1);
+          load_pt(xyzc, tv[b].z, p2);
+          load_pt(xyzc, tv[b].w, p3);
+#pragma unroll
+          for (int d = 0; d < 3; d++) cc[b][d] = 0.25 * ((p0[d] + p1[d]) + (p2[d] + p3[d]));
+        }
+        continue;
+      }
       if (ok[b] && (v0only & 1)) { // measurement build (PMMG_HIP_SEEDV0=1): the first vertex stands for the centroid
         const int *q0 = bg.xq + kXqStride * (size_t)(tv[b].x - 1);
 #pragma unroll
@@ -524,8 +549,9 @@ __global__ __launch_bounds__(kBlock) void k_seed_vol(Bg bg, Frame *fr, unsigned 
         float d2 = 0.f;
 #pragma unroll
         for (int d = 0; d < 3; d++) {
-          double t = sa[d] + sb[d] * (double)sq[b][d];
-          if ((adaptive >> d) & 1) t = seed_pos(fr, d, fr->qc[d] + 0.25 * (double)sq[b][d] / fr->qs, g);
+          double t = xyzc ? (cc[b][d] - fr->lo[d]) * fr->inv_vol[d] : sa[d] + sb[d] * (double)sq[b][d];
+          if ((adaptive >> d) & 1)
+            t = seed_pos(fr, d, xyzc ? cc[b][d] : fr->qc[d] + 0.25 * (double)sq[b][d] / fr->qs, g);
           c[d] = seed_cell(t, g);
           float f = (float)(t - c[d]);
           f = f < 0.f ? 0.f : (f > 0.999f ? 0.999f : f);
