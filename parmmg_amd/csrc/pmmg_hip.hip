@@ -1844,17 +1844,19 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
                        (const ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->maxstep, FbInit{(int *)c->best.p},
                        FbGridBufs{(int *)c->fbg_vol_c.p, (int *)c->fbg_vol_u.p, (int *)c->fbg_vol_i.p});
   HIPCK(c, hipGetLastError());
-  if (!c->no_fb)
-    hipLaunchKernelGGL(k_fb_grid, dim3(1), dim3(kBlock), 0, s, xyz_new, (const int *)c->fb_vol.p, st, 0,
-                       FbGridBufs{(int *)c->fbg_vol_c.p, (int *)c->fbg_vol_u.p, (int *)c->fbg_vol_i.p});
   if (vsplit) { // the volume stage ends with the interpolation's last chunk
     HIPCK(c, hipEventRecord(c->ev_interp, c->stream_i));
     HIPCK(c, hipStreamWaitEvent(s, c->ev_interp, 0));
   }
   HIPCK(c, hipEventRecord(c->ev[EV_VOL], s));
   // ---- exhaustive fallbacks of the volume queries (lists and counts on the
-  // device; the surface ones ran on the surface stream after k_bdy)
-  if (!c->no_fb) launch_vol_fallbacks(c, S, xyz_new, elem_out, hit_out);
+  // device; the surface ones ran on the surface stream after k_bdy): the
+  // list's query grid, then the searches
+  if (!c->no_fb) {
+    hipLaunchKernelGGL(k_fb_grid, dim3(1), dim3(kBlock), 0, s, xyz_new, (const int *)c->fb_vol.p, st, 0,
+                       FbGridBufs{(int *)c->fbg_vol_c.p, (int *)c->fbg_vol_u.p, (int *)c->fbg_vol_i.p});
+    launch_vol_fallbacks(c, S, xyz_new, elem_out, hit_out);
+  }
   if (!c->no_fb && c->bdy_wave && bg.nt > 0) {
     HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_BDYFB], 0));
     launch_bdy_fallbacks(c, s, S, xyz_new, elem_out, hit_out);
