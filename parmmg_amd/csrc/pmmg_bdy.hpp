@@ -11,7 +11,7 @@ namespace pmmg {
 __device__ __forceinline__ int bdy_query(const Bg &bg, const Frame *fr, const unsigned long long *sgrid, int gs,
                                          const double *qxyz,
                                          int ip, const Slots &S, int *elem_out, int8_t *hit_out, int maxstep,
-                                         int &steps, int &scans) {
+                                         int &steps, int &scans, bool interp = true) {
   int hit = 0;
   double x[3];
   load_pt(qxyz, ip, x);
@@ -105,7 +105,7 @@ __device__ __forceinline__ int bdy_query(const Bg &bg, const Frame *fr, const un
     k = next;
   }
   if (hit) {
-    interp_bdy(S, ip, t.v, phi, edge, vertex);
+    if (interp) interp_bdy(S, ip, t.v, phi, edge, vertex);
     if (elem_out) elem_out[ip - 1] = k;
     if (hit_out) hit_out[ip - 1] = (int8_t)(hit | ((vertex >= 0 ? vertex : (edge >= 0 ? edge : 0)) << 4));
   }
@@ -138,7 +138,7 @@ __global__ __launch_bounds__(kBlock) void k_bdy(Bg bg, const Frame *fr, const un
   const XcdChunk ch = xcd_chunk(n); // static split (dyn == 0)
   for (int it = 0;; it++) {
     long long i;
-    if (dyn) {
+    if (dyn & 1) {
       int base = 0;
       if (__lane_id() == 0) base = atomicAdd(&st->bdy_next[x], 64);
       base = __shfl(base, 0);
@@ -148,11 +148,19 @@ __global__ __launch_bounds__(kBlock) void k_bdy(Bg bg, const Frame *fr, const un
       if (it >= ch.iters) break;
       i = ch.start + it * ch.stride;
     }
-    const bool active = i < (dyn ? hi : ch.hi);
+    const bool active = i < ((dyn & 1) ? hi : ch.hi);
     int steps = 0, hit = 0, ip = 0, scans = 0;
     if (active) {
       ip = order[i];
+      // (measurement build, dyn bit 1 = PMMG_HIP_BDYNOINTERP=1: the walks without the interpolation; r06w:
+      // the interpolation is ~half of a surface wave's lifetime.  r06x: a cooperative version — the three
+      // vertices' rows gathered by the wave through LDS, 8-byte pieces — made the waves longer, 32 vs 30 us,
+      // and the step +27 us: not kept)
+#ifdef PMMG_HIP_MEASURE
+      hit = bdy_query(bg, fr, sgrid, gs, qxyz, ip, S, elem_out, hit_out, maxstep, steps, scans, !(dyn & 2));
+#else
       hit = bdy_query(bg, fr, sgrid, gs, qxyz, ip, S, elem_out, hit_out, maxstep, steps, scans);
+#endif
     }
     wave_count(&bs, kCntFanScan, active && scans > 0);
     int slot = wave_append(&st->nfb_bdy, active && hit == 0);

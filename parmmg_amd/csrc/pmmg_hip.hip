@@ -732,7 +732,7 @@ static pmmg_hip_ctx *create_ctx(int device, int options, bool srf_prio, pmmg_hip
   c->seed_v0 = (env_int("PMMG_HIP_SEEDV0", 0) == 1 ? 1 : 0) | (env_int("PMMG_HIP_SEEDNOATOM", 0) == 1 ? 2 : 0);
   c->bbox_stride = env_int("PMMG_HIP_BBOX", c->bbox_stride);
   c->hist_stride = env_int("PMMG_HIP_HIST", c->hist_stride);
-  c->bdy_dyn = env_int("PMMG_HIP_BDYDYN", 2) == 1;
+  c->bdy_dyn = (env_int("PMMG_HIP_BDYDYN", 2) == 1 ? 1 : 0) | (env_int("PMMG_HIP_BDYNOINTERP", 0) == 1 ? 2 : 0);
   c->bdy_bpx = env_int("PMMG_HIP_BDYBPX", c->bdy_bpx);
   c->bdy_wave = env_int("PMMG_HIP_BDYWAVE", c->bdy_wave);
   c->host_order = env_int("PMMG_HIP_HOSTORDER", c->host_order);
