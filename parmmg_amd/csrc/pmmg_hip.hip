@@ -248,6 +248,7 @@ struct pmmg_hip_ctx {
   int hist_stride = 256; // 256 instead of 64 for the axis histograms: preparation -0.15 ms at cfg4, same walks)
   int bdy_bpx = 512;     // k_bdy blocks per XCD at most (PMMG_HIP_BDYBPX), in blocks of kBlock threads
   int bdy_wave = 0;      // k_bdy in one-wave blocks (PMMG_HIP_BDYWAVE)
+  int ev_vol0 = EV_VOL0, ev_vol = EV_VOL; // the events that open / close the call's volume stage (collect_stats)
   int quant_side = 0;    // a large call's fixed-point copy beside the seed grid (PMMG_HIP_QUANTSIDE)
   int fuse_cont = 1;     // the exact continuation inside the volume kernel (PMMG_HIP_FUSECONT=0: the list and
                          // k_vol_walk_exact, as before r06)
@@ -707,7 +708,17 @@ static pmmg_hip_ctx *create_ctx(int device, int options, bool srf_prio, pmmg_hip
     delete c;
     return nullptr;
   }
-  for (int i = 0; i < EV_COUNT; i++) (void)hipEventCreate(&c->ev[i]);
+  {
+    // measurement build, PMMG_HIP_EVFLAGS: 1 = the call's events without the system-scope fence, 2 = with a
+    // device-scope release; the order decision's EV_FRAME (read by the host) and EV_END keep the default
+    int evf = 0;
+#ifdef PMMG_HIP_MEASURE
+    evf = env_int("PMMG_HIP_EVFLAGS", 0);
+#endif
+    const unsigned fl = evf == 1 ? hipEventDisableSystemFence : (evf == 2 ? hipEventReleaseToDevice : 0u);
+    for (int i = 0; i < EV_COUNT; i++)
+      (void)hipEventCreateWithFlags(&c->ev[i], (i == EV_FRAME || i == EV_END) ? hipEventDefault : fl);
+  }
   // documented options, each clamped to its valid range
   c->tpc = std::min(4096, env_int("PMMG_HIP_TPC", c->tpc));
   c->srf_mult = std::min(4096, env_int("PMMG_HIP_SRFMULT", c->srf_mult));
@@ -1557,7 +1568,9 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   hipLaunchKernelGGL(k_reset, dim3(blocks_for(ng_clr > nsg_clr ? ng_clr : nsg_clr, 2048)), dim3(kBlock), 0, s, fr, st,
                      grid, ng_clr, sgrid, nsg_clr, (int *)c->oflag.p, force, c->bin_bits);
   // the input order's surface list needs only the zeroed counters (and the coherence flag), not the frame
-  HIPCK(c, hipEventRecord(c->ev[EV_RESET], s));
+  // (r06: an event between two kernels of a stream costs the device a few us; EV_RESET is waited for only
+  // in a forced order, EV_VOL0 / EV_VOL only when a kernel separates them from EV_PREP / EV_WALK)
+  if (force >= 0) HIPCK(c, hipEventRecord(c->ev[EV_RESET], s));
   // bbox (its last block finalises the frame), the seed grid's axis maps
   // (auto order: the queries' coherence test rides along, its flag read by the order and volume kernels)
   hipLaunchKernelGGL(k_bbox, dim3(std::max(force < 0 ? kCohBlocks : 1, blocks_for(bg.np / c->bbox_stride + 1, 256))),
@@ -1608,7 +1621,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   // waits for the ~19 binning launches, which return at once but take ~130 us in a row (r05n, 8-way rank).
   // Below 2^23 queries: a larger call's seed grid outlasts the binning chain anyway (cfg4's preparation
   // 0.41 ms) and keeps one volume launch per call.
-  const bool split = force < 0 && sc != sb && np_new < (1 << 23);
+  bool split = force < 0 && sc != sb && np_new < (1 << 23);
   HIPCK(c, hipGetLastError());
 
   // ---- seed grid (main stream): volume seeds
@@ -1623,15 +1636,6 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   }
   HIPCK(c, hipGetLastError());
   HIPCK(c, hipEventRecord(c->ev[EV_PREP], s));
-  if (host_order) { // the decision, written by k_bbox's last block (coherence_final); from here on a forced order
-    HIPCK(c, hipEventSynchronize(c->ev[EV_FRAME]));
-    const int f = __atomic_load_n(&c->flag_host[0], __ATOMIC_ACQUIRE);
-    if (f != 0 && f != 1) {
-      set_err(c, "locate_interp: the query order decision did not arrive (%d)", f);
-      return 0;
-    }
-    force = f;
-  }
 
   // ---- query order (second stream, after the frame): the kernels of both
   // orders, each gated on the coherence test's flag (k_bbox's extra block) on the device — no host read.
@@ -1778,6 +1782,26 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
                          (const DevStats *)st, np_new, S, flag, ixr, want, b0);
     }
   };
+  // host_order: the launches that do not depend on the order (the input order's surface list, gated on the
+  // device flag; the surface seeds) go out before the host waits for the decision, so that after it only the
+  // chosen order's kernels are enqueued, the volume kernel first (r06ze: the device idled ~20 us between the
+  // seed grid and the volume kernel of an 8-way rank while the host enqueued ~10 launches ahead of it)
+  const bool pre = host_order;
+  if (pre) {
+    launch_cls();
+    HIPCK(c, hipEventRecord(c->ev[EV_ORDER], sb));
+    if (!srf_head()) return 0;
+    HIPCK(c, hipGetLastError());
+    // the decision, written by k_bbox's last block (coherence_final); from here on a forced order
+    HIPCK(c, hipEventSynchronize(c->ev[EV_FRAME]));
+    const int f = __atomic_load_n(&c->flag_host[0], __ATOMIC_ACQUIRE);
+    if (f != 0 && f != 1) {
+      set_err(c, "locate_interp: the query order decision did not arrive (%d)", f);
+      return 0;
+    }
+    force = f;
+    split = false; // (the order is known: only its kernels are enqueued, no gated launches of the other)
+  }
   if (split) {
     // Host enqueue order (r05q trace): the input order's kernels first — the surface list, the surface
     // seeds and walk, the volume kernel — then the ~19 binning launches and the Morton order's launches.
@@ -1787,6 +1811,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     HIPCK(c, hipEventRecord(c->ev[EV_ORDER], sb));
     if (!srf_head()) return 0;
     if (bg.nt > 0) bdy(0);
+    c->ev_vol0 = EV_VOL0;
     HIPCK(c, hipEventRecord(c->ev[EV_VOL0], s));
     vol(0);
     if (!launch_morton()) return 0;
@@ -1800,26 +1825,37 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_ORDER2], 0));
     vol(1);
   } else {
-    launch_cls();
+    if (!pre) launch_cls();
     if (!launch_morton()) return 0;
     HIPCK(c, hipGetLastError());
-    HIPCK(c, hipEventRecord(c->ev[EV_ORDER], sb));
+    if (!pre) HIPCK(c, hipEventRecord(c->ev[EV_ORDER], sb));
     HIPCK(c, hipEventRecord(c->ev[EV_ORDER2], sc)); // (sc == sb: the same point)
-    if (sc != sb) HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_ORDER2], 0)); // the Morton surface list
-    if (!srf_head()) return 0;
+    // the volume kernel reads the order branch's lists only in Morton order (or when it may be chosen); in
+    // forced input order its queries are the input's volume points and the wait is dropped (r05: the
+    // cross-stream wait was ~20 us of a small group's main chain)
+    bool vol_first = pre && !c->bdy_first;
+#ifdef PMMG_HIP_MEASURE
+    vol_first = vol_first && c->brick <= 0;
+#endif
+    // the volume kernel right after the seed grid (input order, nothing to wait for): the stage opens at EV_PREP
+    c->ev_vol0 = (vol_first && force == 0) ? EV_PREP : EV_VOL0;
+    auto vol_main = [&]() {
+      if (force < 0) (void)hipStreamWaitEvent(s, c->ev[EV_ORDER], 0);
+      if (force != 0 && sc != sb) (void)hipStreamWaitEvent(s, c->ev[EV_ORDER2], 0);
+      if (c->bdy_first) (void)hipStreamWaitEvent(s, c->ev[EV_BDY1], 0);
+      if (c->ev_vol0 == EV_VOL0) (void)hipEventRecord(c->ev[EV_VOL0], s);
+      vol(-1);
+    };
+    if (vol_first) vol_main();
+    if (sc != sb && force != 0) HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_ORDER2], 0)); // the Morton surface list
+    if (!pre && !srf_head()) return 0;
     if (bg.nt > 0) bdy(-1);
     if (!srf_tail()) return 0;
 #ifdef PMMG_HIP_MEASURE
     if (c->brick > 0 && !brick_renumber(c, s, bg, S, fr, g)) return 0;
 #endif
-    // the volume kernel reads the order branch's lists only in Morton order (or when it may be chosen); in
-    // forced input order its queries are the input's volume points and the wait is dropped (r05: the
-    // cross-stream wait was ~20 us of a small group's main chain)
-    if (force < 0) HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_ORDER], 0));
-    if (force != 0 && sc != sb) HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_ORDER2], 0));
-    if (c->bdy_first) HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_BDY1], 0));
-    HIPCK(c, hipEventRecord(c->ev[EV_VOL0], s));
-    vol(-1);
+    if (!vol_first) vol_main();
+    HIPCK(c, hipGetLastError());
   }
   HIPCK(c, hipEventRecord(c->ev[EV_WALK], s));
   // the volume seed grid refilled for the next call as soon as the volume kernel is done with it, on its own
@@ -1848,7 +1884,8 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     HIPCK(c, hipEventRecord(c->ev_interp, c->stream_i));
     HIPCK(c, hipStreamWaitEvent(s, c->ev_interp, 0));
   }
-  HIPCK(c, hipEventRecord(c->ev[EV_VOL], s));
+  c->ev_vol = (fuse_cont && !vsplit) ? EV_WALK : EV_VOL;
+  if (c->ev_vol == EV_VOL) HIPCK(c, hipEventRecord(c->ev[EV_VOL], s));
   // ---- exhaustive fallbacks of the volume queries (lists and counts on the
   // device; the surface ones ran on the surface stream after k_bdy): the
   // list's query grid, then the searches
@@ -1928,13 +1965,13 @@ static int collect_stats(pmmg_hip_ctx *c, pmmg_hip_stats *out) {
   out->ms_prepare = ms;
   HIPCK(c, hipEventElapsedTime(&ms, c->ev[EV_SB0], c->ev[EV_ORDER]));
   out->ms_sort = ms; // on the second (and third) stream, concurrent with the seed grid
-  HIPCK(c, hipEventElapsedTime(&ms, c->ev[EV_VOL0], c->ev[EV_VOL]));
+  HIPCK(c, hipEventElapsedTime(&ms, c->ev[c->ev_vol0], c->ev[c->ev_vol]));
   out->ms_vol = ms;
-  HIPCK(c, hipEventElapsedTime(&ms, c->ev[EV_VOL0], c->ev[EV_WALK]));
+  HIPCK(c, hipEventElapsedTime(&ms, c->ev[c->ev_vol0], c->ev[EV_WALK]));
   out->ms_vol_locate = ms;
   HIPCK(c, hipEventElapsedTime(&ms, c->ev[EV_BDY0], c->ev[EV_BDY1]));
   out->ms_bdy = ms; // on the surface stream, concurrent with the volume kernels
-  HIPCK(c, hipEventElapsedTime(&ms, c->ev[EV_VOL], c->ev[EV_JOIN]));
+  HIPCK(c, hipEventElapsedTime(&ms, c->ev[c->ev_vol], c->ev[EV_JOIN]));
   out->ms_fallback = ms; // the volume queries' exhaustive search (the surface one is in ms_bdy)
   HIPCK(c, hipEventElapsedTime(&ms, c->ev[EV_START], c->ev[EV_END]));
   out->ms_total = ms;
