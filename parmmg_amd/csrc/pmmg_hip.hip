@@ -18,6 +18,7 @@
 //                   device) | fp32 filter walk + exact acceptance | exact
 //                   continuation | interpolation | join | fallbacks
 //   surface stream  (after the order) surface seeds, node->tria CSR, k_bdy
+#include <hip/hip_ext.h> // hipExtLaunchKernelGGL: events recorded by the kernel dispatch itself
 #include <hip/hip_runtime.h>
 #ifdef PMMG_HIP_MEASURE
 #include <rocprim/device/device_radix_sort.hpp> // the brick renumbering's sort (measurement build)
@@ -1351,7 +1352,7 @@ static int blocks_for(long long n, int cap) {
 // continuation) and of the surface queries (surface stream, after k_bdy): the
 // lists and their counts live on the device, every kernel reads its count
 static void launch_vol_fallbacks(pmmg_hip_ctx *c, const Slots &S, const double *xyz_new, int *elem_out,
-                                 int8_t *hit_out) {
+                                 int8_t *hit_out, hipEvent_t stop = nullptr) {
   const Bg &bg = c->bg;
   hipStream_t s = c->stream;
   DevStats *st = (DevStats *)c->stats.p;
@@ -1362,12 +1363,12 @@ static void launch_vol_fallbacks(pmmg_hip_ctx *c, const Slots &S, const double *
   hipLaunchKernelGGL(k_vol_exhaust_accept, dim3(gv), dim3(kBlock), 0, s, bg, xyz_new, fb, st,
                      (int *)c->best.p, (int *)c->nac.p, (const int *)c->fbg_vol_c.p, (const int *)c->fbg_vol_i.p, S,
                      elem_out, hit_out);
-  hipLaunchKernelGGL(k_vol_exhaust_closest, dim3(gv), dim3(kBlock), 0, s, bg, xyz_new, fb, st,
-                     (const int *)c->nac.p, (FbPart *)c->fbp_vol.p, (int *)c->cres.p, S, elem_out, hit_out);
+  hipExtLaunchKernelGGL(k_vol_exhaust_closest, dim3(gv), dim3(kBlock), 0, s, nullptr, stop, 0, bg, xyz_new, fb, st,
+                        (const int *)c->nac.p, (FbPart *)c->fbp_vol.p, (int *)c->cres.p, S, elem_out, hit_out);
 }
 
 static void launch_bdy_fallbacks(pmmg_hip_ctx *c, hipStream_t s, const Slots &S, const double *xyz_new,
-                                 int *elem_out, int8_t *hit_out) {
+                                 int *elem_out, int8_t *hit_out, hipEvent_t stop = nullptr) {
   const Bg &bg = c->bg;
   DevStats *st = (DevStats *)c->stats.p;
   const int *fb = (const int *)c->fb_bdy.p;
@@ -1375,8 +1376,8 @@ static void launch_bdy_fallbacks(pmmg_hip_ctx *c, hipStream_t s, const Slots &S,
   hipLaunchKernelGGL(k_bdy_exhaust_accept, dim3(gb), dim3(kBlock), 0, s, bg, xyz_new, fb, st,
                      (int *)c->bbest.p, (int *)c->bnac.p, (const int *)c->fbg_bdy_c.p, (const int *)c->fbg_bdy_i.p, S,
                      elem_out, hit_out);
-  hipLaunchKernelGGL(k_bdy_exhaust_closest, dim3(gb), dim3(kBlock), 0, s, bg, xyz_new, fb, st,
-                     (const int *)c->bnac.p, (FbPart *)c->fbp_bdy.p, (int *)c->bcres.p, S, elem_out, hit_out);
+  hipExtLaunchKernelGGL(k_bdy_exhaust_closest, dim3(gb), dim3(kBlock), 0, s, nullptr, stop, 0, bg, xyz_new, fb, st,
+                        (const int *)c->bnac.p, (FbPart *)c->fbp_bdy.p, (int *)c->bcres.p, S, elem_out, hit_out);
 }
 
 #ifdef PMMG_HIP_MEASURE
@@ -1557,28 +1558,29 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   }
   if (host_order) c->flag_host[0] = -1;
 
-  // ---- frame (main stream)
-  HIPCK(c, hipEventRecord(c->ev[EV_START], s));
+  // ---- frame (main stream).  The call's events ride on its kernels' dispatches where a kernel is at hand
+  // (hipExtLaunchKernelGGL start / stop events): a separate marker between two kernels of a stream cost the
+  // device ~4 us, an event on the dispatch ~1.7 (tools/calib/ext_event.hip, profiles/r06zj)
   // seed grids: cleared here unless the previous call left them clean (a
   // large grid is refilled at the end of the call that used it, beside the
   // other stream's tail: r05, cfg4 k_reset 32 us -> the stats only)
   const long long ng_clr = (c->grid.p == c->grid_clean_p && ng <= c->grid_clean_n) ? 0 : ng;
   const long long nsg_clr = (c->sgrid.p == c->sgrid_clean_p && nsg <= c->sgrid_clean_n) ? 0 : nsg;
   c->grid_clean_n = c->sgrid_clean_n = 0; // dirty until this call's refill is enqueued
-  hipLaunchKernelGGL(k_reset, dim3(blocks_for(ng_clr > nsg_clr ? ng_clr : nsg_clr, 2048)), dim3(kBlock), 0, s, fr, st,
-                     grid, ng_clr, sgrid, nsg_clr, (int *)c->oflag.p, force, c->bin_bits);
   // the input order's surface list needs only the zeroed counters (and the coherence flag), not the frame
-  // (r06: an event between two kernels of a stream costs the device a few us; EV_RESET is waited for only
-  // in a forced order, EV_VOL0 / EV_VOL only when a kernel separates them from EV_PREP / EV_WALK)
-  if (force >= 0) HIPCK(c, hipEventRecord(c->ev[EV_RESET], s));
+  // (r06: EV_RESET is waited for only in a forced order, EV_VOL0 / EV_VOL only when a kernel separates them
+  // from EV_PREP / EV_WALK)
+  hipExtLaunchKernelGGL(k_reset, dim3(blocks_for(ng_clr > nsg_clr ? ng_clr : nsg_clr, 2048)), dim3(kBlock), 0, s,
+                        c->ev[EV_START], force >= 0 ? c->ev[EV_RESET] : nullptr, 0, fr, st, grid, ng_clr, sgrid,
+                        nsg_clr, (int *)c->oflag.p, force, c->bin_bits);
   // bbox (its last block finalises the frame), the seed grid's axis maps
   // (auto order: the queries' coherence test rides along, its flag read by the order and volume kernels)
-  hipLaunchKernelGGL(k_bbox, dim3(std::max(force < 0 ? kCohBlocks : 1, blocks_for(bg.np / c->bbox_stride + 1, 256))),
-                     dim3(kBlock), 0, s, bg.xyz, bg.np, fr, c->bbox_stride, g, gs, gb, xyz_new, np_new,
-                     force < 0 ? (int *)c->oflag.p : nullptr, (double *)c->cohd.p, host_order ? c->flag_host_dev : nullptr);
   // the second stream needs the frame only (lo, inv_bin, inv_srf), not the
   // axis maps (r04: EV_FRAME moved here from after k_axis_map)
-  HIPCK(c, hipEventRecord(c->ev[EV_FRAME], s));
+  hipExtLaunchKernelGGL(k_bbox, dim3(std::max(force < 0 ? kCohBlocks : 1, blocks_for(bg.np / c->bbox_stride + 1, 256))),
+                        dim3(kBlock), 0, s, nullptr, c->ev[EV_FRAME], 0, (const double *)bg.xyz, bg.np, fr,
+                        c->bbox_stride, g, gs, gb, xyz_new, np_new, force < 0 ? (int *)c->oflag.p : nullptr,
+                        (double *)c->cohd.p, host_order ? c->flag_host_dev : nullptr);
   // fixed-point vertex copy + the axis histograms (first kHistBlocks blocks), then the axis maps.
   // quant_side (r06, large calls): the histograms alone on the main stream, the copy on a stream of its own
   // beside the seed grid, which then takes its centroids from the fp64 rows; the volume kernel waits for both
@@ -1629,13 +1631,15 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     const long long nsamp = ng < bg.ne ? ng : bg.ne;
     // kSeedBatch samples per thread in flight together (r05m: one per thread, the 8-way rank's 1.65M samples
     // took 107 us — the grid's latency in rounds of waves — where cfg4's 12.6M take 262 us)
-    hipLaunchKernelGGL(k_seed_vol, dim3((blocks_for((nsamp + kSeedBatch - 1) / kSeedBatch, 8192) + 7) & ~7),
-                       dim3(kBlock), 0, s, bg, fr, grid, g, nsamp, c->seed_lanes, c->seed_v0,
-                       quant_side ? bg.xyz : (const double *)nullptr);
-    if (quant_side) HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_QUANT], 0)); // (the walk reads the fixed-point copy)
+    hipExtLaunchKernelGGL(k_seed_vol, dim3((blocks_for((nsamp + kSeedBatch - 1) / kSeedBatch, 8192) + 7) & ~7),
+                          dim3(kBlock), 0, s, nullptr, quant_side ? nullptr : c->ev[EV_PREP], 0, bg, fr, grid, g,
+                          nsamp, c->seed_lanes, c->seed_v0, quant_side ? bg.xyz : (const double *)nullptr);
+    if (quant_side) { // (the walk reads the fixed-point copy)
+      HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_QUANT], 0));
+      HIPCK(c, hipEventRecord(c->ev[EV_PREP], s));
+    }
   }
   HIPCK(c, hipGetLastError());
-  HIPCK(c, hipEventRecord(c->ev[EV_PREP], s));
 
   // ---- query order (second stream, after the frame): the kernels of both
   // orders, each gated on the coherence test's flag (k_bbox's extra block) on the device — no host read.
@@ -1727,6 +1731,8 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     return 1;
   };
   auto srf_tail = [&]() {
+    bool rec = false; // EV_BDY1 recorded by the branch's last launch
+    const bool fill = nsg >= kRefillCells;
     if (bg.nt > 0) {
       if (!c->no_fb) {
         hipLaunchKernelGGL(k_fb_grid, dim3(1), dim3(bdy_tpb), 0, sb, xyz_new, (const int *)c->fb_bdy.p, st, 1,
@@ -1735,32 +1741,35 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
         // kernel's one-wave blocks would keep waiting for four free slots) run on the main stream after the
         // volume ones
         if (c->bdy_wave) HIPCK(c, hipEventRecord(c->ev[EV_BDYFB], sb));
-        else launch_bdy_fallbacks(c, sb, S, xyz_new, elem_out, hit_out);
+        else launch_bdy_fallbacks(c, sb, S, xyz_new, elem_out, hit_out, fill ? nullptr : c->ev[EV_BDY1]);
+        rec = !c->bdy_wave && !fill;
       }
       HIPCK(c, hipGetLastError());
-      if (nsg >= kRefillCells) { // the surface grid refilled for the next call (see k_reset above)
-        hipLaunchKernelGGL(k_fill64, dim3(blocks_for((nsg + 1) / 2, 2048) * (kBlock / bdy_tpb)), dim3(bdy_tpb), 0, sb,
-                           sgrid, nsg, ~0ULL);
+      if (fill) { // the surface grid refilled for the next call (see k_reset above)
+        hipExtLaunchKernelGGL(k_fill64, dim3(blocks_for((nsg + 1) / 2, 2048) * (kBlock / bdy_tpb)), dim3(bdy_tpb), 0,
+                              sb, nullptr, c->ev[EV_BDY1], 0, sgrid, nsg, ~0ULL);
+        rec = true;
         c->sgrid_clean_p = c->sgrid.p;
         c->sgrid_clean_n = nsg;
       }
     }
-    HIPCK(c, hipEventRecord(c->ev[EV_BDY1], sb));
+    if (!rec) HIPCK(c, hipEventRecord(c->ev[EV_BDY1], sb));
     return 1;
   };
   // ---- volume (main stream): walk + exact test + interpolation in one
   // kernel, then the exact continuation of the few queries it did not settle
   const bool fuse_cont = c->fuse_cont && !vsplit;
   const ContArgs ca{(int *)c->fb_vol.p, FbInit{(int *)c->best.p}, c->maxstep, fuse_cont ? 1 : 0};
-  auto vol = [&](int want) {
+  // (stop: an event the launch records, EV_WALK when it is the call's only volume launch)
+  auto vol = [&](int want, hipEvent_t stop) {
     // (measurement build; a plain call: HIPCK's `return 0` would give this void lambda a return type)
     if (c->vol_wait_seed && bg.nt > 0 && want <= 0) (void)hipStreamWaitEvent(s, c->ev[EV_SRFSEED], 0);
     const int nb = (np_new + 63) / 64;
     if (!vsplit) {
-      hipLaunchKernelGGL(vol_fn, dim3(nb), dim3(64), 0, s, bg, (const Frame *)fr, (const unsigned long long *)grid,
-                         g, xyz_new, pclass, (const int *)order_v, c->bin_qs ? (const double *)c->qs.p : nullptr,
-                         np_new, (ContEntry *)c->cont.p, st, S, elem_out, hit_out, c->filter_steps, flag,
-                         c->xcd_run, c->pad, want, lb, 0, ca);
+      hipExtLaunchKernelGGL(vol_fn, dim3(nb), dim3(64), 0, s, nullptr, stop, 0, bg, (const Frame *)fr,
+                            (const unsigned long long *)grid, g, xyz_new, pclass, (const int *)order_v,
+                            c->bin_qs ? (const double *)c->qs.p : nullptr, np_new, (ContEntry *)c->cont.p, st, S,
+                            elem_out, hit_out, c->filter_steps, flag, c->xcd_run, c->pad, want, lb, 0, ca);
       return;
     }
     // split stage: walk chunk j (main stream), then its interpolation on stream_i, beside walk chunk j + 1
@@ -1813,7 +1822,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     if (bg.nt > 0) bdy(0);
     c->ev_vol0 = EV_VOL0;
     HIPCK(c, hipEventRecord(c->ev[EV_VOL0], s));
-    vol(0);
+    vol(0, nullptr);
     if (!launch_morton()) return 0;
     HIPCK(c, hipGetLastError());
     HIPCK(c, hipEventRecord(c->ev[EV_ORDER2], sc));
@@ -1823,7 +1832,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     }
     if (!srf_tail()) return 0;
     HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_ORDER2], 0));
-    vol(1);
+    vol(1, nullptr);
   } else {
     if (!pre) launch_cls();
     if (!launch_morton()) return 0;
@@ -1844,7 +1853,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
       if (force != 0 && sc != sb) (void)hipStreamWaitEvent(s, c->ev[EV_ORDER2], 0);
       if (c->bdy_first) (void)hipStreamWaitEvent(s, c->ev[EV_BDY1], 0);
       if (c->ev_vol0 == EV_VOL0) (void)hipEventRecord(c->ev[EV_VOL0], s);
-      vol(-1);
+      vol(-1, vsplit ? nullptr : c->ev[EV_WALK]);
     };
     if (vol_first) vol_main();
     if (sc != sb && force != 0) HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_ORDER2], 0)); // the Morton surface list
@@ -1857,7 +1866,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     if (!vol_first) vol_main();
     HIPCK(c, hipGetLastError());
   }
-  HIPCK(c, hipEventRecord(c->ev[EV_WALK], s));
+  if (split || vsplit) HIPCK(c, hipEventRecord(c->ev[EV_WALK], s)); // (else recorded by the volume launch)
   // the volume seed grid refilled for the next call as soon as the volume kernel is done with it, on its own
   // stream beside the main stream's tail (the exact continuation, the fallbacks: latency-bound) and the
   // surface stream's; r06: at the end of the main stream it added ~36 us to a cfg4 call (r05ao: on the
@@ -1866,10 +1875,9 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   if (refill) {
     if (!c->stream_f) HIPCK(c, hipStreamCreateWithFlags(&c->stream_f, hipStreamNonBlocking));
     HIPCK(c, hipStreamWaitEvent(c->stream_f, c->ev[EV_WALK], 0));
-    hipLaunchKernelGGL(k_fill64, dim3(blocks_for((ng + 1) / 2, 2048)), dim3(kBlock), 0, c->stream_f, grid, ng,
-                       ~0ULL);
+    hipExtLaunchKernelGGL(k_fill64, dim3(blocks_for((ng + 1) / 2, 2048)), dim3(kBlock), 0, c->stream_f, nullptr,
+                          c->ev[EV_FILL], 0, grid, ng, ~0ULL);
     HIPCK(c, hipGetLastError());
-    HIPCK(c, hipEventRecord(c->ev[EV_FILL], c->stream_f));
     c->grid_clean_p = c->grid.p;
     c->grid_clean_n = ng;
   }
@@ -1889,17 +1897,18 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   // ---- exhaustive fallbacks of the volume queries (lists and counts on the
   // device; the surface ones ran on the surface stream after k_bdy): the
   // list's query grid, then the searches
+  const bool bdy_fb_main = !c->no_fb && c->bdy_wave && bg.nt > 0;
   if (!c->no_fb) {
     hipLaunchKernelGGL(k_fb_grid, dim3(1), dim3(kBlock), 0, s, xyz_new, (const int *)c->fb_vol.p, st, 0,
                        FbGridBufs{(int *)c->fbg_vol_c.p, (int *)c->fbg_vol_u.p, (int *)c->fbg_vol_i.p});
-    launch_vol_fallbacks(c, S, xyz_new, elem_out, hit_out);
+    launch_vol_fallbacks(c, S, xyz_new, elem_out, hit_out, bdy_fb_main ? nullptr : c->ev[EV_JOIN]);
   }
-  if (!c->no_fb && c->bdy_wave && bg.nt > 0) {
+  if (bdy_fb_main) {
     HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_BDYFB], 0));
     launch_bdy_fallbacks(c, s, S, xyz_new, elem_out, hit_out);
   }
   HIPCK(c, hipGetLastError());
-  HIPCK(c, hipEventRecord(c->ev[EV_JOIN], s));
+  if (c->no_fb || bdy_fb_main) HIPCK(c, hipEventRecord(c->ev[EV_JOIN], s)); // (else the last fallback's stop)
   HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_BDY1], 0));
   if (refill) HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_FILL], 0));
   HIPCK(c, hipEventRecord(c->ev[EV_END], s));
