@@ -1605,7 +1605,8 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   // cost 10 groups 0.11 -> 0.25 ms per group and the 8-way rank +0.02 ms for
   // -0.0 at cfg4, `profiles/r04s`: not kept)
   HIPCK(c, hipStreamWaitEvent(sb, c->ev[force < 0 ? EV_FRAME : EV_RESET], 0)); // (the order flag)
-  HIPCK(c, hipEventRecord(c->ev[EV_SB0], sb));
+  // (EV_SB0: the start of the surface list's first kernel when there is one, launch_cls)
+  if (force == 1 || bg.nt <= 0) HIPCK(c, hipEventRecord(c->ev[EV_SB0], sb));
   // the Morton binning on a third stream (r05, `profiles/r05m`: on the second stream its ~19 launches, each
   // returning at once when the coherence test picks input order, held the 8-way rank's volume kernel 86 us
   // behind the seed grid)
@@ -1653,14 +1654,17 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   // input order: the surface points in input order (stable compaction:
   // per-block counts, their scan, the scatter; rocPRIM's select took 0.2 ms
   // longer here, r03o)
-  auto launch_cls = [&]() {
-    if (force == 1 || bg.nt <= 0) return;
+  // (EV_SB0 on its first kernel; EV_ORDER on its last with order_end; returns whether EV_ORDER was recorded)
+  auto launch_cls = [&](bool order_end) -> bool {
+    if (force == 1 || bg.nt <= 0) return false;
     int *bc = (int *)c->cls_cnt.p;
-    hipLaunchKernelGGL(k_cls_count, dim3((unsigned)ncls), dim3(kBlock), 0, sb, pclass, (long long)np_new,
-                       (int)PMMG_PT_BDY, bc, flag, 0);
+    hipExtLaunchKernelGGL(k_cls_count, dim3((unsigned)ncls), dim3(kBlock), 0, sb, c->ev[EV_SB0], nullptr, 0,
+                          pclass, (long long)np_new, (int)PMMG_PT_BDY, bc, flag, 0);
     hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, sb, bc, (int)ncls, &st->nbdy, flag, 0);
-    hipLaunchKernelGGL(k_cls_scatter, dim3((unsigned)ncls), dim3(kBlock), 0, sb, pclass, (long long)np_new,
-                       (int)PMMG_PT_BDY, (const int *)bc, order_b, flag, 0);
+    hipExtLaunchKernelGGL(k_cls_scatter, dim3((unsigned)ncls), dim3(kBlock), 0, sb, nullptr,
+                          order_end ? c->ev[EV_ORDER] : nullptr, 0, pclass, (long long)np_new, (int)PMMG_PT_BDY,
+                          (const int *)bc, order_b, flag, 0);
+    return order_end;
   };
   // Morton order: stable LSD radix sort of the keys (<= 3 * 7 + 2 bits) in 3 passes of 8 bits
   // (pmmg_sort.hpp); the key kernel writes the first pass's digit table
@@ -1721,11 +1725,11 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   auto srf_head = [&]() {
     if (c->srf_solo > 0 || (c->srf_solo < 0 && np_new >= kSmallGroup))
       HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_PREP], 0));
-    HIPCK(c, hipEventRecord(c->ev[EV_BDY0], sb));
+    if (bg.nt <= 0) HIPCK(c, hipEventRecord(c->ev[EV_BDY0], sb)); // (else the start of the surface seeds)
     if (bg.nt > 0) {
       if (force == 0) HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_FRAME], 0)); // (the surface seeds need the frame)
-      hipLaunchKernelGGL(k_seed_srf, dim3(blocks_for(bg.nt, 4096) * (kBlock / bdy_tpb)), dim3(bdy_tpb), 0, sb, bg,
-                         (const Frame *)fr, sgrid, gs);
+      hipExtLaunchKernelGGL(k_seed_srf, dim3(blocks_for(bg.nt, 4096) * (kBlock / bdy_tpb)), dim3(bdy_tpb), 0, sb,
+                            c->ev[EV_BDY0], nullptr, 0, bg, (const Frame *)fr, sgrid, gs);
       if (c->vol_wait_seed) HIPCK(c, hipEventRecord(c->ev[EV_SRFSEED], sb));
     }
     return 1;
@@ -1797,8 +1801,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
   // seed grid and the volume kernel of an 8-way rank while the host enqueued ~10 launches ahead of it)
   const bool pre = host_order;
   if (pre) {
-    launch_cls();
-    HIPCK(c, hipEventRecord(c->ev[EV_ORDER], sb));
+    if (!launch_cls(true)) HIPCK(c, hipEventRecord(c->ev[EV_ORDER], sb));
     if (!srf_head()) return 0;
     HIPCK(c, hipGetLastError());
     // the decision, written by k_bbox's last block (coherence_final); from here on a forced order
@@ -1816,8 +1819,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     // seeds and walk, the volume kernel — then the ~19 binning launches and the Morton order's launches.
     // Enqueued after the binning chain, the input order's volume kernel started ~200 us after the seed grid
     // had finished: the host was still enqueueing (~8 us per launch), the device idle.
-    launch_cls();
-    HIPCK(c, hipEventRecord(c->ev[EV_ORDER], sb));
+    if (!launch_cls(true)) HIPCK(c, hipEventRecord(c->ev[EV_ORDER], sb));
     if (!srf_head()) return 0;
     if (bg.nt > 0) bdy(0);
     c->ev_vol0 = EV_VOL0;
@@ -1834,11 +1836,13 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     HIPCK(c, hipStreamWaitEvent(s, c->ev[EV_ORDER2], 0));
     vol(1, nullptr);
   } else {
-    if (!pre) launch_cls();
+    // (EV_ORDER on the surface list's last kernel unless the Morton lists may follow on the same stream;
+    // EV_ORDER2 is waited for only when the order is Morton)
+    const bool ord = !pre && launch_cls(force == 0);
     if (!launch_morton()) return 0;
     HIPCK(c, hipGetLastError());
-    if (!pre) HIPCK(c, hipEventRecord(c->ev[EV_ORDER], sb));
-    HIPCK(c, hipEventRecord(c->ev[EV_ORDER2], sc)); // (sc == sb: the same point)
+    if (!pre && !ord) HIPCK(c, hipEventRecord(c->ev[EV_ORDER], sb));
+    if (force != 0) HIPCK(c, hipEventRecord(c->ev[EV_ORDER2], sc)); // (sc == sb: the same point)
     // the volume kernel reads the order branch's lists only in Morton order (or when it may be chosen); in
     // forced input order its queries are the input's volume points and the wait is dropped (r05: the
     // cross-stream wait was ~20 us of a small group's main chain)
@@ -1846,8 +1850,13 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
 #ifdef PMMG_HIP_MEASURE
     vol_first = vol_first && c->brick <= 0;
 #endif
-    // the volume kernel right after the seed grid (input order, nothing to wait for): the stage opens at EV_PREP
-    c->ev_vol0 = (vol_first && force == 0) ? EV_PREP : EV_VOL0;
+    // the volume kernel right after the seed grid (input order, nothing to wait for, nothing launched on the
+    // main stream in between): the stage opens at EV_PREP
+    bool vol_direct = force == 0 && !c->bdy_first;
+#ifdef PMMG_HIP_MEASURE
+    vol_direct = vol_direct && c->brick <= 0 && !c->set_order && !c->quant_side;
+#endif
+    c->ev_vol0 = vol_direct ? EV_PREP : EV_VOL0;
     auto vol_main = [&]() {
       if (force < 0) (void)hipStreamWaitEvent(s, c->ev[EV_ORDER], 0);
       if (force != 0 && sc != sb) (void)hipStreamWaitEvent(s, c->ev[EV_ORDER2], 0);
