@@ -668,6 +668,15 @@ static int env_int(const char *name, int def) { // positive values only
   if (e && atoi(e) > 0) return atoi(e);
   return def;
 }
+// switches whose 0 (or -1) is a setting of its own (env_int reads 0 as unset: up to r06zm the
+// PMMG_HIP_HOSTORDER=0, FUSECONT=0, SRFSOLO=0, LANE0=0, STREAM3=0 and IXCDRUN=0 variants ran the default)
+static int env_int_any(const char *name, int def) {
+  const char *e = getenv(name);
+  if (!e || !*e) return def;
+  char *end = nullptr;
+  const long v = strtol(e, &end, 10);
+  return (end && *end == 0) ? (int)v : def;
+}
 
 extern "C" {
 
@@ -747,26 +756,26 @@ static pmmg_hip_ctx *create_ctx(int device, int options, bool srf_prio, pmmg_hip
   c->bdy_dyn = (env_int("PMMG_HIP_BDYDYN", 2) == 1 ? 1 : 0) | (env_int("PMMG_HIP_BDYNOINTERP", 0) == 1 ? 2 : 0);
   c->bdy_bpx = env_int("PMMG_HIP_BDYBPX", c->bdy_bpx);
   c->bdy_wave = env_int("PMMG_HIP_BDYWAVE", c->bdy_wave);
-  c->host_order = env_int("PMMG_HIP_HOSTORDER", c->host_order);
-  c->fuse_cont = env_int("PMMG_HIP_FUSECONT", c->fuse_cont);
+  c->host_order = env_int_any("PMMG_HIP_HOSTORDER", c->host_order);
+  c->fuse_cont = env_int_any("PMMG_HIP_FUSECONT", c->fuse_cont);
   c->quant_side = env_int("PMMG_HIP_QUANTSIDE", c->quant_side);
   c->bin_qs = env_int("PMMG_HIP_BINQS", 2) == 1;
   c->brick = env_int("PMMG_HIP_BRICK", 0);
-  c->srf_solo = env_int("PMMG_HIP_SRFSOLO", -1);
+  c->srf_solo = env_int_any("PMMG_HIP_SRFSOLO", -1);
   c->set_order = env_int("PMMG_HIP_SETORDER", 0);
   if (const char *e = getenv("PMMG_HIP_XCDRUN"))
     if (*e && atoi(e) >= 0) c->xcd_run = atoi(e);
   c->pad = env_int("PMMG_HIP_PAD", 0);
-  c->ixcd_run = env_int("PMMG_HIP_IXCDRUN", -1);
+  c->ixcd_run = env_int_any("PMMG_HIP_IXCDRUN", -1);
   c->null_sync = env_int("PMMG_HIP_NULLSYNC", 0);
   c->eager_lanes = env_int("PMMG_HIP_EAGERLANES", 0);
   c->wave_time = env_int("PMMG_HIP_WAVETIME", 0);
   c->lane_streams = std::max(1, std::min(3, env_int("PMMG_HIP_LANE_STREAMS", c->lane_streams)));
-  c->lane0 = env_int("PMMG_HIP_LANE0", 1) ? 1 : 0;
+  c->lane0 = env_int_any("PMMG_HIP_LANE0", 1) ? 1 : 0;
   c->bdy_first = env_int("PMMG_HIP_BDYFIRST", 0);
   c->vol_wait_seed = env_int("PMMG_HIP_VOLWAIT", 0);
   c->no_fb = env_int("PMMG_HIP_NOFB", 0);
-  c->stream3_mode = env_int("PMMG_HIP_STREAM3", c->stream3_mode);
+  c->stream3_mode = env_int_any("PMMG_HIP_STREAM3", c->stream3_mode);
   if (c->stream3_mode == 2 && hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess)
     c->stream3 = nullptr; // the exhaustive kernels not launched (a launch's price; wrong results
                                            // wherever a query needs them)

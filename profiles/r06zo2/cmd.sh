@@ -1,0 +1,9 @@
+set -o pipefail
+export TMPDIR=/tmp
+M="PMMG_HIP_SO=parmmg_amd/libpmmg_hip_measure.so"
+python3 tools/gpu_job.py --tag r06zo2 \
+ "sweep --config cfg4 --rounds 5 --steps 5 --variants TPC=8;SRFSOLO=0" \
+ "sweep --config cfg4 --rounds 3 --steps 5 --variants perm=mmg;perm=mmg,SRFSOLO=0;perm=shuffle;perm=shuffle,SRFSOLO=0" \
+ "sweep --config cfg3 --rounds 3 --steps 5 --variants TPC=8;SRFSOLO=0" \
+ "py $M PMMG_HIP_SRFSOLO=0 tools/shard_step.py --config cfg4 --world 8 --ranks 0,1,2,3,4,5,6,7 --steps 20" \
+ "py $M PMMG_HIP_SRFSOLO=-1 tools/shard_step.py --config cfg4 --world 8 --ranks 0,1,2,3,4,5,6,7 --steps 20"
