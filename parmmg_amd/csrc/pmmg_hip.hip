@@ -322,6 +322,7 @@ struct pmmg_hip_ctx {
   int lane_streams = 1; // a group lane's streams: 2 = its own surface stream, 1 = the surface branch on the
                         // main stream (measurement build: PMMG_HIP_LANE_STREAMS)
   int bdy_first = 0; // measurement build, PMMG_HIP_BDYFIRST=1: the volume kernel waits for the surface branch
+  int bdy_after = 0; // measurement build, PMMG_HIP_BDYAFTER=1: k_bdy waits for the volume kernel (large calls)
   int vol_wait_seed = 0; // measurement build, PMMG_HIP_VOLWAIT=1: the volume kernel waits for the surface seeds
   int lane0 = 1; // lane 0 enqueues on this context's streams (measurement build: PMMG_HIP_LANE0=0 gives it
                  // streams of its own)
@@ -773,6 +774,7 @@ static pmmg_hip_ctx *create_ctx(int device, int options, bool srf_prio, pmmg_hip
   c->lane_streams = std::max(1, std::min(3, env_int("PMMG_HIP_LANE_STREAMS", c->lane_streams)));
   c->lane0 = env_int_any("PMMG_HIP_LANE0", 1) ? 1 : 0;
   c->bdy_first = env_int("PMMG_HIP_BDYFIRST", 0);
+  c->bdy_after = env_int("PMMG_HIP_BDYAFTER", 0);
   c->vol_wait_seed = env_int("PMMG_HIP_VOLWAIT", 0);
   c->no_fb = env_int("PMMG_HIP_NOFB", 0);
   c->stream3_mode = env_int_any("PMMG_HIP_STREAM3", c->stream3_mode);
@@ -1876,6 +1878,7 @@ static int run_device(pmmg_hip_ctx *c, int np_new, const double *xyz_new, const 
     if (vol_first) vol_main();
     if (sc != sb && force != 0) HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_ORDER2], 0)); // the Morton surface list
     if (!pre && !srf_head()) return 0;
+    if (c->bdy_after && vol_first) HIPCK(c, hipStreamWaitEvent(sb, c->ev[EV_WALK], 0));
     if (bg.nt > 0) bdy(-1);
     if (!srf_tail()) return 0;
 #ifdef PMMG_HIP_MEASURE
